@@ -1,0 +1,48 @@
+// assoc.h -- EAO association engine (host side of assoc.hip / replay.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/eao_accel.h"
+#include "match.h"
+
+namespace eao {
+
+constexpr int NP_MAXN = 8192;   // object points per NP pair handled in LDS
+constexpr int IF_MAXN = 8192;   // points per isolation-forest cloud (LDS ids)
+
+class AssocEngine {
+ public:
+  int dev = 0, max_points = 0;
+  hipStream_t stream = nullptr;
+  // staging
+  float* d_pts = nullptr;        // [2 * max_points * 3]
+  uint8_t* d_valid = nullptr;    // [2 * max_points]
+  int* d_meta = nullptr;         // [8 * max_pairs]
+  eao_np_stats* d_np = nullptr;  // [max_pairs]
+  int* d_rect = nullptr;         // [4 * max_pairs]
+  uint8_t* d_ok = nullptr;
+  float* d_T = nullptr;
+  // isolation forest scratch
+  uint32_t* d_seeds = nullptr;   // [trees]
+  uint16_t* d_ids = nullptr;     // [max_clouds * trees * max_points/2] sample ids
+  float* d_tree = nullptr;       // [max_clouds * trees * 2*IF nodes * 4] (dim,split,size,right)
+  double* d_scores = nullptr;    // [max_points]
+  int max_pairs = 256, max_clouds = 64, max_trees = 64;
+
+  int init(int device, int max_points);
+  ~AssocEngine();
+  // device-level entry points (inputs already on device, stream s)
+  int np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
+               const int* d_flen, const float* d_op, const uint8_t* d_ov, const int* d_ooff,
+               const int* d_olen, eao_np_stats* d_out, hipStream_t s);
+  int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
+                    uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
+                    hipStream_t s);
+  int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
+            const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
+};
+
+}  // namespace eao

@@ -1,0 +1,787 @@
+// match.hip -- ORB matching on gfx950: the MI355X replacement of the Frame
+// grid (reference src/Frame.cc:351-513) and ORBmatcher searches
+// (src/ORBmatcher.cc:45-137, 405-520, 1328-1663).
+//
+// Sequential first-wins semantics are kept exactly: each
+// search runs one wave per frame pair that walks the queries in reference
+// order; inside a query the 64 lanes evaluate the grid window in parallel
+// and reduce on the key (distance, window order), which reproduces the
+// reference's strict-< scan. Assignment state lives in LDS.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <vector>
+
+#include "common.h"
+#include "match.h"
+
+namespace eao {
+
+constexpr int MAXK = 8192;  // keypoints per frame handled by one wave (LDS state)
+constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;  // ORBmatcher.cc:37-39
+
+CamDev make_cam(const eao_camera& c) {
+  CamDev d;
+  d.fx = c.fx;
+  d.fy = c.fy;
+  d.cx = c.cx;
+  d.cy = c.cy;
+  d.minX = 0.0f;
+  d.maxX = (float)c.img_w;
+  d.minY = 0.0f;
+  d.maxY = (float)c.img_h;
+  d.invW = (float)GRID_COLS / (d.maxX - d.minX);
+  d.invH = (float)GRID_ROWS / (d.maxY - d.minY);
+  return d;
+}
+
+__device__ __forceinline__ int hamming256(const uint8_t* a, const uint8_t* b) {
+  const uint4* pa = (const uint4*)a;
+  const uint4* pb = (const uint4*)b;
+  const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+  return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+         __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// Frame::PosInGrid, Frame.cc:503-513
+__device__ __forceinline__ int grid_cell(const CamDev& c, float x, float y) {
+  const int px = (int)roundf(fmul(fsub(x, c.minX), c.invW));
+  const int py = (int)roundf(fmul(fsub(y, c.minY), c.invH));
+  if (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) return -1;
+  return px * GRID_ROWS + py;  // ix-major so window order is (ix, iy)
+}
+
+// AssignFeaturesToGrid (Frame.cc:351-366) as CSR; cells keep ascending index
+__global__ __launch_bounds__(256) void k_grid(const eao_keypoint_dev* __restrict__ kps,
+                                              const int* __restrict__ counts, int n_single,
+                                              int cap, CamDev cam, int* __restrict__ gstart,
+                                              int* __restrict__ gitems) {
+  __shared__ int cnt[GRID_CELLS];
+  __shared__ int part[256];
+  const int f = blockIdx.x, t = threadIdx.x;
+  const int n = counts ? counts[f] : n_single;
+  const eao_keypoint_dev* K = kps + (long long)f * cap;
+  int* S = gstart + (long long)f * (GRID_CELLS + 1);
+  int* I = gitems + (long long)f * cap;
+  for (int i = t; i < GRID_CELLS; i += 256) cnt[i] = 0;
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const int c = grid_cell(cam, K[i].x, K[i].y);
+    if (c >= 0) atomicAdd(&cnt[c], 1);
+  }
+  __syncthreads();
+  // exclusive scan, 12 cells per thread
+  const int per = GRID_CELLS / 256;
+  int loc = 0;
+  for (int k = 0; k < per; k++) loc += cnt[t * per + k];
+  part[t] = loc;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int k = 0; k < 256; k++) {
+      const int v = part[k];
+      part[k] = run;
+      run += v;
+    }
+  }
+  __syncthreads();
+  int run = part[t];
+  for (int k = 0; k < per; k++) {
+    const int c = t * per + k;
+    const int v = cnt[c];
+    S[c] = run;
+    cnt[c] = run;  // becomes the fill cursor
+    run += v;
+  }
+  if (t == 255) S[GRID_CELLS] = run;
+  __syncthreads();
+  for (int i = t; i < n; i += 256) {
+    const int c = grid_cell(cam, K[i].x, K[i].y);
+    if (c >= 0) I[atomicAdd(&cnt[c], 1)] = i;
+  }
+  __syncthreads();
+  // restore ascending index order inside each cell (insertion sort, tiny cells)
+  for (int c = t; c < GRID_CELLS; c += 256) {
+    const int b = S[c], e = S[c + 1];
+    for (int i = b + 1; i < e; i++) {
+      const int v = I[i];
+      int j = i - 1;
+      while (j >= b && I[j] > v) {
+        I[j + 1] = I[j];
+        j--;
+      }
+      I[j + 1] = v;
+    }
+  }
+}
+
+// cv::Mat small gemm: float dot then (float)(t + c) in double (see oracle)
+__device__ __forceinline__ void transform_point(const float* T, const float* P, float* out) {
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const float t = fadd(fadd(fmul(T[4 * r], P[0]), fmul(T[4 * r + 1], P[1])), fmul(T[4 * r + 2], P[2]));
+    out[r] = (float)((double)t + (double)T[4 * r + 3]);
+  }
+}
+
+struct Window {
+  int x0, x1, y0, y1;  // cell ranges, inclusive
+  bool empty;
+};
+
+// Frame::GetFeaturesInArea cell range, Frame.cc:448-473
+__device__ __forceinline__ Window window_cells(const CamDev& c, float x, float y, float r) {
+  Window w;
+  w.empty = true;
+  w.x0 = max(0, (int)floorf(fmul(fsub(fsub(x, c.minX), r), c.invW)));
+  if (w.x0 >= GRID_COLS) return w;
+  w.x1 = min(GRID_COLS - 1, (int)ceilf(fmul(fadd(fsub(x, c.minX), r), c.invW)));
+  if (w.x1 < 0) return w;
+  w.y0 = max(0, (int)floorf(fmul(fsub(fsub(y, c.minY), r), c.invH)));
+  if (w.y0 >= GRID_ROWS) return w;
+  w.y1 = min(GRID_ROWS - 1, (int)ceilf(fmul(fadd(fsub(y, c.minY), r), c.invH)));
+  if (w.y1 < 0) return w;
+  w.empty = false;
+  return w;
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int rot_bin(float a_last, float a_cur) {
+  const float factor = 1.0f / HISTO_LENGTH;
+  float rot = fsub(a_last, a_cur);
+  if (rot < 0.0f) rot = fadd(rot, 360.0f);
+  int bin = (int)roundf(fmul(rot, factor));
+  if (bin == HISTO_LENGTH) bin = 0;
+  return bin;
+}
+
+// ComputeThreeMaxima, ORBmatcher.cc:1601-1642 (run by one lane)
+__device__ void three_maxima(const int* h, int& ind1, int& ind2, int& ind3) {
+  int max1 = 0, max2 = 0, max3 = 0;
+  ind1 = ind2 = ind3 = -1;
+  for (int i = 0; i < HISTO_LENGTH; i++) {
+    const int s = h[i];
+    if (s > max1) {
+      max3 = max2; max2 = max1; max1 = s;
+      ind3 = ind2; ind2 = ind1; ind1 = i;
+    } else if (s > max2) {
+      max3 = max2; max2 = s;
+      ind3 = ind2; ind2 = i;
+    } else if (s > max3) {
+      max3 = s;
+      ind3 = i;
+    }
+  }
+  if (max2 < fmul(0.1f, (float)max1)) {
+    ind2 = -1;
+    ind3 = -1;
+  } else if (max3 < fmul(0.1f, (float)max1)) {
+    ind3 = -1;
+  }
+}
+
+constexpr unsigned long long KEY_NONE = ~0ull;
+__device__ __forceinline__ unsigned long long make_key(int dist, int cellk, int idx) {
+  return ((unsigned long long)dist << 42) | ((unsigned long long)cellk << 21) | (unsigned long long)idx;
+}
+__device__ __forceinline__ int key_dist(unsigned long long k) { return (int)(k >> 42); }
+__device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(k & 0x1fffff); }
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono=true), ORBmatcher.cc:1328-1470.
+// One wave per pair p: last = slot p, current = slot p+1.
+__global__ __launch_bounds__(64) void k_match_motion(
+    CamDev cam, const float* __restrict__ Tcw, float th, int check_ori,
+    const eao_keypoint_dev* __restrict__ kps, const uint8_t* __restrict__ desc,
+    const int* __restrict__ counts, int cap, const uint8_t* __restrict__ has_mp,
+    const float* __restrict__ mp_pos, const uint8_t* __restrict__ mp_desc,
+    const float* __restrict__ scales, const int* __restrict__ gstart,
+    const int* __restrict__ gitems, int* __restrict__ cur_match, int* __restrict__ nmatches_out) {
+  __shared__ int match[MAXK];
+  __shared__ signed char bins[MAXK];
+  __shared__ int hist[HISTO_LENGTH];
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const int ls = p, cs = p + 1;
+  const int n_last = counts[ls], n_cur = counts[cs];
+  const eao_keypoint_dev* LK = kps + (long long)ls * cap;
+  const eao_keypoint_dev* CK = kps + (long long)cs * cap;
+  const uint8_t* CD = desc + (long long)cs * cap * 32;
+  const uint8_t* HM = has_mp + (long long)ls * cap;
+  const float* MP = mp_pos + (long long)ls * cap * 3;
+  const uint8_t* MD = mp_desc + (long long)ls * cap * 32;
+  const int* GS = gstart + (long long)cs * (GRID_CELLS + 1);
+  const int* GI = gitems + (long long)cs * cap;
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
+  for (int i = lane; i < n_cur; i += 64) {
+    match[i] = -1;
+    bins[i] = -1;
+  }
+  __syncthreads();
+  int nmatches = 0;
+  for (int i = 0; i < n_last; i++) {
+    if (!HM[i]) continue;
+    float x3Dc[3];
+    transform_point(T, MP + 3 * i, x3Dc);
+    const float xc = x3Dc[0], yc = x3Dc[1];
+    const float invzc = (float)(1.0 / (double)x3Dc[2]);
+    if (invzc < 0) continue;
+    const float u = fadd(fmul(fmul(cam.fx, xc), invzc), cam.cx);
+    const float v = fadd(fmul(fmul(cam.fy, yc), invzc), cam.cy);
+    if (u < cam.minX || u > cam.maxX) continue;
+    if (v < cam.minY || v > cam.maxY) continue;
+    const int oct = LK[i].octave;
+    const float r = fmul(th, scales[oct]);
+    const Window w = window_cells(cam, u, v, r);
+    if (w.empty) continue;
+    const int minL = oct - 1, maxL = oct + 1;
+    const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+    const uint8_t* d = MD + 32 * (long long)i;
+    unsigned long long best = KEY_NONE;
+    for (int ck = lane; ck < ncell; ck += 64) {
+      const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
+      const int cell = ix * GRID_ROWS + iy;
+      for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+        const int i2 = GI[q];
+        const eao_keypoint_dev& kp = CK[i2];
+        if (kp.octave < minL) continue;
+        if (kp.octave > maxL) continue;
+        if (!(fabsf(fsub(kp.x, u)) < r && fabsf(fsub(kp.y, v)) < r)) continue;
+        if (match[i2] >= 0) continue;  // mvpMapPoints[i2] && Observations() > 0
+        const int dist = hamming256(d, CD + 32 * (long long)i2);
+        const unsigned long long key = make_key(dist, ck, i2);
+        best = key < best ? key : best;
+      }
+    }
+    best = wave_min_u64(best);
+    if (best != KEY_NONE && key_dist(best) <= TH_HIGH) {
+      const int i2 = key_idx(best);
+      if (lane == 0) {
+        match[i2] = i;
+        if (check_ori) bins[i2] = (signed char)rot_bin(LK[i].angle, CK[i2].angle);
+      }
+      nmatches++;
+    }
+    __syncthreads();
+  }
+  if (check_ori) {
+    for (int b = lane; b < HISTO_LENGTH; b += 64) hist[b] = 0;
+    __syncthreads();
+    for (int i2 = lane; i2 < n_cur; i2 += 64)
+      if (match[i2] >= 0) atomicAdd(&hist[bins[i2]], 1);
+    __syncthreads();
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    int removed = 0;
+    for (int i2 = lane; i2 < n_cur; i2 += 64) {
+      if (match[i2] >= 0) {
+        const int b = bins[i2];
+        if (b != ind1 && b != ind2 && b != ind3) {
+          match[i2] = -1;
+          removed++;
+        }
+      }
+    }
+    nmatches -= wave_sum(removed);
+    __syncthreads();
+  }
+  int* out = cur_match + (long long)cs * cap;
+  for (int i2 = lane; i2 < n_cur; i2 += 64) out[i2] = match[i2];
+  if (lane == 0) nmatches_out[cs] = nmatches;
+}
+
+// Frame::isInFrustum + MapPoint::PredictScale (see oracle/match_ref.cpp)
+__global__ __launch_bounds__(256) void k_frustum(CamDev cam, const float* __restrict__ T, int n,
+                                                 const float* __restrict__ pos,
+                                                 const float* __restrict__ nrm,
+                                                 const float* __restrict__ mind,
+                                                 const float* __restrict__ maxd, float vclim,
+                                                 float logsf, uint8_t* __restrict__ in_view,
+                                                 float* __restrict__ proj, int* __restrict__ level,
+                                                 float* __restrict__ vcos) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float Ow[3];
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    double s = (double)T[c] * (double)T[3];
+    s = __dadd_rn(s, (double)T[4 + c] * (double)T[7]);
+    s = __dadd_rn(s, (double)T[8 + c] * (double)T[11]);
+    Ow[c] = (float)(s * -1.0);
+  }
+  in_view[i] = 0;
+  const float* P = pos + 3 * i;
+  float Pc[3];
+  transform_point(T, P, Pc);
+  if (Pc[2] < 0.0f) return;
+  const float invz = fdiv(1.0f, Pc[2]);
+  const float u = fadd(fmul(fmul(cam.fx, Pc[0]), invz), cam.cx);
+  const float v = fadd(fmul(fmul(cam.fy, Pc[1]), invz), cam.cy);
+  if (u < cam.minX || u > cam.maxX) return;
+  if (v < cam.minY || v > cam.maxY) return;
+  const float maxDistance = fmul(1.2f, maxd[i]);
+  const float minDistance = fmul(0.8f, mind[i]);
+  const float PO[3] = {fsub(P[0], Ow[0]), fsub(P[1], Ow[1]), fsub(P[2], Ow[2])};
+  double s = 0;
+  for (int k = 0; k < 3; k++) s = __dadd_rn(s, __dmul_rn((double)PO[k], (double)PO[k]));
+  const float dist = (float)sqrt(s);
+  if (dist < minDistance || dist > maxDistance) return;
+  double dot = 0;
+  for (int k = 0; k < 3; k++) dot = __dadd_rn(dot, __dmul_rn((double)PO[k], (double)nrm[3 * i + k]));
+  const float viewCos = (float)(dot / (double)dist);
+  if (viewCos < vclim) return;
+  const float ratio = fdiv(maxd[i], dist);
+  const int lvl = (int)ceilf(fdiv((float)log((double)ratio), logsf));
+  in_view[i] = 1;
+  proj[2 * i] = u;
+  proj[2 * i + 1] = v;
+  level[i] = lvl;
+  vcos[i] = viewCos;
+}
+
+// SearchByProjection(Frame&, vector<MapPoint*>, th), ORBmatcher.cc:45-129
+__global__ __launch_bounds__(64) void k_match_local(
+    CamDev cam, float th, float nnratio, int n_mp, const uint8_t* __restrict__ inview,
+    const float* __restrict__ proj,
+    const int* __restrict__ level, const float* __restrict__ vcos,
+    const uint8_t* __restrict__ mdesc, int n_cur, const eao_keypoint_dev* __restrict__ CK,
+    const uint8_t* __restrict__ CD, const int* __restrict__ pre, int nlevels,
+    const float* __restrict__ scales, const int* __restrict__ GS, const int* __restrict__ GI,
+    int* __restrict__ out, int* __restrict__ nmatch_out) {
+  __shared__ int match[MAXK];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < n_cur; i += 64) match[i] = pre ? pre[i] : -1;
+  __syncthreads();
+  const bool bFactor = th != 1.0f;
+  int nmatches = 0;
+  for (int iMP = 0; iMP < n_mp; iMP++) {
+    if (!inview[iMP]) continue;
+    const int L = min(max(level[iMP], 0), nlevels - 1);  // Q13 clamp
+    float r = vcos[iMP] > 0.998f ? 2.5f : 4.0f;
+    if (bFactor) r = fmul(r, th);
+    const float rr = fmul(r, scales[L]);
+    const float x = proj[2 * iMP], y = proj[2 * iMP + 1];
+    const Window w = window_cells(cam, x, y, rr);
+    if (w.empty) continue;
+    const int minL = L - 1, maxL = L;
+    const bool checkL = (minL > 0) || (maxL >= 0);
+    const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+    const uint8_t* d = mdesc + 32 * (long long)iMP;
+    unsigned long long b1 = KEY_NONE, b2 = KEY_NONE;
+    for (int ck = lane; ck < ncell; ck += 64) {
+      const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
+      const int cell = ix * GRID_ROWS + iy;
+      for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+        const int idx = GI[q];
+        const eao_keypoint_dev& kp = CK[idx];
+        if (checkL) {
+          if (kp.octave < minL) continue;
+          if (maxL >= 0 && kp.octave > maxL) continue;
+        }
+        if (!(fabsf(fsub(kp.x, x)) < rr && fabsf(fsub(kp.y, y)) < rr)) continue;
+        if (match[idx] >= 0) continue;
+        const int dist = hamming256(d, CD + 32 * (long long)idx);
+        const unsigned long long key = make_key(dist, ck, idx);
+        if (key < b1) {
+          b2 = b1;
+          b1 = key;
+        } else if (key < b2) {
+          b2 = key;
+        }
+      }
+    }
+    const unsigned long long m1 = wave_min_u64(b1);
+    const unsigned long long m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    if (m1 == KEY_NONE) continue;
+    const int bestDist = key_dist(m1);
+    if (bestDist <= TH_HIGH) {
+      const int bestIdx = key_idx(m1);
+      const int bestLevel = CK[bestIdx].octave;
+      const int bestDist2 = m2 == KEY_NONE ? 256 : key_dist(m2);
+      const int bestLevel2 = m2 == KEY_NONE ? -1 : CK[key_idx(m2)].octave;
+      if (bestLevel == bestLevel2 && (float)bestDist > fmul(nnratio, (float)bestDist2)) continue;
+      if (lane == 0) match[bestIdx] = iMP;
+      nmatches++;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  for (int i = lane; i < n_cur; i += 64) out[i] = match[i];
+  if (lane == 0) *nmatch_out = nmatches;
+}
+
+// SearchForInitialization, ORBmatcher.cc:405-520
+__global__ __launch_bounds__(64) void k_match_init(
+    CamDev cam, float nnratio, int check_ori, int n1, const eao_keypoint_dev* __restrict__ K1,
+    const uint8_t* __restrict__ D1, int n2, const eao_keypoint_dev* __restrict__ K2,
+    const uint8_t* __restrict__ D2, float* __restrict__ prev, int window,
+    const int* __restrict__ GS, const int* __restrict__ GI, int* __restrict__ m12,
+    int* __restrict__ nmatch_out) {
+  __shared__ int mdist[MAXK];
+  __shared__ int m21[MAXK];
+  __shared__ signed char bins1[MAXK];
+  __shared__ int hist[HISTO_LENGTH];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < n2; i += 64) {
+    mdist[i] = INT_MAX;
+    m21[i] = -1;
+  }
+  for (int i = lane; i < n1; i += 64) {
+    m12[i] = -1;
+    bins1[i] = -1;
+  }
+  __syncthreads();
+  int nmatches = 0;
+  const float r = (float)window;
+  for (int i1 = 0; i1 < n1; i1++) {
+    if (K1[i1].octave > 0) continue;
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+    const Window w = window_cells(cam, x, y, r);
+    if (w.empty) continue;
+    const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+    const uint8_t* d1 = D1 + 32 * (long long)i1;
+    unsigned long long b1 = KEY_NONE, b2 = KEY_NONE;
+    for (int ck = lane; ck < ncell; ck += 64) {
+      const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
+      const int cell = ix * GRID_ROWS + iy;
+      for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+        const int i2 = GI[q];
+        const eao_keypoint_dev& kp = K2[i2];
+        if (kp.octave < 0 || kp.octave > 0) continue;
+        if (!(fabsf(fsub(kp.x, x)) < r && fabsf(fsub(kp.y, y)) < r)) continue;
+        const int dist = hamming256(d1, D2 + 32 * (long long)i2);
+        if (mdist[i2] <= dist) continue;
+        const unsigned long long key = make_key(dist, ck, i2);
+        if (key < b1) {
+          b2 = b1;
+          b1 = key;
+        } else if (key < b2) {
+          b2 = key;
+        }
+      }
+    }
+    const unsigned long long m1 = wave_min_u64(b1);
+    const unsigned long long m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    if (m1 == KEY_NONE) continue;
+    const int bestDist = key_dist(m1);
+    const int bestDist2 = m2 == KEY_NONE ? INT_MAX : key_dist(m2);
+    if (bestDist <= TH_LOW && (float)bestDist < fmul((float)bestDist2, nnratio)) {
+      const int bestIdx2 = key_idx(m1);
+      const int prev21 = m21[bestIdx2];
+      if (prev21 >= 0) nmatches--;
+      if (lane == 0) {
+        if (prev21 >= 0) m12[prev21] = -1;
+        m12[i1] = bestIdx2;
+        m21[bestIdx2] = i1;
+        mdist[bestIdx2] = bestDist;
+        if (check_ori) bins1[i1] = (signed char)rot_bin(K1[i1].angle, K2[bestIdx2].angle);
+      }
+      nmatches++;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  if (check_ori) {
+    for (int b = lane; b < HISTO_LENGTH; b += 64) hist[b] = 0;
+    __syncthreads();
+    for (int i = lane; i < n1; i += 64)
+      if (bins1[i] >= 0) atomicAdd(&hist[bins1[i]], 1);
+    __syncthreads();
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    int removed = 0;
+    for (int i = lane; i < n1; i += 64) {
+      const int b = bins1[i];
+      if (b < 0 || b == ind1 || b == ind2 || b == ind3) continue;
+      if (m12[i] >= 0) {
+        m12[i] = -1;
+        removed++;
+      }
+    }
+    nmatches -= wave_sum(removed);
+  }
+  __syncthreads();
+  for (int i = lane; i < n1; i += 64)
+    if (m12[i] >= 0) {
+      prev[2 * i] = K2[m12[i]].x;
+      prev[2 * i + 1] = K2[m12[i]].y;
+    }
+  if (lane == 0) *nmatch_out = nmatches;
+}
+
+__global__ void k_hamming_pairs(const uint8_t* __restrict__ q, const uint8_t* __restrict__ t,
+                                const int* __restrict__ qi, const int* __restrict__ ti, int n,
+                                int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = hamming256(q + 32 * (long long)qi[i], t + 32 * (long long)ti[i]);
+}
+
+// ================================================================ host
+int MatchEngine::init(int device, int mk, int mb) {
+  dev = device;
+  max_kps = mk;
+  max_batch = std::max(mb, 2);
+  if (mk < 1 || mk > MAXK) {
+    set_error("eao_matcher_create: max_kps outside [1, 8192]");
+    return EAO_E_ARG;
+  }
+  EAO_HIP_CHECK(hipSetDevice(dev));
+  EAO_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  EAO_HIP_CHECK(hipMalloc(&d_gstart, sizeof(int) * (GRID_CELLS + 1) * max_batch));
+  EAO_HIP_CHECK(hipMalloc(&d_gitems, sizeof(int) * (size_t)mk * max_batch));
+  EAO_HIP_CHECK(hipMalloc(&d_kps, sizeof(eao_keypoint_dev) * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_desc, (size_t)32 * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_u8, (size_t)mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_f, sizeof(float) * 3 * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_f2, sizeof(float) * 3 * mk));
+  EAO_HIP_CHECK(hipMalloc(&d_f3, sizeof(float) * 3 * mk));
+  EAO_HIP_CHECK(hipMalloc(&d_f4, sizeof(float) * 3 * mk));
+  EAO_HIP_CHECK(hipMalloc(&d_mdesc, (size_t)32 * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_i32, sizeof(int) * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_i32b, sizeof(int) * mk * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_out, sizeof(int) * (mk * 2 + 16)));
+  EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16 * 2));
+  EAO_HIP_CHECK(hipMalloc(&d_scales, sizeof(float) * 32));
+  return EAO_OK;
+}
+
+MatchEngine::~MatchEngine() {
+  void* ptrs[] = {d_gstart, d_gitems, d_kps, d_desc, d_u8, d_f, d_f2, d_f3, d_f4,
+                  d_mdesc, d_i32, d_i32b, d_out, d_T, d_scales};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+int MatchEngine::build_grid(const CamDev& cam, const eao_keypoint_dev* kps, const int* counts,
+                            int n_single, int cap, int nframes, hipStream_t s) {
+  hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), 0, s, kps, counts, n_single, cap, cam,
+                     d_gstart, d_gitems);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+}  // namespace eao
+
+// ---------------------------------------------------------------- C ABI
+using namespace eao;
+
+struct eao_matcher {
+  MatchEngine e;
+};
+
+
+extern "C" {
+
+int eao_matcher_create(int device, int max_kps, int max_batch, eao_matcher** out) {
+  if (!out) return EAO_E_ARG;
+  *out = nullptr;
+  if (!eao_device_ok(device)) {
+    set_error("no usable gfx950 device (the engine has no CPU fallback)");
+    return EAO_E_NODEVICE;
+  }
+  eao_matcher* m = new eao_matcher();
+  int rc = m->e.init(device, max_kps, max_batch);
+  if (rc) {
+    delete m;
+    return rc;
+  }
+  *out = m;
+  return EAO_OK;
+}
+
+int eao_matcher_destroy(eao_matcher* m) {
+  delete m;
+  return EAO_OK;
+}
+
+int eao_hamming_pairs(eao_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                      const int32_t* qidx, const int32_t* tidx, int npairs, int32_t* dist) {
+  if (!m || npairs < 0 || nq > m->e.max_kps || nt > m->e.max_kps || npairs > 2 * m->e.max_kps)
+    return EAO_E_ARG;
+  if (npairs == 0) return EAO_OK;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, q, (size_t)nq * 32, hipMemcpyHostToDevice, e.stream));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_mdesc, t, (size_t)nt * 32, hipMemcpyHostToDevice, e.stream));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32, qidx, sizeof(int) * npairs, hipMemcpyHostToDevice, e.stream));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32b, tidx, sizeof(int) * npairs, hipMemcpyHostToDevice, e.stream));
+  hipLaunchKernelGGL(k_hamming_pairs, dim3((npairs + 255) / 256), dim3(256), 0, e.stream, e.d_desc,
+                     e.d_mdesc, e.d_i32, e.d_i32b, npairs, e.d_out);
+  EAO_HIP_CHECK(hipMemcpyAsync(dist, e.d_out, sizeof(int) * npairs, hipMemcpyDeviceToHost, e.stream));
+  EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
+  return EAO_OK;
+}
+
+int eao_match_motion(eao_matcher* m, const eao_camera* cam, const float* Tcw, float th,
+                     int check_ori, int n_last, const eao_keypoint* last_kps,
+                     const uint8_t* last_has_mp, const float* last_mp_pos,
+                     const uint8_t* last_mp_desc, int n_cur, const eao_keypoint* cur_kps,
+                     const uint8_t* cur_desc, int nlevels, const float* scale_factors,
+                     int32_t* cur_match) {
+  if (!m || !cam || !Tcw || n_last < 0 || n_cur < 0 || nlevels < 1 || nlevels > 32) return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  const int K = e.max_kps;
+  if (n_last > K || n_cur > K) {
+    set_error("eao_match_motion: more keypoints than max_kps");
+    return EAO_E_CAPACITY;
+  }
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = e.stream;
+  const int counts[2] = {n_last, n_cur};
+  float T2[32];
+  for (int k = 0; k < 16; k++) T2[k] = T2[16 + k] = Tcw[k];
+  // slot 0 = last, slot 1 = current; cap = K
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, last_kps, sizeof(eao_keypoint) * n_last, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, cur_kps, sizeof(eao_keypoint) * n_cur, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + (size_t)K * 32, cur_desc, (size_t)n_cur * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_u8, last_has_mp, n_last, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, last_mp_pos, sizeof(float) * 3 * n_last, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_mdesc, last_mp_desc, (size_t)n_last * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32, counts, sizeof(counts), hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_T, T2, sizeof(T2), hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  int rc = e.build_grid(cd, e.d_kps, e.d_i32, 0, K, 2, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_match_motion, dim3(1), dim3(64), 0, s, cd, e.d_T, th, check_ori, e.d_kps,
+                     e.d_desc, e.d_i32, K, e.d_u8, e.d_f, e.d_mdesc, e.d_scales, e.d_gstart,
+                     e.d_gitems, e.d_out, e.d_out + 2 * K);
+  EAO_HIP_CHECK(hipGetLastError());
+  int nm[2] = {0, 0};
+  EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out + K, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(nm, e.d_out + 2 * K, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return nm[1];
+}
+
+int eao_match_motion_batch_device(eao_matcher* m, const eao_camera* cam, int nframes, int cap,
+                                  const float* d_Tcw, float th, int check_ori,
+                                  const eao_keypoint* d_kps, const uint8_t* d_desc,
+                                  const int32_t* d_counts, const uint8_t* d_has_mp,
+                                  const float* d_mp_pos, const uint8_t* d_mp_desc, int nlevels,
+                                  const float* scale_factors, int32_t* d_cur_match,
+                                  int32_t* d_nmatches, void* stream) {
+  if (!m || !cam || nframes < 2 || nframes > m->e.max_batch || cap > m->e.max_kps || nlevels < 1 ||
+      nlevels > 32)
+    return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  int rc = e.build_grid(cd, (const eao_keypoint_dev*)d_kps, d_counts, 0, cap, nframes, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_match_motion, dim3(nframes - 1), dim3(64), 0, s, cd, d_Tcw, th, check_ori,
+                     (const eao_keypoint_dev*)d_kps, d_desc, d_counts, cap, d_has_mp, d_mp_pos,
+                     d_mp_desc, e.d_scales, e.d_gstart, e.d_gitems, d_cur_match, d_nmatches);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+int eao_is_in_frustum(eao_matcher* m, const eao_camera* cam, const float* Tcw, int n_mp,
+                      const float* mp_pos, const float* mp_normal, const float* mp_min_dist,
+                      const float* mp_max_dist, float view_cos_limit, float log_scale_factor,
+                      uint8_t* in_view, float* proj_xy, int32_t* pred_level, float* view_cos) {
+  if (!m || !cam || n_mp < 0 || n_mp > m->e.max_kps) return EAO_E_ARG;
+  if (n_mp == 0) return 0;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = e.stream;
+  const int K = e.max_kps;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_T, Tcw, sizeof(float) * 16, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, mp_pos, sizeof(float) * 3 * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f2, mp_normal, sizeof(float) * 3 * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f3, mp_min_dist, sizeof(float) * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f3 + K, mp_max_dist, sizeof(float) * n_mp, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  hipLaunchKernelGGL(k_frustum, dim3((n_mp + 255) / 256), dim3(256), 0, s, cd, e.d_T, n_mp, e.d_f,
+                     e.d_f2, e.d_f3, e.d_f3 + K, view_cos_limit, log_scale_factor, e.d_u8, e.d_f4,
+                     e.d_i32, e.d_f4 + 2 * K);
+  EAO_HIP_CHECK(hipGetLastError());
+  EAO_HIP_CHECK(hipMemcpyAsync(in_view, e.d_u8, n_mp, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(proj_xy, e.d_f4, sizeof(float) * 2 * n_mp, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(pred_level, e.d_i32, sizeof(int) * n_mp, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(view_cos, e.d_f4 + 2 * K, sizeof(float) * n_mp, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  int c = 0;
+  for (int i = 0; i < n_mp; i++) c += in_view[i] ? 1 : 0;
+  return c;
+}
+
+int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnratio, int n_mp,
+                    const uint8_t* in_view, const float* proj_xy, const int32_t* pred_level,
+                    const float* view_cos,
+                    const uint8_t* mp_desc, int n_cur, const eao_keypoint* cur_kps,
+                    const uint8_t* cur_desc, const int32_t* cur_preassigned, int nlevels,
+                    const float* scale_factors, int32_t* cur_match) {
+  if (!m || !cam || n_mp < 0 || n_cur < 0 || nlevels < 1 || nlevels > 32) return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  const int K = e.max_kps;
+  if (n_mp > K || n_cur > K) return EAO_E_CAPACITY;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = e.stream;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, cur_kps, sizeof(eao_keypoint) * n_cur, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, cur_desc, (size_t)n_cur * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, proj_xy, sizeof(float) * 2 * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32, pred_level, sizeof(int) * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f2, view_cos, sizeof(float) * n_mp, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_mdesc, mp_desc, (size_t)n_mp * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_u8, in_view, n_mp, hipMemcpyHostToDevice, s));
+  if (cur_preassigned)
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32b, cur_preassigned, sizeof(int) * n_cur, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  int rc = e.build_grid(cd, e.d_kps, nullptr, n_cur, K, 1, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_match_local, dim3(1), dim3(64), 0, s, cd, th, nnratio, n_mp, e.d_u8, e.d_f, e.d_i32,
+                     e.d_f2, e.d_mdesc, n_cur, e.d_kps, e.d_desc,
+                     cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart,
+                     e.d_gitems, e.d_out, e.d_out + 2 * K);
+  EAO_HIP_CHECK(hipGetLastError());
+  int nm = 0;
+  EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return nm;
+}
+
+int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int check_ori, int n1,
+                   const eao_keypoint* kps1, const uint8_t* desc1, int n2,
+                   const eao_keypoint* kps2, const uint8_t* desc2, float* prev_matched_xy,
+                   int window, int32_t* matches12) {
+  if (!m || !cam || n1 < 0 || n2 < 0) return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  const int K = e.max_kps;
+  if (n1 > K || n2 > K) return EAO_E_CAPACITY;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = e.stream;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, kps2, sizeof(eao_keypoint) * n2, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, kps1, sizeof(eao_keypoint) * n1, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + (size_t)K * 32, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, prev_matched_xy, sizeof(float) * 2 * n1, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  int rc = e.build_grid(cd, e.d_kps, nullptr, n2, K, 1, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_match_init, dim3(1), dim3(64), 0, s, cd, nnratio, check_ori, n1,
+                     e.d_kps + K, e.d_desc + (size_t)K * 32, n2, e.d_kps, e.d_desc, e.d_f, window,
+                     e.d_gstart, e.d_gitems, e.d_out, e.d_out + 2 * K);
+  EAO_HIP_CHECK(hipGetLastError());
+  int nm = 0;
+  EAO_HIP_CHECK(hipMemcpyAsync(matches12, e.d_out, sizeof(int) * n1, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(prev_matched_xy, e.d_f, sizeof(float) * 2 * n1, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return nm;
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// orb.h -- ORB extraction engine (host side of orb.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/eao_accel.h"
+
+namespace eao {
+
+// same layout as eao_keypoint / cv::KeyPoint
+struct eao_keypoint_dev {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+};
+static_assert(sizeof(eao_keypoint_dev) == sizeof(eao_keypoint), "keypoint layout");
+
+// Per pyramid level geometry (ORBextractor.cc:765-853, :1107-1132)
+struct LevelDev {
+  int w, h, pitch;
+  int pad0;
+  long long plane_off;        // byte offset of the level plane in a frame's pyramid area
+  int minBX, minBY, maxBX, maxBY;
+  int nCols, nRows, wCell, hCell;
+  int nfeat;                  // mnFeaturesPerLevel
+  int cell_begin, cell_count;
+  int cand_off, cand_cap;     // candidate slots (uint32) of this level in a frame
+  int sel_off, sel_cap;       // selected keypoint slots of this level in a frame
+  int nIni;                   // initial quadtree nodes
+  float hX;
+  float scale, size;          // mvScaleFactor[l], PATCH_SIZE*scale truncated
+  int tab_x, tab_y, xmax;     // resize tables
+};
+
+struct CellDev {
+  int16_t level, i, j, pad;
+  int16_t x0, y0, x1, y1;     // ROI in level coordinates
+  int slot;                   // first candidate slot in the frame's candidate area
+  int cap;                    // NMS bound on corners in this cell
+};
+
+class OrbEngine {
+ public:
+  eao_orb_params p{};
+  int dev = 0;
+  std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+  std::vector<int> quotas, umax, gk;
+  std::vector<LevelDev> levels;
+  std::vector<CellDev> cells;
+  std::vector<int> resize_xofs, resize_yrows;
+  std::vector<short> resize_ia, resize_ib;
+  std::vector<int2> slot_map;
+  long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;
+  int cap = 0, roi_stride = 0, roi_rows = 0;
+
+  hipStream_t stream = nullptr;
+  LevelDev* d_levels = nullptr;
+  CellDev* d_cells = nullptr;
+  int *d_xofs = nullptr, *d_yrows = nullptr, *d_umax = nullptr, *d_gk = nullptr;
+  short *d_ia = nullptr, *d_ib = nullptr;
+  int2* d_slot_map = nullptr;
+  uint8_t* d_pyr = nullptr;
+  uint32_t *d_cand = nullptr, *d_qbuf = nullptr, *d_sel = nullptr;
+  int *d_cell_cnt = nullptr, *d_sel_cnt = nullptr;
+  uint8_t* d_img = nullptr;
+  eao_keypoint_dev* d_out_kps = nullptr;
+  uint8_t* d_out_desc = nullptr;
+  int* d_out_cnt = nullptr;
+
+  int plan(const eao_orb_params& prm, int device);
+  int init(const eao_orb_params& prm, int device);
+  int run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint_dev* d_kps, uint8_t* d_desc,
+          int* d_counts, int out_cap, hipStream_t s);
+  ~OrbEngine();
+};
+
+}  // namespace eao

@@ -1,0 +1,943 @@
+// orb.hip -- ORB extraction on gfx950: the MI355X replacement of
+// ORBextractor::operator() (reference src/ORBextractor.cc:1043-1105).
+//
+// Pipeline per batch of frames (all HBM-resident, one stream):
+//   k_resize      x7  level l from level l-1 (cv::resize INTER_LINEAR 8U,
+//                     fixed point, ORBextractor.cc:1120)
+//   k_fast        x1  one wave per (grid cell, frame): ROI staged in LDS,
+//                     FAST-9/16 + cornerScore + in-cell 3x3 NMS, iniTh with
+//                     minTh retry for empty cells (ORBextractor.cc:789-829)
+//   k_distribute  x1  one wave per (level, frame): DistributeOctTree with
+//                     the reference's list order (ORBextractor.cc:539-763)
+//   k_describe    x1  one wave per selected keypoint: IC_Angle on the level,
+//                     7x7 Gaussian evaluated in LDS at the 512 rBRIEF taps,
+//                     256-bit descriptor, final scaling (:77-147, :1076-1104)
+// Bit-exactness: integer paths are exact; float paths use __f*_rn intrinsics
+// and -ffp-contract=off so every rounding matches the oracle.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+#include "orb.h"
+
+namespace eao {
+
+__constant__ int c_pattern[1024] = {
+#include "orb_pattern.inc"
+};
+
+// ---------------------------------------------------------------- resize
+// dst(level l) = resize(src(level l-1)); tables precomputed on the host with
+// OpenCV's coefficient rounding. One thread per output pixel.
+__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, int spitch,
+                                                long long sstride, uint8_t* __restrict__ dst,
+                                                int dpitch, long long dstride, int dw, int dh,
+                                                const int* __restrict__ xofs,
+                                                const short* __restrict__ ialpha, int xmax,
+                                                const int* __restrict__ yrows,
+                                                const short* __restrict__ ibeta) {
+  const int dx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int dy = blockIdx.y;
+  const int f = blockIdx.z;
+  if (dx >= dw) return;
+  const uint8_t* s0 = src + f * sstride + (long long)yrows[2 * dy] * spitch;
+  const uint8_t* s1 = src + f * sstride + (long long)yrows[2 * dy + 1] * spitch;
+  const int sx = xofs[dx];
+  int d0, d1;
+  if (dx < xmax) {
+    const int a0 = ialpha[2 * dx], a1 = ialpha[2 * dx + 1];
+    d0 = s0[sx] * a0 + s0[sx + 1] * a1;
+    d1 = s1[sx] * a0 + s1[sx + 1] * a1;
+  } else {
+    d0 = s0[sx] * 2048;
+    d1 = s1[sx] * 2048;
+  }
+  int v = (d0 * ibeta[2 * dy] + d1 * ibeta[2 * dy + 1] + (1 << 21)) >> 22;
+  dst[f * dstride + (long long)dy * dpitch + dx] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ---------------------------------------------------------------- FAST
+__constant__ int c_off16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
+                                   {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
+                                   {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
+
+// FAST-9/16 test + OpenCV cornerScore<16>; returns 0 when not a corner.
+__device__ __forceinline__ int fast_pixel(const uint8_t* roi, int RS, int r, int c, int th) {
+  const int v = roi[r * RS + c];
+  int d[25];
+  uint32_t dk = 0, br = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int p = roi[(r + c_off16[k][1]) * RS + c + c_off16[k][0]];
+    d[k] = v - p;
+    dk |= (uint32_t)(p < v - th) << k;
+    br |= (uint32_t)(p > v + th) << k;
+  }
+  uint32_t md = dk | (dk << 16), mb = br | (br << 16);
+  uint32_t rd = md, rb = mb;
+#pragma unroll
+  for (int s = 1; s <= 8; s++) {
+    rd &= md >> s;
+    rb &= mb >> s;
+  }
+  if (((rd | rb) & 0xffffu) == 0) return 0;
+#pragma unroll
+  for (int k = 16; k < 25; k++) d[k] = d[k - 16];
+  int a0 = th;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]);
+    a = min(a, d[k + 3]);
+    a = min(a, d[k + 4]);
+    a = min(a, d[k + 5]);
+    a = min(a, d[k + 6]);
+    a = min(a, d[k + 7]);
+    a = min(a, d[k + 8]);
+    a0 = max(a0, min(a, d[k]));
+    a0 = max(a0, min(a, d[k + 9]));
+  }
+  int b0 = -a0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int b = max(d[k + 1], d[k + 2]);
+    b = max(b, d[k + 3]);
+    b = max(b, d[k + 4]);
+    b = max(b, d[k + 5]);
+    b = max(b, d[k + 6]);
+    b = max(b, d[k + 7]);
+    b = max(b, d[k + 8]);
+    b0 = min(b0, max(b, d[k]));
+    b0 = min(b0, max(b, d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+__global__ __launch_bounds__(64) void k_fast(const uint8_t* __restrict__ frames, int fpitch,
+                                             long long fstride, const uint8_t* __restrict__ pyr,
+                                             long long pstride, const LevelDev* __restrict__ levels,
+                                             const CellDev* __restrict__ cells, int iniTh, int minTh,
+                                             int RS, int RH, uint32_t* __restrict__ cand,
+                                             long long cand_stride, int* __restrict__ cell_cnt,
+                                             int ncells) {
+  extern __shared__ uint8_t smem[];
+  uint8_t* roi = smem;
+  uint8_t* sc = smem + RS * RH;
+  const int ci = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const CellDev c = cells[ci];
+  const LevelDev& L = levels[c.level];
+  const uint8_t* img;
+  int pitch;
+  if (c.level == 0) {
+    img = frames + f * fstride;
+    pitch = fpitch;
+  } else {
+    img = pyr + f * pstride + L.plane_off;
+    pitch = L.pitch;
+  }
+  const int rw = c.x1 - c.x0, rh = c.y1 - c.y0;
+  for (int idx = lane; idx < rw * rh; idx += 64) {
+    const int r = idx / rw, cc = idx - r * rw;
+    roi[r * RS + cc] = img[(long long)(c.y0 + r) * pitch + c.x0 + cc];
+  }
+  uint32_t* out = cand + f * cand_stride + c.slot;
+  int n = 0;
+  for (int pass = 0; pass < 2; pass++) {
+    int th = pass == 0 ? iniTh : minTh;
+    th = min(max(th, 0), 255);
+    for (int idx = lane; idx < rw * rh; idx += 64) sc[(idx / rw) * RS + idx % rw] = 0;
+    __syncthreads();
+    for (int r = 3; r < rh - 3; r++)
+      for (int cc = 3 + lane; cc < rw - 3; cc += 64) sc[r * RS + cc] = (uint8_t)fast_pixel(roi, RS, r, cc, th);
+    __syncthreads();
+    n = 0;
+    for (int r = 3; r < rh - 3; r++) {
+      for (int c0 = 3; c0 < rw - 3; c0 += 64) {
+        const int cc = c0 + lane;
+        bool keep = false;
+        int s = 0;
+        if (cc < rw - 3) {
+          s = sc[r * RS + cc];
+          const uint8_t* p = sc + r * RS + cc;
+          keep = s > p[1] && s > p[-1] && s > p[-RS - 1] && s > p[-RS] && s > p[-RS + 1] &&
+                 s > p[RS - 1] && s > p[RS] && s > p[RS + 1];
+        }
+        const uint64_t m = ballot(keep);
+        if (keep) {
+          const int pos = n + popc64(m & lanes_below());
+          if (pos < c.cap) out[pos] = pack_kp(cc + c.j * L.wCell, r + c.i * L.hCell, s);
+        }
+        n += popc64(m);
+      }
+    }
+    if (n > 0) break;  // ORBextractor.cc:812 -- retry with minTh only when empty
+    __syncthreads();
+  }
+  if (lane == 0) cell_cnt[f * ncells + ci] = n;
+}
+
+// ---------------------------------------------------------------- quadtree
+// One wave per (level, frame). Node list order is kept explicitly in an
+// ordered slot array with push-front semantics; ties in the final-phase sort
+// are broken by node creation id.
+struct QNode {
+  int16_t x0, y0, x1, y1;
+  int beg, cnt;
+  int id;
+  int pos;
+  uint8_t buf, nomore, alive, pad;
+};
+
+constexpr int QCAP = 1024;        // nodes alive at once (N + 4*nIni + margin)
+constexpr int QOS = 5 * QCAP;     // order array (one pass pushes <= 4*QCAP)
+
+struct QShared {
+  QNode node[QCAP];
+  int16_t order[QOS];
+  int16_t freel[QCAP];
+  int16_t vcur[QCAP];
+  int16_t vprev[QCAP];
+  unsigned long long skey[QCAP];
+};
+
+__device__ __forceinline__ int child_of(uint32_t k, int mx, int my) {
+  const int x = kp_x(k), y = kp_y(k);
+  return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
+}
+
+__global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ cand,
+                                                   long long cand_stride,
+                                                   const int* __restrict__ cell_cnt, int ncells,
+                                                   const LevelDev* __restrict__ levels,
+                                                   const CellDev* __restrict__ cells,
+                                                   uint32_t* __restrict__ qbuf, long long qstride,
+                                                   uint32_t* __restrict__ sel, long long sel_stride,
+                                                   int* __restrict__ sel_cnt, int nlevels) {
+  __shared__ QShared S;
+  const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  const LevelDev& L = levels[l];
+  const uint32_t* C = cand + f * cand_stride;
+  uint32_t* B0 = qbuf + f * qstride + L.cand_off;
+  uint32_t* B1 = B0 + L.cand_cap;
+  uint32_t* bufs[2] = {B0, B1};
+  // ---- gather candidates in vToDistributeKeys order (cells row-major)
+  int n = 0;
+  for (int k = 0; k < L.cell_count; k++) {
+    const CellDev& c = cells[L.cell_begin + k];
+    const int cnt = min(cell_cnt[f * ncells + L.cell_begin + k], c.cap);
+    for (int i = lane; i < cnt; i += 64) B0[n + i] = C[c.slot + i];
+    n += cnt;
+  }
+  __syncthreads();
+  uint32_t* S_out = sel + f * sel_stride + L.sel_off;
+  const int N = L.nfeat;
+  if (n == 0) {
+    if (lane == 0) sel_cnt[f * nlevels + l] = 0;
+    return;
+  }
+  // ---- free list
+  for (int i = lane; i < QCAP; i += 64) {
+    S.freel[i] = (int16_t)(QCAP - 1 - i);
+    S.node[i].alive = 0;
+  }
+  __syncthreads();
+  int nfree = QCAP;
+  int next_id = 0;
+  int alive = 0;
+  int head = QOS;  // list occupies order[head .. QOS)
+  bool overflow = false;
+
+  auto alloc = [&]() -> int {
+    if (nfree == 0) {
+      overflow = true;
+      return -1;
+    }
+    return S.freel[--nfree];
+  };
+
+  // ---- initial nodes (ORBextractor.cc:543-585)
+  const int nIni = L.nIni;
+  const float hX = L.hX;
+  {
+    // stable partition of keys by initial node, B0 -> B1
+    int base = 0;
+    int slots[16];
+    for (int i = 0; i < nIni && i < 16; i++) {
+      int cnt = 0;
+      for (int c0 = 0; c0 < n; c0 += 64) {
+        const int idx = c0 + lane;
+        bool in = false;
+        if (idx < n) in = (int)((float)kp_x(B0[idx]) / hX) == i;
+        const uint64_t m = ballot(in);
+        if (in) B1[base + cnt + popc64(m & lanes_below())] = B0[idx];
+        cnt += popc64(m);
+      }
+      const int id = next_id++;
+      slots[i] = -1;
+      if (cnt > 0) {
+        const int s = alloc();
+        slots[i] = s;
+        if (lane == 0 && s >= 0) {
+          QNode& q = S.node[s];
+          q.x0 = (int16_t)(int)(hX * (float)i);
+          q.x1 = (int16_t)(int)(hX * (float)(i + 1));
+          q.y0 = 0;
+          q.y1 = (int16_t)(L.maxBY - L.minBY);
+          q.beg = base;
+          q.cnt = cnt;
+          q.id = id;
+          q.buf = 1;
+          q.nomore = cnt == 1;
+          q.alive = 1;
+        }
+        alive++;
+      }
+      base += cnt;
+    }
+    // push_back order: list = [ini0, ini1, ...] at the tail of order[]
+    head = QOS - alive;
+    int p = head;
+    for (int i = 0; i < nIni && i < 16; i++)
+      if (slots[i] >= 0) {
+        if (lane == 0) {
+          S.order[p] = (int16_t)slots[i];
+          S.node[slots[i]].pos = p;
+        }
+        p++;
+      }
+    __syncthreads();
+  }
+
+  int nvcur = 0;
+  int nToExpand = 0;
+
+  // divide node s: partition its keys into the other buffer, push children
+  // to the front (n1..n4), record children with >1 keys in vcur.
+  auto divide = [&](int s) {
+    const QNode q = S.node[s];
+    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
+    const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
+    const int mx = q.x0 + hx, my = q.y0 + hy;
+    const uint32_t* src = bufs[q.buf] + q.beg;
+    uint32_t* dst = bufs[q.buf ^ 1] + q.beg;
+    int cnt4[4] = {0, 0, 0, 0};
+    for (int c0 = 0; c0 < q.cnt; c0 += 64) {
+      const int idx = c0 + lane;
+      const int ch = idx < q.cnt ? child_of(src[idx], mx, my) : 4;
+#pragma unroll
+      for (int c = 0; c < 4; c++) cnt4[c] += popc64(ballot(ch == c));
+    }
+    int off4[4] = {0, cnt4[0], cnt4[0] + cnt4[1], cnt4[0] + cnt4[1] + cnt4[2]};
+    int run4[4] = {0, 0, 0, 0};
+    for (int c0 = 0; c0 < q.cnt; c0 += 64) {
+      const int idx = c0 + lane;
+      uint32_t k = 0;
+      int ch = 4;
+      if (idx < q.cnt) {
+        k = src[idx];
+        ch = child_of(k, mx, my);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint64_t m = ballot(ch == c);
+        if (ch == c) dst[off4[c] + run4[c] + popc64(m & lanes_below())] = k;
+        run4[c] += popc64(m);
+      }
+    }
+    const int16_t rx0[4] = {q.x0, (int16_t)mx, q.x0, (int16_t)mx};
+    const int16_t ry0[4] = {q.y0, q.y0, (int16_t)my, (int16_t)my};
+    const int16_t rx1[4] = {(int16_t)mx, q.x1, (int16_t)mx, q.x1};
+    const int16_t ry1[4] = {(int16_t)my, (int16_t)my, q.y1, q.y1};
+    for (int c = 0; c < 4; c++) {
+      if (cnt4[c] == 0) continue;
+      const int ns = alloc();
+      const int id = next_id++;
+      head--;
+      if (ns >= 0 && lane == 0) {
+        QNode& d = S.node[ns];
+        d.x0 = rx0[c];
+        d.y0 = ry0[c];
+        d.x1 = rx1[c];
+        d.y1 = ry1[c];
+        d.beg = q.beg + off4[c];
+        d.cnt = cnt4[c];
+        d.id = id;
+        d.buf = q.buf ^ 1;
+        d.nomore = cnt4[c] == 1;
+        d.alive = 1;
+        d.pos = head;
+        S.order[head] = (int16_t)ns;
+      }
+      alive++;
+      if (cnt4[c] > 1) {
+        nToExpand++;
+        if (lane == 0 && ns >= 0) S.vcur[nvcur] = (int16_t)ns;
+        nvcur++;
+      }
+    }
+    // erase the parent
+    if (lane == 0) {
+      S.order[q.pos] = -1;
+      S.node[s].alive = 0;
+      S.freel[nfree] = (int16_t)s;
+    }
+    nfree++;
+    alive--;
+    __syncthreads();
+  };
+
+  // move live entries of order[head..QOS) to the tail, preserving order
+  auto compact = [&]() {
+    int w = 0;
+    for (int c0 = head; c0 < QOS; c0 += 64) {
+      const int idx = c0 + lane;
+      const int v = idx < QOS ? S.order[idx] : -1;
+      const uint64_t m = ballot(v >= 0);
+      const int p = w + popc64(m & lanes_below());
+      // write into vprev as a staging area (reused; vprev is free here)
+      if (v >= 0) S.skey[p] = (unsigned long long)v;
+      w += popc64(m);
+    }
+    __syncthreads();
+    head = QOS - w;
+    for (int i = lane; i < w; i += 64) {
+      const int s = (int)S.skey[i];
+      S.order[head + i] = (int16_t)s;
+      S.node[s].pos = head + i;
+    }
+    __syncthreads();
+  };
+
+  bool finish = false;
+  while (!finish && !overflow) {
+    const int prevSize = alive;
+    nToExpand = 0;
+    nvcur = 0;
+    const int end = QOS;
+    for (int i = head; i < end; i++) {
+      const int s = S.order[i];
+      if (s < 0) continue;
+      if (S.node[s].nomore) continue;
+      divide(s);
+      if (overflow) break;
+    }
+    compact();
+    if (alive >= N || alive == prevSize) {
+      finish = true;
+    } else if (alive + nToExpand * 3 > N) {
+      while (!finish && !overflow) {
+        const int prev2 = alive;
+        const int nv = nvcur;
+        for (int i = lane; i < nv; i += 64) S.vprev[i] = S.vcur[i];
+        __syncthreads();
+        nvcur = 0;
+        // sort vprev by (size, id) ascending: bitonic over P = next pow2.
+        // key = size << 32 | id << 11 | slot (ids unique, slot < QCAP=2^11)
+        int P = 1;
+        while (P < nv) P <<= 1;
+        for (int i = lane; i < P; i += 64) {
+          if (i < nv) {
+            const int sl = S.vprev[i];
+            const QNode& q = S.node[sl];
+            S.skey[i] = ((unsigned long long)(uint32_t)q.cnt << 32) |
+                        ((unsigned long long)(uint32_t)q.id << 11) | (unsigned long long)sl;
+          } else
+            S.skey[i] = ~0ull;
+        }
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1) {
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = lane; i < P; i += 64) {
+              const int ixj = i ^ j;
+              if (ixj > i) {
+                const unsigned long long a = S.skey[i], b = S.skey[ixj];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) {
+                  S.skey[i] = b;
+                  S.skey[ixj] = a;
+                }
+              }
+            }
+            __syncthreads();
+          }
+        }
+        for (int i = lane; i < nv; i += 64) S.vprev[i] = (int16_t)(S.skey[i] & 0x7ffu);
+        __syncthreads();
+        for (int j = nv - 1; j >= 0; j--) {
+          const int s = S.vprev[j];
+          divide(s);
+          if (overflow) break;
+          if (alive >= N) break;
+        }
+        compact();
+        if (alive >= N || alive == prev2) finish = true;
+      }
+    }
+  }
+  // ---- retain the best keypoint per node, in list order
+  int outn = 0;
+  for (int i = head; i < QOS; i++) {
+    const int s = S.order[i];
+    if (s < 0) continue;
+    const QNode q = S.node[s];
+    const uint32_t* src = bufs[q.buf] + q.beg;
+    int best_s = -1, best_i = 0x7fffffff;
+    for (int idx = lane; idx < q.cnt; idx += 64) {
+      const int sc = kp_s(src[idx]);
+      if (sc > best_s) {
+        best_s = sc;
+        best_i = idx;
+      }
+    }
+    const int mx = wave_max_int(best_s);
+    const int cand_i = best_s == mx ? best_i : 0x7fffffff;
+    const int bi = wave_min_int(cand_i);
+    if (lane == 0 && outn < L.sel_cap) S_out[outn] = src[bi];
+    outn++;
+  }
+  if (lane == 0) sel_cnt[f * nlevels + l] = overflow ? -1 : min(outn, L.sel_cap);
+}
+
+// ---------------------------------------------------------------- describe
+__device__ __forceinline__ int reflect101(int p, int len) {
+  if (len == 1) return 0;
+  while (p < 0 || p >= len) {
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - 2 - p;
+  }
+  return p;
+}
+
+// fastAtan2 (OpenCV 3.2), fp32, no contraction
+__device__ float fast_atan2(float y, float x) {
+  const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+  const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+  const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+  const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+  const float ax = fabsf(x), ay = fabsf(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = fdiv(ay, fadd(ax, (float)2.220446049250313e-16));
+    c2 = fmul(c, c);
+    a = fmul(fadd(fmul(fadd(fmul(fadd(fmul(p7, c2), p5), c2), p3), c2), p1), c);
+  } else {
+    c = fdiv(ax, fadd(ay, (float)2.220446049250313e-16));
+    c2 = fmul(c, c);
+    a = fsub(90.f, fmul(fadd(fmul(fadd(fmul(fadd(fmul(p7, c2), p5), c2), p3), c2), p1), c));
+  }
+  if (x < 0) a = fsub(180.f, a);
+  if (y < 0) a = fsub(360.f, a);
+  return a;
+}
+
+constexpr int PATCH = 43;  // 2*(18+3)+1: rBRIEF reach 18 px + 3-px blur taps
+
+__global__ __launch_bounds__(256) void k_describe(
+    const uint8_t* __restrict__ frames, int fpitch, long long fstride,
+    const uint8_t* __restrict__ pyr, long long pstride, const LevelDev* __restrict__ levels,
+    const uint32_t* __restrict__ sel, long long sel_stride, const int* __restrict__ sel_cnt,
+    const int2* __restrict__ slot_map, int nslots, int nlevels, const int* __restrict__ umax,
+    const int* __restrict__ gk, eao_keypoint_dev* __restrict__ out_kps,
+    uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt, int cap) {
+  __shared__ uint8_t patch[4][PATCH * PATCH];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int slot = blockIdx.x * 4 + w;
+  const int f = blockIdx.y;
+  const int* cnts = sel_cnt + f * nlevels;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    int tot = 0;
+    for (int i = 0; i < nlevels; i++) tot += max(cnts[i], 0);
+    out_cnt[f] = tot;
+  }
+  int l = 0, k = 0;
+  bool active = slot < nslots;
+  if (active) {
+    const int2 sm = slot_map[slot];  // (level, index within level)
+    l = sm.x;
+    k = sm.y;
+    active = k < cnts[l];
+  }
+  int off = 0;
+  for (int i = 0; i < l; i++) off += max(cnts[i], 0);
+  const LevelDev& L = levels[l];
+  uint32_t pk = 0;
+  if (active) pk = sel[f * sel_stride + L.sel_off + k];
+  const int x = kp_x(pk) + L.minBX, y = kp_y(pk) + L.minBY;
+  const uint8_t* img;
+  int pitch;
+  if (l == 0) {
+    img = frames + f * fstride;
+    pitch = fpitch;
+  } else {
+    img = pyr + f * pstride + L.plane_off;
+    pitch = L.pitch;
+  }
+  float angle = 0.f;
+  uint8_t* P = patch[w];
+  if (active) {
+    // ---- IC_Angle (ORBextractor.cc:77-104): integer moments, wave reduction
+    int m10 = 0, m01 = 0;
+    const uint8_t* center = img + (long long)y * pitch + x;
+    if (lane < 31) m10 += (lane - 15) * center[lane - 15];
+    for (int v = 1 + (lane >> 5); v <= 15; v += 2) {
+      const int d = umax[v];
+      const int u = (lane & 31) - d;
+      if (u <= d) {
+        const int vp = center[u + v * pitch], vm = center[u - v * pitch];
+        m10 += u * (vp + vm);
+        m01 += v * (vp - vm);
+      }
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    angle = fast_atan2((float)m01, (float)m10);
+    // ---- stage the 43x43 raw patch (REFLECT_101 at the level border)
+    for (int i = lane; i < PATCH * PATCH; i += 64) {
+      const int r = i / PATCH, c = i - r * PATCH;
+      const int yy = reflect101(y - 21 + r, L.h), xx = reflect101(x - 21 + c, L.w);
+      P[i] = img[(long long)yy * pitch + xx];
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  // ---- rBRIEF (ORBextractor.cc:108-147) on the 7x7 sigma-2 blur (:1086)
+  const float factorPI = (float)(M_PI / 180.f);
+  const float ang = fmul(angle, factorPI);
+  const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  const int byte = lane >> 1, half = lane & 1;
+  int nib = 0;
+  for (int t = 0; t < 4; t++) {
+    int val[2];
+    for (int e = 0; e < 2; e++) {
+      const int pi = 16 * byte + 8 * half + 2 * t + e;
+      const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
+      const int dy = dev_round(fadd(fmul(px, b), fmul(py, a)));
+      const int dx = dev_round(fsub(fmul(px, a), fmul(py, b)));
+      const int cy = 21 + dy, cx = 21 + dx;
+      int s = 0;
+#pragma unroll
+      for (int j = 0; j < 7; j++) {
+        const uint8_t* row = P + (cy + j - 3) * PATCH + cx - 3;
+        int rs = 0;
+#pragma unroll
+        for (int i = 0; i < 7; i++) rs += gk[i] * row[i];
+        s += gk[j] * rs;
+      }
+      val[e] = min(max((s + (1 << 15)) >> 16, 0), 255);
+    }
+    nib |= (val[0] < val[1]) << t;
+  }
+  const int other = __shfl_xor(nib, 1, 64);
+  const long long oi = (long long)f * cap + off + k;
+  if (half == 0) out_desc[oi * 32 + byte] = (uint8_t)(nib | (other << 4));
+  if (lane == 0) {
+    eao_keypoint_dev kp;
+    if (l == 0) {
+      kp.x = (float)x;
+      kp.y = (float)y;
+    } else {
+      kp.x = fmul((float)x, L.scale);
+      kp.y = fmul((float)y, L.scale);
+    }
+    kp.size = L.size;
+    kp.angle = angle;
+    kp.response = (float)kp_s(pk);
+    kp.octave = l;
+    kp.class_id = -1;
+    out_kps[oi] = kp;
+  }
+}
+
+// ================================================================ host plan
+static inline int cv_round(float v) { return (int)lrintf(v); }
+static inline short sat_s16(float v) {
+  int iv = cv_round(v);
+  return (short)(iv < -32768 ? -32768 : (iv > 32767 ? 32767 : iv));
+}
+
+int OrbEngine::plan(const eao_orb_params& prm, int device) {
+  p = prm;
+  dev = device;
+  const int nl = p.nlevels;
+  if (nl < 1 || nl > 16 || p.width < 64 || p.height < 64 || p.width > 4096 || p.height > 4096 ||
+      p.max_batch < 1 || p.nfeatures < 1) {
+    set_error("eao_orb_create: bad parameters");
+    return EAO_E_ARG;
+  }
+  // ORBextractor::ORBextractor, ORBextractor.cc:410-470
+  const double sf = (double)p.scale_factor;
+  scale.assign(nl, 1.f);
+  sigma2.assign(nl, 1.f);
+  for (int i = 1; i < nl; i++) {
+    scale[i] = (float)((double)scale[i - 1] * sf);
+    sigma2[i] = scale[i] * scale[i];
+  }
+  inv_scale.resize(nl);
+  inv_sigma2.resize(nl);
+  for (int i = 0; i < nl; i++) {
+    inv_scale[i] = 1.0f / scale[i];
+    inv_sigma2[i] = 1.0f / sigma2[i];
+  }
+  quotas.resize(nl);
+  {
+    float factor = (float)(1.0f / sf);
+    float nd = (float)p.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)nl));
+    int sum = 0;
+    for (int l = 0; l < nl - 1; l++) {
+      quotas[l] = cv_round(nd);
+      sum += quotas[l];
+      nd *= factor;
+    }
+    quotas[nl - 1] = std::max(p.nfeatures - sum, 0);
+  }
+  {
+    int v, v0;
+    const int HP = 15;
+    int vmax = (int)std::floor((float)HP * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil((float)HP * std::sqrt(2.f) / 2);
+    const double hp2 = HP * HP;
+    umax.assign(HP + 1, 0);
+    for (v = 0; v <= vmax; ++v) umax[v] = (int)lrint(std::sqrt(hp2 - v * v));
+    for (v = HP, v0 = 0; v >= vmin; --v) {
+      while (umax[v0] == umax[v0 + 1]) ++v0;
+      umax[v] = v0;
+      ++v0;
+    }
+  }
+  {
+    // getGaussianKernel(7, 2, CV_32F) -> x256 integer taps
+    float cf[7];
+    double s = 0;
+    const double scale2X = -0.5 / (2.0 * 2.0);
+    for (int i = 0; i < 7; i++) {
+      double x = i - 3.0;
+      cf[i] = (float)std::exp(scale2X * x * x);
+      s += cf[i];
+    }
+    s = 1. / s;
+    gk.resize(7);
+    for (int i = 0; i < 7; i++) {
+      cf[i] = (float)(cf[i] * s);
+      gk[i] = (int)lrint((double)cf[i] * 256.0);
+    }
+  }
+  levels.assign(nl, LevelDev{});
+  cells.clear();
+  resize_xofs.clear();
+  resize_ia.clear();
+  resize_yrows.clear();
+  resize_ib.clear();
+  long long poff = 0;
+  int cand_total = 0, sel_total = 0, rsmax = 0, rhmax = 0;
+  for (int l = 0; l < nl; l++) {
+    LevelDev& L = levels[l];
+    L.w = cv_round((float)p.width * inv_scale[l]);
+    L.h = cv_round((float)p.height * inv_scale[l]);
+    L.pitch = (L.w + 63) & ~63;
+    if (l > 0) {
+      L.plane_off = poff;
+      poff += (long long)L.pitch * L.h;
+    }
+    L.minBX = 16;
+    L.minBY = 16;
+    L.maxBX = L.w - 16;
+    L.maxBY = L.h - 16;
+    L.nfeat = quotas[l];
+    L.scale = scale[l];
+    L.size = (float)(int)(31 * scale[l]);
+    // cells, ORBextractor.cc:769-829
+    const float W = 30;
+    const float width = (float)(L.maxBX - L.minBX), height = (float)(L.maxBY - L.minBY);
+    const int nCols = (int)(width / W), nRows = (int)(height / W);
+    if (nCols < 1 || nRows < 1) {
+      set_error("eao_orb_create: image too small for the pyramid");
+      return EAO_E_ARG;
+    }
+    L.wCell = (int)std::ceil(width / nCols);
+    L.hCell = (int)std::ceil(height / nRows);
+    L.cell_begin = (int)cells.size();
+    L.cand_off = cand_total;
+    for (int i = 0; i < nRows; i++) {
+      const float iniY = (float)(L.minBY + i * L.hCell);
+      float maxY = iniY + L.hCell + 6;
+      if (iniY >= L.maxBY - 3) continue;
+      if (maxY > L.maxBY) maxY = (float)L.maxBY;
+      for (int j = 0; j < nCols; j++) {
+        const float iniX = (float)(L.minBX + j * L.wCell);
+        float maxX = iniX + L.wCell + 6;
+        if (iniX >= L.maxBX - 6) continue;
+        if (maxX > L.maxBX) maxX = (float)L.maxBX;
+        CellDev c{};
+        c.level = (int16_t)l;
+        c.i = (int16_t)i;
+        c.j = (int16_t)j;
+        c.x0 = (int16_t)(int)iniX;
+        c.y0 = (int16_t)(int)iniY;
+        c.x1 = (int16_t)(int)maxX;
+        c.y1 = (int16_t)(int)maxY;
+        const int iw = std::max(c.x1 - c.x0 - 6, 0), ih = std::max(c.y1 - c.y0 - 6, 0);
+        c.cap = ((iw + 1) / 2) * ((ih + 1) / 2);
+        c.slot = cand_total;
+        cand_total += c.cap;
+        rsmax = std::max(rsmax, c.x1 - c.x0);
+        rhmax = std::max(rhmax, c.y1 - c.y0);
+        cells.push_back(c);
+      }
+    }
+    L.cell_count = (int)cells.size() - L.cell_begin;
+    L.cand_cap = cand_total - L.cand_off;
+    L.nIni = (int)std::round((float)(L.maxBX - L.minBX) / (L.maxBY - L.minBY));
+    L.hX = (float)(L.maxBX - L.minBX) / L.nIni;
+    if (L.nIni < 1 || L.nIni > 16 || L.nfeat + 4 * L.nIni + 16 > QCAP) {
+      set_error("eao_orb_create: level geometry outside the quadtree kernel limits");
+      return EAO_E_ARG;
+    }
+    L.sel_off = sel_total;
+    L.sel_cap = std::max(L.nfeat + 2, 4 * L.nIni) + 8;
+    sel_total += L.sel_cap;
+    // resize tables (levels >= 1), OpenCV resize INTER_LINEAR
+    if (l > 0) {
+      const LevelDev& S = levels[l - 1];
+      const int sw = S.w, sh = S.h, dw = L.w, dh = L.h;
+      const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+      L.tab_x = (int)resize_xofs.size();
+      L.tab_y = (int)resize_yrows.size() / 2;
+      int xmax = dw;
+      for (int dx = 0; dx < dw; dx++) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)std::floor(fx);
+        fx -= sx;
+        if (sx < 0) {
+          fx = 0;
+          sx = 0;
+        }
+        if (sx + 1 >= sw) {
+          xmax = std::min(xmax, dx);
+          if (sx >= sw - 1) {
+            fx = 0;
+            sx = sw - 1;
+          }
+        }
+        resize_xofs.push_back(sx);
+        resize_ia.push_back(sat_s16((1.f - fx) * 2048));
+        resize_ia.push_back(sat_s16(fx * 2048));
+      }
+      L.xmax = xmax;
+      for (int dy = 0; dy < dh; dy++) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = (int)std::floor(fy);
+        fy -= sy;
+        resize_ib.push_back(sat_s16((1.f - fy) * 2048));
+        resize_ib.push_back(sat_s16(fy * 2048));
+        resize_yrows.push_back(std::min(std::max(sy, 0), sh - 1));
+        resize_yrows.push_back(std::min(std::max(sy + 1, 0), sh - 1));
+      }
+    }
+  }
+  pyr_bytes = (long long)((poff + 255) & ~255LL);
+  cand_stride = ((long long)cand_total + 63) & ~63LL;
+  sel_stride = ((long long)sel_total + 63) & ~63LL;
+  cap = sel_total;
+  roi_stride = (rsmax + 3) & ~3;
+  roi_rows = rhmax;
+  slot_map.clear();
+  for (int l = 0; l < nl; l++)
+    for (int k = 0; k < levels[l].sel_cap; k++) slot_map.push_back({l, k});
+  return EAO_OK;
+}
+
+int OrbEngine::init(const eao_orb_params& prm, int device) {
+  int rc = plan(prm, device);
+  if (rc) return rc;
+  EAO_HIP_CHECK(hipSetDevice(dev));
+  EAO_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  const int B = p.max_batch;
+  auto up = [&](void** d, const void* h, size_t n) -> int {
+    EAO_HIP_CHECK(hipMalloc(d, std::max<size_t>(n, 16)));
+    if (n) EAO_HIP_CHECK(hipMemcpy(*d, h, n, hipMemcpyHostToDevice));
+    return 0;
+  };
+  if ((rc = up((void**)&d_levels, levels.data(), levels.size() * sizeof(LevelDev)))) return rc;
+  if ((rc = up((void**)&d_cells, cells.data(), cells.size() * sizeof(CellDev)))) return rc;
+  if ((rc = up((void**)&d_xofs, resize_xofs.data(), resize_xofs.size() * sizeof(int)))) return rc;
+  if ((rc = up((void**)&d_ia, resize_ia.data(), resize_ia.size() * sizeof(short)))) return rc;
+  if ((rc = up((void**)&d_yrows, resize_yrows.data(), resize_yrows.size() * sizeof(int)))) return rc;
+  if ((rc = up((void**)&d_ib, resize_ib.data(), resize_ib.size() * sizeof(short)))) return rc;
+  if ((rc = up((void**)&d_umax, umax.data(), umax.size() * sizeof(int)))) return rc;
+  if ((rc = up((void**)&d_gk, gk.data(), gk.size() * sizeof(int)))) return rc;
+  if ((rc = up((void**)&d_slot_map, slot_map.data(), slot_map.size() * sizeof(int2)))) return rc;
+  EAO_HIP_CHECK(hipMalloc(&d_pyr, std::max<long long>(pyr_bytes, 256) * B));
+  EAO_HIP_CHECK(hipMalloc(&d_cand, cand_stride * sizeof(uint32_t) * B));
+  EAO_HIP_CHECK(hipMalloc(&d_qbuf, 2 * cand_stride * sizeof(uint32_t) * B));
+  EAO_HIP_CHECK(hipMalloc(&d_cell_cnt, cells.size() * sizeof(int) * B));
+  EAO_HIP_CHECK(hipMalloc(&d_sel, sel_stride * sizeof(uint32_t) * B));
+  EAO_HIP_CHECK(hipMalloc(&d_sel_cnt, p.nlevels * sizeof(int) * B));
+  // single-image staging
+  EAO_HIP_CHECK(hipMalloc(&d_img, (size_t)p.width * p.height));
+  EAO_HIP_CHECK(hipMalloc(&d_out_kps, (size_t)cap * sizeof(eao_keypoint_dev)));
+  EAO_HIP_CHECK(hipMalloc(&d_out_desc, (size_t)cap * 32));
+  EAO_HIP_CHECK(hipMalloc(&d_out_cnt, sizeof(int)));
+  return EAO_OK;
+}
+
+OrbEngine::~OrbEngine() {
+  void* ptrs[] = {d_levels, d_cells, d_xofs, d_ia, d_yrows, d_ib, d_umax, d_gk, d_slot_map,
+                  d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
+                  d_out_desc, d_out_cnt};
+  for (void* q : ptrs)
+    if (q) (void)hipFree(q);
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint_dev* d_kps,
+                   uint8_t* d_desc, int* d_counts, int out_cap, hipStream_t s) {
+  if (nframes < 1 || nframes > p.max_batch || pitch < p.width || out_cap < cap) {
+    set_error("eao_orb_extract_batch_device: bad batch arguments");
+    return EAO_E_ARG;
+  }
+  if (!s) s = stream;
+  const long long fstride = (long long)pitch * p.height;
+  const int nl = p.nlevels;
+  // pyramid
+  for (int l = 1; l < nl; l++) {
+    const LevelDev& L = levels[l];
+    const LevelDev& S = levels[l - 1];
+    const uint8_t* src = l == 1 ? d_frames : d_pyr + S.plane_off;
+    const int spitch = l == 1 ? pitch : S.pitch;
+    const long long sstride = l == 1 ? fstride : pyr_bytes;
+    dim3 g((L.w + 255) / 256, L.h, nframes);
+    hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, src, spitch, sstride, d_pyr + L.plane_off,
+                       L.pitch, pyr_bytes, L.w, L.h, d_xofs + L.tab_x, d_ia + 2 * L.tab_x, L.xmax,
+                       d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
+  }
+  // FAST per cell
+  {
+    dim3 g((unsigned)cells.size(), nframes);
+    size_t lds = (size_t)roi_stride * roi_rows * 2;
+    hipLaunchKernelGGL(k_fast, g, dim3(64), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
+                       d_levels, d_cells, p.ini_th_fast, p.min_th_fast, roi_stride, roi_rows,
+                       d_cand, cand_stride, d_cell_cnt, (int)cells.size());
+  }
+  // quadtree distribution
+  {
+    dim3 g(nl, nframes);
+    hipLaunchKernelGGL(k_distribute, g, dim3(64), 0, s, d_cand, cand_stride, d_cell_cnt,
+                       (int)cells.size(), d_levels, d_cells, d_qbuf, 2 * cand_stride, d_sel,
+                       sel_stride, d_sel_cnt, nl);
+  }
+  // orientation + descriptors
+  {
+    const int nslots = (int)slot_map.size();
+    dim3 g((nslots + 3) / 4, nframes);
+    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
+                       d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax,
+                       d_gk, d_kps, d_desc, d_counts, out_cap);
+  }
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+}  // namespace eao

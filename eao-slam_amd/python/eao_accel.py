@@ -1,0 +1,275 @@
+"""ctypes binding of the MI355X engine's C ABI (include/eao_accel.h).
+
+This is a thin harness binding used by tests/, bench.py and __graft_entry__;
+the product is the shared library eao-slam_amd/lib/libeao_accel.so. There is
+no fallback: if the library or a gfx950 device is missing, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libeao_accel.so")
+
+EAO_OK, EAO_E_ARG, EAO_E_NODEVICE, EAO_E_HIP, EAO_E_CAPACITY, EAO_E_STATE = 0, -1, -2, -3, -4, -5
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+NP_DTYPE = np.dtype([("verdict", "<i4"), ("m", "<i4"), ("n", "<i4"), ("w", "<f4", 3), ("r1", "<f4"),
+                     ("r2", "<f4"), ("cnt_gt", "<f4", 3), ("cnt_lt", "<f4", 3), ("cnt_eq", "<f4", 3)])
+
+
+class EaoError(RuntimeError):
+    pass
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int32), ("scale_factor", ctypes.c_float),
+                ("nlevels", ctypes.c_int32), ("ini_th_fast", ctypes.c_int32),
+                ("min_th_fast", ctypes.c_int32), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("max_batch", ctypes.c_int32)]
+
+
+class Camera(ctypes.Structure):
+    _fields_ = [("img_w", ctypes.c_int32), ("img_h", ctypes.c_int32), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EaoError("engine library not built: %s (run __graft_entry__.build())" % LIB_PATH)
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.eao_version.restype = ctypes.c_char_p
+        _lib.eao_last_error.restype = ctypes.c_char_p
+    return _lib
+
+
+def P(a):
+    """numpy array -> void pointer (None passes NULL)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def check(rc, what):
+    if rc < 0:
+        raise EaoError("%s failed (%d): %s" % (what, rc, lib().eao_last_error().decode()))
+    return rc
+
+
+def device_ok(dev=0):
+    return bool(lib().eao_device_ok(dev))
+
+
+def camera(w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
+    return Camera(w, h, *[float(k) for k in K])
+
+
+class Orb:
+    """ORBextractor replacement (reference src/ORBextractor.cc)."""
+
+    def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
+                 width=640, height=480, max_batch=1, device=0):
+        self.p = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, width, height, max_batch)
+        self.h = ctypes.c_void_p()
+        check(lib().eao_orb_create(ctypes.byref(self.p), device, ctypes.byref(self.h)), "eao_orb_create")
+        self.nlevels = nlevels
+        self.cap = check(lib().eao_orb_frame_capacity(self.h), "eao_orb_frame_capacity")
+
+    def close(self):
+        if self.h:
+            lib().eao_orb_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def scale_tables(self):
+        t = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        check(lib().eao_orb_scale_tables(self.h, *[P(x) for x in t]), "scale_tables")
+        return t
+
+    def quotas(self):
+        q = np.zeros(self.nlevels, np.int32)
+        check(lib().eao_orb_level_quotas(self.h, P(q)), "level_quotas")
+        return q
+
+    def extract(self, gray):
+        gray = np.ascontiguousarray(gray, np.uint8)
+        h, w = gray.shape
+        kps = np.zeros(self.cap, KP_DTYPE)
+        desc = np.zeros((self.cap, 32), np.uint8)
+        n = ctypes.c_int()
+        check(lib().eao_orb_extract(self.h, P(gray), w, h, w, P(kps), P(desc), self.cap, ctypes.byref(n)),
+              "eao_orb_extract")
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def pyramid(self, gray):
+        gray = np.ascontiguousarray(gray, np.uint8)
+        tot = 0
+        sizes = []
+        for l in range(self.nlevels):
+            s = 1.0
+            for _ in range(l):
+                s = float(np.float32(np.float64(np.float32(s)) * np.float64(np.float32(self.p.scale_factor))))
+            inv = np.float32(1.0) / np.float32(s)
+            lw = int(np.rint(np.float32(gray.shape[1]) * inv))
+            lh = int(np.rint(np.float32(gray.shape[0]) * inv))
+            sizes.append((lw, lh))
+            tot += lw * lh
+        out = np.zeros(tot, np.uint8)
+        check(lib().eao_orb_debug_pyramid(self.h, P(gray), P(out)), "debug_pyramid")
+        levels, o = [], 0
+        for lw, lh in sizes:
+            levels.append(out[o:o + lw * lh].reshape(lh, lw))
+            o += lw * lh
+        return levels
+
+    def extract_batch_device(self, frames_ptr, nframes, pitch, kps_ptr, desc_ptr, counts_ptr, cap, stream=None):
+        check(lib().eao_orb_extract_batch_device(self.h, ctypes.c_void_p(frames_ptr), nframes, pitch,
+                                                 ctypes.c_void_p(kps_ptr), ctypes.c_void_p(desc_ptr),
+                                                 ctypes.c_void_p(counts_ptr), cap,
+                                                 ctypes.c_void_p(stream) if stream else None),
+              "eao_orb_extract_batch_device")
+
+
+class Matcher:
+    """ORBmatcher + Frame grid replacement (reference src/ORBmatcher.cc, src/Frame.cc)."""
+
+    def __init__(self, max_kps=4096, max_batch=2, device=0):
+        self.h = ctypes.c_void_p()
+        check(lib().eao_matcher_create(device, max_kps, max_batch, ctypes.byref(self.h)), "eao_matcher_create")
+
+    def close(self):
+        if self.h:
+            lib().eao_matcher_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def motion(self, cam, Tcw, th, check_ori, last_kps, has_mp, mp_pos, mp_desc, cur_kps, cur_desc, scales):
+        cur_match = np.full(len(cur_kps), -1, np.int32)
+        T = np.ascontiguousarray(Tcw, np.float32)
+        n = check(lib().eao_match_motion(self.h, ctypes.byref(cam), P(T), ctypes.c_float(th), int(check_ori),
+                                         len(last_kps), P(last_kps), P(np.ascontiguousarray(has_mp, np.uint8)),
+                                         P(np.ascontiguousarray(mp_pos, np.float32)),
+                                         P(np.ascontiguousarray(mp_desc, np.uint8)), len(cur_kps), P(cur_kps),
+                                         P(np.ascontiguousarray(cur_desc, np.uint8)), len(scales),
+                                         P(np.ascontiguousarray(scales, np.float32)), P(cur_match)),
+                  "eao_match_motion")
+        return n, cur_match
+
+    def frustum(self, cam, Tcw, pos, normal, mind, maxd, vclim, logsf):
+        n = len(pos)
+        inv = np.zeros(n, np.uint8)
+        proj = np.zeros((n, 2), np.float32)
+        lvl = np.zeros(n, np.int32)
+        vc = np.zeros(n, np.float32)
+        c = check(lib().eao_is_in_frustum(self.h, ctypes.byref(cam), P(np.ascontiguousarray(Tcw, np.float32)), n,
+                                          P(np.ascontiguousarray(pos, np.float32)),
+                                          P(np.ascontiguousarray(normal, np.float32)),
+                                          P(np.ascontiguousarray(mind, np.float32)),
+                                          P(np.ascontiguousarray(maxd, np.float32)), ctypes.c_float(vclim),
+                                          ctypes.c_float(logsf), P(inv), P(proj), P(lvl), P(vc)),
+                  "eao_is_in_frustum")
+        return c, inv, proj, lvl, vc
+
+    def local(self, cam, th, nnratio, inv, proj, lvl, vc, mp_desc, cur_kps, cur_desc, pre, scales):
+        out = np.full(len(cur_kps), -1, np.int32)
+        n = check(lib().eao_match_local(self.h, ctypes.byref(cam), ctypes.c_float(th), ctypes.c_float(nnratio),
+                                        len(inv), P(inv), P(proj), P(lvl), P(vc),
+                                        P(np.ascontiguousarray(mp_desc, np.uint8)), len(cur_kps), P(cur_kps),
+                                        P(np.ascontiguousarray(cur_desc, np.uint8)),
+                                        P(pre) if pre is not None else None, len(scales),
+                                        P(np.ascontiguousarray(scales, np.float32)), P(out)),
+                  "eao_match_local")
+        return n, out
+
+    def init(self, cam, nnratio, check_ori, kps1, desc1, kps2, desc2, prev_xy, window):
+        m12 = np.full(len(kps1), -1, np.int32)
+        prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+        n = check(lib().eao_match_init(self.h, ctypes.byref(cam), ctypes.c_float(nnratio), int(check_ori),
+                                       len(kps1), P(kps1), P(np.ascontiguousarray(desc1, np.uint8)), len(kps2),
+                                       P(kps2), P(np.ascontiguousarray(desc2, np.uint8)), P(prev), window, P(m12)),
+                  "eao_match_init")
+        return n, m12, prev
+
+    def hamming(self, q, t, qi, ti):
+        out = np.zeros(len(qi), np.int32)
+        check(lib().eao_hamming_pairs(self.h, P(np.ascontiguousarray(q, np.uint8)), len(q),
+                                      P(np.ascontiguousarray(t, np.uint8)), len(t),
+                                      P(np.ascontiguousarray(qi, np.int32)), P(np.ascontiguousarray(ti, np.int32)),
+                                      len(qi), P(out)), "eao_hamming_pairs")
+        return out
+
+    def motion_batch_device(self, cam, nframes, cap, T_ptr, th, check_ori, kps_ptr, desc_ptr, counts_ptr,
+                            has_mp_ptr, mp_pos_ptr, mp_desc_ptr, scales, match_ptr, nmatch_ptr, stream=None):
+        sc = np.ascontiguousarray(scales, np.float32)
+        v = ctypes.c_void_p
+        check(lib().eao_match_motion_batch_device(self.h, ctypes.byref(cam), nframes, cap, v(T_ptr),
+                                                  ctypes.c_float(th), int(check_ori), v(kps_ptr), v(desc_ptr),
+                                                  v(counts_ptr), v(has_mp_ptr), v(mp_pos_ptr), v(mp_desc_ptr),
+                                                  len(sc), P(sc), v(match_ptr), v(nmatch_ptr),
+                                                  v(stream) if stream else None),
+              "eao_match_motion_batch_device")
+
+
+class Assoc:
+    """Object_2D / Object_Map math replacement (reference src/Object.cc, isolation_forest.h)."""
+
+    def __init__(self, max_points=65536, device=0):
+        self.h = ctypes.c_void_p()
+        check(lib().eao_assoc_create(device, max_points, ctypes.byref(self.h)), "eao_assoc_create")
+
+    def close(self):
+        if self.h:
+            lib().eao_assoc_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def np_batch(self, frame_sets, obj_sets):
+        """frame_sets/obj_sets: lists of (pts (n,3) f32, valid (n,) u8 or None)."""
+        def cat(sets):
+            pts = [np.asarray(p, np.float32).reshape(-1, 3) for p, _ in sets]
+            val = [np.ones(len(p), np.uint8) if v is None else np.asarray(v, np.uint8) for (_, v), p in zip(sets, pts)]
+            lens = np.array([len(p) for p in pts], np.int32)
+            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int32)
+            allp = np.concatenate(pts) if len(pts) else np.zeros((0, 3), np.float32)
+            allv = np.concatenate(val) if len(val) else np.zeros(0, np.uint8)
+            return np.ascontiguousarray(allp), np.ascontiguousarray(allv), offs, lens
+        fp, fv, fo, fl = cat(frame_sets)
+        op, ov, oo, ol = cat(obj_sets)
+        out = np.zeros(len(frame_sets), NP_DTYPE)
+        check(lib().eao_np_test_batch(self.h, len(frame_sets), P(fp), P(fv), P(fo), P(fl), P(op), P(ov), P(oo),
+                                      P(ol), P(out)), "eao_np_test_batch")
+        return out
+
+    def iforest(self, clouds, trees=50, seed=12345, samples=None):
+        pts = [np.asarray(c, np.float32).reshape(-1, 3) for c in clouds]
+        lens = np.array([len(p) for p in pts], np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int32)
+        if samples is None:
+            samples = lens // 2
+        samples = np.asarray(samples, np.uint32)
+        allp = np.ascontiguousarray(np.concatenate(pts))
+        scores = np.zeros(len(allp), np.float64)
+        check(lib().eao_iforest_scores_batch(self.h, len(pts), P(allp), P(offs), P(lens), trees, seed, P(samples),
+                                             P(scores)), "eao_iforest_scores_batch")
+        return [scores[o:o + l] for o, l in zip(offs, lens)]
+
+    def rects(self, cam, Tcw, clouds):
+        pts = [np.asarray(c, np.float32).reshape(-1, 3) for c in clouds]
+        lens = np.array([len(p) for p in pts], np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int32)
+        allp = np.ascontiguousarray(np.concatenate(pts)) if len(pts) else np.zeros((0, 3), np.float32)
+        rect = np.zeros((len(pts), 4), np.int32)
+        ok = np.zeros(len(pts), np.uint8)
+        check(lib().eao_project_rects(self.h, ctypes.byref(cam), P(np.ascontiguousarray(Tcw, np.float32)),
+                                      len(pts), P(allp), P(offs), P(lens), P(rect), P(ok)), "eao_project_rects")
+        return rect, ok

@@ -1,0 +1,210 @@
+/*
+ * eao_accel.h -- C ABI of the MI355X-native EAO-SLAM front-end + object
+ * association engine (gfx950, HIP).
+ *
+ * Plain C: opaque handles, plain pointers and sizes, caller-owned buffers,
+ * int status (0 ok, <0 error, see EAO_E_*). No torch / OpenCV / Eigen types.
+ * Every entry point names the reference interface it replaces (paths relative
+ * to the reference repository yanmin-wu/EAO-SLAM). INTEGRATION.md shows the
+ * reference-side shims (ORBextractor::operator(), ORBmatcher::SearchBy*,
+ * Object_2D / Object_Map) that bind these symbols so mono_tum links unchanged.
+ *
+ * Device pointers: functions with the suffix _device take HIP device pointers
+ * (inputs resident in HBM) and a hipStream_t passed as void* (NULL = the
+ * handle's own stream). All other functions take host pointers.
+ *
+ * The engine has NO CPU fallback: without a usable gfx950 device every call
+ * returns EAO_E_NODEVICE.
+ */
+#ifndef EAO_ACCEL_H
+#define EAO_ACCEL_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EAO_OK 0
+#define EAO_E_ARG (-1)
+#define EAO_E_NODEVICE (-2)
+#define EAO_E_HIP (-3)
+#define EAO_E_CAPACITY (-4)
+#define EAO_E_STATE (-5)
+
+/* mirrors cv::KeyPoint {pt.x, pt.y, size, angle, response, octave, class_id}
+   (28 bytes, same field order) -- the element type of Frame::mvKeys */
+typedef struct {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} eao_keypoint;
+
+/* ORB parameters: ORBextractor::ORBextractor(nfeatures, scaleFactor, nlevels,
+   iniThFAST, minThFAST) (include/ORBextractor.h:50-51); max_* size the
+   handle's HBM workspace (batch of frames of at most max_width x max_height). */
+typedef struct {
+  int32_t nfeatures;
+  float scale_factor;
+  int32_t nlevels;
+  int32_t ini_th_fast;
+  int32_t min_th_fast;
+  int32_t width, height; /* frame size the handle is planned for */
+  int32_t max_batch;     /* frames per batched call */
+} eao_orb_params;
+
+typedef struct eao_orb eao_orb;
+
+/* library / device */
+const char* eao_version(void);
+int eao_device_ok(int device); /* 1 when a gfx950 device is usable */
+const char* eao_last_error(void);
+
+/* --- ORB extraction: replaces ORBextractor (src/ORBextractor.cc:410-1132) --- */
+/* ctor, src/ORBextractor.cc:410-470 */
+int eao_orb_create(const eao_orb_params* p, int device, eao_orb** out);
+int eao_orb_destroy(eao_orb* h);
+/* GetScaleFactors/GetInverseScaleFactors/GetScaleSigmaSquares/
+   GetInverseScaleSigmaSquares (include/ORBextractor.h:63-83); arrays of nlevels */
+int eao_orb_scale_tables(const eao_orb* h, float* scale, float* inv_scale, float* sigma2,
+                         float* inv_sigma2);
+/* per-level feature quotas mnFeaturesPerLevel (src/ORBextractor.cc:435-446) */
+int eao_orb_level_quotas(const eao_orb* h, int32_t* quotas);
+/* output capacity (keypoints) per frame slot of the batched API */
+int eao_orb_frame_capacity(const eao_orb* h);
+/* ORBextractor::operator()(image, mask, keypoints, descriptors)
+   (src/ORBextractor.cc:1043-1105) on one host image. Keypoints in the
+   reference order (level 0..7, quadtree order within a level); desc = n x 32
+   bytes. An empty image (w*h == 0) returns n_out = 0 like the reference's
+   early return; 0 keypoints means "descriptors.release()". */
+int eao_orb_extract(eao_orb* h, const uint8_t* gray, int w, int h_, int stride,
+                    eao_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+/* batched, HBM-resident: frames [n][h][pitch] u8 device; outputs per frame slot
+   f: kps[f*cap .. f*cap+counts[f]), desc[(f*cap+i)*32], counts[f]. cap must be
+   >= eao_orb_frame_capacity(). */
+int eao_orb_extract_batch_device(eao_orb* h, const uint8_t* d_frames, int nframes, int pitch,
+                                 eao_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap,
+                                 void* stream);
+/* debug taps for parity tests (device work, host results) */
+int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out /* concatenated levels */);
+
+/* --- matching: replaces ORBmatcher (src/ORBmatcher.cc) + Frame grid ---------- */
+typedef struct {
+  int32_t img_w, img_h; /* Frame::mnMinX=0..mnMaxX=w, mnMinY=0..mnMaxY=h (k1 == 0) */
+  float fx, fy, cx, cy;
+} eao_camera;
+
+typedef struct eao_matcher eao_matcher;
+int eao_matcher_create(int device, int max_kps, int max_batch, eao_matcher** out);
+int eao_matcher_destroy(eao_matcher* m);
+
+/* DescriptorDistance (src/ORBmatcher.cc:1647-1663) for candidate lists:
+   dist[i] = hamming(q[qidx[i]], t[tidx[i]]) -- host arrays, GPU compute */
+int eao_hamming_pairs(eao_matcher* m, const uint8_t* q, int nq, const uint8_t* t, int nt,
+                      const int32_t* qidx, const int32_t* tidx, int npairs, int32_t* dist);
+
+/* SearchByProjection(CurrentFrame, LastFrame, th, bMono=true)
+   (src/ORBmatcher.cc:1328-1470) with the Frame grid (src/Frame.cc:351-513).
+   last_has_mp[i]: LastFrame.mvpMapPoints[i] && !mvbOutlier[i]; last_mp_pos /
+   last_mp_desc: that map point's GetWorldPos() / GetDescriptor().
+   cur_match[i2] = index i of the last-frame keypoint whose map point was
+   assigned to current keypoint i2, -1 if none. Returns nmatches (>= 0). */
+int eao_match_motion(eao_matcher* m, const eao_camera* cam, const float* Tcw, float th,
+                     int check_ori, int n_last, const eao_keypoint* last_kps,
+                     const uint8_t* last_has_mp, const float* last_mp_pos,
+                     const uint8_t* last_mp_desc, int n_cur, const eao_keypoint* cur_kps,
+                     const uint8_t* cur_desc, int nlevels, const float* scale_factors,
+                     int32_t* cur_match);
+
+/* batched motion-model search, HBM-resident: pair p matches frame slot p+1
+   (current) against slot p (last) for p in [0, nframes-1). Frame slot arrays
+   are [nframes][cap] (kps, desc*32, has_mp, mp_pos*3, mp_desc*32); Tcw[nframes][16].
+   cur_match[(p+1)*cap + i2], nmatches[p+1]. */
+int eao_match_motion_batch_device(eao_matcher* m, const eao_camera* cam, int nframes, int cap,
+                                  const float* d_Tcw, float th, int check_ori,
+                                  const eao_keypoint* d_kps, const uint8_t* d_desc,
+                                  const int32_t* d_counts, const uint8_t* d_has_mp,
+                                  const float* d_mp_pos, const uint8_t* d_mp_desc, int nlevels,
+                                  const float* scale_factors, int32_t* d_cur_match,
+                                  int32_t* d_nmatches, void* stream);
+
+/* Frame::isInFrustum (src/Frame.cc:390-446) + MapPoint::PredictScale
+   (src/MapPoint.cc:385-394) for a batch of map points. */
+int eao_is_in_frustum(eao_matcher* m, const eao_camera* cam, const float* Tcw, int n_mp,
+                      const float* mp_pos, const float* mp_normal, const float* mp_min_dist,
+                      const float* mp_max_dist, float view_cos_limit, float log_scale_factor,
+                      uint8_t* in_view, float* proj_xy, int32_t* pred_level, float* view_cos);
+
+/* SearchByProjection(Frame&, const vector<MapPoint*>&, th)
+   (src/ORBmatcher.cc:45-129). in_view[i] = mbTrackInView (isInFrustum);
+   pred_level is clamped to [0, nlevels-1].
+   cur_preassigned[i] >= 0 marks keypoints that already hold a map point. */
+int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnratio, int n_mp,
+                    const uint8_t* in_view, const float* proj_xy, const int32_t* pred_level,
+                    const float* view_cos,
+                    const uint8_t* mp_desc, int n_cur, const eao_keypoint* cur_kps,
+                    const uint8_t* cur_desc, const int32_t* cur_preassigned, int nlevels,
+                    const float* scale_factors, int32_t* cur_match);
+
+/* SearchForInitialization (src/ORBmatcher.cc:405-520); prev_matched_xy is
+   updated in place like vbPrevMatched. */
+int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int check_ori, int n1,
+                   const eao_keypoint* kps1, const uint8_t* desc1, int n2,
+                   const eao_keypoint* kps2, const uint8_t* desc2, float* prev_matched_xy,
+                   int window, int32_t* matches12);
+
+/* --- EAO association: replaces Object_2D / Object_Map math (src/Object.cc) -- */
+typedef struct {
+  int32_t verdict; /* 0: m<20, 1: pass, 2: fail -- NoParaDataAssociation return */
+  int32_t m, n;
+  float w[3];
+  float r1, r2;
+  float cnt_gt[3], cnt_lt[3], cnt_eq[3];
+} eao_np_stats;
+
+typedef struct eao_assoc eao_assoc;
+int eao_assoc_create(int device, int max_points, eao_assoc** out);
+int eao_assoc_destroy(eao_assoc* a);
+
+/* Object_2D::NoParaDataAssociation (src/Object.cc:714-930) for a batch of
+   (detection, object) pairs. Point sets are float3 arrays with validity
+   flags (!isBad && !out_point); pair p uses frame set fs[p] and object set
+   os[p] given as offsets/lengths into the concatenated arrays. */
+int eao_np_test_batch(eao_assoc* a, int npairs, const float* frame_pts, const uint8_t* frame_valid,
+                      const int32_t* frame_off, const int32_t* frame_len, const float* obj_pts,
+                      const uint8_t* obj_valid, const int32_t* obj_off, const int32_t* obj_len,
+                      eao_np_stats* out);
+
+/* IsolationForest::Build(trees, seed, data, sample) + GetAnomalyScores
+   (include/isolation_forest.h:448-530) as called by
+   Object_Map::IsolationForestDeleteOutliers (src/Object.cc:1257-1270), for a
+   batch of point clouds (cloud c = pts[off[c] .. off[c]+len[c])). */
+int eao_iforest_scores_batch(eao_assoc* a, int nclouds, const float* pts, const int32_t* off,
+                             const int32_t* len, uint32_t trees, uint32_t seed,
+                             const uint32_t* sample_size, double* scores);
+
+/* Object_Map::ComputeProjectRectFrame (src/Object.cc:1558-1603) for a batch of
+   clouds under one pose; rect[c*4] = x,y,w,h (cv::Rect). Empty cloud -> rect
+   left untouched and ok[c] = 0. */
+int eao_project_rects(eao_assoc* a, const eao_camera* cam, const float* Tcw, int nclouds,
+                      const float* pts, const int32_t* off, const int32_t* len, int32_t* rect,
+                      uint8_t* ok);
+
+/* Deterministic association replay: the object section
+   of Tracking::TrackWithMotionModel (src/Tracking.cc:1241-1696) with
+   ObjectDataAssociation / DataAssociateUpdate / iForest on the GPU, and the
+   LocalMapping object maintenance (src/LocalMapping.cc:772-882). */
+typedef struct eao_replay eao_replay;
+int eao_replay_create(eao_assoc* a, const char* flag, int img_w, int img_h, const float* K4,
+                      eao_replay** out);
+int eao_replay_destroy(eao_replay* r);
+int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
+                     const int32_t* boxes, int n_pts, const int32_t* mp_ids, const float* mp_pos,
+                     const float* kp_uv, const uint8_t* mp_bad, int32_t* det_out);
+int eao_replay_local_mapping(eao_replay* r);
+int eao_replay_num_objects(eao_replay* r);
+int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats);
+int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,702 @@
+/*
+ * orb_ref.cpp -- CPU restatement of ORBextractor (TEST INFRASTRUCTURE ONLY).
+ *
+ * Follows reference src/ORBextractor.cc line by line in semantics; OpenCV 3.2
+ * primitives it calls are restated from their scalar C++ paths (SURVEY.md
+ * appendix A). Compiled with -O2 -ffp-contract=off so float expressions round
+ * exactly as written.
+ */
+#include "oracle.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <list>
+#include <utility>
+#include <vector>
+
+namespace orc {
+
+static const int kPattern[1024] = {
+#include "../eao-slam_amd/csrc/orb_pattern.inc"
+};
+
+const int PATCH_SIZE = 31;       // ORBextractor.cc:72
+const int HALF_PATCH_SIZE = 15;  // ORBextractor.cc:73
+const int EDGE_THRESHOLD = 19;   // ORBextractor.cc:74
+
+// cvRound: SSE2 cvtss2si/cvtsd2si under default MXCSR = round half to even.
+static inline int cvRound(float v) { return (int)std::lrintf(v); }
+static inline int cvRound(double v) { return (int)std::lrint(v); }
+static inline int cvFloor(float v) { return (int)std::floor(v); }
+static inline int cvFloor(double v) { return (int)std::floor(v); }
+static inline int cvCeil(float v) { return (int)std::ceil(v); }
+static inline uint8_t sat_u8(int v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+static inline short sat_s16(float v) {
+  int iv = cvRound(v);
+  return (short)(iv < -32768 ? -32768 : (iv > 32767 ? 32767 : iv));
+}
+
+struct Params {
+  int nfeatures;
+  double scaleFactor;  // member is double in the reference (ORBextractor.h:101)
+  int nlevels, iniTh, minTh;
+  std::vector<float> scale, invScale, sigma2, invSigma2;
+  std::vector<int> nfeat;
+  int umax[HALF_PATCH_SIZE + 1];
+};
+
+// ORBextractor::ORBextractor, ORBextractor.cc:410-470
+static Params make_params(int nfeatures, float scaleFactorF, int nlevels, int iniTh, int minTh) {
+  Params p;
+  p.nfeatures = nfeatures;
+  p.scaleFactor = scaleFactorF;
+  p.nlevels = nlevels;
+  p.iniTh = iniTh;
+  p.minTh = minTh;
+  p.scale.resize(nlevels);
+  p.sigma2.resize(nlevels);
+  p.scale[0] = 1.0f;
+  p.sigma2[0] = 1.0f;
+  for (int i = 1; i < nlevels; i++) {
+    p.scale[i] = (float)((double)p.scale[i - 1] * p.scaleFactor);
+    p.sigma2[i] = p.scale[i] * p.scale[i];
+  }
+  p.invScale.resize(nlevels);
+  p.invSigma2.resize(nlevels);
+  for (int i = 0; i < nlevels; i++) {
+    p.invScale[i] = 1.0f / p.scale[i];
+    p.invSigma2[i] = 1.0f / p.sigma2[i];
+  }
+  p.nfeat.resize(nlevels);
+  float factor = (float)(1.0f / p.scaleFactor);
+  float nDesired = (float)nfeatures * (1 - factor) /
+                   (1 - (float)std::pow((double)factor, (double)nlevels));
+  int sum = 0;
+  for (int level = 0; level < nlevels - 1; level++) {
+    p.nfeat[level] = cvRound(nDesired);
+    sum += p.nfeat[level];
+    nDesired *= factor;
+  }
+  p.nfeat[nlevels - 1] = std::max(nfeatures - sum, 0);
+
+  int v, v0;
+  int vmax = cvFloor((float)HALF_PATCH_SIZE * std::sqrt(2.f) / 2 + 1);
+  int vmin = cvCeil((float)HALF_PATCH_SIZE * std::sqrt(2.f) / 2);
+  const double hp2 = HALF_PATCH_SIZE * HALF_PATCH_SIZE;
+  for (v = 0; v <= vmax; ++v) p.umax[v] = cvRound(std::sqrt(hp2 - v * v));
+  for (v = HALF_PATCH_SIZE, v0 = 0; v >= vmin; --v) {
+    while (p.umax[v0] == p.umax[v0 + 1]) ++v0;
+    p.umax[v] = v0;
+    ++v0;
+  }
+  return p;
+}
+
+// Level size: ComputePyramid, ORBextractor.cc:1112
+static void level_sizes(int w, int h, const Params& p, std::vector<int>& lw, std::vector<int>& lh) {
+  lw.resize(p.nlevels);
+  lh.resize(p.nlevels);
+  for (int l = 0; l < p.nlevels; l++) {
+    float s = p.invScale[l];
+    lw[l] = cvRound((float)w * s);
+    lh[l] = cvRound((float)h * s);
+  }
+}
+
+// cv::resize(src, dst, dsize, 0, 0, INTER_LINEAR) for 8UC1, scalar path of
+// OpenCV 3.2 imgwarp.cpp (resizeGeneric_ + HResizeLinear + VResizeLinear with
+// FixedPtCast<int,uchar,22>). Call site ORBextractor.cc:1120.
+void resize_linear_u8(const uint8_t* src, int sw, int sh, uint8_t* dst, int dw, int dh) {
+  const double inv_scale_x = (double)dw / sw, inv_scale_y = (double)dh / sh;
+  const double scale_x = 1. / inv_scale_x, scale_y = 1. / inv_scale_y;
+  const int ONE = 2048;  // INTER_RESIZE_COEF_SCALE
+  std::vector<int> xofs(dw);
+  std::vector<short> ia(2 * dw);
+  int xmax = dw;
+  for (int dx = 0; dx < dw; dx++) {
+    float fx = (float)((dx + 0.5) * scale_x - 0.5);
+    int sx = cvFloor(fx);
+    fx -= sx;
+    if (sx < 0) { fx = 0; sx = 0; }
+    if (sx + 1 >= sw) {
+      xmax = std::min(xmax, dx);
+      if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+    }
+    xofs[dx] = sx;
+    ia[2 * dx] = sat_s16((1.f - fx) * ONE);
+    ia[2 * dx + 1] = sat_s16(fx * ONE);
+  }
+  std::vector<int> r0(dw), r1(dw);
+  auto hres = [&](const uint8_t* S, int* D) {
+    int dx = 0;
+    for (; dx < xmax; dx++) {
+      int sx = xofs[dx];
+      D[dx] = S[sx] * ia[2 * dx] + S[sx + 1] * ia[2 * dx + 1];
+    }
+    for (; dx < dw; dx++) D[dx] = S[xofs[dx]] * ONE;
+  };
+  for (int dy = 0; dy < dh; dy++) {
+    float fy = (float)((dy + 0.5) * scale_y - 0.5);
+    int sy = cvFloor(fy);
+    fy -= sy;
+    short b0 = sat_s16((1.f - fy) * ONE), b1 = sat_s16(fy * ONE);
+    int y0 = std::min(std::max(sy, 0), sh - 1);
+    int y1 = std::min(std::max(sy + 1, 0), sh - 1);
+    hres(src + (size_t)y0 * sw, r0.data());
+    hres(src + (size_t)y1 * sw, r1.data());
+    uint8_t* d = dst + (size_t)dy * dw;
+    for (int x = 0; x < dw; x++) d[x] = sat_u8((r0[x] * b0 + r1[x] * b1 + (1 << 21)) >> 22);
+  }
+}
+
+static void pyramid(const uint8_t* img, int w, int h, const Params& p,
+                    std::vector<std::vector<uint8_t>>& L, std::vector<int>& lw, std::vector<int>& lh) {
+  level_sizes(w, h, p, lw, lh);
+  L.resize(p.nlevels);
+  L[0].assign(img, img + (size_t)w * h);
+  for (int l = 1; l < p.nlevels; l++) {
+    L[l].resize((size_t)lw[l] * lh[l]);
+    resize_linear_u8(L[l - 1].data(), lw[l - 1], lh[l - 1], L[l].data(), lw[l], lh[l]);
+  }
+}
+
+// OpenCV 3.2 fast.cpp cornerScore<16>
+static int corner_score16(const uint8_t* ptr, const int* pixel, int threshold) {
+  const int K = 8, N = K * 3 + 1;
+  int k, v = ptr[0];
+  short d[N];
+  for (k = 0; k < N; k++) d[k] = (short)(v - ptr[pixel[k]]);
+  int a0 = threshold;
+  for (k = 0; k < 16; k += 2) {
+    int a = std::min((int)d[k + 1], (int)d[k + 2]);
+    a = std::min(a, (int)d[k + 3]);
+    if (a <= a0) continue;
+    a = std::min(a, (int)d[k + 4]);
+    a = std::min(a, (int)d[k + 5]);
+    a = std::min(a, (int)d[k + 6]);
+    a = std::min(a, (int)d[k + 7]);
+    a = std::min(a, (int)d[k + 8]);
+    a0 = std::max(a0, std::min(a, (int)d[k]));
+    a0 = std::max(a0, std::min(a, (int)d[k + 9]));
+  }
+  int b0 = -a0;
+  for (k = 0; k < 16; k += 2) {
+    int b = std::max((int)d[k + 1], (int)d[k + 2]);
+    b = std::max(b, (int)d[k + 3]);
+    b = std::max(b, (int)d[k + 4]);
+    b = std::max(b, (int)d[k + 5]);
+    if (b >= b0) continue;
+    b = std::max(b, (int)d[k + 6]);
+    b = std::max(b, (int)d[k + 7]);
+    b = std::max(b, (int)d[k + 8]);
+    b0 = std::min(b0, std::max(b, (int)d[k]));
+    b0 = std::min(b0, std::max(b, (int)d[k + 9]));
+  }
+  return -b0 - 1;
+}
+
+// cv::FAST(roi, kps, threshold, nonmax=true) with TYPE_9_16: OpenCV 3.2
+// fast.cpp FAST_t<16>. ROI = rows x cols window of an image with row stride.
+// Call sites ORBextractor.cc:809-816.
+static void fast_roi(const uint8_t* img, int stride, int rows, int cols, int threshold,
+                     std::vector<orc_keypoint>& kps) {
+  static const int off[16][2] = {{0, 3}, {1, 3}, {2, 2}, {3, 1}, {3, 0}, {3, -1}, {2, -2}, {1, -3},
+                                 {0, -3}, {-1, -3}, {-2, -2}, {-3, -1}, {-3, 0}, {-3, 1}, {-2, 2}, {-1, 3}};
+  const int K = 8, N = 25;
+  int pixel[25];
+  for (int k = 0; k < 16; k++) pixel[k] = off[k][0] + off[k][1] * stride;
+  for (int k = 16; k < 25; k++) pixel[k] = pixel[k - 16];
+  threshold = std::min(std::max(threshold, 0), 255);
+  uint8_t tab[512];
+  for (int i = -255; i <= 255; i++) tab[i + 255] = (uint8_t)(i < -threshold ? 1 : i > threshold ? 2 : 0);
+  std::vector<uint8_t> buf(3 * (size_t)cols, 0);
+  std::vector<int> cpbuf(3 * (size_t)(cols + 1), 0);
+  uint8_t* bufs[3] = {buf.data(), buf.data() + cols, buf.data() + 2 * cols};
+  int* cps[3] = {cpbuf.data() + 1, cpbuf.data() + 1 + (cols + 1), cpbuf.data() + 1 + 2 * (cols + 1)};
+  for (int i = 3; i < rows - 2; i++) {
+    const uint8_t* ptr = img + (size_t)i * stride + 3;
+    uint8_t* curr = bufs[(i - 3) % 3];
+    int* cornerpos = cps[(i - 3) % 3];
+    std::memset(curr, 0, cols);
+    int ncorners = 0;
+    if (i < rows - 3) {
+      for (int j = 3; j < cols - 3; j++, ptr++) {
+        int v = ptr[0];
+        const uint8_t* t = tab - v + 255;
+        int d = t[ptr[pixel[0]]] | t[ptr[pixel[8]]];
+        if (d == 0) continue;
+        d &= t[ptr[pixel[2]]] | t[ptr[pixel[10]]];
+        d &= t[ptr[pixel[4]]] | t[ptr[pixel[12]]];
+        d &= t[ptr[pixel[6]]] | t[ptr[pixel[14]]];
+        if (d == 0) continue;
+        d &= t[ptr[pixel[1]]] | t[ptr[pixel[9]]];
+        d &= t[ptr[pixel[3]]] | t[ptr[pixel[11]]];
+        d &= t[ptr[pixel[5]]] | t[ptr[pixel[13]]];
+        d &= t[ptr[pixel[7]]] | t[ptr[pixel[15]]];
+        if (d & 1) {
+          int vt = v - threshold, count = 0;
+          for (int k = 0; k < N; k++) {
+            int x = ptr[pixel[k]];
+            if (x < vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else
+              count = 0;
+          }
+        }
+        if (d & 2) {
+          int vt = v + threshold, count = 0;
+          for (int k = 0; k < N; k++) {
+            int x = ptr[pixel[k]];
+            if (x > vt) {
+              if (++count > K) {
+                cornerpos[ncorners++] = j;
+                curr[j] = (uint8_t)corner_score16(ptr, pixel, threshold);
+                break;
+              }
+            } else
+              count = 0;
+          }
+        }
+      }
+    }
+    cornerpos[-1] = ncorners;
+    if (i == 3) continue;
+    const uint8_t* prev = bufs[(i - 4 + 3) % 3];
+    const uint8_t* pprev = bufs[(i - 5 + 3) % 3];
+    cornerpos = cps[(i - 4 + 3) % 3];
+    ncorners = cornerpos[-1];
+    for (int k = 0; k < ncorners; k++) {
+      int j = cornerpos[k];
+      int score = prev[j];
+      if (score > prev[j + 1] && score > prev[j - 1] && score > pprev[j - 1] && score > pprev[j] &&
+          score > pprev[j + 1] && score > curr[j - 1] && score > curr[j] && score > curr[j + 1]) {
+        orc_keypoint kp;
+        kp.x = (float)j;
+        kp.y = (float)(i - 1);
+        kp.size = 7.f;
+        kp.angle = -1.f;
+        kp.response = (float)score;
+        kp.octave = 0;
+        kp.class_id = -1;
+        kps.push_back(kp);
+      }
+    }
+  }
+}
+
+// Cell loop of ComputeKeyPointsOctTree, ORBextractor.cc:769-829.
+static void level_candidates(const uint8_t* L, int cols, int rows, int iniTh, int minTh,
+                             std::vector<orc_keypoint>& out) {
+  const float W = 30;
+  const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+  const int maxBorderX = cols - EDGE_THRESHOLD + 3, maxBorderY = rows - EDGE_THRESHOLD + 3;
+  const float width = (float)(maxBorderX - minBorderX), height = (float)(maxBorderY - minBorderY);
+  const int nCols = (int)(width / W), nRows = (int)(height / W);
+  const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+  std::vector<orc_keypoint> cell;
+  for (int i = 0; i < nRows; i++) {
+    const float iniY = (float)(minBorderY + i * hCell);
+    float maxY = iniY + hCell + 6;
+    if (iniY >= maxBorderY - 3) continue;
+    if (maxY > maxBorderY) maxY = (float)maxBorderY;
+    for (int j = 0; j < nCols; j++) {
+      const float iniX = (float)(minBorderX + j * wCell);
+      float maxX = iniX + wCell + 6;
+      if (iniX >= maxBorderX - 6) continue;
+      if (maxX > maxBorderX) maxX = (float)maxBorderX;
+      const int y0 = (int)iniY, y1 = (int)maxY, x0 = (int)iniX, x1 = (int)maxX;
+      cell.clear();
+      fast_roi(L + (size_t)y0 * cols + x0, cols, y1 - y0, x1 - x0, iniTh, cell);
+      if (cell.empty()) fast_roi(L + (size_t)y0 * cols + x0, cols, y1 - y0, x1 - x0, minTh, cell);
+      for (auto& kp : cell) {
+        kp.x += j * wCell;
+        kp.y += i * hCell;
+        out.push_back(kp);
+      }
+    }
+  }
+}
+
+// ExtractorNode + DistributeOctTree, ORBextractor.cc:481-763.
+// Nodes hold indices into the level's candidate vector (order preserved).
+// Q14: equal-size ties in the final sort are broken by node creation order
+// (ascending), standing in for the reference's heap-address order.
+struct Node {
+  std::vector<int> keys;
+  int ulx, uly, urx, ury, blx, bly, brx, bry;
+  bool noMore = false;
+  long id = 0;
+  std::list<Node>::iterator lit;
+};
+
+static void divide_node(const Node& n, const std::vector<orc_keypoint>& K, Node& n1, Node& n2,
+                        Node& n3, Node& n4) {
+  const int halfX = (int)std::ceil((float)(n.urx - n.ulx) / 2);
+  const int halfY = (int)std::ceil((float)(n.bry - n.uly) / 2);
+  n1.ulx = n.ulx; n1.uly = n.uly;
+  n1.urx = n.ulx + halfX; n1.ury = n.uly;
+  n1.blx = n.ulx; n1.bly = n.uly + halfY;
+  n1.brx = n.ulx + halfX; n1.bry = n.uly + halfY;
+  n2.ulx = n1.urx; n2.uly = n1.ury;
+  n2.urx = n.urx; n2.ury = n.ury;
+  n2.blx = n1.brx; n2.bly = n1.bry;
+  n2.brx = n.urx; n2.bry = n.uly + halfY;
+  n3.ulx = n1.blx; n3.uly = n1.bly;
+  n3.urx = n1.brx; n3.ury = n1.bry;
+  n3.blx = n.blx; n3.bly = n.bly;
+  n3.brx = n1.brx; n3.bry = n.bly;
+  n4.ulx = n3.urx; n4.uly = n3.ury;
+  n4.urx = n2.brx; n4.ury = n2.bry;
+  n4.blx = n3.brx; n4.bly = n3.bry;
+  n4.brx = n.brx; n4.bry = n.bry;
+  for (int idx : n.keys) {
+    const orc_keypoint& kp = K[idx];
+    if (kp.x < n1.urx) {
+      if (kp.y < n1.bry) n1.keys.push_back(idx);
+      else n3.keys.push_back(idx);
+    } else if (kp.y < n1.bry)
+      n2.keys.push_back(idx);
+    else
+      n4.keys.push_back(idx);
+  }
+  if (n1.keys.size() == 1) n1.noMore = true;
+  if (n2.keys.size() == 1) n2.noMore = true;
+  if (n3.keys.size() == 1) n3.noMore = true;
+  if (n4.keys.size() == 1) n4.noMore = true;
+}
+
+static std::vector<int> distribute_octtree(const std::vector<orc_keypoint>& K, int minX, int maxX,
+                                           int minY, int maxY, int N) {
+  std::vector<int> result;
+  if (K.empty()) return result;
+  const int nIni = (int)std::round((float)(maxX - minX) / (maxY - minY));
+  const float hX = (float)(maxX - minX) / nIni;
+  std::list<Node> lNodes;
+  long next_id = 0;
+  std::vector<Node*> ini(nIni);
+  for (int i = 0; i < nIni; i++) {
+    Node ni;
+    ni.ulx = (int)(hX * (float)i); ni.uly = 0;
+    ni.urx = (int)(hX * (float)(i + 1)); ni.ury = 0;
+    ni.blx = ni.ulx; ni.bly = maxY - minY;
+    ni.brx = ni.urx; ni.bry = maxY - minY;
+    ni.id = next_id++;
+    lNodes.push_back(ni);
+    ini[i] = &lNodes.back();
+  }
+  for (size_t i = 0; i < K.size(); i++) ini[(int)(K[i].x / hX)]->keys.push_back((int)i);
+  for (auto lit = lNodes.begin(); lit != lNodes.end();) {
+    if (lit->keys.size() == 1) {
+      lit->noMore = true;
+      lit++;
+    } else if (lit->keys.empty())
+      lit = lNodes.erase(lit);
+    else
+      lit++;
+  }
+  bool finish = false;
+  std::vector<std::pair<std::pair<int, long>, Node*>> vSize;
+  auto push_child = [&](Node& c, std::vector<std::pair<std::pair<int, long>, Node*>>& dst, int* nExp) {
+    if (c.keys.size() > 0) {
+      c.id = next_id++;
+      lNodes.push_front(c);
+      if (c.keys.size() > 1) {
+        if (nExp) (*nExp)++;
+        dst.push_back({{(int)c.keys.size(), lNodes.front().id}, &lNodes.front()});
+        lNodes.front().lit = lNodes.begin();
+      }
+    }
+  };
+  while (!finish) {
+    int prevSize = (int)lNodes.size();
+    auto lit = lNodes.begin();
+    int nToExpand = 0;
+    vSize.clear();
+    while (lit != lNodes.end()) {
+      if (lit->noMore) {
+        lit++;
+        continue;
+      }
+      Node n1, n2, n3, n4;
+      divide_node(*lit, K, n1, n2, n3, n4);
+      push_child(n1, vSize, &nToExpand);
+      push_child(n2, vSize, &nToExpand);
+      push_child(n3, vSize, &nToExpand);
+      push_child(n4, vSize, &nToExpand);
+      lit = lNodes.erase(lit);
+    }
+    if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) {
+      finish = true;
+    } else if (((int)lNodes.size() + nToExpand * 3) > N) {
+      while (!finish) {
+        prevSize = (int)lNodes.size();
+        auto vPrev = vSize;
+        vSize.clear();
+        std::sort(vPrev.begin(), vPrev.end(),
+                  [](const std::pair<std::pair<int, long>, Node*>& a,
+                     const std::pair<std::pair<int, long>, Node*>& b) { return a.first < b.first; });
+        for (int j = (int)vPrev.size() - 1; j >= 0; j--) {
+          Node n1, n2, n3, n4;
+          divide_node(*vPrev[j].second, K, n1, n2, n3, n4);
+          push_child(n1, vSize, nullptr);
+          push_child(n2, vSize, nullptr);
+          push_child(n3, vSize, nullptr);
+          push_child(n4, vSize, nullptr);
+          lNodes.erase(vPrev[j].second->lit);
+          if ((int)lNodes.size() >= N) break;
+        }
+        if ((int)lNodes.size() >= N || (int)lNodes.size() == prevSize) finish = true;
+      }
+    }
+  }
+  for (auto& n : lNodes) {
+    int best = n.keys[0];
+    float maxResp = K[best].response;
+    for (size_t k = 1; k < n.keys.size(); k++) {
+      if (K[n.keys[k]].response > maxResp) {
+        best = n.keys[k];
+        maxResp = K[best].response;
+      }
+    }
+    result.push_back(best);
+  }
+  return result;
+}
+
+// cv::fastAtan2 (OpenCV 3.2 mathfuncs), call site ORBextractor.cc:103
+float fast_atan2(float y, float x) {
+  static const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+  static const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+  static const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+  static const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+  float ax = std::fabs(x), ay = std::fabs(y);
+  float a, c, c2;
+  if (ax >= ay) {
+    c = ay / (ax + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  } else {
+    c = ax / (ay + (float)DBL_EPSILON);
+    c2 = c * c;
+    a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+  }
+  if (x < 0) a = 180.f - a;
+  if (y < 0) a = 360.f - a;
+  return a;
+}
+
+// IC_Angle, ORBextractor.cc:77-104 (image = level, row stride = cols)
+static float ic_angle(const uint8_t* img, int stride, float px, float py, const int* umax) {
+  int m_01 = 0, m_10 = 0;
+  const uint8_t* center = img + (size_t)cvRound(py) * stride + cvRound(px);
+  for (int u = -HALF_PATCH_SIZE; u <= HALF_PATCH_SIZE; ++u) m_10 += u * center[u];
+  for (int v = 1; v <= HALF_PATCH_SIZE; ++v) {
+    int v_sum = 0;
+    int d = umax[v];
+    for (int u = -d; u <= d; ++u) {
+      int val_plus = center[u + v * stride], val_minus = center[u - v * stride];
+      v_sum += (val_plus - val_minus);
+      m_10 += u * (val_plus + val_minus);
+    }
+    m_01 += v * v_sum;
+  }
+  return fast_atan2((float)m_01, (float)m_10);
+}
+
+// getGaussianKernel(7, 2, CV_32F) -> integer kernel of the 8U separable path
+// (createSeparableLinearFilter: convertTo(CV_32S, 1<<8)). Call site :1086.
+static void gauss_kernel7(int* k) {
+  float cf[7];
+  double sum = 0;
+  const double sigma = 2.0, scale2X = -0.5 / (sigma * sigma);
+  for (int i = 0; i < 7; i++) {
+    double x = i - (7 - 1) * 0.5;
+    double t = std::exp(scale2X * x * x);
+    cf[i] = (float)t;
+    sum += cf[i];
+  }
+  sum = 1. / sum;
+  for (int i = 0; i < 7; i++) {
+    cf[i] = (float)(cf[i] * sum);
+    k[i] = cvRound((double)cf[i] * 256.0);
+  }
+}
+
+static inline int reflect101(int p, int len) {
+  if (len == 1) return 0;
+  while (p < 0 || p >= len) {
+    if (p < 0) p = -p;
+    if (p >= len) p = 2 * len - 2 - p;
+  }
+  return p;
+}
+
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) on an isolated 8U image:
+// int row pass, column pass (sum + 2^15) >> 16 (FixedPtCastEx, bits=16).
+void gaussian_blur7(const uint8_t* src, int w, int h, uint8_t* dst) {
+  int k[7];
+  gauss_kernel7(k);
+  std::vector<int> R((size_t)w * h);
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int s = 0;
+      for (int i = 0; i < 7; i++) s += k[i] * src[(size_t)y * w + reflect101(x + i - 3, w)];
+      R[(size_t)y * w + x] = s;
+    }
+  for (int y = 0; y < h; y++)
+    for (int x = 0; x < w; x++) {
+      int s = 0;
+      for (int j = 0; j < 7; j++) s += k[j] * R[(size_t)reflect101(y + j - 3, h) * w + x];
+      dst[(size_t)y * w + x] = sat_u8((s + (1 << 15)) >> 16);
+    }
+}
+
+// computeOrbDescriptor, ORBextractor.cc:108-147
+static void orb_descriptor(const orc_keypoint& kpt, const uint8_t* img, int stride, uint8_t* desc) {
+  const float factorPI = (float)(M_PI / 180.f);
+  float angle = (float)kpt.angle * factorPI;
+  // Q26: the reference calls the float overloads (libm cosf/sinf), whose last
+  // bit depends on the libm version (glibc 2.35 differs from correctly rounded
+  // on ~0.04% / 0.09% of inputs; the Ubuntu 16.04 original used yet another
+  // kernel). The engine defines a and b as the correctly rounded float cos/sin
+  // of the float angle, evaluated in double and rounded once.
+  float a = (float)std::cos((double)angle), b = (float)std::sin((double)angle);
+  const uint8_t* center = img + (size_t)cvRound(kpt.y) * stride + cvRound(kpt.x);
+  const int* pattern = kPattern;
+  auto get = [&](int idx) {
+    float px = (float)pattern[2 * idx], py = (float)pattern[2 * idx + 1];
+    return (int)center[cvRound(px * b + py * a) * stride + cvRound(px * a - py * b)];
+  };
+  for (int i = 0; i < 32; ++i, pattern += 32) {
+    int val = 0;
+    for (int bit = 0; bit < 8; bit++) {
+      int t0 = get(2 * bit), t1 = get(2 * bit + 1);
+      val |= (t0 < t1) << bit;
+    }
+    desc[i] = (uint8_t)val;
+  }
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+extern "C" {
+
+int orc_orb_params(int nfeatures, float scale_factor, int nlevels, float* scale, float* inv_scale,
+                   float* sigma2, float* inv_sigma2, int* feats_per_level, int* umax16) {
+  Params p = make_params(nfeatures, scale_factor, nlevels, 20, 7);
+  for (int i = 0; i < nlevels; i++) {
+    if (scale) scale[i] = p.scale[i];
+    if (inv_scale) inv_scale[i] = p.invScale[i];
+    if (sigma2) sigma2[i] = p.sigma2[i];
+    if (inv_sigma2) inv_sigma2[i] = p.invSigma2[i];
+    if (feats_per_level) feats_per_level[i] = p.nfeat[i];
+  }
+  if (umax16)
+    for (int i = 0; i <= HALF_PATCH_SIZE; i++) umax16[i] = p.umax[i];
+  return 0;
+}
+
+int orc_orb_level_sizes(int w, int h, float scale_factor, int nlevels, int* sizes) {
+  Params p = make_params(1000, scale_factor, nlevels, 20, 7);
+  std::vector<int> lw, lh;
+  level_sizes(w, h, p, lw, lh);
+  for (int l = 0; l < nlevels; l++) {
+    sizes[2 * l] = lw[l];
+    sizes[2 * l + 1] = lh[l];
+  }
+  return 0;
+}
+
+int orc_orb_pyramid(const uint8_t* img, int w, int h, float scale_factor, int nlevels, uint8_t* out) {
+  Params p = make_params(1000, scale_factor, nlevels, 20, 7);
+  std::vector<std::vector<uint8_t>> L;
+  std::vector<int> lw, lh;
+  pyramid(img, w, h, p, L, lw, lh);
+  for (int l = 0; l < nlevels; l++) {
+    std::memcpy(out, L[l].data(), L[l].size());
+    out += L[l].size();
+  }
+  return 0;
+}
+
+int orc_orb_level_candidates(const uint8_t* level, int w, int h, int iniTh, int minTh,
+                             orc_keypoint* out, int cap, int* n_out) {
+  std::vector<orc_keypoint> c;
+  level_candidates(level, w, h, iniTh, minTh, c);
+  *n_out = (int)c.size();
+  if ((int)c.size() > cap) return -1;
+  std::copy(c.begin(), c.end(), out);
+  return 0;
+}
+
+int orc_gaussian_blur7(const uint8_t* src, int w, int h, uint8_t* dst) {
+  gaussian_blur7(src, w, h, dst);
+  return 0;
+}
+
+float orc_fast_atan2(float y, float x) { return fast_atan2(y, x); }
+
+// ORBextractor::operator(), ORBextractor.cc:1043-1105 (+ ComputeKeyPointsOctTree :765-853)
+int orc_orb_extract(const uint8_t* img, int w, int h, int nfeatures, float scale_factor, int nlevels,
+                    int iniTh, int minTh, orc_keypoint* kps, uint8_t* desc, int cap, int* n_out) {
+  *n_out = 0;
+  if (!img || w <= 0 || h <= 0) return 0;  // _image.empty() -> return
+  Params p = make_params(nfeatures, scale_factor, nlevels, iniTh, minTh);
+  std::vector<std::vector<uint8_t>> L;
+  std::vector<int> lw, lh;
+  pyramid(img, w, h, p, L, lw, lh);
+  std::vector<std::vector<orc_keypoint>> all(nlevels);
+  for (int level = 0; level < nlevels; level++) {
+    const int minBorderX = EDGE_THRESHOLD - 3, minBorderY = minBorderX;
+    const int maxBorderX = lw[level] - EDGE_THRESHOLD + 3, maxBorderY = lh[level] - EDGE_THRESHOLD + 3;
+    std::vector<orc_keypoint> cand;
+    level_candidates(L[level].data(), lw[level], lh[level], p.iniTh, p.minTh, cand);
+    std::vector<int> sel = distribute_octtree(cand, minBorderX, maxBorderX, minBorderY, maxBorderY,
+                                              p.nfeat[level]);
+    const int scaledPatchSize = (int)(PATCH_SIZE * p.scale[level]);
+    for (int idx : sel) {
+      orc_keypoint kp = cand[idx];
+      kp.x += minBorderX;
+      kp.y += minBorderY;
+      kp.octave = level;
+      kp.size = (float)scaledPatchSize;
+      all[level].push_back(kp);
+    }
+  }
+  for (int level = 0; level < nlevels; level++)
+    for (auto& kp : all[level]) kp.angle = ic_angle(L[level].data(), lw[level], kp.x, kp.y, p.umax);
+  int total = 0;
+  for (int level = 0; level < nlevels; level++) total += (int)all[level].size();
+  *n_out = total;
+  if (total > cap) return -1;
+  int offset = 0;
+  std::vector<uint8_t> blurred;
+  for (int level = 0; level < nlevels; level++) {
+    auto& K = all[level];
+    if (K.empty()) continue;
+    blurred.resize(L[level].size());
+    gaussian_blur7(L[level].data(), lw[level], lh[level], blurred.data());
+    for (size_t i = 0; i < K.size(); i++)
+      orb_descriptor(K[i], blurred.data(), lw[level], desc + 32 * (size_t)(offset + i));
+    if (level != 0) {
+      float scale = p.scale[level];
+      for (auto& kp : K) {
+        kp.x *= scale;
+        kp.y *= scale;
+      }
+    }
+    std::copy(K.begin(), K.end(), kps + offset);
+    offset += (int)K.size();
+  }
+  return 0;
+}
+
+}  // extern "C"

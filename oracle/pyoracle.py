@@ -1,0 +1,212 @@
+"""ctypes binding of the CPU restatement (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker -- never by the product.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+KP_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                     ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+NP_DTYPE = np.dtype([("verdict", "<i4"), ("m", "<i4"), ("n", "<i4"), ("w", "<f4", 3), ("r1", "<f4"),
+                     ("r2", "<f4"), ("cnt_gt", "<f4", 3), ("cnt_lt", "<f4", 3), ("cnt_eq", "<f4", 3)])
+
+
+class Cam(ctypes.Structure):
+    _fields_ = [("img_w", ctypes.c_int), ("img_h", ctypes.c_int), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.orc_fast_atan2.restype = ctypes.c_float
+        for f in ("orc_bbox_iou", "orc_bbox_former", "orc_bbox_latter"):
+            getattr(_lib, f).restype = ctypes.c_float
+        _lib.orc_replay_create.restype = ctypes.c_void_p
+        _lib.orc_replay_destroy.argtypes = [ctypes.c_void_p]
+        for f in ("orc_replay_frame", "orc_replay_local_mapping", "orc_replay_num_objects",
+                  "orc_replay_object", "orc_replay_object_points"):
+            getattr(_lib, f).argtypes = None
+    return _lib
+
+
+def P(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def cam(w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
+    return Cam(w, h, *[float(k) for k in K])
+
+
+def orb_params(nfeatures=1000, scale=1.2, nlevels=8):
+    sc, inv, s2, is2 = [np.zeros(nlevels, np.float32) for _ in range(4)]
+    q = np.zeros(nlevels, np.int32)
+    umax = np.zeros(16, np.int32)
+    lib().orc_orb_params(nfeatures, ctypes.c_float(scale), nlevels, P(sc), P(inv), P(s2), P(is2), P(q), P(umax))
+    return dict(scale=sc, inv_scale=inv, sigma2=s2, inv_sigma2=is2, quotas=q, umax=umax)
+
+
+def level_sizes(w, h, scale=1.2, nlevels=8):
+    s = np.zeros(2 * nlevels, np.int32)
+    lib().orc_orb_level_sizes(w, h, ctypes.c_float(scale), nlevels, P(s))
+    return [(int(s[2 * i]), int(s[2 * i + 1])) for i in range(nlevels)]
+
+
+def pyramid(img, scale=1.2, nlevels=8):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    sizes = level_sizes(w, h, scale, nlevels)
+    out = np.zeros(sum(a * b for a, b in sizes), np.uint8)
+    lib().orc_orb_pyramid(P(img), w, h, ctypes.c_float(scale), nlevels, P(out))
+    levels, o = [], 0
+    for lw, lh in sizes:
+        levels.append(out[o:o + lw * lh].reshape(lh, lw))
+        o += lw * lh
+    return levels
+
+
+def extract(img, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7):
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    cap = nfeatures + 64 * nlevels + 64
+    kps = np.zeros(cap, KP_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_int()
+    rc = lib().orc_orb_extract(P(img), w, h, nfeatures, ctypes.c_float(scale), nlevels, ini, mn, P(kps), P(desc),
+                               cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def blur7(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros_like(img)
+    lib().orc_gaussian_blur7(P(img), img.shape[1], img.shape[0], P(out))
+    return out
+
+
+def fast_atan2(y, x):
+    return lib().orc_fast_atan2(ctypes.c_float(y), ctypes.c_float(x))
+
+
+def hamming(a, b):
+    return lib().orc_descriptor_distance(P(np.ascontiguousarray(a, np.uint8)), P(np.ascontiguousarray(b, np.uint8)))
+
+
+def match_motion(c, Tcw, th, check_ori, last_kps, has_mp, mp_pos, mp_desc, cur_kps, cur_desc, scales):
+    out = np.full(len(cur_kps), -1, np.int32)
+    n = lib().orc_search_by_projection_motion(
+        ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), ctypes.c_float(th), int(check_ori),
+        len(last_kps), P(last_kps), P(np.ascontiguousarray(has_mp, np.uint8)),
+        P(np.ascontiguousarray(mp_pos, np.float32)), P(np.ascontiguousarray(mp_desc, np.uint8)), len(cur_kps),
+        P(cur_kps), P(np.ascontiguousarray(cur_desc, np.uint8)), len(scales),
+        P(np.ascontiguousarray(scales, np.float32)), P(out))
+    return n, out
+
+
+def frustum(c, Tcw, pos, normal, mind, maxd, vclim, logsf):
+    n = len(pos)
+    inv = np.zeros(n, np.uint8)
+    proj = np.zeros((n, 2), np.float32)
+    lvl = np.zeros(n, np.int32)
+    vc = np.zeros(n, np.float32)
+    cnt = lib().orc_is_in_frustum(ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), n,
+                                  P(np.ascontiguousarray(pos, np.float32)),
+                                  P(np.ascontiguousarray(normal, np.float32)),
+                                  P(np.ascontiguousarray(mind, np.float32)),
+                                  P(np.ascontiguousarray(maxd, np.float32)), ctypes.c_float(vclim),
+                                  ctypes.c_float(logsf), P(inv), P(proj), P(lvl), P(vc))
+    return cnt, inv, proj, lvl, vc
+
+
+def match_local(c, th, nnratio, inv, proj, lvl, vc, mp_desc, cur_kps, cur_desc, pre, scales):
+    out = np.full(len(cur_kps), -1, np.int32)
+    n = lib().orc_search_by_projection_local(
+        ctypes.byref(c), ctypes.c_float(th), ctypes.c_float(nnratio), len(inv), P(inv), P(proj), P(lvl), P(vc),
+        P(np.ascontiguousarray(mp_desc, np.uint8)), len(cur_kps), P(cur_kps),
+        P(np.ascontiguousarray(cur_desc, np.uint8)), P(pre) if pre is not None else None, len(scales),
+        P(np.ascontiguousarray(scales, np.float32)), P(out))
+    return n, out
+
+
+def match_init(c, nnratio, check_ori, kps1, desc1, kps2, desc2, prev_xy, window):
+    m12 = np.full(len(kps1), -1, np.int32)
+    prev = np.ascontiguousarray(prev_xy, np.float32).copy()
+    n = lib().orc_search_for_initialization(ctypes.byref(c), ctypes.c_float(nnratio), int(check_ori), len(kps1),
+                                            P(kps1), P(np.ascontiguousarray(desc1, np.uint8)), len(kps2), P(kps2),
+                                            P(np.ascontiguousarray(desc2, np.uint8)), P(prev), window, P(m12))
+    return n, m12, prev
+
+
+def np_test(fpts, fvalid, opts, ovalid):
+    fpts = np.ascontiguousarray(fpts, np.float32)
+    opts = np.ascontiguousarray(opts, np.float32)
+    out = np.zeros(1, NP_DTYPE)
+    lib().orc_np_test(len(fpts), P(fpts), P(None if fvalid is None else np.ascontiguousarray(fvalid, np.uint8)),
+                      len(opts), P(opts), P(None if ovalid is None else np.ascontiguousarray(ovalid, np.uint8)),
+                      P(out))
+    return out[0]
+
+
+def iforest(pts, trees=50, seed=12345, sample=None):
+    pts = np.ascontiguousarray(pts, np.float32)
+    n = len(pts)
+    sample = n // 2 if sample is None else sample
+    s = np.zeros(n, np.float64)
+    rc = lib().orc_iforest_scores(P(pts), n, trees, seed, sample, P(s))
+    assert rc == 0
+    return s
+
+
+def mt_stream(seed, n):
+    o = np.zeros(n, np.uint32)
+    lib().orc_mt19937_stream(ctypes.c_uint32(seed), n, P(o))
+    return o
+
+
+def lemire(seed, n, rng):
+    o = np.zeros(n, np.uint32)
+    lib().orc_lemire_u32(ctypes.c_uint32(seed), n, ctypes.c_uint32(rng), P(o))
+    return o
+
+
+def shuffle(seed, n):
+    o = np.zeros(n, np.uint32)
+    lib().orc_shuffle_ids(ctypes.c_uint32(seed), n, P(o))
+    return o
+
+
+def canonical(seed, n, lo, hi):
+    o = np.zeros(n, np.float32)
+    lib().orc_canonical_float(ctypes.c_uint32(seed), n, ctypes.c_float(lo), ctypes.c_float(hi), P(o))
+    return o
+
+
+def bbox(fn, a, b):
+    a = np.asarray(a, np.int32)
+    b = np.asarray(b, np.int32)
+    return getattr(lib(), "orc_bbox_" + fn)(P(a), P(b))
+
+
+def project_rect(c, Tcw, pts):
+    pts = np.ascontiguousarray(pts, np.float32)
+    r = np.zeros(4, np.int32)
+    rc = lib().orc_project_rect(ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), len(pts), P(pts), P(r))
+    return r if rc == 0 else None

@@ -1,0 +1,75 @@
+"""GPU association kernels vs the CPU restatement.
+
+NoParaDataAssociation (src/Object.cc:714-930): counts bit-exact, W/r within
+1e-5 (north-star tolerance), verdicts identical. Isolation forest
+(include/isolation_forest.h): scores within 1e-5. ComputeProjectRectFrame
+(src/Object.cc:1558-1603): rects identical.
+"""
+import numpy as np
+import pytest
+
+import eao_accel as ea
+import pyoracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _cloud(rng, n, center, spread, quant=None):
+    p = rng.normal(center, spread, (n, 3)).astype(np.float32)
+    if quant:
+        p = (np.round(p / quant) * quant).astype(np.float32)
+    return p
+
+
+def test_np_pairs():
+    rng = np.random.default_rng(21)
+    fs, os_, exp = [], [], []
+    for k in range(40):
+        m = int(rng.integers(5, 300))
+        n = int(rng.integers(5, 2500))
+        same = rng.random() < 0.5
+        f = _cloud(rng, m, [1, 2, 3], 0.1, quant=0.01 if k % 3 == 0 else None)
+        o = _cloud(rng, n, [1, 2, 3] if same else [1.05, 2, 3.1], 0.1, quant=0.01 if k % 3 == 0 else None)
+        fv = (rng.random(m) > 0.05).astype(np.uint8)
+        ov = (rng.random(n) > 0.05).astype(np.uint8)
+        fs.append((f, fv))
+        os_.append((o, ov))
+        exp.append(orc.np_test(f, fv, o, ov))
+    a = ea.Assoc()
+    got = a.np_batch(fs, os_)
+    for g, o in zip(got, exp):
+        assert g["verdict"] == o["verdict"]
+        if o["verdict"] == 0:
+            continue
+        assert g["m"] == o["m"] and g["n"] == o["n"]
+        if o["verdict"] in (1, 2) and o["n"] >= 20:
+            assert np.array_equal(g["cnt_gt"], o["cnt_gt"]) and np.array_equal(g["cnt_lt"], o["cnt_lt"])
+            assert np.array_equal(g["cnt_eq"], o["cnt_eq"])
+            assert np.allclose(g["w"], o["w"], rtol=1e-5, atol=1e-5)
+            assert np.allclose([g["r1"], g["r2"]], [o["r1"], o["r2"]], rtol=1e-5, atol=1e-5)
+
+
+def test_iforest_scores():
+    rng = np.random.default_rng(31)
+    clouds = []
+    for n in (30, 31, 64, 200, 777, 2000):
+        c = _cloud(rng, n, [0, 0, 2], 0.05)
+        c[: max(1, n // 20)] += rng.uniform(-0.5, 0.5, (max(1, n // 20), 3)).astype(np.float32)
+        clouds.append(c)
+    a = ea.Assoc()
+    got = a.iforest(clouds)
+    for c, g in zip(clouds, got):
+        o = orc.iforest(c)
+        assert np.allclose(g, o, rtol=1e-5, atol=1e-9)
+        assert np.array_equal(g > 0.6, o > 0.6)
+
+
+def test_project_rects(frames):
+    _, poses = frames
+    rng = np.random.default_rng(41)
+    clouds = [_cloud(rng, int(rng.integers(1, 500)), [0.2 * k - 0.5, 0.1, 2.0], 0.15) for k in range(12)]
+    a = ea.Assoc()
+    got, ok = a.rects(ea.camera(), poses[1], clouds)
+    for c, g in zip(clouds, got):
+        assert np.array_equal(g, orc.project_rect(orc.cam(), poses[1], c))
+    assert ok.all()
