@@ -45,4 +45,6 @@ class AssocEngine {
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
 };
 
+AssocEngine* assoc_engine(eao_assoc* a);
+
 }  // namespace eao

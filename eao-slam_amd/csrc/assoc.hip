@@ -594,6 +594,10 @@ struct eao_assoc {
   AssocEngine e;
 };
 
+namespace eao {
+AssocEngine* assoc_engine(eao_assoc* a) { return &a->e; }
+}  // namespace eao
+
 extern "C" {
 
 int eao_assoc_create(int device, int max_points, eao_assoc** out) {

@@ -1,0 +1,1455 @@
+// replay.cpp -- the EAO association pass on the engine (host orchestration).
+//
+// Mirrors the object section of Tracking::TrackWithMotionModel
+// (reference src/Tracking.cc:1241-1696), Object_2D::ObjectDataAssociation /
+// Object_Map::DataAssociateUpdate (src/Object.cc:162-710, 1313-1554) and the
+// LocalMapping object maintenance (src/LocalMapping.cc:772-882) as a
+// deterministic single-threaded replay.
+//
+// Work split (DESIGN.md "Association"):
+//   GPU  NoParaDataAssociation rank statistics for every (detection, object)
+//        pair of a frame in ONE launch (k_np_pairs), re-issued only for a
+//        class whose objects an earlier detection of the frame changed;
+//        isolation forests of every object updated in the frame in ONE launch
+//        (k_iforest_build/score), deferred until the object's points are next
+//        read (exact: only same-class detections or end-of-frame read them);
+//        projected rects of all recent objects in ONE launch (k_rects).
+//   host the sequential decision logic (first-wins order is part of the
+//        semantics), O(n) bookkeeping, and the duplicate-point test as an
+//        O(m+n) exact-bit-pattern hash instead of the reference's O(m*n) scan.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/eao_accel.h"
+#include "assoc.h"
+#include "common.h"
+
+namespace eao {
+
+static const float kTTable[122][9] = {
+#include "t_table.inc"
+};
+
+namespace {
+
+struct IRect {
+  int x = 0, y = 0, w = 0, h = 0;
+  IRect() {}
+  IRect(int a, int b, int c, int d) : x(a), y(b), w(c), h(d) {}
+  int area() const { return w * h; }
+  bool contains_f(float u, float v) const {  // Rect::contains(Point(cvRound(u), cvRound(v)))
+    const int px = (int)lrintf(u), py = (int)lrintf(v);
+    return x <= px && px < x + w && y <= py && py < y + h;
+  }
+};
+inline IRect rect_trunc(float x, float y, float w, float h) { return IRect((int)x, (int)y, (int)w, (int)h); }
+inline IRect rect_and(const IRect& a, const IRect& b) {
+  const int x1 = std::max(a.x, b.x), y1 = std::max(a.y, b.y);
+  const int w = std::min(a.x + a.w, b.x + b.w) - x1, h = std::min(a.y + a.h, b.y + b.h) - y1;
+  return (w <= 0 || h <= 0) ? IRect() : IRect(x1, y1, w, h);
+}
+// Converter::bboxOverlapratio / Former / Latter, src/Converter.cc:194-212
+inline float ov_iou(const IRect& a, const IRect& b) {
+  const int o = rect_and(a, b).area();
+  return (float)o / ((float)(a.area() + b.area() - o));
+}
+inline float ov_former(const IRect& a, const IRect& b) { return (float)rect_and(a, b).area() / ((float)a.area()); }
+inline float ov_latter(const IRect& a, const IRect& b) { return (float)rect_and(a, b).area() / ((float)b.area()); }
+
+struct Pose {
+  float T[16];
+  float fx, fy, cx, cy;
+  int cols, rows;
+  // Rcw*P + tcw (OpenCV small-gemm rounding) then the Object.cc projection
+  void cam(const float* P, float* pc) const {
+    for (int r = 0; r < 3; r++) {
+      const float t = T[4 * r] * P[0] + T[4 * r + 1] * P[1] + T[4 * r + 2] * P[2];
+      pc[r] = (float)((double)t + (double)T[4 * r + 3]);
+    }
+  }
+  void proj(const float* P, float& u, float& v) const {
+    float pc[3];
+    cam(P, pc);
+    const float iz = (float)(1.0 / pc[2]);
+    u = fx * pc[0] * iz + cx;
+    v = fy * pc[1] * iz + cy;
+  }
+};
+
+struct MapPt {
+  int id = 0;
+  float pos[3] = {0, 0, 0};
+  bool bad = false;
+  float fu = 0, fv = 0;  // MapPoint::feature (current-frame keypoint)
+  std::map<int, int> votes;  // object_id_vector
+};
+
+struct Obj;
+struct Det {  // Object_2D
+  int cls = -1;
+  float score = 0;  // always 0
+  int bx = 0, by = 0, bw = 0, bh = 0;
+  IRect box, feat;
+  std::vector<MapPt*> pts;
+  float sum[3] = {0, 0, 0}, pos[3] = {0, 0, 0};
+  bool bad = false;
+  int mnId = -1, method = 0, index = -1;
+  Obj* alias = nullptr;  // _Pos shares mCenter3D's buffer (Object.cc:677, Tracking.cc:2563)
+  const float* P() const;
+};
+
+struct Obj {  // Object_Map
+  std::vector<Det*> frames;
+  IRect last, lastlast, proj;
+  int id = 0, cls = 0, conf = 0, last_add = 0, lastlast_add = 0;
+  std::vector<MapPt*> pts;
+  float sum[3] = {0, 0, 0}, center[3] = {0, 0, 0}, sd[3] = {0, 0, 0}, csd[3] = {0, 0, 0};
+  float csd_all = 0;
+  std::map<int, int> reobj, same;
+  bool bad = false;
+  // cuboid (Cuboid3D)
+  double corner[8][3], center_c[3] = {0, 0, 0};
+  float xmn = 0, xmx = 0, ymn = 0, ymx = 0, zmn = 0, zmx = 0, lenth = 0, width = 0, height = 0;
+  double q[4] = {1, 0, 0, 0}, t[3] = {0, 0, 0}, qn[4] = {1, 0, 0, 0}, tn[3] = {0, 0, 0};
+  float rotY = 0, rotP = 0, rotR = 0, rmax = 0;
+  int pending = 0;  // 0 none, 1 iForest, 2 iForest then ComputeMeanAndStandard
+};
+const float* Det::P() const { return alias ? alias->center : pos; }
+
+// Eigen 3.2 Quaternion(Matrix3d) + g2o SE3Quat::normalizeRotation
+void quat_from_R(const double R[3][3], double q[4]) {
+  double t = (R[0][0] + R[1][1]) + R[2][2];
+  if (t > 0) {
+    t = std::sqrt(t + 1.0);
+    q[0] = 0.5 * t;
+    t = 0.5 / t;
+    q[1] = (R[2][1] - R[1][2]) * t;
+    q[2] = (R[0][2] - R[2][0]) * t;
+    q[3] = (R[1][0] - R[0][1]) * t;
+  } else {
+    int i = 0;
+    if (R[1][1] > R[0][0]) i = 1;
+    if (R[2][2] > R[i][i]) i = 2;
+    const int j = (i + 1) % 3, k = (j + 1) % 3;
+    t = std::sqrt(R[i][i] - R[j][j] - R[k][k] + 1.0);
+    double c[3];
+    c[i] = 0.5 * t;
+    t = 0.5 / t;
+    q[0] = (R[k][j] - R[j][k]) * t;
+    c[j] = (R[j][i] + R[i][j]) * t;
+    c[k] = (R[k][i] + R[i][k]) * t;
+    q[1] = c[0];
+    q[2] = c[1];
+    q[3] = c[2];
+  }
+  if (q[0] < 0)
+    for (int a = 0; a < 4; a++) q[a] = -q[a];
+  const double nrm = std::sqrt(((q[1] * q[1] + q[3] * q[3]) + (q[2] * q[2] + q[0] * q[0])));
+  for (int a = 0; a < 4; a++) q[a] = q[a] / nrm;
+}
+void qrot(const double q[4], const double v[3], double o[3]) {
+  const double x = q[1], y = q[2], z = q[3], w = q[0];
+  double uv[3] = {y * v[2] - z * v[1], z * v[0] - x * v[2], x * v[1] - y * v[0]};
+  for (int a = 0; a < 3; a++) uv[a] += uv[a];
+  const double c2[3] = {y * uv[2] - z * uv[1], z * uv[0] - x * uv[2], x * uv[1] - y * uv[0]};
+  for (int a = 0; a < 3; a++) o[a] = v[a] + w * uv[a] + c2[a];
+}
+void se3_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
+  double r[3];
+  qrot(q, v, r);
+  for (int a = 0; a < 3; a++) o[a] = r[a] + t[a];
+}
+void se3_inv_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
+  const double qc[4] = {q[0], -q[1], -q[2], -q[3]};
+  const double mt[3] = {t[0] * -1., t[1] * -1., t[2] * -1.};
+  double ti[3];
+  qrot(qc, mt, ti);
+  se3_apply(qc, ti, v, o);
+}
+
+// exact-equality key for the duplicate test cv::countNonZero(a - b) == 0
+// (Object.cc:1464-1477): equal iff every coordinate difference is 0, i.e.
+// same value with -0 == +0; NaN/Inf never compare equal (Inf - Inf = NaN).
+struct PosKey {
+  uint32_t a, b, c;
+  bool operator==(const PosKey& o) const { return a == o.a && b == o.b && c == o.c; }
+};
+struct PosHash {
+  size_t operator()(const PosKey& k) const {
+    uint64_t h = k.a * 0x9E3779B97F4A7C15ull;
+    h ^= (k.b + 0x7F4A7C15ull) * 0xC2B2AE3D27D4EB4Full;
+    h ^= (k.c + 0x165667B1ull) * 0x27D4EB2F165667C5ull;
+    return (size_t)(h ^ (h >> 29));
+  }
+};
+bool pos_key(const float* p, PosKey& k) {
+  uint32_t u[3];
+  for (int i = 0; i < 3; i++) {
+    if (!std::isfinite(p[i])) return false;
+    const float v = p[i] == 0.0f ? 0.0f : p[i];
+    std::memcpy(&u[i], &v, 4);
+  }
+  k = PosKey{u[0], u[1], u[2]};
+  return true;
+}
+
+}  // namespace
+
+class ReplayEngine {
+ public:
+  AssocEngine* A = nullptr;
+  std::string flag;
+  Pose pz;
+  CamDev camdev;
+  bool biForest = true;  // Object.cc:31 (sticky)
+  std::vector<std::unique_ptr<Obj>> objs;
+  std::map<int, std::unique_ptr<MapPt>> mps;
+  std::vector<std::unique_ptr<Det>> dets;
+  bool ini = false;
+  long ini_frame = 0;
+  unsigned long cur = 0;
+  // GPU staging (pinned host + device)
+  std::vector<float> h_pts;
+  std::vector<uint8_t> h_valid;
+  std::vector<int> h_meta;
+  float* d_pts = nullptr;
+  uint8_t* d_valid = nullptr;
+  int* d_meta = nullptr;
+  eao_np_stats* d_np = nullptr;
+  double* d_scores = nullptr;
+  int* d_rect = nullptr;
+  uint8_t* d_ok = nullptr;
+  float* d_T = nullptr;
+  int cap_pts = 0, cap_pairs = 0;
+  // per frame NP results: (det index, object index) -> stats
+  std::map<std::pair<int, int>, eao_np_stats> np_cache;
+  std::vector<char> odirty;  // objects modified in this frame (NP cache invalid)
+
+  ~ReplayEngine() {
+    void* ps[] = {d_pts, d_valid, d_meta, d_np, d_scores, d_rect, d_ok, d_T};
+    for (void* p : ps)
+      if (p) (void)hipFree(p);
+  }
+
+  int reserve(int npts, int npairs) {
+    if (npts > cap_pts) {
+      const int c = std::max(npts, cap_pts * 2);
+      if (d_pts) (void)hipFree(d_pts);
+      if (d_valid) (void)hipFree(d_valid);
+      if (d_scores) (void)hipFree(d_scores);
+      EAO_HIP_CHECK(hipMalloc(&d_pts, sizeof(float) * 3 * (size_t)c));
+      EAO_HIP_CHECK(hipMalloc(&d_valid, (size_t)c));
+      EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)c));
+      cap_pts = c;
+    }
+    if (npairs > cap_pairs) {
+      const int c = std::max(npairs, std::max(64, cap_pairs * 2));
+      if (d_meta) (void)hipFree(d_meta);
+      if (d_np) (void)hipFree(d_np);
+      if (d_rect) (void)hipFree(d_rect);
+      if (d_ok) (void)hipFree(d_ok);
+      EAO_HIP_CHECK(hipMalloc(&d_meta, sizeof(int) * 8 * (size_t)c));
+      EAO_HIP_CHECK(hipMalloc(&d_np, sizeof(eao_np_stats) * (size_t)c));
+      EAO_HIP_CHECK(hipMalloc(&d_rect, sizeof(int) * 4 * (size_t)c));
+      EAO_HIP_CHECK(hipMalloc(&d_ok, (size_t)c));
+      cap_pairs = c;
+    }
+    if (!d_T) EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16));
+    return EAO_OK;
+  }
+
+  // ---------------------------------------------------------------- cuboid / stats
+  void update_pose(Obj* o) {  // Object_Map::UpdateObjPose, Object.cc:2193-2248
+    const float cp = std::cos(o->rotP), sp = std::sin(o->rotP), sr = std::sin(o->rotR),
+                cr = std::cos(o->rotR), sy = std::sin(o->rotY), cy = std::cos(o->rotY);
+    const float Rf[3][3] = {{cp * cy, (sr * sp * cy) - (cr * sy), (cr * sp * cy) + (sr * sy)},
+                            {cp * sy, (sr * sp * sy) + (cr * cy), (cr * sp * sy) - (sr * cy)},
+                            {-sp, sr * cp, cr * cp}};
+    double R[3][3];
+    for (int a = 0; a < 3; a++)
+      for (int b = 0; b < 3; b++) R[a][b] = (double)Rf[a][b];
+    quat_from_R(R, o->q);
+    for (int a = 0; a < 3; a++) o->t[a] = (double)(float)o->center_c[a];
+    const double I[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    quat_from_R(I, o->qn);
+    o->tn[0] = (double)o->center[0];
+    o->tn[1] = (double)(float)o->center_c[1];
+    o->tn[2] = (double)o->center[2];
+  }
+
+  // Object_Map::ComputeMeanAndStandard, Object.cc:967-1198 (min/max replace the sorts)
+  void mean_std(Obj* o) {
+    for (int a = 0; a < 3; a++) o->sum[a] = 0;
+    size_t w = 0;
+    for (size_t i = 0; i < o->pts.size(); i++) {
+      MapPt* p = o->pts[i];
+      if (p->bad) continue;
+      for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
+      o->pts[w++] = p;
+    }
+    o->pts.resize(w);
+    const size_t n = o->pts.size();
+    const float sc = (float)(1. / (double)n);
+    for (int a = 0; a < 3; a++) o->center[a] = o->sum[a] * sc + 0.0f;
+    float s2[3] = {0, 0, 0};
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (MapPt* p : o->pts)
+      for (int a = 0; a < 3; a++) {
+        s2[a] += (p->pos[a] - o->center[a]) * (p->pos[a] - o->center[a]);
+        mn[a] = std::min(mn[a], p->pos[a]);
+        mx[a] = std::max(mx[a], p->pos[a]);
+      }
+    for (int a = 0; a < 3; a++) o->sd[a] = std::sqrt(s2[a] / (float)n);
+    if (n == 0) return;
+    float c2[3] = {0, 0, 0};
+    for (Det* f : o->frames) {
+      const float* fp = f->P();
+      for (int a = 0; a < 3; a++) c2[a] += (fp[a] - o->center[a]) * (fp[a] - o->center[a]);
+    }
+    for (int a = 0; a < 3; a++) o->csd[a] = std::sqrt(c2[a] / (float)o->frames.size());
+    static const int cx[8] = {0, 1, 1, 0, 0, 1, 1, 0}, cy[8] = {0, 0, 1, 1, 0, 0, 1, 1},
+                     cz[8] = {0, 0, 0, 0, 1, 1, 1, 1};
+    if (o->frames.size() < 5) {
+      o->center_c[0] = (mx[0] + mn[0]) / 2;
+      o->center_c[1] = (mx[1] + mn[1]) / 2;
+      o->center_c[2] = (mx[2] + mn[2]) / 2;
+      o->xmn = mn[0]; o->xmx = mx[0];
+      o->ymn = mn[1]; o->ymx = mx[1];
+      o->zmn = mn[2]; o->zmx = mx[2];
+      o->lenth = mx[0] - mn[0];
+      o->width = mx[1] - mn[1];
+      o->height = mx[2] - mn[2];
+    }
+    update_pose(o);
+    float omn[3] = {INFINITY, INFINITY, INFINITY}, omx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (MapPt* p : o->pts) {
+      const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
+      double r[3];
+      se3_inv_apply(o->q, o->t, v, r);
+      for (int a = 0; a < 3; a++) {
+        const float f = (float)r[a];
+        omn[a] = std::min(omn[a], f);
+        omx[a] = std::max(omx[a], f);
+      }
+    }
+    for (int k = 0; k < 8; k++) {
+      const double v[3] = {cx[k] ? omx[0] : omn[0], cy[k] ? omx[1] : omn[1], cz[k] ? omx[2] : omn[2]};
+      se3_apply(o->q, o->t, v, o->corner[k]);
+    }
+    o->lenth = omx[0] - omn[0];
+    o->width = omx[1] - omn[1];
+    o->height = omx[2] - omn[2];
+    for (int a = 0; a < 3; a++) o->center_c[a] = (o->corner[1][a] + o->corner[7][a]) / 2;
+    update_pose(o);
+    float rm = 0.0f;
+    for (int k = 0; k < 8; k++) {
+      float d[3];
+      for (int a = 0; a < 3; a++) d[a] = o->center[a] - (float)o->corner[k][a];
+      rm = std::max(rm, std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]));
+    }
+    o->rmax = rm;
+    float dis = 0;
+    for (Det* f : o->frames) {
+      const float* fp = f->P();
+      float e[3];
+      for (int a = 0; a < 3; a++) e[a] = (fp[a] - o->center[a]) * (fp[a] - o->center[a]);
+      dis += std::sqrt(e[0] + e[1] + e[2]);
+    }
+    o->csd_all = std::sqrt(dis / (float)o->frames.size());
+  }
+
+  bool iforest_applies(const Obj* o) const {
+    return biForest && !(o->cls == 75 || o->cls == 64 || o->cls == 65) && o->pts.size() >= 30;
+  }
+
+  // run the pending isolation forests (Object.cc:1202-1309) of the selected
+  // objects in one batched launch; erase outliers in list order (Q8).
+  int flush(int cls) {
+    std::vector<Obj*> todo;
+    for (auto& up : objs)
+      if (up->pending && (cls < 0 || up->cls == cls)) todo.push_back(up.get());
+    return flush_list(todo);
+  }
+  // an object's points are about to be read: run its deferred forest first
+  int touch(Obj* o) { return o->pending ? flush_list({o}) : EAO_OK; }
+
+  int flush_list(const std::vector<Obj*>& todo) {
+    size_t i = 0;
+    while (i < todo.size()) {
+      std::vector<Obj*> batch;
+      int np = 0;
+      for (; i < todo.size() && batch.size() < 16; i++) {
+        Obj* o = todo[i];
+        if (!o->pending) continue;
+        if (iforest_applies(o)) {
+          if ((int)o->pts.size() > IF_MAXN) {
+            set_error("replay: object exceeds the isolation-forest capacity");
+            return EAO_E_CAPACITY;
+          }
+          batch.push_back(o);
+          np += (int)o->pts.size();
+        } else if (o->pending == 2) {
+          mean_std(o);
+          o->pending = 0;
+        } else {
+          o->pending = 0;
+        }
+      }
+      if (batch.empty()) continue;
+      int rc = reserve(np, (int)batch.size());
+      if (rc) return rc;
+      h_pts.resize(3 * (size_t)np);
+      h_meta.assign(3 * batch.size(), 0);
+      int off = 0;
+      for (size_t b = 0; b < batch.size(); b++) {
+        Obj* o = batch[b];
+        h_meta[b] = off;
+        h_meta[batch.size() + b] = (int)o->pts.size();
+        h_meta[2 * batch.size() + b] = (int)((int)o->pts.size() / 2);
+        for (MapPt* p : o->pts)
+          std::memcpy(&h_pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
+      }
+      const int nb = (int)batch.size();
+      EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * np, hipMemcpyHostToDevice, A->stream));
+      EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 3 * nb, hipMemcpyHostToDevice, A->stream));
+      rc = A->iforest_batch(nb, d_pts, d_meta, d_meta + nb, 50, 12345, (const uint32_t*)(d_meta + 2 * nb),
+                            d_scores, A->stream);
+      if (rc) return rc;
+      std::vector<double> sc(np);
+      EAO_HIP_CHECK(hipMemcpyAsync(sc.data(), d_scores, sizeof(double) * np, hipMemcpyDeviceToHost, A->stream));
+      EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+      for (size_t b = 0; b < batch.size(); b++) {
+        Obj* o = batch[b];
+        const float th = o->cls == 62 ? 0.65f : 0.6f;
+        const double* s = sc.data() + h_meta[b];
+        size_t w = 0;
+        const size_t n = o->pts.size();
+        for (size_t k = 0; k < n; k++) {
+          if (s[k] > th) {
+            for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
+          } else {
+            o->pts[w++] = o->pts[k];
+          }
+        }
+        o->pts.resize(w);
+        if (o->pending == 2) mean_std(o);
+        o->pending = 0;
+      }
+    }
+    return EAO_OK;
+  }
+
+  void project_rect_host(Obj* o) {  // Object_Map::ComputeProjectRectFrame (one-off)
+    if (touch(o)) return;
+    if (o->pts.empty()) return;
+    float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+    for (MapPt* p : o->pts) {
+      float u, v;
+      pz.proj(p->pos, u, v);
+      xmn = std::min(xmn, u);
+      xmx = std::max(xmx, u);
+      ymn = std::min(ymn, v);
+      ymx = std::max(ymx, v);
+    }
+    if (xmn < 0) xmn = 0;
+    if (ymn < 0) ymn = 0;
+    if (xmx > pz.cols) xmx = (float)pz.cols;
+    if (ymx > pz.rows) ymx = (float)pz.rows;
+    o->proj = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
+  }
+
+  // step 10.1 for all recent objects: one k_rects launch
+  int project_rects_gpu(const std::vector<Obj*>& list) {
+    if (list.empty()) return EAO_OK;
+    int np = 0;
+    for (Obj* o : list) np += (int)o->pts.size();
+    int rc = reserve(std::max(np, 1), (int)list.size());
+    if (rc) return rc;
+    h_pts.resize(3 * (size_t)std::max(np, 1));
+    h_meta.assign(2 * list.size(), 0);
+    int off = 0;
+    for (size_t b = 0; b < list.size(); b++) {
+      h_meta[b] = off;
+      h_meta[list.size() + b] = (int)list[b]->pts.size();
+      for (MapPt* p : list[b]->pts)
+        std::memcpy(&h_pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
+    }
+    const int nb = (int)list.size();
+    EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * std::max(np, 1), hipMemcpyHostToDevice, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 2 * nb, hipMemcpyHostToDevice, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(d_T, pz.T, sizeof(float) * 16, hipMemcpyHostToDevice, A->stream));
+    rc = A->rects(camdev, d_T, nb, d_pts, d_meta, d_meta + nb, d_rect, d_ok, A->stream);
+    if (rc) return rc;
+    std::vector<int> r(4 * nb);
+    std::vector<uint8_t> ok(nb);
+    EAO_HIP_CHECK(hipMemcpyAsync(r.data(), d_rect, sizeof(int) * 4 * nb, hipMemcpyDeviceToHost, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(ok.data(), d_ok, nb, hipMemcpyDeviceToHost, A->stream));
+    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    for (int b = 0; b < nb; b++)
+      if (ok[b]) list[b]->proj = IRect(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
+    return EAO_OK;
+  }
+
+  // NoParaDataAssociation statistics for the given (det, obj) pairs, one launch
+  int np_pairs(const std::vector<std::pair<Det*, Obj*>>& pairs, const std::vector<int>& di,
+               const std::vector<int>& oi) {
+    if (pairs.empty()) return EAO_OK;
+    // distinct detections / objects are uploaded once
+    std::map<Det*, int> doff;
+    std::map<Obj*, int> ooff;
+    int np = 0;
+    h_pts.clear();
+    h_valid.clear();
+    for (auto& pr : pairs) {
+      if (!doff.count(pr.first)) {
+        doff[pr.first] = np;
+        for (MapPt* p : pr.first->pts) {
+          h_pts.insert(h_pts.end(), p->pos, p->pos + 3);
+          h_valid.push_back(p->bad ? 0 : 1);  // out_point is never set (Q7)
+        }
+        np += (int)pr.first->pts.size();
+      }
+      if (!ooff.count(pr.second)) {
+        ooff[pr.second] = np;
+        for (MapPt* p : pr.second->pts) {
+          h_pts.insert(h_pts.end(), p->pos, p->pos + 3);
+          h_valid.push_back(p->bad ? 0 : 1);
+        }
+        np += (int)pr.second->pts.size();
+      }
+    }
+    const int npairs = (int)pairs.size();
+    int rc = reserve(std::max(np, 1), npairs);
+    if (rc) return rc;
+    h_meta.assign(4 * (size_t)npairs, 0);
+    for (int k = 0; k < npairs; k++) {
+      h_meta[k] = doff[pairs[k].first];
+      h_meta[npairs + k] = (int)pairs[k].first->pts.size();
+      h_meta[2 * npairs + k] = ooff[pairs[k].second];
+      h_meta[3 * npairs + k] = (int)pairs[k].second->pts.size();
+      if (h_meta[3 * npairs + k] > NP_MAXN) {
+        set_error("replay: object exceeds the NP kernel capacity");
+        return EAO_E_CAPACITY;
+      }
+    }
+    EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * np, hipMemcpyHostToDevice, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(d_valid, h_valid.data(), np, hipMemcpyHostToDevice, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 4 * npairs, hipMemcpyHostToDevice, A->stream));
+    rc = A->np_batch(npairs, d_pts, d_valid, d_meta, d_meta + npairs, d_pts, d_valid, d_meta + 2 * npairs,
+                     d_meta + 3 * npairs, d_np, A->stream);
+    if (rc) return rc;
+    std::vector<eao_np_stats> out(npairs);
+    EAO_HIP_CHECK(hipMemcpyAsync(out.data(), d_np, sizeof(eao_np_stats) * npairs, hipMemcpyDeviceToHost, A->stream));
+    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    for (int k = 0; k < npairs; k++) np_cache[{di[k], oi[k]}] = out[k];
+    return EAO_OK;
+  }
+
+  int np_for_detection(Det* f) {
+    std::vector<std::pair<Det*, Obj*>> pairs;
+    std::vector<int> di, oi;
+    for (size_t i = 0; i < objs.size(); i++) {
+      Obj* o = objs[i].get();
+      if (o->cls != f->cls || o->bad) continue;
+      pairs.push_back({f, o});
+      di.push_back(f->index);
+      oi.push_back((int)i);
+    }
+    return np_pairs(pairs, di, oi);
+  }
+
+  static void vote(MapPt* p, int id) {
+    auto it = p->votes.find(id);
+    if (it != p->votes.end()) it->second += 1;
+    else p->votes[id] = 1;
+  }
+  static void reobj(Obj* o, int id) {
+    auto it = o->reobj.find(id);
+    if (it != o->reobj.end()) it->second += 1;
+    else o->reobj[id] = 1;
+  }
+
+  void mark_dirty(Obj* o) {
+    if ((size_t)o->id >= odirty.size()) odirty.resize(o->id + 1, 0);
+    odirty[o->id] = 1;
+  }
+  bool is_dirty(int i) const { return (size_t)i < odirty.size() && odirty[i]; }
+
+  // Object_Map::DataAssociateUpdate, Object.cc:1313-1554
+  bool update(Obj* o, Det* f, int Flag) {
+    if (f->cls != o->cls) return false;
+    if (touch(o)) return false;
+    if (Flag != 1 && Flag != 4) {
+      project_rect_host(o);
+      const IRect r1 = o->proj;
+      float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+      auto acc = [&](MapPt* p) {
+        float u, v;
+        pz.proj(p->pos, u, v);
+        xmn = std::min(xmn, u);
+        xmx = std::max(xmx, u);
+        ymn = std::min(ymn, v);
+        ymx = std::max(ymx, v);
+      };
+      for (MapPt* p : f->pts) acc(p);
+      for (MapPt* p : o->pts) acc(p);
+      if (xmn < 0) xmn = 0;
+      if (ymn < 0) ymn = 0;
+      if (xmx > pz.cols) xmx = (float)pz.cols;
+      if (ymx > pz.rows) ymx = (float)pz.rows;
+      const IRect r2 = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
+      if ((ov_iou(r1, r2) < 0.5) && (ov_former(r2, f->box) < 0.8)) return false;
+    }
+    if (o->last_add != (int)cur) {
+      o->lastlast_add = o->last_add;
+      o->last_add = (int)cur;
+      o->lastlast = o->last;
+      o->last = f->box;
+      o->conf++;
+      o->frames.push_back(f);
+    } else
+      return false;
+    mark_dirty(o);
+    f->mnId = o->id;
+    std::unordered_set<PosKey, PosHash> have;
+    have.reserve(o->pts.size() * 2 + f->pts.size());
+    for (MapPt* q : o->pts) {
+      PosKey k;
+      if (pos_key(q->pos, k)) have.insert(k);
+    }
+    for (MapPt* p : f->pts) {
+      float d[3];
+      for (int a = 0; a < 3; a++) d[a] = o->center[a] - p->pos[a];
+      const float fDis = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+      const float th = o->frames.size() > 5 ? 0.9f : 1.0f;
+      if (fDis > th * o->rmax) continue;
+      if (o->frames.size() >= 10 && (o->cls == 56 || o->cls == 77)) {
+        const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
+        double s[3];
+        se3_inv_apply(o->q, o->t, v, s);
+        if (std::fabs(s[0]) > 1.2 * o->lenth / 2 || std::fabs(s[1]) > 1.2 * o->width / 2 ||
+            std::fabs(s[2]) > 1.2 * o->height / 2)
+          continue;
+      }
+      vote(p, o->id);
+      PosKey k;
+      const bool finite = pos_key(p->pos, k);
+      if (!finite || !have.count(k)) {
+        o->pts.push_back(p);
+        for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
+        if (finite) have.insert(k);
+      }
+    }
+    if (f->bx > 25 && f->by > 25 && f->bx + f->bw < pz.cols - 25 && f->by + f->bh < pz.rows - 25) {
+      size_t w = 0;
+      const size_t n = o->pts.size();
+      for (size_t i = 0; i < n; i++) {
+        MapPt* p = o->pts[i];
+        int votes = 0;
+        auto it = p->votes.find(o->id);
+        if (it != p->votes.end()) votes = it->second;
+        bool erase = false;
+        if (votes <= 8) {
+          float u, v;
+          pz.proj(p->pos, u, v);
+          if ((u > 0 && u < pz.cols) && (v > 0 && v < pz.rows) && !f->box.contains_f(u, v)) erase = true;
+        }
+        if (erase) {
+          for (int a = 0; a < 3; a++) o->sum[a] -= p->pos[a];
+        } else {
+          o->pts[w++] = p;
+        }
+      }
+      o->pts.resize(w);
+    }
+    mean_std(o);
+    o->pending = std::max(o->pending, 1);  // isolation forest deferred (flush)
+    return true;
+  }
+
+  // Object_2D::ObjectDataAssociation, Object.cc:162-710
+  int associate(Det* f) {
+    if (flag == "None") biForest = false;
+    int rc = flush(f->cls);
+    if (rc) return rc;
+    const IRect RC = f->box;
+    float IouMax = 0;
+    bool byIou = false;
+    int iouId = -1, iouMax = -1;
+    float IouThreshold = 0.5;
+    if (flag != "NA" && flag != "NP") {
+      for (int i = 0; i < (int)objs.size(); i++) {
+        Obj* o = objs[i].get();
+        if (f->cls != o->cls || o->bad) continue;
+        if ((unsigned long)(long)o->last_add == cur - 1) {
+          IRect RP;
+          if ((unsigned long)(long)o->lastlast_add == cur - 2) {
+            float ltx = (float)(o->last.x * 2 - o->lastlast.x);
+            if (ltx < 0) ltx = 0;
+            float lty = (float)(o->last.y * 2 - o->lastlast.y);
+            if (lty < 0) lty = 0;
+            float rdx = (float)((o->last.x + o->last.w) * 2 - (o->lastlast.x + o->lastlast.w));
+            if (ltx > pz.cols) rdx = (float)pz.cols;
+            float rdy = (float)((o->last.y + o->last.h) * 2 - (o->lastlast.y + o->lastlast.h));
+            if (lty > pz.rows) rdy = (float)pz.rows;
+            RP = rect_trunc(ltx, lty, rdx - ltx, rdy - lty);
+            IouThreshold = 0.6f;
+          } else
+            RP = o->last;
+          const float I = ov_iou(RC, RP);
+          if ((I > IouThreshold) && I > IouMax) {
+            IouMax = I;
+            iouMax = i;
+          }
+        }
+      }
+      if (IouMax > 0 && iouMax >= 0 && update(objs[iouMax].get(), f, 1)) {
+        byIou = true;
+        iouId = iouMax;
+        f->method = 1;
+      }
+    }
+    bool byNp = false;
+    int npId = -1;
+    std::vector<int> vNP;
+    if (flag != "NA" && flag != "IoU") {
+      // m counts valid frame points (bad ones were dropped in ComputeMeanAndStandardFrame;
+      // out_point is never set, Q7). m < 20 breaks the loop at its first object (Q9).
+      const bool m_small = f->pts.size() < 20;
+      std::vector<int> need;
+      if (!m_small) {
+        for (int i = (int)objs.size() - 1; i >= 0; i--) {
+          Obj* o = objs[i].get();
+          if (f->cls != o->cls || o->bad) continue;
+          if (byIou && i == iouId) continue;  // its verdict is never used (Object.cc:283-284)
+          if (is_dirty(i) || !np_cache.count({f->index, i})) need.push_back(i);
+        }
+      }
+      if (!need.empty()) {
+        std::vector<Obj*> tl;
+        for (int i : need) tl.push_back(objs[i].get());
+        rc = flush_list(tl);
+        if (rc) return rc;
+        std::vector<std::pair<Det*, Obj*>> pairs;
+        std::vector<int> di;
+        for (int i : need) {
+          pairs.push_back({f, objs[i].get()});
+          di.push_back(f->index);
+        }
+        rc = np_pairs(pairs, di, need);
+        if (rc) return rc;
+      }
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {
+        Obj* o = objs[i].get();
+        if (f->cls != o->cls || o->bad) continue;
+        if (m_small) break;  // verdict 0
+        if (byIou && i == iouId) continue;
+        const int v = np_cache[{f->index, i}].verdict;
+        if (v < 0) {
+          set_error("replay: NP pair outside kernel capacity");
+          return EAO_E_CAPACITY;
+        }
+        if (v == 2) continue;
+        vNP.push_back(i);
+      }
+      if (!vNP.empty()) {
+        if (byIou) {
+          for (int k : vNP)
+            if (k != iouId) reobj(objs[iouId].get(), objs[k]->id);
+        } else {
+          for (size_t i = 0; i < vNP.size(); i++) {
+            if (update(objs[vNP[i]].get(), f, 2)) {
+              byNp = true;
+              npId = vNP[i];
+              f->method = 2;
+              if (vNP.size() > i + 1) {
+                for (size_t j = i + 1; j < vNP.size(); j++) reobj(objs[vNP[i]].get(), objs[vNP[j]]->id);
+                break;
+              }
+            }
+          }
+        }
+      }
+    }
+    bool byPro = false;
+    int proId = -1;
+    std::vector<int> vPro;
+    if (flag != "NA" && flag != "IoU" && flag != "NP") {
+      float fmax = 0.0f;
+      int pmax = -1;
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {
+        Obj* o = objs[i].get();
+        if (f->cls != o->cls || o->bad) continue;
+        if (f->pts.size() >= 10 && (int)o->frames.size() > 8) continue;
+        const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
+        if (a >= 0.25 && a > fmax) {
+          fmax = a;
+          pmax = i;
+          vPro.push_back(i);
+        }
+      }
+      if (fmax >= 0.25) {
+        std::sort(vPro.begin(), vPro.end());
+        if (byIou || byNp) {
+          for (int j = (int)vPro.size() - 1; j >= 0; j--) {
+            int re = -1;
+            if (byIou) re = iouId;
+            if (byNp) re = npId;
+            if (vPro[j] != re) reobj(objs[re].get(), objs[vPro[j]]->id);
+          }
+        } else {
+          if (update(objs[pmax].get(), f, 4)) {
+            byPro = true;
+            proId = pmax;
+            f->method = 4;
+          }
+          for (int j = (int)vPro.size() - 1; j >= 0; j--)
+            if (vPro[j] != pmax) reobj(objs[pmax].get(), objs[vPro[j]]->id);
+        }
+      }
+    }
+    bool byT = false;
+    std::vector<int> vT, vTL;
+    if (flag != "NA" && flag != "IoU" && flag != "NP") {
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {
+        Obj* o = objs[i].get();
+        if (f->cls != o->cls || o->bad) continue;
+        const int df = (int)o->frames.size();
+        if (df <= 8) continue;
+        const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
+        const float dx = std::fabs(o->center[0] - f->pos[0]), dy = std::fabs(o->center[1] - f->pos[1]),
+                    dz = std::fabs(o->center[2] - f->pos[2]);
+        const float tx = (float)(dx / (o->csd[0] / std::sqrt((double)df)));
+        const float ty = (float)(dy / (o->csd[1] / std::sqrt((double)df)));
+        const float tz = (float)(dz / (o->csd[2] / std::sqrt((double)df)));
+        const float* row = kTTable[std::min(df - 1, 121)];
+        if (tx < row[5] && ty < row[5] && tz < row[5]) {
+          vT.push_back(i);
+        } else if (a > 0.25) {
+          if (tx < row[8] && ty < row[8] && tz < row[8])
+            vT.push_back(i);
+          else if ((a > 0.25) && ((tx + ty + tz) / 3 < 10))
+            vT.push_back(i);
+          else
+            vTL.push_back(i);
+        } else if ((tx + ty + tz) / 3 < 4) {
+          project_rect_host(o);
+          if (std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj)) > 0.25) vTL.push_back(i);
+        }
+      }
+      if (byIou || byNp || byPro) {
+        int re = -1;
+        if (byIou) re = iouId;
+        if (byNp) re = npId;
+        if (byPro) re = proId;
+        for (int k : vT)
+          if (k != re) reobj(objs[re].get(), objs[k]->id);
+        for (int k : vTL)
+          if (k != re) reobj(objs[re].get(), objs[k]->id);
+      } else {
+        for (size_t i = 0; i < vT.size(); i++) {
+          if (update(objs[vT[i]].get(), f, 3)) {
+            byT = true;
+            const int tid = vT[i];
+            f->method = 3;
+            for (size_t j = i + 1; j < vT.size(); j++) reobj(objs[tid].get(), objs[vT[j]]->id);
+            for (int k : vTL)
+              if (k != tid) reobj(objs[tid].get(), objs[k]->id);
+            break;
+          }
+        }
+      }
+    }
+    if (byIou || byNp || byPro || byT) return EAO_OK;
+    if (f->bx < 10 || f->by < 10 || f->bx + f->bw > pz.cols - 10 || f->by + f->bh > pz.rows - 10) {
+      f->bad = true;
+      return EAO_OK;
+    }
+    std::unique_ptr<Obj> o(new Obj());
+    o->frames.push_back(f);
+    o->id = (int)objs.size();
+    o->cls = f->cls;
+    o->conf = 1;
+    o->last_add = o->lastlast_add = (int)cur;
+    o->last = f->box;
+    for (int a = 0; a < 3; a++) {
+      o->sum[a] = f->sum[a];
+      o->center[a] = f->pos[a];
+    }
+    for (MapPt* p : f->pts) {
+      p->votes.insert(std::make_pair(o->id, 1));
+      o->pts.push_back(p);
+    }
+    f->mnId = o->id;
+    f->method = 5;
+    f->alias = o.get();
+    o->pending = 2;  // IsolationForestDeleteOutliers then ComputeMeanAndStandard
+    Obj* op = o.get();
+    objs.push_back(std::move(o));
+    mark_dirty(op);
+    return EAO_OK;
+  }
+
+  void frame_mean(Det* f) {  // Object_2D::ComputeMeanAndStandardFrame, Object.cc:63-102
+    size_t w = 0;
+    for (size_t i = 0; i < f->pts.size(); i++) {
+      MapPt* p = f->pts[i];
+      if (p->bad) {
+        for (int a = 0; a < 3; a++) f->sum[a] -= p->pos[a];
+      } else
+        f->pts[w++] = p;
+    }
+    f->pts.resize(w);
+    const float sc = (float)(1. / (double)f->pts.size());
+    for (int a = 0; a < 3; a++) f->pos[a] = f->sum[a] * sc + 0.0f;
+  }
+
+  void boxplot(Det* f) {  // Object_2D::RemoveOutliersByBoxPlot, Object.cc:106-158
+    std::vector<float> zc(f->pts.size());
+    for (size_t i = 0; i < f->pts.size(); i++) {
+      float pc[3];
+      pz.cam(f->pts[i]->pos, pc);
+      zc[i] = pc[2];
+    }
+    std::vector<float> zs = zc;
+    std::sort(zs.begin(), zs.end());
+    if ((zs.size() / 4 <= 0) || (zs.size() * 3 / 4 >= zs.size() - 1)) return;
+    const float Q1 = zs[zs.size() / 4], Q3 = zs[zs.size() * 3 / 4];
+    const float IQR = Q3 - Q1;
+    const float max_th = (float)(Q3 + 1.5 * IQR);
+    size_t w = 0;
+    for (size_t i = 0; i < f->pts.size(); i++)
+      if (!(zc[i] > max_th)) f->pts[w++] = f->pts[i];
+    f->pts.resize(w);
+    frame_mean(f);
+  }
+
+  bool overlap(Obj* a, Obj* b) {  // Object_Map::WhetherOverlap, Object.cc:1906-1922
+    const float dx = (float)std::fabs(a->center_c[0] - b->center_c[0]);
+    const float dy = (float)std::fabs(a->center_c[1] - b->center_c[1]);
+    const float dz = (float)std::fabs(a->center_c[2] - b->center_c[2]);
+    return dx < a->lenth / 2 + b->lenth / 2 && dy < a->width / 2 + b->width / 2 &&
+           dz < a->height / 2 + b->height / 2;
+  }
+
+  int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
+            const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
+    cur = fid;
+    std::memcpy(pz.T, Tcw, sizeof(pz.T));
+    np_cache.clear();
+    std::vector<Det*> o2;
+    int maxcls = 0;
+    for (int k = 0; k < nb; k++) {
+      std::unique_ptr<Det> f(new Det());
+      f->cls = boxes[5 * k];
+      f->bx = boxes[5 * k + 1];
+      f->by = boxes[5 * k + 2];
+      f->bw = boxes[5 * k + 3];
+      f->bh = boxes[5 * k + 4];
+      f->box = IRect(f->bx, f->by, f->bw, f->bh);
+      f->index = k;
+      maxcls = std::max(maxcls, f->cls);
+      o2.push_back(f.get());
+      dets.push_back(std::move(f));
+    }
+    odirty.assign(objs.size(), 0);
+    std::vector<MapPt*> tr(npts);
+    for (int i = 0; i < npts; i++) {
+      auto it = mps.find(ids[i]);
+      MapPt* p;
+      if (it == mps.end()) {
+        p = new MapPt();
+        p->id = ids[i];
+        mps[ids[i]].reset(p);
+      } else
+        p = it->second.get();
+      for (int a = 0; a < 3; a++) p->pos[a] = pos[3 * i + a];
+      p->bad = bad ? bad[i] != 0 : false;
+      tr[i] = p;
+    }
+    // STEP 2 AssociateObjAndPoints, Tracking.cc:2434-2468
+    for (int i = 0; i < npts; i++) {
+      MapPt* p = tr[i];
+      if (p->bad) continue;
+      for (Det* f : o2)
+        if (f->box.contains_f(uv[2 * i], uv[2 * i + 1])) {
+          p->fu = uv[2 * i];
+          p->fv = uv[2 * i + 1];
+          f->pts.push_back(p);
+          for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
+        }
+    }
+    for (Det* f : o2) {  // STEP 4
+      frame_mean(f);
+      if (f->pts.size() >= 8) boxplot(f);
+    }
+    for (Det* f : o2) {  // STEP 5
+      const float sc = (float)(1. / (double)f->pts.size());
+      for (int a = 0; a < 3; a++) f->pos[a] = f->sum[a] * sc + 0.0f;
+      if (f->pts.size() < 4) continue;
+      float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+      for (MapPt* p : f->pts) {
+        xmn = std::min(xmn, p->fu);
+        xmx = std::max(xmx, p->fu);
+        ymn = std::min(ymn, p->fv);
+        ymx = std::max(ymx, p->fv);
+      }
+      if (xmn < 0) xmn = 0;
+      if (ymn < 0) ymn = 0;
+      if (xmx > pz.cols) xmx = (float)pz.cols;
+      if (ymx > pz.rows) ymx = (float)pz.rows;
+      f->feat = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
+    }
+    // STEP 6 filters, Tracking.cc:1383-1487
+    for (size_t a = 0; a < o2.size(); a++) {
+      int num = 0;
+      for (size_t b = 0; b < o2.size(); b++)
+        if (a != b && ov_latter(o2[a]->box, o2[b]->box) > 0.05) num++;
+      if (num > 4) o2[a]->bad = true;
+    }
+    for (size_t a = 0; a < o2.size(); a++) {
+      Det* f = o2[a];
+      if (f->bad) continue;
+      if (f->cls == 0 || f->cls == 63 || f->cls == 15) f->bad = true;
+      if ((float)f->box.area() / (float)(pz.cols * pz.rows) > 0.5) f->bad = true;
+      if (f->pts.size() < 5)
+        f->bad = true;
+      else if (f->pts.size() < 10 &&
+               (f->bx < 20 || f->by < 20 || f->bx + f->bw > pz.cols - 20 || f->by + f->bh > pz.rows - 20))
+        f->bad = true;
+      for (size_t b = 0; b < o2.size(); b++) {
+        Det* g = o2[b];
+        if (g->bad || a == b) continue;
+        if (ov_iou(f->box, g->box) > 0.3) {
+          if (f->score < g->score) f->bad = true;
+          else if (f->score >= g->score) g->bad = true;
+        }
+        if (ov_iou(f->box, g->box) > 0.05) {
+          if (ov_former(f->box, g->box) > 0.85) f->bad = true;
+          if (ov_latter(f->box, g->box) > 0.85) g->bad = true;
+        }
+      }
+    }
+    std::vector<Det*> kept;
+    for (Det* f : o2) {
+      if (!f->bad) kept.push_back(f);
+      else f->method = -1;
+    }
+    // STEP 9 InitObjMap, Tracking.cc:2531-2598
+    if (!ini) {
+      int good = -1;
+      for (Det* f : kept) {
+        if (f->pts.size() < 10) {
+          f->method = 6;
+          continue;
+        }
+        good++;
+        ini = true;
+        ini_frame = (long)fid;
+        std::unique_ptr<Obj> o(new Obj());
+        o->frames.push_back(f);
+        o->id = good;
+        o->cls = f->cls;
+        o->conf = 1;
+        o->last_add = o->lastlast_add = (int)fid;
+        o->last = f->box;
+        for (int a = 0; a < 3; a++) {
+          o->sum[a] = f->sum[a];
+          o->center[a] = f->pos[a];
+        }
+        for (MapPt* p : f->pts) {
+          p->votes.insert(std::make_pair(o->id, 1));
+          o->pts.push_back(p);
+        }
+        f->mnId = o->id;
+        f->method = 7;
+        f->alias = o.get();
+        mean_std(o.get());
+        objs.push_back(std::move(o));
+      }
+    }
+    // STEP 10
+    if ((long)fid > ini_frame && ini) {
+      std::vector<Obj*> recent;
+      for (auto& up : objs) {
+        Obj* o = up.get();
+        if (o->bad) continue;
+        if ((unsigned long)(long)o->last_add > fid - 30) recent.push_back(o);
+        else o->proj = IRect(0, 0, 0, 0);
+      }
+      int rc = project_rects_gpu(recent);
+      if (rc) return rc;
+      // NP statistics of every (kept detection, same-class object) pair: one launch
+      if (flag != "NA" && flag != "IoU") {
+        std::vector<std::pair<Det*, Obj*>> pairs;
+        std::vector<int> di, oi;
+        for (Det* f : kept) {
+          if (f->pts.size() < 5) continue;
+          for (size_t i = 0; i < objs.size(); i++) {
+            Obj* o = objs[i].get();
+            if (o->cls != f->cls || o->bad) continue;
+            pairs.push_back({f, o});
+            di.push_back(f->index);
+            oi.push_back((int)i);
+          }
+        }
+        for (size_t s = 0; s < pairs.size(); s += 4096) {
+          const size_t e = std::min(pairs.size(), s + 4096);
+          std::vector<std::pair<Det*, Obj*>> pp(pairs.begin() + s, pairs.begin() + e);
+          std::vector<int> dd(di.begin() + s, di.begin() + e), ooi(oi.begin() + s, oi.begin() + e);
+          rc = np_pairs(pp, dd, ooi);
+          if (rc) return rc;
+        }
+      }
+      for (Det* f : kept) {
+        if (f->pts.size() < 5) {
+          f->method = 6;
+          continue;
+        }
+        rc = associate(f);
+        if (rc) return rc;
+      }
+      rc = flush(-1);
+      if (rc) return rc;
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
+        if (flag == "NA") continue;
+        Obj* o = objs[i].get();
+        if (o->bad) continue;
+        const int df = (int)o->frames.size();
+        if (df < 10 && (unsigned long)(long)o->last_add < (fid - 30)) {
+          if (df < 5)
+            o->bad = true;
+          else {
+            bool ov = false;
+            for (int j = (int)objs.size() - 1; j >= 0; j--) {
+              if (objs[j]->bad || i == j) continue;
+              if (overlap(o, objs[j].get())) {
+                ov = true;
+                break;
+              }
+            }
+            if (ov) o->bad = true;
+          }
+        }
+      }
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.4
+        if ((unsigned long)(long)objs[i]->last_add != fid) continue;
+        for (int j = (int)objs.size() - 1; j >= 0; j--) {
+          if (i == j) continue;
+          if ((unsigned long)(long)objs[j]->last_add == fid) {
+            auto& m = objs[i]->same;
+            auto it = m.find(objs[j]->id);
+            if (it != m.end()) it->second += 1;
+            else m[objs[j]->id] = 1;
+          }
+        }
+      }
+    }
+    for (Det* f : o2) {
+      const int k = f->index;
+      out[4 * k] = f->method;
+      out[4 * k + 1] = f->mnId;
+      out[4 * k + 2] = f->cls;
+      out[4 * k + 3] = (int)f->pts.size();
+    }
+    return EAO_OK;
+  }
+
+  // ---- LocalMapping object maintenance, LocalMapping.cc:772-882
+  bool double_ttest(Obj* a, Obj* b) {  // Object.cc:1659-1712 (Q5)
+    const int n1 = (int)a->frames.size(), n2 = (int)b->frames.size();
+    float t[3];
+    for (int k = 0; k < 3; k++) {
+      const float m1 = a->center[k], m2 = b->center[k];
+      const float d = std::sqrt(((((float)(n1 - 1) * m1 * m1) + ((float)(n2 - 1) * m2 * m2)) /
+                                 (float)(n1 + n2 - 2)) * (float)(1 / n1 + 1 / n2));
+      t[k] = (m1 - m2) / d;
+    }
+    const float* row = kTTable[std::min(n1 + n2 - 2, 121)];
+    return t[0] < row[5] && t[1] < row[5] && t[2] < row[5];
+  }
+
+  void merge(Obj* a, Obj* b) {  // Object_Map::MergeTwoMapObjs, Object.cc:1716-1902
+    std::unordered_set<PosKey, PosHash> have;
+    for (MapPt* q : a->pts) {
+      PosKey k;
+      if (pos_key(q->pos, k)) have.insert(k);
+    }
+    for (MapPt* p : b->pts) {
+      const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
+      double s[3];
+      se3_inv_apply(a->q, a->t, v, s);
+      if (std::fabs(s[0]) > 1.1 * a->lenth / 2 || std::fabs(s[1]) > 1.1 * a->width / 2 ||
+          std::fabs(s[2]) > 1.1 * a->height / 2)
+        continue;
+      vote(p, a->id);
+      PosKey k;
+      const bool finite = pos_key(p->pos, k);
+      if (!finite || !have.count(k)) {
+        a->pts.push_back(p);
+        for (int c = 0; c < 3; c++) a->sum[c] += p->pos[c];
+        if (finite) have.insert(k);
+      }
+    }
+    for (Det* f : b->frames) {
+      f->mnId = a->id;
+      a->conf++;
+      a->frames.push_back(f);
+    }
+    for (auto& kv : b->same) {
+      auto it = a->same.find(kv.first);
+      if (it != a->same.end()) it->second = it->second + kv.second;
+      else a->same[kv.first] = 1;
+    }
+    const int oLast = a->last_add, oLastLast = a->lastlast_add;
+    const IRect oRect = a->last;
+    if (a->last_add > b->last_add) {
+      if (!(oLastLast > b->last_add)) {
+        a->lastlast_add = b->last_add;
+        a->lastlast = b->frames.back()->box;
+      }
+    } else {
+      a->last_add = b->last_add;
+      a->last = b->frames.back()->box;
+      if (oLast > b->lastlast_add) {
+        a->lastlast_add = oLast;
+        a->lastlast = oRect;
+      } else {
+        a->lastlast_add = b->lastlast_add;
+        a->lastlast = b->frames.size() >= 2 ? b->frames[b->frames.size() - 2]->box : b->frames.front()->box;
+      }
+    }
+  }
+
+  int iforest_now(Obj* o) {  // synchronous forest (LocalMapping merge path)
+    o->pending = std::max(o->pending, 1);
+    return flush_list({o});
+  }
+
+  int whether_merge(Obj* o) {  // Object_Map::WhetherMergeTwoMapObjs, Object.cc:1607-1655
+    for (auto& kv : o->reobj) {
+      const int nid = kv.first;
+      if (kv.second < 3) continue;
+      if (objs[nid]->bad) continue;
+      const bool dt = double_ttest(o, objs[nid].get());
+      if (o->same.find(nid) != o->same.end()) continue;
+      const bool same = false;
+      if (!same || dt) {
+        Obj* b = objs[nid].get();
+        if (o->frames.size() > b->frames.size()) {
+          merge(o, b);
+          mean_std(o);
+          int rc = iforest_now(o);
+          if (rc) return rc;
+          b->bad = true;
+        } else {
+          merge(b, o);
+          mean_std(b);
+          int rc = iforest_now(b);
+          if (rc) return rc;
+          o->bad = true;
+        }
+      }
+    }
+    return EAO_OK;
+  }
+
+  void divide_equally(Obj* a, Obj* b, float ox, float oy, float oz) {  // Object.cc:2044-2073
+    size_t w = 0;
+    for (size_t i = 0; i < a->pts.size(); i++) {
+      const float* P = a->pts[i]->pos;
+      const bool in =
+          (P[0] > b->center_c[0] - (b->lenth / 2 - ox / 2) && P[0] < b->center_c[0] + (b->lenth / 2 - ox / 2)) &&
+          (P[1] > b->center_c[1] - (b->width / 2 - oy / 2) && P[1] < b->center_c[1] + (b->width / 2 - oy / 2)) &&
+          (P[2] > b->center_c[2] - (b->height / 2 - oz / 2) && P[2] < b->center_c[2] + (b->height / 2 - oz / 2));
+      if (!in) a->pts[w++] = a->pts[i];
+    }
+    a->pts.resize(w);
+  }
+
+  void big_to_small(Obj* a, Obj* s) {  // Object.cc:1926-2040
+    size_t w = 0;
+    for (size_t i = 0; i < a->pts.size(); i++) {
+      const float* P = a->pts[i]->pos;
+      const bool in = P[0] > s->xmn && P[0] < s->xmx && P[1] > s->ymn && P[1] < s->ymx && P[2] > s->zmn &&
+                      P[2] < s->zmx;
+      if (!in) a->pts[w++] = a->pts[i];
+    }
+    a->pts.resize(w);
+    mean_std(a);
+  }
+
+  void deal_overlap(Obj* a, Obj* b, float ox, float oy, float oz) {  // Object.cc:2077-2178
+    const float va = (a->lenth * a->width) * a->height, vb = (b->lenth * b->width) * b->height;
+    const float ov = (ox * oy) * oz;
+    const bool bIou = (ov / (va + vb - ov)) >= 0.3;
+    const bool bVol = (va > 2 * vb) || (vb > 2 * va);
+    bool bSame = false;
+    auto it = a->same.find(b->id);
+    if (it != a->same.end()) bSame = it->second > 3;
+    const bool bCls = a->cls == b->cls;
+    if (bIou && !bVol && !bSame && bCls) {
+      if (a->frames.size() >= b->frames.size()) {
+        merge(a, b);
+        b->bad = true;
+      } else {
+        merge(b, a);
+        a->bad = true;
+      }
+    } else if (bVol && !bSame && bCls) {
+      if (a->frames.size() >= b->frames.size() && va > vb) b->bad = true;
+      else if (a->frames.size() < b->frames.size() && va < vb) a->bad = true;
+    } else if (bIou && !bVol && bSame && bCls) {
+      divide_equally(a, b, ox, oy, oz);
+      divide_equally(b, b, ox, oy, oz);
+      mean_std(a);
+      mean_std(b);
+    } else if (!bIou && bVol && bSame && !bCls) {
+      if (va > vb) big_to_small(a, b);
+      else if (va < vb) big_to_small(b, a);
+    } else if (bIou && !bSame && bCls) {
+      if (a->frames.size() / 2 >= b->frames.size()) {
+        merge(a, b);
+        b->bad = true;
+      } else if (b->frames.size() / 2 >= a->frames.size()) {
+        merge(b, a);
+        a->bad = true;
+      }
+    }
+  }
+
+  int local_mapping() {
+    int rc = flush(-1);
+    if (rc) return rc;
+    for (auto& up : objs) {
+      Obj* o = up.get();
+      if (o->pts.size() < 10 || o->bad) continue;
+      mean_std(o);
+    }
+    if (flag == "NA" || flag == "IoU" || flag == "NP") return EAO_OK;
+    for (auto& up : objs) {
+      Obj* o = up.get();
+      if (o->bad) continue;
+      if (o->frames.size() >= 10 && !o->reobj.empty()) {
+        rc = whether_merge(o);
+        if (rc) return rc;
+      }
+    }
+    for (size_t i = 0; i < objs.size(); i++) {
+      Obj* a = objs[i].get();
+      if (a->pts.size() < 10 || a->bad || a->frames.size() < 10) continue;
+      for (size_t j = 0; j < objs.size(); j++) {
+        if (i == j) continue;
+        Obj* b = objs[j].get();
+        if (b->pts.size() < 10 || b->bad || b->frames.size() < 10) continue;
+        const float dx = (float)std::fabs(a->center_c[0] - b->center_c[0]);
+        const float dy = (float)std::fabs(a->center_c[1] - b->center_c[1]);
+        const float dz = (float)std::fabs(a->center_c[2] - b->center_c[2]);
+        const float sl = a->lenth / 2 + b->lenth / 2, sw = a->width / 2 + b->width / 2,
+                    sh = a->height / 2 + b->height / 2;
+        if (dx < sl && dy < sw && dz < sh) deal_overlap(a, b, sl - dx, sw - dy, sh - dz);
+      }
+    }
+    return EAO_OK;
+  }
+};
+
+}  // namespace eao
+
+using namespace eao;
+
+struct eao_replay {
+  ReplayEngine r;
+};
+
+extern "C" {
+
+int eao_replay_create(eao_assoc* a, const char* flag, int img_w, int img_h, const float* K4,
+                      eao_replay** out) {
+  if (!a || !flag || !K4 || !out || img_w <= 0 || img_h <= 0) return EAO_E_ARG;
+  std::unique_ptr<eao_replay> r(new eao_replay());
+  r->r.A = assoc_engine(a);
+  r->r.flag = flag;
+  r->r.pz.fx = K4[0];
+  r->r.pz.fy = K4[1];
+  r->r.pz.cx = K4[2];
+  r->r.pz.cy = K4[3];
+  r->r.pz.cols = img_w;
+  r->r.pz.rows = img_h;
+  eao_camera c{img_w, img_h, K4[0], K4[1], K4[2], K4[3]};
+  r->r.camdev = make_cam(c);
+  *out = r.release();
+  return EAO_OK;
+}
+
+int eao_replay_destroy(eao_replay* r) {
+  delete r;
+  return EAO_OK;
+}
+
+int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes, const int32_t* boxes,
+                     int n_pts, const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                     const uint8_t* mp_bad, int32_t* det_out) {
+  if (!r || !Tcw || n_boxes < 0 || n_pts < 0 || (n_boxes && (!boxes || !det_out)) ||
+      (n_pts && (!mp_ids || !mp_pos || !kp_uv)))
+    return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
+  const int rc = r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv,
+                            mp_bad, det_out);
+  return rc ? rc : (int)r->r.objs.size();
+}
+
+int eao_replay_local_mapping(eao_replay* r) {
+  if (!r) return EAO_E_ARG;
+  return r->r.local_mapping();
+}
+
+int eao_replay_num_objects(eao_replay* r) { return r ? (int)r->r.objs.size() : EAO_E_ARG; }
+
+int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
+  if (!r || i < 0 || i >= (int)r->r.objs.size() || !ints || !floats) return EAO_E_ARG;
+  int rc = r->r.flush(-1);
+  if (rc) return rc;
+  const Obj* o = r->r.objs[i].get();
+  ints[0] = o->id;
+  ints[1] = o->cls;
+  ints[2] = o->bad;
+  ints[3] = (int)o->frames.size();
+  ints[4] = (int)o->pts.size();
+  ints[5] = o->last_add;
+  ints[6] = (int)o->reobj.size();
+  ints[7] = (int)o->same.size();
+  for (int a = 0; a < 3; a++) {
+    floats[a] = o->center[a];
+    floats[3 + a] = o->sd[a];
+    floats[6 + a] = o->csd[a];
+  }
+  floats[9] = o->lenth;
+  floats[10] = o->width;
+  floats[11] = o->height;
+  floats[12] = o->rmax;
+  floats[13] = o->csd_all;
+  floats[14] = (float)o->proj.x;
+  floats[15] = (float)o->proj.w;
+  return EAO_OK;
+}
+
+int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap) {
+  if (!r || i < 0 || i >= (int)r->r.objs.size()) return EAO_E_ARG;
+  int rc = r->r.flush(-1);
+  if (rc) return rc;
+  const Obj* o = r->r.objs[i].get();
+  const int n = (int)o->pts.size();
+  for (int k = 0; k < n && k < cap; k++) ids[k] = o->pts[k]->id;
+  return n;
+}
+
+}  // extern "C"

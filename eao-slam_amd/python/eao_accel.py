@@ -273,3 +273,49 @@ class Assoc:
         check(lib().eao_project_rects(self.h, ctypes.byref(cam), P(np.ascontiguousarray(Tcw, np.float32)),
                                       len(pts), P(allp), P(offs), P(lens), P(rect), P(ok)), "eao_project_rects")
         return rect, ok
+
+
+class Replay:
+    """Deterministic association replay on the engine:
+    the object section of Tracking::TrackWithMotionModel + LocalMapping object
+    maintenance, with NP / iForest / projected rects on the GPU."""
+
+    def __init__(self, assoc, flag="iForest", w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
+        self.assoc = assoc
+        self.h = ctypes.c_void_p()
+        K4 = np.asarray(K, np.float32)
+        check(lib().eao_replay_create(assoc.h, flag.encode(), w, h, P(K4), ctypes.byref(self.h)),
+              "eao_replay_create")
+
+    def close(self):
+        if self.h:
+            lib().eao_replay_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def frame(self, fid, T, boxes, ids, pos, uv, bad=None):
+        boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 5)
+        out = np.zeros((len(boxes), 4), np.int32)
+        bad = np.zeros(len(ids), np.uint8) if bad is None else np.ascontiguousarray(bad, np.uint8)
+        check(lib().eao_replay_frame(self.h, int(fid), P(np.ascontiguousarray(T, np.float32)), len(boxes),
+                                     P(boxes), len(ids), P(np.ascontiguousarray(ids, np.int32)),
+                                     P(np.ascontiguousarray(pos, np.float32)),
+                                     P(np.ascontiguousarray(uv, np.float32)), P(bad), P(out)),
+              "eao_replay_frame")
+        return out
+
+    def local_mapping(self):
+        check(lib().eao_replay_local_mapping(self.h), "eao_replay_local_mapping")
+
+    def objects(self):
+        n = check(lib().eao_replay_num_objects(self.h), "eao_replay_num_objects")
+        ints = np.zeros((n, 8), np.int32)
+        fl = np.zeros((n, 16), np.float32)
+        pts = []
+        for i in range(n):
+            check(lib().eao_replay_object(self.h, i, P(ints[i]), P(fl[i])), "eao_replay_object")
+            ids = np.zeros(max(1, ints[i, 4]), np.int32)
+            k = check(lib().eao_replay_object_points(self.h, i, P(ids), len(ids)), "eao_replay_object_points")
+            pts.append(ids[:k].copy())
+        return ints, fl, pts

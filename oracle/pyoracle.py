@@ -210,3 +210,43 @@ def project_rect(c, Tcw, pts):
     r = np.zeros(4, np.int32)
     rc = lib().orc_project_rect(ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), len(pts), P(pts), P(r))
     return r if rc == 0 else None
+
+
+class Replay:
+    """CPU restatement of the association replay (oracle/assoc_ref.cpp)."""
+
+    def __init__(self, flag="iForest", w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
+        K4 = np.asarray(K, np.float32)
+        self.h = lib().orc_replay_create(flag.encode(), w, h, P(K4))
+
+    def close(self):
+        if self.h:
+            lib().orc_replay_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def frame(self, fid, T, boxes, ids, pos, uv, bad=None):
+        boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 5)
+        out = np.zeros((len(boxes), 4), np.int32)
+        bad = np.zeros(len(ids), np.uint8) if bad is None else np.ascontiguousarray(bad, np.uint8)
+        lib().orc_replay_frame(ctypes.c_void_p(self.h), int(fid), P(np.ascontiguousarray(T, np.float32)),
+                               len(boxes), P(boxes), len(ids), P(np.ascontiguousarray(ids, np.int32)),
+                               P(np.ascontiguousarray(pos, np.float32)), P(np.ascontiguousarray(uv, np.float32)),
+                               P(bad), P(out))
+        return out
+
+    def local_mapping(self):
+        lib().orc_replay_local_mapping(ctypes.c_void_p(self.h))
+
+    def objects(self):
+        n = lib().orc_replay_num_objects(ctypes.c_void_p(self.h))
+        ints = np.zeros((n, 8), np.int32)
+        fl = np.zeros((n, 16), np.float32)
+        pts = []
+        for i in range(n):
+            lib().orc_replay_object(ctypes.c_void_p(self.h), i, P(ints[i]), P(fl[i]))
+            ids = np.zeros(max(1, ints[i, 4]), np.int32)
+            k = lib().orc_replay_object_points(ctypes.c_void_p(self.h), i, P(ids), len(ids))
+            pts.append(ids[:k].copy())
+        return ints, fl, pts

@@ -1,0 +1,36 @@
+// Host-only stand-in for <hip/hip_runtime.h>: lets tests/native compile the
+// engine's HOST orchestration (replay.cpp) with g++ and drive it against the
+// oracle on a machine without a GPU. Test infrastructure only.
+#pragma once
+#include <cstdlib>
+#include <cstring>
+#include <cstdint>
+#define __device__
+#define __host__
+#define __global__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+typedef int hipError_t;
+typedef void* hipStream_t;
+enum { hipSuccess = 0, hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipStreamNonBlocking = 1 };
+struct int2 { int x, y; };
+struct int4 { int x, y, z, w; };
+inline const char* hipGetErrorString(hipError_t) { return "fake"; }
+inline hipError_t hipSetDevice(int) { return 0; }
+inline hipError_t hipMalloc(void* p, size_t n) { *(void**)p = std::malloc(n ? n : 1); return 0; }
+inline hipError_t hipFree(void* p) { std::free(p); return 0; }
+inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, int, hipStream_t) { if (n) std::memmove(d, s, n); return 0; }
+inline hipError_t hipStreamSynchronize(hipStream_t) { return 0; }
+inline hipError_t hipGetLastError() { return 0; }
+inline int __float2int_rn(float v) { return (int)__builtin_rintf(v); }
+inline float __fmul_rn(float a, float b) { return a * b; }
+inline float __fadd_rn(float a, float b) { return a + b; }
+inline float __fsub_rn(float a, float b) { return a - b; }
+inline float __fdiv_rn(float a, float b) { return a / b; }
+#include <algorithm>
+using std::max; using std::min;
+struct dim3_ { unsigned x, y, z; };
+static struct { unsigned x; } threadIdx;
+template <typename T> T __shfl_xor(T v, int, int) { return v; }
+inline unsigned long long __ballot(bool p) { return p; }
+inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }

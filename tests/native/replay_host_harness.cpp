@@ -1,0 +1,48 @@
+// CPU harness for the engine's host-side association orchestration
+// (eao-slam_amd/csrc/replay.cpp): the three GPU primitives are served by the
+// oracle so the decision logic can be debugged without a device. Test
+// infrastructure only -- never part of the product.
+#include "../../eao-slam_amd/csrc/assoc.h"
+#include "../../oracle/oracle.h"
+#include <string>
+#include <vector>
+
+namespace eao {
+static std::string g_err;
+void set_error(const std::string& s) { g_err = s; }
+CamDev make_cam(const eao_camera& c) {
+  CamDev d;
+  d.fx = c.fx; d.fy = c.fy; d.cx = c.cx; d.cy = c.cy;
+  d.minX = 0; d.maxX = (float)c.img_w; d.minY = 0; d.maxY = (float)c.img_h;
+  d.invW = 64.0f / d.maxX; d.invH = 48.0f / d.maxY;
+  return d;
+}
+int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
+                          const float* op, const uint8_t* ov, const int* ooff, const int* olen,
+                          eao_np_stats* out, hipStream_t) {
+  for (int p = 0; p < npairs; p++) {
+    orc_np_stats s;
+    orc_np_test(flen[p], fp + 3 * foff[p], fv + foff[p], olen[p], op + 3 * ooff[p], ov + ooff[p], &s);
+    static_assert(sizeof(s) == sizeof(eao_np_stats), "layout");
+    std::memcpy(&out[p], &s, sizeof(s));
+  }
+  return 0;
+}
+int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
+                               uint32_t seed, const uint32_t* sample, double* scores, hipStream_t) {
+  for (int c = 0; c < nclouds; c++)
+    if (orc_iforest_scores(pts + 3 * off[c], len[c], trees, seed, sample[c], scores + off[c])) return -4;
+  return 0;
+}
+int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const float* pts, const int* off,
+                       const int* len, int* rect, uint8_t* ok, hipStream_t) {
+  orc_camera c{(int)cam.maxX, (int)cam.maxY, cam.fx, cam.fy, cam.cx, cam.cy};
+  for (int k = 0; k < nclouds; k++) ok[k] = orc_project_rect(&c, T, len[k], pts + 3 * off[k], rect + 4 * k) == 0;
+  return 0;
+}
+AssocEngine::~AssocEngine() {}
+}  // namespace eao
+
+struct eao_assoc { eao::AssocEngine e; };
+namespace eao { AssocEngine* assoc_engine(eao_assoc* a) { return &a->e; } }
+extern "C" eao_assoc* harness_assoc_create() { auto* a = new eao_assoc(); a->e.dev = 0; return a; }

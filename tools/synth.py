@@ -113,3 +113,98 @@ def frame_stream(n, w=640, h=480, seed=0xEA0, step=0.004):
     poses = camera_path(n, seed, step)
     frames = np.stack([render(tex, poses[i], w, h) for i in range(n)])
     return frames, poses
+
+
+# ----------------------------------------------------------------------------
+# Association workload: objects with point clouds
+# seen along a camera path, YOLO-like boxes, tracked map points per frame.
+# Class mix follows the reference's data/yolo_txts (39 bottle, 56 chair,
+# 73 book, 62 tv, 41 cup, 66 keyboard, 64 mouse, 77 teddy bear, 0 person).
+OFFICE_CLASSES = [39, 39, 39, 56, 56, 73, 73, 62, 41, 66, 64, 77, 0, 72]
+CLASS_EXTENT = {39: (0.07, 0.07, 0.22), 56: (0.45, 0.45, 0.8), 73: (0.2, 0.05, 0.25),
+                62: (0.5, 0.08, 0.35), 41: (0.08, 0.08, 0.1), 66: (0.45, 0.15, 0.03),
+                64: (0.06, 0.1, 0.04), 77: (0.25, 0.2, 0.3), 0: (0.5, 0.3, 1.6), 72: (0.4, 0.3, 0.6)}
+
+
+def _look_at(eye, target):
+    z = target - eye
+    z = z / np.linalg.norm(z)
+    up = np.array([0.0, 0.0, 1.0])
+    x = np.cross(z, up)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    Rwc = np.stack([x, y, z], 1)  # columns = camera axes in world
+    Rcw = Rwc.T
+    T = np.eye(4)
+    T[:3, :3] = Rcw
+    T[:3, 3] = -Rcw @ eye
+    return T.astype(np.float32)
+
+
+def assoc_scene(seed=0xEA1, classes=None, pts_range=(150, 600), n_background=800):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    classes = OFFICE_CLASSES if classes is None else classes
+    objs = []
+    mp_pos = []
+    mp_obj = []
+    for k, c in enumerate(classes):
+        ang = 2 * np.pi * k / len(classes) + rng.uniform(-0.2, 0.2)
+        rad = rng.uniform(0.2, 0.9)
+        center = np.array([rad * np.cos(ang), rad * np.sin(ang), 0.0])
+        ext = np.array(CLASS_EXTENT.get(c, (0.2, 0.2, 0.2)))
+        center[2] = ext[2] / 2 + rng.uniform(0, 0.3)
+        n = int(rng.integers(*pts_range))
+        p = rng.normal(0, 1, (n, 3)) * (ext / 4)
+        p = np.clip(p, -ext / 2, ext / 2) + center
+        n_out = max(1, n // 20)
+        p[:n_out] = center + rng.uniform(-1, 1, (n_out, 3)) * (ext / 2 + 0.25)
+        objs.append(dict(cls=c, center=center, ext=ext, first=len(mp_pos), n=n))
+        mp_pos.extend(p.tolist())
+        mp_obj.extend([k] * n)
+    bg = rng.uniform([-2.5, -2.5, 0], [2.5, 2.5, 2.0], (n_background, 3))
+    mp_pos.extend(bg.tolist())
+    mp_obj.extend([-1] * n_background)
+    return objs, np.asarray(mp_pos, np.float32), np.asarray(mp_obj, np.int32)
+
+
+def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None, obs_frac=0.7,
+                 kf_every=5, pts_range=(150, 600)):
+    """Per-frame replay inputs for the association path."""
+    fx, fy, cx, cy = K
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    objs, P, owner = assoc_scene(seed, classes, pts_range)
+    frames = []
+    for t in range(n_frames):
+        a = -0.6 + 1.6 * t / max(1, n_frames - 1)
+        eye = np.array([2.3 * np.cos(a), 2.3 * np.sin(a), 1.3 + 0.1 * np.sin(3 * a)])
+        T = _look_at(eye, np.array([0.0, 0.0, 0.3]))
+        Pc = P @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+        z = Pc[:, 2]
+        u = fx * Pc[:, 0] / z + cx
+        v = fy * Pc[:, 1] / z + cy
+        vis = (z > 0.1) & (u >= 0) & (u < w) & (v >= 0) & (v < h)
+        boxes = []
+        for k, o in enumerate(objs):
+            sel = np.arange(o["first"], o["first"] + o["n"])
+            sv = sel[vis[sel]]
+            if len(sv) < 0.6 * o["n"] or rng.random() > 0.9:
+                continue
+            core = sv[o["n"] // 20 <= sv - o["first"]]
+            if len(core) < 3:
+                continue
+            x0, x1 = np.percentile(u[core], [1, 99])
+            y0, y1 = np.percentile(v[core], [1, 99])
+            j = rng.integers(-3, 4, 4)
+            bx, by = int(max(0, x0 + j[0])), int(max(0, y0 + j[1]))
+            bw, bh = int(min(w - 1, x1 + j[2]) - bx), int(min(h - 1, y1 + j[3]) - by)
+            if bw > 4 and bh > 4:
+                boxes.append([o["cls"], bx, by, bw, bh])
+        order = rng.permutation(len(boxes))
+        boxes = np.asarray([boxes[i] for i in order], np.int32).reshape(-1, 5)
+        obs = np.nonzero(vis & (rng.random(len(P)) < obs_frac))[0]
+        obs = obs[rng.permutation(len(obs))]
+        uv = np.stack([u[obs], v[obs]], 1)
+        uv = (np.round(uv * 10) / 10).astype(np.float32)
+        frames.append(dict(T=T, boxes=boxes, ids=obs.astype(np.int32), pos=P[obs],
+                           uv=uv, bad=np.zeros(len(obs), np.uint8), kf=(t % kf_every == kf_every - 1)))
+    return frames
