@@ -122,6 +122,22 @@ int eao_orb_extract_batch_device(eao_orb* h, const uint8_t* d_frames, int nframe
                   (hipStream_t)stream);
 }
 
+int eao_orb_set_timing(eao_orb* h, int on) {
+  if (!h) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(h->e.dev));
+  if (on && !h->e.ev[0])
+    for (auto& e : h->e.ev) EAO_HIP_CHECK(hipEventCreate(&e));
+  h->e.timing = on != 0;
+  return EAO_OK;
+}
+
+int eao_orb_stage_ms(eao_orb* h, float* ms4) {
+  if (!h || !ms4 || !h->e.timing) return EAO_E_STATE;
+  EAO_HIP_CHECK(hipEventSynchronize(h->e.ev[4]));
+  for (int i = 0; i < 4; i++) EAO_HIP_CHECK(hipEventElapsedTime(&ms4[i], h->e.ev[i], h->e.ev[i + 1]));
+  return EAO_OK;
+}
+
 int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out) {
   if (!h || !gray || !out) return EAO_E_ARG;
   OrbEngine& e = h->e;

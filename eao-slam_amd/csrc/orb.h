@@ -53,6 +53,9 @@ class OrbEngine {
   std::vector<int2> slot_map;
   long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;
   int cap = 0, roi_stride = 0, roi_rows = 0;
+  // optional per-stage timing: events around resize / fast / distribute / describe
+  bool timing = false;
+  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
 
   hipStream_t stream = nullptr;
   LevelDev* d_levels = nullptr;

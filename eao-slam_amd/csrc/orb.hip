@@ -890,6 +890,8 @@ OrbEngine::~OrbEngine() {
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
+  for (auto& e : ev)
+    if (e) (void)hipEventDestroy(e);
 }
 
 int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint_dev* d_kps,
@@ -901,6 +903,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   if (!s) s = stream;
   const long long fstride = (long long)pitch * p.height;
   const int nl = p.nlevels;
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[0], s));
   // pyramid
   for (int l = 1; l < nl; l++) {
     const LevelDev& L = levels[l];
@@ -913,6 +916,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        L.pitch, pyr_bytes, L.w, L.h, d_xofs + L.tab_x, d_ia + 2 * L.tab_x, L.xmax,
                        d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
   }
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[1], s));
   // FAST per cell
   {
     dim3 g((unsigned)cells.size(), nframes);
@@ -921,6 +925,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        d_levels, d_cells, p.ini_th_fast, p.min_th_fast, roi_stride, roi_rows,
                        d_cand, cand_stride, d_cell_cnt, (int)cells.size());
   }
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[2], s));
   // quadtree distribution
   {
     dim3 g(nl, nframes);
@@ -928,6 +933,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        (int)cells.size(), d_levels, d_cells, d_qbuf, 2 * cand_stride, d_sel,
                        sel_stride, d_sel_cnt, nl);
   }
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[3], s));
   // orientation + descriptors
   {
     const int nslots = (int)slot_map.size();
@@ -936,6 +942,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax,
                        d_gk, d_kps, d_desc, d_counts, out_cap);
   }
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }

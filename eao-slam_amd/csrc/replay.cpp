@@ -1409,6 +1409,7 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
 
 int eao_replay_local_mapping(eao_replay* r) {
   if (!r) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   return r->r.local_mapping();
 }
 
@@ -1416,6 +1417,7 @@ int eao_replay_num_objects(eao_replay* r) { return r ? (int)r->r.objs.size() : E
 
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
   if (!r || i < 0 || i >= (int)r->r.objs.size() || !ints || !floats) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   int rc = r->r.flush(-1);
   if (rc) return rc;
   const Obj* o = r->r.objs[i].get();
@@ -1444,6 +1446,7 @@ int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
 
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap) {
   if (!r || i < 0 || i >= (int)r->r.objs.size()) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   int rc = r->r.flush(-1);
   if (rc) return rc;
   const Obj* o = r->r.objs[i].get();

@@ -130,6 +130,14 @@ class Orb:
             o += lw * lh
         return levels
 
+    def set_timing(self, on=True):
+        check(lib().eao_orb_set_timing(self.h, int(on)), "eao_orb_set_timing")
+
+    def stage_ms(self):
+        ms = np.zeros(4, np.float32)
+        check(lib().eao_orb_stage_ms(self.h, P(ms)), "eao_orb_stage_ms")
+        return ms
+
     def extract_batch_device(self, frames_ptr, nframes, pitch, kps_ptr, desc_ptr, counts_ptr, cap, stream=None):
         check(lib().eao_orb_extract_batch_device(self.h, ctypes.c_void_p(frames_ptr), nframes, pitch,
                                                  ctypes.c_void_p(kps_ptr), ctypes.c_void_p(desc_ptr),
