@@ -11,7 +11,8 @@
 namespace eao {
 
 constexpr int NP_MAXN = 8192;   // object points per NP pair handled in LDS
-constexpr int IF_MAXN = 8192;   // points per isolation-forest cloud (LDS ids)
+constexpr int IF_MAXN = 7168;   // points per isolation-forest cloud (tree + sample in LDS)
+constexpr int IF_LDS = 160 * 1024;  // LDS per workgroup on gfx950
 
 class AssocEngine {
  public:
@@ -27,8 +28,9 @@ class AssocEngine {
   float* d_T = nullptr;
   // isolation forest scratch
   uint32_t* d_seeds = nullptr;   // [trees]
-  uint16_t* d_ids = nullptr;     // [max_clouds * trees * max_points/2] sample ids
-  float* d_tree = nullptr;       // [max_clouds * trees * 2*IF nodes * 4] (dim,split,size,right)
+  double* d_contrib = nullptr;   // [max_trees][max_points] path length per (tree, point)
+  uint32_t cached_seed = 0, cached_trees = 0;
+  size_t lds_limit = 0;
   double* d_scores = nullptr;    // [max_points]
   int max_pairs = 256, max_clouds = 64, max_trees = 64;
 
@@ -40,7 +42,7 @@ class AssocEngine {
                const int* d_olen, eao_np_stats* d_out, hipStream_t s);
   int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
-                    hipStream_t s);
+                    hipStream_t s, int max_len, int max_sample, int npts_total);
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
 };

@@ -5,11 +5,13 @@
 //                  rank-sum of NoParaDataAssociation (Object.cc:714-930) as
 //                  sort + rank counting (counts identical to the O(m*n) loop)
 //   k_rects        one workgroup per cloud: ComputeProjectRectFrame (:1558-1603)
-//   k_iforest_build one wave per (tree, cloud): IsolationTree::Build with the
-//                  libstdc++-11 mt19937 / Lemire / shuffle / canonical-float
-//                  stream replicated exactly (isolation_forest.h:165-224,300-345)
-//   k_iforest_score one thread per point: average path length over the trees
-//                  in order, score 2^(-E[h]/c(psi)) (isolation_forest.h:499-530)
+//   k_iforest_tree one workgroup per (tree, cloud): IsolationTree::Build with
+//                  the libstdc++-11 mt19937 / Lemire / shuffle / canonical-float
+//                  stream replicated exactly (isolation_forest.h:165-224,300-345),
+//                  tree and sample resident in LDS, then every point's path
+//                  length through it
+//   k_iforest_sum  one thread per point: path lengths summed in tree order,
+//                  score 2^(-E[h]/c(psi)) (isolation_forest.h:499-530)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -234,9 +236,19 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 }
 
 // ---------------------------------------------------------------- iForest
-struct WaveMT {
+// Compiler barrier between the phases of a one-wave algorithm: a wave's LDS
+// operations execute in program order, so only compiler reordering across
+// lanes' data dependencies has to be prevented.
+#define WAVE_FENCE() __asm__ volatile("" ::: "memory")
+
+// std::mt19937 for one wave: state in LDS, tempered outputs buffered one per
+// lane in a VGPR and handed out in stream order with v_readlane.
+struct WaveRng {
   uint32_t* mt;  // LDS [624]
-  int idx;
+  int idx;       // next untempered state word (uniform)
+  uint32_t buf;  // lane j: draw number (base + j) of the current chunk
+  int bp, blen;  // uniform read position / valid length of buf
+
   __device__ void seed(uint32_t s) {
     if (lane_id() == 0) {
       uint32_t x = s;
@@ -247,10 +259,12 @@ struct WaveMT {
       }
     }
     idx = 624;
-    __syncthreads();
+    bp = blen = 0;
+    WAVE_FENCE();
   }
-  // libstdc++ _M_gen_rand, 64 lanes; chunks in increasing order keep the
-  // in-place read-after-write order of the sequential recurrence.
+  // libstdc++ _M_gen_rand in chunks of 64 words in increasing order: word k
+  // reads k+1 (old) and (k+397)%624 (new for k >= 227, written by an earlier
+  // chunk), exactly the in-place order of the sequential recurrence.
   __device__ void twist() {
     const int l = lane_id();
     for (int c0 = 0; c0 < 623; c0 += 64) {
@@ -260,26 +274,35 @@ struct WaveMT {
         const uint32_t y = (mt[k] & 0x80000000u) | (mt[k + 1] & 0x7fffffffu);
         nv = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
       }
-      __syncthreads();
+      WAVE_FENCE();
       if (k < 623) mt[k] = nv;
-      __syncthreads();
+      WAVE_FENCE();
     }
     if (l == 0) {
       const uint32_t y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
       mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
     }
-    __syncthreads();
+    WAVE_FENCE();
     idx = 0;
   }
-  __device__ uint32_t next() {
+  __device__ void refill() {
     if (idx >= 624) twist();
-    uint32_t y = mt[idx++];
+    blen = min(64, 624 - idx);
+    const int l = lane_id();
+    uint32_t y = l < blen ? mt[idx + l] : 0u;
     y ^= (y >> 11);
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
-    return y;
+    buf = y;
+    idx += blen;
+    bp = 0;
   }
+  __device__ uint32_t next() {
+    if (bp >= blen) refill();
+    return (uint32_t)__builtin_amdgcn_readlane((int)buf, bp++);
+  }
+  // uniform_int_distribution<uint32_t>(0, range-1) with a 32-bit URNG (Lemire)
   __device__ uint32_t lemire(uint32_t range) {
     uint64_t product = (uint64_t)next() * (uint64_t)range;
     uint32_t low = (uint32_t)product;
@@ -292,6 +315,7 @@ struct WaveMT {
     }
     return (uint32_t)(product >> 32);
   }
+  // uniform_real_distribution<float>(a, b): generate_canonical<float, 24>
   __device__ float uniform_real(float a, float b) {
     float ret = fdiv(fmul((float)next(), 1.0f), 4294967296.0f);
     if (ret >= 1.0f) ret = __uint_as_float(0x3f7fffffu);  // nextafter(1, 0)
@@ -299,154 +323,7 @@ struct WaveMT {
   }
 };
 
-// node record: x = dim (-1 leaf), y = split bits, z = size, w = right child
-__global__ __launch_bounds__(64) void k_iforest_build(const float* __restrict__ pts,
-                                                      const int* __restrict__ off,
-                                                      const int* __restrict__ len,
-                                                      const uint32_t* __restrict__ seeds,
-                                                      const uint32_t* __restrict__ sample,
-                                                      int node_stride, int4* __restrict__ tree_out) {
-  __shared__ uint32_t mts[624];
-  __shared__ uint16_t ids[IF_MAXN];
-  __shared__ uint16_t tmp[IF_MAXN / 2];
-  __shared__ int stk[4 * 64];
-  const int tr = blockIdx.x, c = blockIdx.y, lane = threadIdx.x, ntrees = gridDim.x;
-  const int n = len[c];
-  const int psi = (int)sample[c];
-  const float* P = pts + 3 * (long long)off[c];
-  int4* nodes = tree_out + ((long long)c * ntrees + tr) * node_stride;
-  if (n <= 0 || psi <= 0 || psi > n || n > IF_MAXN) {
-    if (lane == 0) nodes[0] = make_int4(-2, 0, 0, 0);  // invalid marker
-    return;
-  }
-  WaveMT g;
-  g.mt = mts;
-  g.seed(seeds[tr]);
-  for (int i = lane; i < n; i += 64) ids[i] = (uint16_t)i;
-  __syncthreads();
-  // std::shuffle (libstdc++ 11), paired draws when n*n <= 2^32-1
-  const uint64_t un = (uint64_t)n;
-  if (0xffffffffull / un >= un) {
-    uint64_t i = 1;
-    if ((n % 2) == 0) {
-      const uint32_t pos = g.lemire(2);
-      if (lane == 0) {
-        const uint16_t t = ids[i];
-        ids[i] = ids[pos];
-        ids[pos] = t;
-      }
-      i++;
-    }
-    while (i != un) {
-      const uint64_t sr = i + 1;
-      const uint32_t x = g.lemire((uint32_t)(sr * (sr + 1)));
-      const uint32_t p1 = (uint32_t)(x / (sr + 1)), p2 = (uint32_t)(x % (sr + 1));
-      if (lane == 0) {
-        uint16_t t = ids[i];
-        ids[i] = ids[p1];
-        ids[p1] = t;
-        t = ids[i + 1];
-        ids[i + 1] = ids[p2];
-        ids[p2] = t;
-      }
-      i += 2;
-    }
-  } else {
-    for (uint64_t i = 1; i < un; i++) {
-      const uint32_t pos = g.lemire((uint32_t)(i + 1));
-      if (lane == 0) {
-        const uint16_t t = ids[i];
-        ids[i] = ids[pos];
-        ids[pos] = t;
-      }
-    }
-  }
-  __syncthreads();
-  // maxDepth = ceil(log2(sampleSize))
-  const int maxDepth = (int)ceil(log2((double)psi));
-  // DFS pre-order build over items ids[0..psi)
-  int nn = 0;  // nodes written
-  int sp = 0;
-  if (lane == 0) {
-    stk[0] = 0;
-    stk[1] = psi - 1;
-    stk[2] = 0;
-    stk[3] = -1;  // parent index whose right child this is (-1: none)
-  }
-  sp = 1;
-  __syncthreads();
-  while (sp > 0) {
-    sp--;
-    const int first = stk[4 * sp], last = stk[4 * sp + 1], depth = stk[4 * sp + 2],
-              parent = stk[4 * sp + 3];
-    __syncthreads();
-    const int me = nn++;
-    if (parent >= 0 && lane == 0) nodes[parent].w = me;
-    const int cnt = last - first + 1;
-    if (last - first < 1 || depth >= maxDepth) {
-      if (lane == 0) nodes[me] = make_int4(-1, 0, cnt, -1);
-      continue;
-    }
-    const uint32_t dim = g.lemire(3);
-    float mn = INFINITY, mx = -INFINITY;
-    for (int i = first + lane; i <= last; i += 64) {
-      const float v = P[3 * ids[i] + dim];
-      mn = fminf(mn, v);
-      mx = fmaxf(mx, v);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      mn = fminf(mn, __shfl_xor(mn, o, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-    }
-    if (mn == mx) {
-      if (lane == 0) nodes[me] = make_int4(-1, 0, cnt, -1);
-      continue;
-    }
-    const float split = g.uniform_real(mn, mx);
-    // partition items: value < split first (membership is what matters)
-    int nl = 0, nr = 0;
-    for (int c0 = first; c0 <= last; c0 += 64) {
-      const int i = c0 + lane;
-      bool in = i <= last;
-      uint16_t id = 0;
-      bool lft = false;
-      if (in) {
-        id = ids[i];
-        lft = P[3 * id + dim] < split;
-      }
-      const uint64_t ml = ballot(in && lft), mr = ballot(in && !lft);
-      if (in && lft) tmp[nl + popc64(ml & lanes_below())] = id;
-      if (in && !lft) tmp[(IF_MAXN / 2) - 1 - (nr + popc64(mr & lanes_below()))] = id;
-      nl += popc64(ml);
-      nr += popc64(mr);
-    }
-    __syncthreads();
-    for (int k = lane; k < nl; k += 64) ids[first + k] = tmp[k];
-    for (int k = lane; k < nr; k += 64) ids[first + nl + k] = tmp[(IF_MAXN / 2) - 1 - k];
-    __syncthreads();
-    const int middle = first + nl;
-    if (middle == first) {
-      if (lane == 0) nodes[me] = make_int4(-1, 0, cnt, -1);
-      continue;
-    }
-    if (lane == 0) nodes[me] = make_int4((int)dim, __float_as_int(split), cnt, -1);
-    // push right then left so the left subtree is built (and draws) first
-    if (lane == 0) {
-      stk[4 * sp] = middle;
-      stk[4 * sp + 1] = last;
-      stk[4 * sp + 2] = depth + 1;
-      stk[4 * sp + 3] = me;
-      stk[4 * sp + 4] = first;
-      stk[4 * sp + 5] = middle - 1;
-      stk[4 * sp + 6] = depth + 1;
-      stk[4 * sp + 7] = -1;
-    }
-    sp += 2;
-    __syncthreads();
-  }
-}
-
-__device__ __forceinline__ double iforest_c(uint32_t n) {
+__device__ __forceinline__ double iforest_c(uint32_t n) {  // CalculateC, isolation_forest.h:97-118
   if (n > 2) {
     const double h = log((double)(n - 1)) + 0.5772156649;
     return __dsub_rn(2.0 * h, (2.0 * (double)(n - 1)) / (double)n);
@@ -455,37 +332,286 @@ __device__ __forceinline__ double iforest_c(uint32_t n) {
   return 0.0;
 }
 
-__global__ __launch_bounds__(256) void k_iforest_score(const float* __restrict__ pts,
-                                                       const int* __restrict__ off,
-                                                       const int* __restrict__ len,
-                                                       const uint32_t* __restrict__ sample,
-                                                       int ntrees, int node_stride,
-                                                       const int4* __restrict__ tree,
-                                                       double* __restrict__ scores) {
-  const int c = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__host__ __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
+struct IfLds {
+  size_t mt, b0, b1, nodes, right, shuf, total;
+  __host__ __device__ IfLds(int N, int S) {
+    mt = 0;
+    b0 = al16(624 * 4);
+    b1 = b0 + al16(12 * (size_t)S);
+    nodes = b1 + al16(12 * (size_t)S);
+    right = nodes + al16(8 * 2 * (size_t)S);
+    const size_t build_end = right + al16(2 * 2 * (size_t)S);
+    shuf = b1;  // shuffle scratch aliases B1 / nodes (dead until the build)
+    const size_t shuf_end = shuf + al16(2 * (size_t)N) + 2 * al16(4 * ((size_t)N + 1)) + al16(2 * (size_t)N);
+    total = build_end > shuf_end ? build_end : shuf_end;
+  }
+};
+
+// One workgroup (4 waves) per (tree, cloud): IsolationTree::Build of
+// isolation_forest.h:165-224,300-345 by wave 0 -- the libstdc++-11 draw stream
+// replicated exactly -- then every wave walks the cloud's points through the
+// tree (GetAnomalyScores' PathLength, :499-530); the per-(tree, point) path
+// length is summed in tree order by k_iforest_sum.
+//
+// Sampling: std::shuffle of ids [0, n) (paired Lemire draws, stl_algo.h) is a
+// Fisher-Yates sequence of positions p_j <= j.  The draws are taken 64 at a
+// time in parallel; the swaps are not replayed: with v_j = j before step j
+// the final content of position k is the last step that wrote k,
+//   final(k)   = max{ j > k : p_j = k }   or else  f(p_k, k)  (k if p_k = k)
+//   f(q, t)    = max{ j in (q, t) : p_j = q } or else f(p_q, q) (q if p_q = q, 0 at q = 0)
+// resolved per lane from per-position writer lists.  Only the sample's set
+// matters to the build (min/max, counts and membership are order-free), so
+// the sampled coordinates are gathered straight into LDS and partitioned
+// between two ping-pong buffers by depth parity.
+__global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ pts,
+                                                      const int* __restrict__ off,
+                                                      const int* __restrict__ len,
+                                                      const uint32_t* __restrict__ seeds,
+                                                      const uint32_t* __restrict__ sample,
+                                                      int maxN, int maxS, int npts_total,
+                                                      double* __restrict__ contrib) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const IfLds L(maxN, maxS);
+  uint32_t* mts = (uint32_t*)(smem + L.mt);
+  float* B0 = (float*)(smem + L.b0);
+  float* B1 = (float*)(smem + L.b1);
+  uint2* nodes = (uint2*)(smem + L.nodes);
+  uint16_t* right = (uint16_t*)(smem + L.right);
+  __shared__ int s_nodes_bad;
+
+  const int tr = blockIdx.x, c = blockIdx.y, ntrees = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n = len[c];
-  if (i >= n) return;
-  const float* x = pts + 3 * ((long long)off[c] + i);
-  double total = 0;
-  for (int t = 0; t < ntrees; t++) {
-    const int4* nodes = tree + ((long long)c * ntrees + t) * node_stride;
-    int k = 0, depth = 0;
-    while (true) {
-      const int4 nd = nodes[k];
-      if (nd.x < 0) {
-        total += (double)depth + iforest_c((uint32_t)nd.z);
-        break;
+  const int psi = (int)sample[c];
+  const float* P = pts + 3 * (long long)off[c];
+  double* out = contrib + (long long)tr * npts_total + off[c];
+  if (n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS) {
+    for (int i = tid; i < n; i += blockDim.x) out[i] = __longlong_as_double(0x7ff8000000000000ll);
+    return;
+  }
+
+  if (wave == 0) {
+    WaveRng g;
+    g.mt = mts;
+    g.seed(seeds[tr]);
+    // ---- shuffle draws: positions p[j], j = 1..n-1
+    uint16_t* p = (uint16_t*)(smem + L.shuf);
+    uint32_t* start = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
+    uint32_t* fill = (uint32_t*)((unsigned char*)start + al16(4 * ((size_t)n + 1)));
+    uint16_t* items = (uint16_t*)((unsigned char*)fill + al16(4 * ((size_t)n + 1)));
+    const bool even = (n % 2) == 0;
+    const int nsteps = even ? n / 2 : (n - 1) / 2;
+    int s = 0;
+    while (s < nsteps) {
+      if (g.bp >= g.blen) g.refill();
+      const int avail = min(g.blen - g.bp, nsteps - s);
+      const uint32_t raw = (uint32_t)__shfl((int)g.buf, g.bp + lane, 64);
+      const int step = s + lane;
+      const bool single = even && step == 0;
+      const uint32_t i = even ? 2u * step : 2u * step + 1u;
+      const uint32_t sr = i + 1u;
+      const uint32_t range = single ? 2u : sr * (sr + 1u);
+      const uint64_t prod = (uint64_t)raw * range;
+      const uint32_t low = (uint32_t)prod;
+      bool rej = false;
+      if (lane < avail && low < range) rej = low < (uint32_t)(0u - range) % range;
+      const uint64_t rm = ballot(rej);
+      const int r = rm ? (int)__ffsll((unsigned long long)rm) - 1 : avail;
+      if (lane < r) {
+        const uint32_t x = (uint32_t)(prod >> 32);
+        if (single) {
+          p[1] = (uint16_t)x;
+        } else {
+          p[i] = (uint16_t)(x / (sr + 1u));
+          p[i + 1] = (uint16_t)(x % (sr + 1u));
+        }
       }
-      if (x[nd.x] < __int_as_float(nd.y))
-        k = k + 1;
-      else
-        k = nd.w;
+      s += r;
+      g.bp += r + (rm ? 1 : 0);  // a rejected draw is consumed; its step retries
+    }
+    WAVE_FENCE();
+    // ---- writer lists: for position q the steps j > q with p_j = q
+    for (int q = lane; q <= n; q += 64) start[q] = 0;
+    WAVE_FENCE();
+    for (int j = 1 + lane; j < n; j += 64) {
+      const int q = p[j];
+      if (q != j) atomicAdd(&start[q], 1u);
+    }
+    WAVE_FENCE();
+    uint32_t carry = 0;
+    for (int b = 0; b <= n; b += 64) {
+      const int q = b + lane;
+      const uint32_t v = q <= n ? start[q] : 0u;
+      uint32_t inc = v;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
+        if (lane >= o) inc += t;
+      }
+      if (q <= n) {
+        start[q] = carry + inc - v;
+        fill[q] = carry + inc - v;
+      }
+      carry += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+    WAVE_FENCE();
+    for (int j = 1 + lane; j < n; j += 64) {
+      const int q = p[j];
+      if (q != j) items[atomicAdd(&fill[q], 1u)] = (uint16_t)j;
+    }
+    WAVE_FENCE();
+    // ---- sample = final content of positions [0, psi): gather into B0
+    for (int k = lane; k < psi; k += 64) {
+      int q = k, t = n, id;
+      while (true) {
+        int m = -1;
+        for (uint32_t e = start[q]; e < start[q + 1]; e++) {
+          const int j = items[e];
+          if (j < t && j > m) m = j;
+        }
+        if (m >= 0) {
+          id = m;
+          break;
+        }
+        if (q == 0) {
+          id = 0;
+          break;
+        }
+        const int pq = p[q];
+        if (pq == q) {
+          id = q;
+          break;
+        }
+        t = q;
+        q = pq;
+      }
+      B0[k] = P[3 * id];
+      B0[psi + k] = P[3 * id + 1];
+      B0[2 * psi + k] = P[3 * id + 2];
+    }
+    WAVE_FENCE();
+    // ---- Node::Build in DFS pre-order; stack entry e lives in lane e
+    const int maxDepth = (int)ceil(log2((double)psi));
+    int sf = 0, sl = psi - 1, sd = 0, spar = -1;  // lane 0 = root
+    int sp = 1, nn = 0, bad = 0;
+    while (sp > 0) {
+      sp--;
+      const int first = __builtin_amdgcn_readlane(sf, sp);
+      const int last = __builtin_amdgcn_readlane(sl, sp);
+      const int depth = __builtin_amdgcn_readlane(sd, sp);
+      const int parent = __builtin_amdgcn_readlane(spar, sp);
+      const int me = nn++;
+      if (parent >= 0 && lane == 0) right[parent] = (uint16_t)me;
+      const int cnt = last - first + 1;
+      if (cnt < 2 || depth >= maxDepth) {
+        if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
+        continue;
+      }
+      const uint32_t dim = g.lemire(3);
+      const float* src = (depth & 1) ? B1 : B0;
+      float* dst = (depth & 1) ? B0 : B1;
+      float mn = INFINITY, mx = -INFINITY;
+      for (int i = first + lane; i <= last; i += 64) {
+        const float v = src[dim * psi + i];
+        mn = fminf(mn, v);
+        mx = fmaxf(mx, v);
+      }
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = fminf(mn, __shfl_xor(mn, o, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+      }
+      if (mn == mx) {
+        if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
+        continue;
+      }
+      const float split = g.uniform_real(mn, mx);
+      int nl = 0, nr = 0;
+      for (int c0 = first; c0 <= last; c0 += 64) {
+        const int i = c0 + lane;
+        const bool in = i <= last;
+        float x = 0.f, y = 0.f, z = 0.f;
+        if (in) {
+          x = src[i];
+          y = src[psi + i];
+          z = src[2 * psi + i];
+        }
+        const float v = dim == 0 ? x : (dim == 1 ? y : z);
+        const bool lft = in && v < split;
+        const uint64_t ml = ballot(lft), mr = ballot(in && !lft);
+        if (in) {
+          const int d = lft ? first + nl + popc64(ml & lanes_below())
+                            : last - (nr + popc64(mr & lanes_below()));
+          dst[d] = x;
+          dst[psi + d] = y;
+          dst[2 * psi + d] = z;
+        }
+        nl += popc64(ml);
+        nr += popc64(mr);
+      }
+      WAVE_FENCE();
+      if (nl == 0) {  // middle == first
+        if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
+        continue;
+      }
+      if (nr == 0) bad = 1;  // right range empty: Node::Build returns false
+      if (lane == 0) nodes[me] = make_uint2(dim + 1u, __float_as_uint(split));
+      const int middle = first + nl;
+      // push right, then left: the left subtree is built (and draws) first
+      if (lane == sp) {
+        sf = middle;
+        sl = last;
+        sd = depth + 1;
+        spar = me;
+      }
+      if (lane == sp + 1) {
+        sf = first;
+        sl = middle - 1;
+        sd = depth + 1;
+        spar = -1;
+      }
+      sp += 2;
+      if (bad) break;
+    }
+    if (lane == 0) s_nodes_bad = bad;
+  }
+  __syncthreads();
+  // ---- path length of every point of the cloud through this tree
+  if (s_nodes_bad) {
+    for (int i = tid; i < n; i += blockDim.x) out[i] = __longlong_as_double(0x7ff8000000000000ll);
+    return;
+  }
+  for (int i = tid; i < n; i += blockDim.x) {
+    const float x0 = P[3 * i], x1 = P[3 * i + 1], x2 = P[3 * i + 2];
+    int k = 0, depth = 0;
+    uint2 nd = nodes[0];
+    while ((nd.x & 3u) != 0u) {
+      const uint32_t d = nd.x & 3u;
+      const float v = d == 1u ? x0 : (d == 2u ? x1 : x2);
+      k = v < __uint_as_float(nd.y) ? k + 1 : (int)right[k];
+      nd = nodes[k];
       depth++;
     }
+    out[i] = (double)depth + iforest_c(nd.x >> 2);
   }
+}
+
+// score = 2^(-E[h(x)] / c(psi)), E[h] summed over the trees in order
+__global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off,
+                                                     const int* __restrict__ len,
+                                                     const uint32_t* __restrict__ sample,
+                                                     int ntrees, int npts_total,
+                                                     const double* __restrict__ contrib,
+                                                     double* __restrict__ scores) {
+  const int c = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= len[c]) return;
+  const long long g = (long long)off[c] + i;
+  double total = 0;
+  for (int t = 0; t < ntrees; t++) total += contrib[(long long)t * npts_total + g];
   const double avg = total / (double)ntrees;
-  scores[(long long)off[c] + i] = pow(2.0, -avg / iforest_c(sample[c]));
+  scores[g] = pow(2.0, -avg / iforest_c(sample[c]));
 }
 
 // ================================================================ host
@@ -507,13 +633,15 @@ int AssocEngine::init(int device, int mp) {
   EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16));
   EAO_HIP_CHECK(hipMalloc(&d_seeds, sizeof(uint32_t) * max_trees));
   EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)mp));
-  const int node_stride = std::min(mp, IF_MAXN) + 8;
-  EAO_HIP_CHECK(hipMalloc(&d_tree, sizeof(int4) * (size_t)node_stride * max_trees * 16));
+  EAO_HIP_CHECK(hipMalloc(&d_contrib, sizeof(double) * (size_t)mp * max_trees));
+  hipDeviceProp_t prop;
+  EAO_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
+  lds_limit = std::min((size_t)IF_LDS, (size_t)prop.sharedMemPerBlock) - 64;  // static LDS of the kernel
   return EAO_OK;
 }
 
 AssocEngine::~AssocEngine() {
-  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_seeds, d_scores, d_tree};
+  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_seeds, d_scores, d_contrib};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -557,22 +685,29 @@ static void forest_seeds(uint32_t seed, uint32_t trees, std::vector<uint32_t>& o
 
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len,
                                uint32_t trees, uint32_t seed, const uint32_t* d_sample,
-                               double* scores, hipStream_t s) {
+                               double* scores, hipStream_t s, int maxN, int maxS, int npts_total) {
   if (nclouds <= 0) return EAO_OK;
-  if ((int)trees > max_trees || nclouds > 16) {
-    set_error("iforest: too many trees or clouds per call");
+  if ((int)trees > max_trees || nclouds > max_clouds || npts_total > max_points) {
+    set_error("iforest: too many trees, clouds or points per call");
     return EAO_E_CAPACITY;
   }
-  std::vector<uint32_t> sd;
-  forest_seeds(seed, trees, sd);
-  EAO_HIP_CHECK(hipMemcpyAsync(d_seeds, sd.data(), sizeof(uint32_t) * trees, hipMemcpyHostToDevice, s));
-  const int node_stride = std::min(max_points, IF_MAXN) + 8;
-  hipLaunchKernelGGL(k_iforest_build, dim3(trees, nclouds), dim3(64), 0, s, pts, off, len, d_seeds,
-                     d_sample, node_stride, (int4*)d_tree);
+  const IfLds L(maxN, maxS);
+  if (maxN > IF_MAXN || L.total > lds_limit) {
+    set_error("iforest: cloud exceeds the LDS-resident tree capacity");
+    return EAO_E_CAPACITY;
+  }
+  if (seed != cached_seed || trees != cached_trees) {
+    std::vector<uint32_t> sd;
+    forest_seeds(seed, trees, sd);
+    EAO_HIP_CHECK(hipMemcpyAsync(d_seeds, sd.data(), sizeof(uint32_t) * trees, hipMemcpyHostToDevice, s));
+    cached_seed = seed;
+    cached_trees = trees;
+  }
+  hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(256), L.total, s, pts, off, len,
+                     d_seeds, d_sample, maxN, maxS, npts_total, d_contrib);
   EAO_HIP_CHECK(hipGetLastError());
-  const int blocks = (std::min(max_points, IF_MAXN) + 255) / 256;
-  hipLaunchKernelGGL(k_iforest_score, dim3(blocks, nclouds), dim3(256), 0, s, pts, off, len,
-                     d_sample, (int)trees, node_stride, (const int4*)d_tree, scores);
+  hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
+                     d_sample, (int)trees, npts_total, (const double*)d_contrib, scores);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -663,12 +798,14 @@ int eao_np_test_batch(eao_assoc* a, int npairs, const float* frame_pts, const ui
 int eao_iforest_scores_batch(eao_assoc* a, int nclouds, const float* pts, const int32_t* off,
                              const int32_t* len, uint32_t trees, uint32_t seed,
                              const uint32_t* sample_size, double* scores) {
-  if (!a || nclouds < 0 || nclouds > 16) return EAO_E_ARG;
+  if (!a || nclouds < 0 || nclouds > a->e.max_clouds) return EAO_E_ARG;
   if (nclouds == 0) return EAO_OK;
   AssocEngine& e = a->e;
-  int np = 0;
+  int np = 0, maxN = 0, maxS = 0;
   for (int c = 0; c < nclouds; c++) {
     np = std::max(np, off[c] + len[c]);
+    maxN = std::max(maxN, len[c]);
+    maxS = std::max(maxS, (int)sample_size[c]);
     if (len[c] > IF_MAXN || len[c] > e.max_points) return EAO_E_CAPACITY;
     if (sample_size[c] == 0 || (int)sample_size[c] > len[c]) return EAO_E_ARG;  // Build() fails
   }
@@ -681,7 +818,7 @@ int eao_iforest_scores_batch(eao_assoc* a, int nclouds, const float* pts, const 
   EAO_HIP_CHECK(hipMemcpyAsync(m + e.max_pairs, len, sizeof(int) * nclouds, hipMemcpyHostToDevice, s));
   EAO_HIP_CHECK(hipMemcpyAsync(m + 2 * e.max_pairs, sample_size, sizeof(int) * nclouds, hipMemcpyHostToDevice, s));
   int rc = e.iforest_batch(nclouds, e.d_pts, m, m + e.max_pairs, trees, seed,
-                           (const uint32_t*)(m + 2 * e.max_pairs), e.d_scores, s);
+                           (const uint32_t*)(m + 2 * e.max_pairs), e.d_scores, s, maxN, maxS, np);
   if (rc) return rc;
   EAO_HIP_CHECK(hipMemcpyAsync(scores, e.d_scores, sizeof(double) * np, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));

@@ -386,7 +386,7 @@ class ReplayEngine {
     while (i < todo.size()) {
       std::vector<Obj*> batch;
       int np = 0;
-      for (; i < todo.size() && batch.size() < 16; i++) {
+      for (; i < todo.size() && (int)batch.size() < A->max_clouds; i++) {
         Obj* o = todo[i];
         if (!o->pending) continue;
         if (iforest_applies(o)) {
@@ -394,6 +394,7 @@ class ReplayEngine {
             set_error("replay: object exceeds the isolation-forest capacity");
             return EAO_E_CAPACITY;
           }
+          if (!batch.empty() && np + (int)o->pts.size() > A->max_points) break;  // next batch
           batch.push_back(o);
           np += (int)o->pts.size();
         } else if (o->pending == 2) {
@@ -420,8 +421,10 @@ class ReplayEngine {
       const int nb = (int)batch.size();
       EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * np, hipMemcpyHostToDevice, A->stream));
       EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 3 * nb, hipMemcpyHostToDevice, A->stream));
+      int maxN = 0;
+      for (Obj* o : batch) maxN = std::max(maxN, (int)o->pts.size());
       rc = A->iforest_batch(nb, d_pts, d_meta, d_meta + nb, 50, 12345, (const uint32_t*)(d_meta + 2 * nb),
-                            d_scores, A->stream);
+                            d_scores, A->stream, maxN, maxN / 2, np);
       if (rc) return rc;
       std::vector<double> sc(np);
       EAO_HIP_CHECK(hipMemcpyAsync(sc.data(), d_scores, sizeof(double) * np, hipMemcpyDeviceToHost, A->stream));

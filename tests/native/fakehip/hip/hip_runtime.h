@@ -12,6 +12,7 @@
 #define __launch_bounds__(...)
 typedef int hipError_t;
 typedef void* hipStream_t;
+typedef void* hipEvent_t;
 enum { hipSuccess = 0, hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipStreamNonBlocking = 1 };
 struct int2 { int x, y; };
 struct int4 { int x, y, z, w; };

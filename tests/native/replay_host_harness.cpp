@@ -2,6 +2,7 @@
 // (eao-slam_amd/csrc/replay.cpp): the three GPU primitives are served by the
 // oracle so the decision logic can be debugged without a device. Test
 // infrastructure only -- never part of the product.
+#include <cmath>
 #include "../../eao-slam_amd/csrc/assoc.h"
 #include "../../oracle/oracle.h"
 #include <string>
@@ -29,11 +30,14 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
   return 0;
 }
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
-                               uint32_t seed, const uint32_t* sample, double* scores, hipStream_t) {
+                               uint32_t seed, const uint32_t* sample, double* scores, hipStream_t, int, int,
+                               int) {
   for (int c = 0; c < nclouds; c++)
-    if (orc_iforest_scores(pts + 3 * off[c], len[c], trees, seed, sample[c], scores + off[c])) return -4;
+    if (orc_iforest_scores(pts + 3 * off[c], len[c], trees, seed, sample[c], scores + off[c]))
+      for (int i = 0; i < len[c]; i++) scores[off[c] + i] = NAN;  // Build() failed: nothing erased
   return 0;
 }
+
 int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const float* pts, const int* off,
                        const int* len, int* rect, uint8_t* ok, hipStream_t) {
   orc_camera c{(int)cam.maxX, (int)cam.maxY, cam.fx, cam.fy, cam.cx, cam.cy};
