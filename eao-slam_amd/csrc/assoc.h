@@ -27,7 +27,7 @@ class AssocEngine {
   uint8_t* d_ok = nullptr;
   float* d_T = nullptr;
   // isolation forest scratch
-  uint32_t* d_seeds = nullptr;   // [trees]
+  uint32_t* d_mtinit = nullptr;  // [trees][624] mt19937 state of each tree after the first twist
   double* d_contrib = nullptr;   // [max_trees][max_points] path length per (tree, point)
   uint32_t cached_seed = 0, cached_trees = 0;
   size_t lds_limit = 0;
@@ -39,7 +39,7 @@ class AssocEngine {
   // device-level entry points (inputs already on device, stream s)
   int np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                const int* d_flen, const float* d_op, const uint8_t* d_ov, const int* d_ooff,
-               const int* d_olen, eao_np_stats* d_out, hipStream_t s);
+               const int* d_olen, eao_np_stats* d_out, hipStream_t s, int max_olen);
   int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
                     hipStream_t s, int max_len, int max_sample, int npts_total);

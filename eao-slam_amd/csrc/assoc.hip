@@ -24,22 +24,91 @@
 namespace eao {
 
 // ---------------------------------------------------------------- NP test
-__device__ void block_bitonic_sort(float* a, int P) {
-  for (int k = 2; k <= P; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < P; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const float x = a[i], y = a[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            a[i] = y;
-            a[ixj] = x;
+__device__ __forceinline__ void cswap(float& a, float& b, bool up) {
+  if ((a > b) == up) {
+    const float t = a;
+    a = b;
+    b = t;
+  }
+}
+
+// ascending bitonic sort of three LDS arrays at once, P = 2^e >= 8 (INF
+// padded). Runs of 8 consecutive elements are merged in registers (strides
+// 4, 2, 1); longer strides go through LDS with 4 pairs per thread in flight.
+__device__ void block_sort3(float* S0, float* S1, float* S2, int P) {
+  float* S[3] = {S0, S1, S2};
+  const int nt = blockDim.x, tid = threadIdx.x;
+  const int groups = P >> 3, half = P >> 1;
+  // k = 2, 4, 8 entirely in registers
+  for (int g = tid; g < groups; g += nt) {
+    const int base = g << 3;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      float v[8];
+      const float4 lo = *(const float4*)(S[a] + base), hi = *(const float4*)(S[a] + base + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+#pragma unroll
+      for (int k = 2; k <= 8; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            if ((i & j) == 0) cswap(v[i], v[i | j], ((base + i) & k) == 0);
+      *(float4*)(S[a] + base) = make_float4(v[0], v[1], v[2], v[3]);
+      *(float4*)(S[a] + base + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+  }
+  __syncthreads();
+  for (int k = 16; k <= P; k <<= 1) {
+    for (int j = k >> 1; j >= 8; j >>= 1) {
+      for (int p0 = tid; p0 < half; p0 += 4 * nt) {
+        float x[4][3], y[4][3];
+        int ii[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int pp = min(p0 + u * nt, half - 1);
+          ii[u] = ((pp & ~(j - 1)) << 1) | (pp & (j - 1));
+#pragma unroll
+          for (int a = 0; a < 3; a++) {
+            x[u][a] = S[a][ii[u]];
+            y[u][a] = S[a][ii[u] + j];
           }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (p0 + u * nt >= half) continue;
+          const bool up = (ii[u] & k) == 0;
+#pragma unroll
+          for (int a = 0; a < 3; a++)
+            if ((x[u][a] > y[u][a]) == up) {
+              S[a][ii[u]] = y[u][a];
+              S[a][ii[u] + j] = x[u][a];
+            }
         }
       }
       __syncthreads();
     }
+    for (int g = tid; g < groups; g += nt) {
+      const int base = g << 3;
+      const bool up = (base & k) == 0;
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        float v[8];
+        const float4 lo = *(const float4*)(S[a] + base), hi = *(const float4*)(S[a] + base + 4);
+        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+#pragma unroll
+        for (int j = 4; j > 0; j >>= 1)
+#pragma unroll
+          for (int i = 0; i < 8; i++)
+            if ((i & j) == 0) cswap(v[i], v[i | j], up);
+        *(float4*)(S[a] + base) = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(S[a] + base + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    }
+    __syncthreads();
+  }
 }
 
 __device__ int block_sum_int(int v, int* red) {
@@ -54,6 +123,25 @@ __device__ int block_sum_int(int v, int* red) {
   return t;
 }
 
+// lower_bound / upper_bound in an ascending LDS array
+__device__ __forceinline__ void bounds(const float* S, int n, float x, int& lo, int& hi) {
+  int a = 0, b = n;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (S[mid] < x) a = mid + 1;
+    else b = mid;
+  }
+  lo = a;
+  b = n;
+  while (a < b) {
+    const int mid = (a + b) >> 1;
+    if (S[mid] <= x) a = mid + 1;
+    else b = mid;
+  }
+  hi = a;
+}
+
+// dynamic LDS: 4 arrays of P floats (3 sorted axes + the subsample)
 __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
@@ -61,9 +149,9 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
                                                   const float* __restrict__ op,
                                                   const uint8_t* __restrict__ ov,
                                                   const int* __restrict__ ooff,
-                                                  const int* __restrict__ olen,
+                                                  const int* __restrict__ olen, int Pmax,
                                                   eao_np_stats* __restrict__ out) {
-  __shared__ float S[NP_MAXN];
+  extern __shared__ __attribute__((aligned(16))) float dsm[];
   __shared__ int red[8];
   __shared__ int wpos[4];
   const int p = blockIdx.x, t = threadIdx.x;
@@ -83,56 +171,48 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   r.n = nvalid;
   for (int a = 0; a < 3; a++) r.w[a] = r.cnt_gt[a] = r.cnt_lt[a] = r.cnt_eq[a] = 0.f;
   r.r1 = r.r2 = 0.f;
-  if (m < 20 || nvalid < 20 || nvalid > NP_MAXN) {
+  int P = 8;
+  while (P < nvalid) P <<= 1;
+  if (m < 20 || nvalid < 20 || nvalid > NP_MAXN || P > Pmax) {
     if (t == 0) {
-      r.verdict = m < 20 ? 0 : (nvalid > NP_MAXN ? -1 : 2);
+      r.verdict = m < 20 ? 0 : ((nvalid > NP_MAXN || P > Pmax) ? -1 : 2);
       out[p] = r;
     }
     return;
   }
+  float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
+  float* T = dsm + 3 * Pmax;
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
-  int P = 1;
-  while (P < nvalid) P <<= 1;
+  // compact the valid object points (order irrelevant: sorted next)
+  if (t == 0) wpos[0] = 0;
+  __syncthreads();
+  for (int i = t; i < nt; i += 256)
+    if (OV[i]) {
+      const int d = atomicAdd(&wpos[0], 1);
+      S[0][d] = O[3 * i];
+      S[1][d] = O[3 * i + 1];
+      S[2][d] = O[3 * i + 2];
+    }
+  for (int i = nvalid + t; i < P; i += 256) S[0][i] = S[1][i] = S[2][i] = INFINITY;
+  __syncthreads();
+  block_sort3(S[0], S[1], S[2], P);
   for (int a = 0; a < 3; a++) {
-    // compact valid coordinates of axis a (order irrelevant: sorted next)
-    if (t == 0) wpos[0] = 0;
-    __syncthreads();
-    for (int i = t; i < nt; i += 256)
-      if (OV[i]) S[atomicAdd(&wpos[0], 1)] = O[3 * i + a];
-    for (int i = nvalid + t; i < P; i += 256) S[i] = INFINITY;
-    __syncthreads();
-    block_bitonic_sort(S, P);
-    if (sub) {
-      // x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-794)
-      float v[NP_MAXN / 256 + 1];
-      int c = 0;
-      for (int k = t; k < nsamp; k += 256) v[c++] = S[k * step];
+    const float* srt = S[a];
+    if (sub) {  // x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-794)
+      for (int k = t; k < nsamp; k += 256) T[k] = S[a][k * step];
       __syncthreads();
-      c = 0;
-      for (int k = t; k < nsamp; k += 256) S[k] = v[c++];
-      __syncthreads();
+      srt = T;
     }
     int gt = 0, lt = 0, eq = 0;
     for (int i = t; i < mt; i += 256) {
       if (!FV[i]) continue;
-      const float x = F[3 * i + a];
-      int lo = 0, hi = nsamp;  // lower_bound
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (S[mid] < x) lo = mid + 1;
-        else hi = mid;
-      }
-      int lo2 = lo, hi2 = nsamp;  // upper_bound
-      while (lo2 < hi2) {
-        const int mid = (lo2 + hi2) >> 1;
-        if (S[mid] <= x) lo2 = mid + 1;
-        else hi2 = mid;
-      }
+      int lo, hi;
+      bounds(srt, nsamp, F[3 * i + a], lo, hi);
       gt += lo;
-      eq += lo2 - lo;
-      lt += nsamp - lo2;
+      eq += hi - lo;
+      lt += nsamp - hi;
     }
     gt = block_sum_int(gt, red);
     lt = block_sum_int(lt, red);
@@ -140,7 +220,6 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
     r.cnt_gt[a] = (float)gt;
     r.cnt_lt[a] = (float)lt;
     r.cnt_eq[a] = (float)eq;
-    __syncthreads();
   }
   if (t == 0) {
     const int n = nsamp;
@@ -241,6 +320,17 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 // lanes' data dependencies has to be prevented.
 #define WAVE_FENCE() __asm__ volatile("" ::: "memory")
 
+// in-kernel phase stamps of k_iforest_tree (workgroup (0,0)), read through
+// eao_debug_iforest_stamps: development instrumentation, a few SALU ops
+__device__ unsigned long long g_if_stamp[12];
+__device__ __forceinline__ void if_stamp(int k) {
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    g_if_stamp[k] = t;
+  }
+}
+
 // std::mt19937 for one wave: state in LDS, tempered outputs buffered one per
 // lane in a VGPR and handed out in stream order with v_readlane.
 struct WaveRng {
@@ -332,6 +422,33 @@ __device__ __forceinline__ double iforest_c(uint32_t n) {  // CalculateC, isolat
   return 0.0;
 }
 
+template <int C>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+}
+// wave-wide min and max (uniform results): DPP within rows of 16, then the
+// four row results through v_readlane -- no LDS round trips
+__device__ __forceinline__ void wave_minmax(float& mn, float& mx) {
+  mn = fminf(mn, dppf<0xB1>(mn));  // quad_perm [1,0,3,2]
+  mx = fmaxf(mx, dppf<0xB1>(mx));
+  mn = fminf(mn, dppf<0x4E>(mn));  // quad_perm [2,3,0,1]
+  mx = fmaxf(mx, dppf<0x4E>(mx));
+  mn = fminf(mn, dppf<0x141>(mn));  // row_half_mirror
+  mx = fmaxf(mx, dppf<0x141>(mx));
+  mn = fminf(mn, dppf<0x140>(mn));  // row_mirror
+  mx = fmaxf(mx, dppf<0x140>(mx));
+  const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 0));
+  const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 16));
+  const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 32));
+  const float a3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 48));
+  const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0));
+  const float b1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16));
+  const float b2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32));
+  const float b3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48));
+  mn = fminf(fminf(a0, a1), fminf(a2, a3));
+  mx = fmaxf(fmaxf(b0, b1), fmaxf(b2, b3));
+}
+
 __host__ __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
@@ -344,11 +461,15 @@ struct IfLds {
     nodes = b1 + al16(12 * (size_t)S);
     right = nodes + al16(8 * 2 * (size_t)S);
     const size_t build_end = right + al16(2 * 2 * (size_t)S);
-    shuf = b1;  // shuffle scratch aliases B1 / nodes (dead until the build)
-    const size_t shuf_end = shuf + al16(2 * (size_t)N) + 2 * al16(4 * ((size_t)N + 1)) + al16(2 * (size_t)N);
+    // sampling scratch (p, head, next, ids) aliases B1 / nodes, dead until the build
+    shuf = b1;
+    const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
+                            al16(2 * (size_t)S);
     total = build_end > shuf_end ? build_end : shuf_end;
   }
 };
+
+#define IF_END 0xffffu
 
 // One workgroup (4 waves) per (tree, cloud): IsolationTree::Build of
 // isolation_forest.h:165-224,300-345 by wave 0 -- the libstdc++-11 draw stream
@@ -362,14 +483,18 @@ struct IfLds {
 // the final content of position k is the last step that wrote k,
 //   final(k)   = max{ j > k : p_j = k }   or else  f(p_k, k)  (k if p_k = k)
 //   f(q, t)    = max{ j in (q, t) : p_j = q } or else f(p_q, q) (q if p_q = q, 0 at q = 0)
-// resolved per lane from per-position writer lists.  Only the sample's set
+// resolved per thread from per-position writer lists.  Only the sample's set
 // matters to the build (min/max, counts and membership are order-free), so
 // the sampled coordinates are gathered straight into LDS and partitioned
-// between two ping-pong buffers by depth parity.
+// between two ping-pong buffers by depth parity; a node of <= 64 items builds
+// its whole subtree in registers (one item per lane, children as lane masks).
+//
+// mt_init: per tree, the mt19937 state after seeding and the first twist
+// (the seeds are fixed per forest, so it is computed once on the host).
 __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ pts,
                                                       const int* __restrict__ off,
                                                       const int* __restrict__ len,
-                                                      const uint32_t* __restrict__ seeds,
+                                                      const uint32_t* __restrict__ mt_init,
                                                       const uint32_t* __restrict__ sample,
                                                       int maxN, int maxS, int npts_total,
                                                       double* __restrict__ contrib) {
@@ -382,26 +507,31 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
   uint16_t* right = (uint16_t*)(smem + L.right);
   __shared__ int s_nodes_bad;
 
-  const int tr = blockIdx.x, c = blockIdx.y, ntrees = gridDim.x;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tr = blockIdx.x, c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nb = blockDim.x;
   const int n = len[c];
   const int psi = (int)sample[c];
   const float* P = pts + 3 * (long long)off[c];
   double* out = contrib + (long long)tr * npts_total + off[c];
-  if (n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS) {
-    for (int i = tid; i < n; i += blockDim.x) out[i] = __longlong_as_double(0x7ff8000000000000ll);
+  if (n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe) {
+    for (int i = tid; i < n; i += nb) out[i] = __longlong_as_double(0x7ff8000000000000ll);
     return;
   }
-
+  uint16_t* p = (uint16_t*)(smem + L.shuf);
+  uint32_t* head = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
+  uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
+  uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
+  if_stamp(0);
+  for (int i = tid; i < 624; i += nb) mts[i] = mt_init[624 * tr + i];
+  for (int q = tid; q < n; q += nb) head[q] = IF_END;
+  __syncthreads();
+  if_stamp(1);
+  WaveRng g;  // used by wave 0 only
+  g.mt = mts;
+  g.idx = 0;  // state already twisted once
+  g.bp = g.blen = 0;
   if (wave == 0) {
-    WaveRng g;
-    g.mt = mts;
-    g.seed(seeds[tr]);
     // ---- shuffle draws: positions p[j], j = 1..n-1
-    uint16_t* p = (uint16_t*)(smem + L.shuf);
-    uint32_t* start = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
-    uint32_t* fill = (uint32_t*)((unsigned char*)start + al16(4 * ((size_t)n + 1)));
-    uint16_t* items = (uint16_t*)((unsigned char*)fill + al16(4 * ((size_t)n + 1)));
     const bool even = (n % 2) == 0;
     const int nsteps = even ? n / 2 : (n - 1) / 2;
     int s = 0;
@@ -432,71 +562,76 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
       s += r;
       g.bp += r + (rm ? 1 : 0);  // a rejected draw is consumed; its step retries
     }
-    WAVE_FENCE();
-    // ---- writer lists: for position q the steps j > q with p_j = q
-    for (int q = lane; q <= n; q += 64) start[q] = 0;
-    WAVE_FENCE();
-    for (int j = 1 + lane; j < n; j += 64) {
-      const int q = p[j];
-      if (q != j) atomicAdd(&start[q], 1u);
-    }
-    WAVE_FENCE();
-    uint32_t carry = 0;
-    for (int b = 0; b <= n; b += 64) {
-      const int q = b + lane;
-      const uint32_t v = q <= n ? start[q] : 0u;
-      uint32_t inc = v;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)inc, o, 64);
-        if (lane >= o) inc += t;
+  }
+  __syncthreads();
+  if_stamp(2);
+  // ---- writer lists (unordered): for position q the steps j > q with p_j = q
+  for (int j = 1 + tid; j < n; j += nb) {
+    const int q = p[j];
+    if (q != j) nxt[j] = (uint16_t)atomicExch(&head[q], (uint32_t)j);
+  }
+  __syncthreads();
+  if_stamp(3);
+  // ---- sample = final content of positions [0, psi)
+  for (int k = tid; k < psi; k += nb) {
+    int q = k, t = n, id;
+    while (true) {
+      int m = -1;
+      for (uint32_t e = head[q]; e != IF_END; e = nxt[e])
+        if ((int)e < t && (int)e > m) m = (int)e;
+      if (m >= 0) {
+        id = m;
+        break;
       }
-      if (q <= n) {
-        start[q] = carry + inc - v;
-        fill[q] = carry + inc - v;
+      if (q == 0) {
+        id = 0;
+        break;
       }
-      carry += (uint32_t)__shfl((int)inc, 63, 64);
-    }
-    WAVE_FENCE();
-    for (int j = 1 + lane; j < n; j += 64) {
-      const int q = p[j];
-      if (q != j) items[atomicAdd(&fill[q], 1u)] = (uint16_t)j;
-    }
-    WAVE_FENCE();
-    // ---- sample = final content of positions [0, psi): gather into B0
-    for (int k = lane; k < psi; k += 64) {
-      int q = k, t = n, id;
-      while (true) {
-        int m = -1;
-        for (uint32_t e = start[q]; e < start[q + 1]; e++) {
-          const int j = items[e];
-          if (j < t && j > m) m = j;
-        }
-        if (m >= 0) {
-          id = m;
-          break;
-        }
-        if (q == 0) {
-          id = 0;
-          break;
-        }
-        const int pq = p[q];
-        if (pq == q) {
-          id = q;
-          break;
-        }
-        t = q;
-        q = pq;
+      const int pq = p[q];
+      if (pq == q) {
+        id = q;
+        break;
       }
-      B0[k] = P[3 * id];
-      B0[psi + k] = P[3 * id + 1];
-      B0[2 * psi + k] = P[3 * id + 2];
+      t = q;
+      q = pq;
     }
-    WAVE_FENCE();
+    ids[k] = (uint16_t)id;
+  }
+  __syncthreads();
+  if_stamp(4);
+  {
+    int k = tid;
+    for (; k + 3 * nb < psi; k += 4 * nb) {
+      float v[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const float* q = P + 3 * (size_t)ids[k + u * nb];
+        v[u][0] = q[0];
+        v[u][1] = q[1];
+        v[u][2] = q[2];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        B0[k + u * nb] = v[u][0];
+        B0[psi + k + u * nb] = v[u][1];
+        B0[2 * psi + k + u * nb] = v[u][2];
+      }
+    }
+    for (; k < psi; k += nb) {
+      const float* q = P + 3 * (size_t)ids[k];
+      B0[k] = q[0];
+      B0[psi + k] = q[1];
+      B0[2 * psi + k] = q[2];
+    }
+  }
+  __syncthreads();
+  if_stamp(5);
+  if (wave == 0) {
     // ---- Node::Build in DFS pre-order; stack entry e lives in lane e
     const int maxDepth = (int)ceil(log2((double)psi));
     int sf = 0, sl = psi - 1, sd = 0, spar = -1;  // lane 0 = root
     int sp = 1, nn = 0, bad = 0;
-    while (sp > 0) {
+    while (sp > 0 && !bad) {
       sp--;
       const int first = __builtin_amdgcn_readlane(sf, sp);
       const int last = __builtin_amdgcn_readlane(sl, sp);
@@ -509,19 +644,73 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
       }
-      const uint32_t dim = g.lemire(3);
       const float* src = (depth & 1) ? B1 : B0;
+      if (cnt <= 64) {
+        // whole subtree in registers: item per lane, node sets as lane masks,
+        // pending right children on a lane-resident stack
+        const bool has = lane < cnt;
+        const float x = has ? src[first + lane] : 0.f;
+        const float y = has ? src[psi + first + lane] : 0.f;
+        const float z = has ? src[2 * psi + first + lane] : 0.f;
+        uint64_t mask = ballot(has);
+        int d = depth, node = me, ssp = 0;
+        int slo = 0, shi = 0, sdd = 0, spp = 0;
+        while (true) {
+          const int cn = popc64(mask);
+          bool leaf = cn < 2 || d >= maxDepth;
+          if (!leaf) {
+            const uint32_t dim = g.lemire(3);
+            const bool in = (mask >> lane) & 1ull;
+            const float v = dim == 0 ? x : (dim == 1 ? y : z);
+            float mn = in ? v : INFINITY, mx = in ? v : -INFINITY;
+            wave_minmax(mn, mx);
+            if (mn == mx) {
+              leaf = true;
+            } else {
+              const float split = g.uniform_real(mn, mx);
+              const uint64_t lm = ballot(in && v < split);
+              if (lm == 0) {
+                leaf = true;
+              } else {
+                const uint64_t rmk = mask & ~lm;
+                if (rmk == 0) bad = 1;  // empty right range: Node::Build fails
+                if (lane == 0) nodes[node] = make_uint2(dim + 1u, __float_as_uint(split));
+                if (lane == ssp) {
+                  slo = (int)(uint32_t)rmk;
+                  shi = (int)(uint32_t)(rmk >> 32);
+                  sdd = d + 1;
+                  spp = node;
+                }
+                ssp++;
+                mask = lm;  // left child next (node + 1)
+                d++;
+                node = nn++;
+                if (bad) break;
+                continue;
+              }
+            }
+          }
+          if (lane == 0) nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
+          if (ssp == 0) break;
+          ssp--;
+          mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(slo, ssp) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(shi, ssp) << 32);
+          d = __builtin_amdgcn_readlane(sdd, ssp);
+          const int par = __builtin_amdgcn_readlane(spp, ssp);
+          node = nn++;
+          if (lane == 0) right[par] = (uint16_t)node;
+        }
+        continue;
+      }
       float* dst = (depth & 1) ? B0 : B1;
+      const uint32_t dim = g.lemire(3);
       float mn = INFINITY, mx = -INFINITY;
       for (int i = first + lane; i <= last; i += 64) {
         const float v = src[dim * psi + i];
         mn = fminf(mn, v);
         mx = fmaxf(mx, v);
       }
-      for (int o = 32; o > 0; o >>= 1) {
-        mn = fminf(mn, __shfl_xor(mn, o, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-      }
+      wave_minmax(mn, mx);
       if (mn == mx) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
@@ -541,11 +730,11 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
         const bool lft = in && v < split;
         const uint64_t ml = ballot(lft), mr = ballot(in && !lft);
         if (in) {
-          const int d = lft ? first + nl + popc64(ml & lanes_below())
-                            : last - (nr + popc64(mr & lanes_below()));
-          dst[d] = x;
-          dst[psi + d] = y;
-          dst[2 * psi + d] = z;
+          const int dd = lft ? first + nl + popc64(ml & lanes_below())
+                             : last - (nr + popc64(mr & lanes_below()));
+          dst[dd] = x;
+          dst[psi + dd] = y;
+          dst[2 * psi + dd] = z;
         }
         nl += popc64(ml);
         nr += popc64(mr);
@@ -572,29 +761,62 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
         spar = -1;
       }
       sp += 2;
-      if (bad) break;
     }
     if (lane == 0) s_nodes_bad = bad;
+    if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
   }
   __syncthreads();
+  if_stamp(6);
   // ---- path length of every point of the cloud through this tree
   if (s_nodes_bad) {
-    for (int i = tid; i < n; i += blockDim.x) out[i] = __longlong_as_double(0x7ff8000000000000ll);
+    for (int i = tid; i < n; i += nb) out[i] = __longlong_as_double(0x7ff8000000000000ll);
     return;
   }
-  for (int i = tid; i < n; i += blockDim.x) {
-    const float x0 = P[3 * i], x1 = P[3 * i + 1], x2 = P[3 * i + 2];
-    int k = 0, depth = 0;
-    uint2 nd = nodes[0];
-    while ((nd.x & 3u) != 0u) {
-      const uint32_t d = nd.x & 3u;
-      const float v = d == 1u ? x0 : (d == 2u ? x1 : x2);
-      k = v < __uint_as_float(nd.y) ? k + 1 : (int)right[k];
-      nd = nodes[k];
-      depth++;
+  // four independent walks per thread in flight (LDS latency-bound chains)
+  for (int i0 = tid; i0 < n; i0 += 4 * nb) {
+    float x[4][3];
+    int k[4], depth[4];
+    uint2 nd[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = min(i0 + u * nb, n - 1);
+      x[u][0] = P[3 * i];
+      x[u][1] = P[3 * i + 1];
+      x[u][2] = P[3 * i + 2];
+      k[u] = 0;
+      depth[u] = 0;
     }
-    out[i] = (double)depth + iforest_c(nd.x >> 2);
+    const uint2 root = nodes[0];
+#pragma unroll
+    for (int u = 0; u < 4; u++) nd[u] = root;
+    bool any = (root.x & 3u) != 0u;
+    while (any) {
+      any = false;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t d = nd[u].x & 3u;
+        if (d != 0u) {
+          const float v = d == 1u ? x[u][0] : (d == 2u ? x[u][1] : x[u][2]);
+          k[u] = v < __uint_as_float(nd[u].y) ? k[u] + 1 : (int)right[k[u]];
+          depth[u]++;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if ((nd[u].x & 3u) != 0u) {
+          nd[u] = nodes[k[u]];
+          any |= (nd[u].x & 3u) != 0u;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * nb;
+      if (i < n) out[i] = (double)depth[u] + iforest_c(nd[u].x >> 2);
+    }
   }
+  __syncthreads();
+  if_stamp(7);
 }
 
 // score = 2^(-E[h(x)] / c(psi)), E[h] summed over the trees in order
@@ -609,6 +831,7 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
   if (i >= len[c]) return;
   const long long g = (long long)off[c] + i;
   double total = 0;
+#pragma unroll 10
   for (int t = 0; t < ntrees; t++) total += contrib[(long long)t * npts_total + g];
   const double avg = total / (double)ntrees;
   scores[g] = pow(2.0, -avg / iforest_c(sample[c]));
@@ -631,7 +854,7 @@ int AssocEngine::init(int device, int mp) {
   EAO_HIP_CHECK(hipMalloc(&d_rect, sizeof(int) * 4 * max_pairs));
   EAO_HIP_CHECK(hipMalloc(&d_ok, max_pairs));
   EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16));
-  EAO_HIP_CHECK(hipMalloc(&d_seeds, sizeof(uint32_t) * max_trees));
+  EAO_HIP_CHECK(hipMalloc(&d_mtinit, sizeof(uint32_t) * 624 * max_trees));
   EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)mp));
   EAO_HIP_CHECK(hipMalloc(&d_contrib, sizeof(double) * (size_t)mp * max_trees));
   hipDeviceProp_t prop;
@@ -641,7 +864,7 @@ int AssocEngine::init(int device, int mp) {
 }
 
 AssocEngine::~AssocEngine() {
-  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_seeds, d_scores, d_contrib};
+  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_mtinit, d_scores, d_contrib};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -650,28 +873,37 @@ AssocEngine::~AssocEngine() {
 int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                           const int* d_flen, const float* d_op, const uint8_t* d_ov,
                           const int* d_ooff, const int* d_olen, eao_np_stats* d_out,
-                          hipStream_t s) {
+                          hipStream_t s, int max_olen) {
   if (npairs <= 0) return EAO_OK;
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), 0, s, d_fp, d_fv, d_foff, d_flen, d_op,
-                     d_ov, d_ooff, d_olen, d_out);
+  int P = 8;
+  while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), sizeof(float) * 4 * P, s, d_fp, d_fv, d_foff,
+                     d_flen, d_op, d_ov, d_ooff, d_olen, P, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
 
 // IsolationForest::Build: per-tree seeds are the raw draws of mt19937(seed)
-// (uniform_int<uint32>(0, UINT32_MAX), isolation_forest.h:463-474)
-static void forest_seeds(uint32_t seed, uint32_t trees, std::vector<uint32_t>& out) {
-  uint32_t mt[624];
-  mt[0] = seed;
+// (uniform_int<uint32>(0, UINT32_MAX), isolation_forest.h:463-474); each
+// tree's generator is returned as its state after seeding and the first twist
+static void mt_twist(uint32_t* mt) {
+  for (int k = 0; k < 624; k++) {
+    const uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
+    mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+  }
+}
+static void mt_seed(uint32_t* mt, uint32_t s) {
+  mt[0] = s;
   for (int i = 1; i < 624; i++) mt[i] = 1812433253u * (mt[i - 1] ^ (mt[i - 1] >> 30)) + (uint32_t)i;
+}
+static void forest_states(uint32_t seed, uint32_t trees, std::vector<uint32_t>& out) {
+  uint32_t mt[624];
+  mt_seed(mt, seed);
   int idx = 624;
-  out.resize(trees);
+  out.resize((size_t)624 * trees);
   for (uint32_t t = 0; t < trees; t++) {
     if (idx >= 624) {
-      for (int k = 0; k < 624; k++) {
-        uint32_t y = (mt[k] & 0x80000000u) | (mt[(k + 1) % 624] & 0x7fffffffu);
-        mt[k] = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
+      mt_twist(mt);
       idx = 0;
     }
     uint32_t y = mt[idx++];
@@ -679,7 +911,9 @@ static void forest_seeds(uint32_t seed, uint32_t trees, std::vector<uint32_t>& o
     y ^= (y << 7) & 0x9d2c5680u;
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
-    out[t] = y;
+    uint32_t* st = out.data() + (size_t)624 * t;
+    mt_seed(st, y);
+    mt_twist(st);
   }
 }
 
@@ -697,14 +931,15 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     return EAO_E_CAPACITY;
   }
   if (seed != cached_seed || trees != cached_trees) {
-    std::vector<uint32_t> sd;
-    forest_seeds(seed, trees, sd);
-    EAO_HIP_CHECK(hipMemcpyAsync(d_seeds, sd.data(), sizeof(uint32_t) * trees, hipMemcpyHostToDevice, s));
+    std::vector<uint32_t> st;
+    forest_states(seed, trees, st);
+    EAO_HIP_CHECK(hipMemcpyAsync(d_mtinit, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, s));
+    EAO_HIP_CHECK(hipStreamSynchronize(s));  // st is pageable and about to go out of scope
     cached_seed = seed;
     cached_trees = trees;
   }
   hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(256), L.total, s, pts, off, len,
-                     d_seeds, d_sample, maxN, maxS, npts_total, d_contrib);
+                     d_mtinit, d_sample, maxN, maxS, npts_total, d_contrib);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
                      d_sample, (int)trees, npts_total, (const double*)d_contrib, scores);
@@ -787,8 +1022,10 @@ int eao_np_test_batch(eao_assoc* a, int npairs, const float* frame_pts, const ui
   EAO_HIP_CHECK(hipMemcpyAsync(m + e.max_pairs, frame_len, sizeof(int) * npairs, hipMemcpyHostToDevice, s));
   EAO_HIP_CHECK(hipMemcpyAsync(m + 2 * e.max_pairs, obj_off, sizeof(int) * npairs, hipMemcpyHostToDevice, s));
   EAO_HIP_CHECK(hipMemcpyAsync(m + 3 * e.max_pairs, obj_len, sizeof(int) * npairs, hipMemcpyHostToDevice, s));
+  int max_olen = 0;
+  for (int p = 0; p < npairs; p++) max_olen = std::max(max_olen, (int)obj_len[p]);
   int rc = e.np_batch(npairs, dF, vF, m, m + e.max_pairs, dO, vO, m + 2 * e.max_pairs,
-                      m + 3 * e.max_pairs, e.d_np, s);
+                      m + 3 * e.max_pairs, e.d_np, s, max_olen);
   if (rc) return rc;
   EAO_HIP_CHECK(hipMemcpyAsync(out, e.d_np, sizeof(eao_np_stats) * npairs, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
@@ -847,6 +1084,12 @@ int eao_project_rects(eao_assoc* a, const eao_camera* cam, const float* Tcw, int
   EAO_HIP_CHECK(hipMemcpyAsync(rect, e.d_rect, sizeof(int) * 4 * nclouds, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipMemcpyAsync(ok, e.d_ok, nclouds, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return EAO_OK;
+}
+
+int eao_debug_iforest_stamps(uint64_t* out12) {
+  if (!out12) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_if_stamp), sizeof(uint64_t) * 12));
   return EAO_OK;
 }
 

@@ -20,11 +20,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -46,9 +48,9 @@ struct IRect {
   IRect(int a, int b, int c, int d) : x(a), y(b), w(c), h(d) {}
   int area() const { return w * h; }
   bool contains_f(float u, float v) const {  // Rect::contains(Point(cvRound(u), cvRound(v)))
-    const int px = (int)lrintf(u), py = (int)lrintf(v);
-    return x <= px && px < x + w && y <= py && py < y + h;
+    return contains_i((int)lrintf(u), (int)lrintf(v));
   }
+  bool contains_i(int px, int py) const { return x <= px && px < x + w && y <= py && py < y + h; }
 };
 inline IRect rect_trunc(float x, float y, float w, float h) { return IRect((int)x, (int)y, (int)w, (int)h); }
 inline IRect rect_and(const IRect& a, const IRect& b) {
@@ -89,7 +91,19 @@ struct MapPt {
   float pos[3] = {0, 0, 0};
   bool bad = false;
   float fu = 0, fv = 0;  // MapPoint::feature (current-frame keypoint)
-  std::map<int, int> votes;  // object_id_vector
+  float pu = 0, pv = 0;  // projection under the current pose (cached per pose epoch)
+  unsigned proj_epoch = 0;
+  // object_id_vector: a handful of (object id, count) entries per point,
+  // only ever looked up (never iterated), so a flat vector suffices
+  std::vector<std::pair<int, int>> votes;
+  int* vote_of(int id) {
+    for (auto& v : votes)
+      if (v.first == id) return &v.second;
+    return nullptr;
+  }
+  void vote_insert(int id, int c) {  // std::map::insert: no-op if present
+    if (!vote_of(id)) votes.push_back({id, c});
+  }
 };
 
 struct Obj;
@@ -167,11 +181,18 @@ void se3_apply(const double q[4], const double t[3], const double v[3], double o
   qrot(q, v, r);
   for (int a = 0; a < 3; a++) o[a] = r[a] + t[a];
 }
-void se3_inv_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
-  const double qc[4] = {q[0], -q[1], -q[2], -q[3]};
+// SE3Quat::inverse(): (conj(q), -(conj(q) * t))
+void se3_inverse(const double q[4], const double t[3], double qc[4], double ti[3]) {
+  qc[0] = q[0];
+  qc[1] = -q[1];
+  qc[2] = -q[2];
+  qc[3] = -q[3];
   const double mt[3] = {t[0] * -1., t[1] * -1., t[2] * -1.};
-  double ti[3];
   qrot(qc, mt, ti);
+}
+void se3_inv_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
+  double qc[4], ti[3];
+  se3_inverse(q, t, qc, ti);
   se3_apply(qc, ti, v, o);
 }
 
@@ -190,6 +211,48 @@ struct PosHash {
     return (size_t)(h ^ (h >> 29));
   }
 };
+// open-addressing set of PosKeys, reused across calls (generation stamps
+// instead of clearing)
+struct PosSet {
+  std::vector<PosKey> key;
+  std::vector<uint32_t> gen;
+  uint32_t cur = 0;
+  size_t mask = 0;
+  void reset(size_t n) {
+    size_t cap = 64;
+    while (cap < 2 * n + 16) cap <<= 1;
+    if (cap > key.size()) {
+      key.assign(cap, PosKey{0, 0, 0});
+      gen.assign(cap, 0);
+      cur = 0;
+    }
+    mask = key.size() - 1;
+    if (++cur == 0) {
+      std::fill(gen.begin(), gen.end(), 0);
+      cur = 1;
+    }
+  }
+  // returns true if k was inserted (absent before)
+  bool insert(const PosKey& k) {
+    size_t h = PosHash()(k) & mask;
+    while (gen[h] == cur) {
+      if (key[h] == k) return false;
+      h = (h + 1) & mask;
+    }
+    gen[h] = cur;
+    key[h] = k;
+    return true;
+  }
+  bool contains(const PosKey& k) const {
+    size_t h = PosHash()(k) & mask;
+    while (gen[h] == cur) {
+      if (key[h] == k) return true;
+      h = (h + 1) & mask;
+    }
+    return false;
+  }
+};
+
 bool pos_key(const float* p, PosKey& k) {
   uint32_t u[3];
   for (int i = 0; i < 3; i++) {
@@ -211,58 +274,85 @@ class ReplayEngine {
   CamDev camdev;
   bool biForest = true;  // Object.cc:31 (sticky)
   std::vector<std::unique_ptr<Obj>> objs;
+  // map points by id: dense table for ids in [0, 2^24), a map beyond
+  std::vector<std::unique_ptr<MapPt>> mps_dense;
   std::map<int, std::unique_ptr<MapPt>> mps;
+  PosSet posset;
+  unsigned epoch = 1;  // bumped whenever the pose changes
+  void proj_pt(MapPt* p, float& u, float& v) {
+    if (p->proj_epoch != epoch) {
+      pz.proj(p->pos, p->pu, p->pv);
+      p->proj_epoch = epoch;
+    }
+    u = p->pu;
+    v = p->pv;
+  }
+  MapPt* mappoint(int id) {
+    if (id >= 0 && id < (1 << 24)) {
+      if ((size_t)id >= mps_dense.size()) mps_dense.resize(std::max((size_t)id + 1, mps_dense.size() * 2));
+      std::unique_ptr<MapPt>& u = mps_dense[id];
+      if (!u) {
+        u.reset(new MapPt());
+        u->id = id;
+      }
+      return u.get();
+    }
+    std::unique_ptr<MapPt>& u = mps[id];
+    if (!u) {
+      u.reset(new MapPt());
+      u->id = id;
+    }
+    return u.get();
+  }
   std::vector<std::unique_ptr<Det>> dets;
   bool ini = false;
   long ini_frame = 0;
   unsigned long cur = 0;
-  // GPU staging (pinned host + device)
-  std::vector<float> h_pts;
-  std::vector<uint8_t> h_valid;
-  std::vector<int> h_meta;
-  float* d_pts = nullptr;
-  uint8_t* d_valid = nullptr;
-  int* d_meta = nullptr;
-  eao_np_stats* d_np = nullptr;
-  double* d_scores = nullptr;
-  int* d_rect = nullptr;
-  uint8_t* d_ok = nullptr;
-  float* d_T = nullptr;
-  int cap_pts = 0, cap_pairs = 0;
+  // GPU staging: pinned host buffers and device mirrors, so every launch is
+  // one packed upload + one download on the association stream
+  unsigned char *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
+  size_t cap_in = 0, cap_out = 0;
   // per frame NP results: (det index, object index) -> stats
   std::map<std::pair<int, int>, eao_np_stats> np_cache;
   std::vector<char> odirty;  // objects modified in this frame (NP cache invalid)
+  // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
+  double prof[24] = {0};
+  static double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  struct Tick {
+    double* acc;
+    double t0;
+    Tick(double* a) : acc(a), t0(now_us()) {}
+    ~Tick() { *acc += now_us() - t0; }
+  };
 
   ~ReplayEngine() {
-    void* ps[] = {d_pts, d_valid, d_meta, d_np, d_scores, d_rect, d_ok, d_T};
-    for (void* p : ps)
-      if (p) (void)hipFree(p);
+    if (h_in) (void)hipHostFree(h_in);
+    if (h_out) (void)hipHostFree(h_out);
+    if (d_in) (void)hipFree(d_in);
+    if (d_out) (void)hipFree(d_out);
   }
 
-  int reserve(int npts, int npairs) {
-    if (npts > cap_pts) {
-      const int c = std::max(npts, cap_pts * 2);
-      if (d_pts) (void)hipFree(d_pts);
-      if (d_valid) (void)hipFree(d_valid);
-      if (d_scores) (void)hipFree(d_scores);
-      EAO_HIP_CHECK(hipMalloc(&d_pts, sizeof(float) * 3 * (size_t)c));
-      EAO_HIP_CHECK(hipMalloc(&d_valid, (size_t)c));
-      EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)c));
-      cap_pts = c;
+  static size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+  // capacity of the staging buffers (the stream is idle between launches)
+  int stage(size_t in_bytes, size_t out_bytes) {
+    if (in_bytes > cap_in) {
+      const size_t c = std::max(in_bytes, 2 * cap_in);
+      if (h_in) (void)hipHostFree(h_in);
+      if (d_in) (void)hipFree(d_in);
+      EAO_HIP_CHECK(hipHostMalloc((void**)&h_in, c, 0));
+      EAO_HIP_CHECK(hipMalloc((void**)&d_in, c));
+      cap_in = c;
     }
-    if (npairs > cap_pairs) {
-      const int c = std::max(npairs, std::max(64, cap_pairs * 2));
-      if (d_meta) (void)hipFree(d_meta);
-      if (d_np) (void)hipFree(d_np);
-      if (d_rect) (void)hipFree(d_rect);
-      if (d_ok) (void)hipFree(d_ok);
-      EAO_HIP_CHECK(hipMalloc(&d_meta, sizeof(int) * 8 * (size_t)c));
-      EAO_HIP_CHECK(hipMalloc(&d_np, sizeof(eao_np_stats) * (size_t)c));
-      EAO_HIP_CHECK(hipMalloc(&d_rect, sizeof(int) * 4 * (size_t)c));
-      EAO_HIP_CHECK(hipMalloc(&d_ok, (size_t)c));
-      cap_pairs = c;
+    if (out_bytes > cap_out) {
+      const size_t c = std::max(out_bytes, 2 * cap_out);
+      if (h_out) (void)hipHostFree(h_out);
+      if (d_out) (void)hipFree(d_out);
+      EAO_HIP_CHECK(hipHostMalloc((void**)&h_out, c, 0));
+      EAO_HIP_CHECK(hipMalloc((void**)&d_out, c));
+      cap_out = c;
     }
-    if (!d_T) EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16));
     return EAO_OK;
   }
 
@@ -330,10 +420,12 @@ class ReplayEngine {
     }
     update_pose(o);
     float omn[3] = {INFINITY, INFINITY, INFINITY}, omx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    double qi[4], ti[3];  // pose inverse, identical for every point
+    se3_inverse(o->q, o->t, qi, ti);
     for (MapPt* p : o->pts) {
       const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
       double r[3];
-      se3_inv_apply(o->q, o->t, v, r);
+      se3_apply(qi, ti, v, r);
       for (int a = 0; a < 3; a++) {
         const float f = (float)r[a];
         omn[a] = std::min(omn[a], f);
@@ -382,6 +474,7 @@ class ReplayEngine {
   int touch(Obj* o) { return o->pending ? flush_list({o}) : EAO_OK; }
 
   int flush_list(const std::vector<Obj*>& todo) {
+    Tick tk(&prof[3]);
     size_t i = 0;
     while (i < todo.size()) {
       std::vector<Obj*> batch;
@@ -405,34 +498,35 @@ class ReplayEngine {
         }
       }
       if (batch.empty()) continue;
-      int rc = reserve(np, (int)batch.size());
-      if (rc) return rc;
-      h_pts.resize(3 * (size_t)np);
-      h_meta.assign(3 * batch.size(), 0);
-      int off = 0;
-      for (size_t b = 0; b < batch.size(); b++) {
-        Obj* o = batch[b];
-        h_meta[b] = off;
-        h_meta[batch.size() + b] = (int)o->pts.size();
-        h_meta[2 * batch.size() + b] = (int)((int)o->pts.size() / 2);
-        for (MapPt* p : o->pts)
-          std::memcpy(&h_pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
-      }
       const int nb = (int)batch.size();
-      EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * np, hipMemcpyHostToDevice, A->stream));
-      EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 3 * nb, hipMemcpyHostToDevice, A->stream));
-      int maxN = 0;
-      for (Obj* o : batch) maxN = std::max(maxN, (int)o->pts.size());
-      rc = A->iforest_batch(nb, d_pts, d_meta, d_meta + nb, 50, 12345, (const uint32_t*)(d_meta + 2 * nb),
-                            d_scores, A->stream, maxN, maxN / 2, np);
+      const size_t o_pts = al16(sizeof(int) * 3 * nb);
+      int rc = stage(o_pts + sizeof(float) * 3 * (size_t)np, sizeof(double) * (size_t)np);
       if (rc) return rc;
-      std::vector<double> sc(np);
-      EAO_HIP_CHECK(hipMemcpyAsync(sc.data(), d_scores, sizeof(double) * np, hipMemcpyDeviceToHost, A->stream));
+      int* meta = (int*)h_in;
+      float* pts = (float*)(h_in + o_pts);
+      int off = 0, maxN = 0;
+      for (int b = 0; b < nb; b++) {
+        Obj* o = batch[b];
+        meta[b] = off;
+        meta[nb + b] = (int)o->pts.size();
+        meta[2 * nb + b] = (int)((int)o->pts.size() / 2);
+        maxN = std::max(maxN, (int)o->pts.size());
+        for (MapPt* p : o->pts) std::memcpy(&pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
+      }
+      prof[2] += 1;
+      EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, o_pts + sizeof(float) * 3 * (size_t)np, hipMemcpyHostToDevice,
+                                   A->stream));
+      const int* dmeta = (const int*)d_in;
+      rc = A->iforest_batch(nb, (const float*)(d_in + o_pts), dmeta, dmeta + nb, 50, 12345,
+                            (const uint32_t*)(dmeta + 2 * nb), (double*)d_out, A->stream, maxN, maxN / 2, np);
+      if (rc) return rc;
+      EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(double) * np, hipMemcpyDeviceToHost, A->stream));
       EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+      const double* sc = (const double*)h_out;
       for (size_t b = 0; b < batch.size(); b++) {
         Obj* o = batch[b];
         const float th = o->cls == 62 ? 0.65f : 0.6f;
-        const double* s = sc.data() + h_meta[b];
+        const double* s = sc + meta[b];
         size_t w = 0;
         const size_t n = o->pts.size();
         for (size_t k = 0; k < n; k++) {
@@ -456,7 +550,7 @@ class ReplayEngine {
     float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
     for (MapPt* p : o->pts) {
       float u, v;
-      pz.proj(p->pos, u, v);
+      proj_pt(p, u, v);
       xmn = std::min(xmn, u);
       xmx = std::max(xmx, u);
       ymn = std::min(ymn, v);
@@ -472,30 +566,34 @@ class ReplayEngine {
   // step 10.1 for all recent objects: one k_rects launch
   int project_rects_gpu(const std::vector<Obj*>& list) {
     if (list.empty()) return EAO_OK;
+    Tick tk(&prof[7]);
+    prof[6] += 1;
+    const int nb = (int)list.size();
     int np = 0;
     for (Obj* o : list) np += (int)o->pts.size();
-    int rc = reserve(std::max(np, 1), (int)list.size());
+    // in: meta [2 nb] | Tcw [16] | points; out: rects [4 nb] | ok [nb]
+    const size_t o_T = al16(sizeof(int) * 2 * nb), o_pts = o_T + sizeof(float) * 16;
+    const size_t in_bytes = o_pts + sizeof(float) * 3 * (size_t)np;
+    int rc = stage(in_bytes, sizeof(int) * 4 * nb + nb);
     if (rc) return rc;
-    h_pts.resize(3 * (size_t)std::max(np, 1));
-    h_meta.assign(2 * list.size(), 0);
+    int* meta = (int*)h_in;
+    float* pts = (float*)(h_in + o_pts);
+    std::memcpy(h_in + o_T, pz.T, sizeof(float) * 16);
     int off = 0;
-    for (size_t b = 0; b < list.size(); b++) {
-      h_meta[b] = off;
-      h_meta[list.size() + b] = (int)list[b]->pts.size();
-      for (MapPt* p : list[b]->pts)
-        std::memcpy(&h_pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
+    for (int b = 0; b < nb; b++) {
+      meta[b] = off;
+      meta[nb + b] = (int)list[b]->pts.size();
+      for (MapPt* p : list[b]->pts) std::memcpy(&pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
     }
-    const int nb = (int)list.size();
-    EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * std::max(np, 1), hipMemcpyHostToDevice, A->stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 2 * nb, hipMemcpyHostToDevice, A->stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(d_T, pz.T, sizeof(float) * 16, hipMemcpyHostToDevice, A->stream));
-    rc = A->rects(camdev, d_T, nb, d_pts, d_meta, d_meta + nb, d_rect, d_ok, A->stream);
+    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
+    const int* dmeta = (const int*)d_in;
+    rc = A->rects(camdev, (const float*)(d_in + o_T), nb, (const float*)(d_in + o_pts), dmeta, dmeta + nb,
+                  (int*)d_out, d_out + sizeof(int) * 4 * nb, A->stream);
     if (rc) return rc;
-    std::vector<int> r(4 * nb);
-    std::vector<uint8_t> ok(nb);
-    EAO_HIP_CHECK(hipMemcpyAsync(r.data(), d_rect, sizeof(int) * 4 * nb, hipMemcpyDeviceToHost, A->stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(ok.data(), d_ok, nb, hipMemcpyDeviceToHost, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(int) * 4 * nb + nb, hipMemcpyDeviceToHost, A->stream));
     EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    const int* r = (const int*)h_out;
+    const uint8_t* ok = h_out + sizeof(int) * 4 * nb;
     for (int b = 0; b < nb; b++)
       if (ok[b]) list[b]->proj = IRect(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
     return EAO_OK;
@@ -505,53 +603,61 @@ class ReplayEngine {
   int np_pairs(const std::vector<std::pair<Det*, Obj*>>& pairs, const std::vector<int>& di,
                const std::vector<int>& oi) {
     if (pairs.empty()) return EAO_OK;
-    // distinct detections / objects are uploaded once
-    std::map<Det*, int> doff;
-    std::map<Obj*, int> ooff;
-    int np = 0;
-    h_pts.clear();
-    h_valid.clear();
-    for (auto& pr : pairs) {
-      if (!doff.count(pr.first)) {
-        doff[pr.first] = np;
-        for (MapPt* p : pr.first->pts) {
-          h_pts.insert(h_pts.end(), p->pos, p->pos + 3);
-          h_valid.push_back(p->bad ? 0 : 1);  // out_point is never set (Q7)
-        }
-        np += (int)pr.first->pts.size();
-      }
-      if (!ooff.count(pr.second)) {
-        ooff[pr.second] = np;
-        for (MapPt* p : pr.second->pts) {
-          h_pts.insert(h_pts.end(), p->pos, p->pos + 3);
-          h_valid.push_back(p->bad ? 0 : 1);
-        }
-        np += (int)pr.second->pts.size();
-      }
-    }
+    Tick tk(&prof[5]);
+    prof[4] += 1;
     const int npairs = (int)pairs.size();
-    int rc = reserve(std::max(np, 1), npairs);
+    // distinct detections / objects are uploaded once
+    std::unordered_map<const void*, int> offs;
+    size_t total = 0;
+    for (auto& pr : pairs) {
+      if (offs.emplace(pr.first, (int)total).second) total += pr.first->pts.size();
+      if (offs.emplace(pr.second, (int)total).second) total += pr.second->pts.size();
+    }
+    // in: meta [4 npairs] | points [3 total] | valid [total]; out: stats [npairs]
+    const size_t o_pts = al16(sizeof(int) * 4 * npairs), o_val = o_pts + sizeof(float) * 3 * total;
+    const size_t in_bytes = o_val + total;
+    int rc = stage(in_bytes, sizeof(eao_np_stats) * npairs);
     if (rc) return rc;
-    h_meta.assign(4 * (size_t)npairs, 0);
+    int* meta = (int*)h_in;
+    float* pts = (float*)(h_in + o_pts);
+    uint8_t* valid = h_in + o_val;
+    auto put = [&](const void* key, const std::vector<MapPt*>& v) {
+      int o = offs[key];
+      for (MapPt* p : v) {
+        std::memcpy(&pts[3 * (size_t)o], p->pos, sizeof(float) * 3);
+        valid[o++] = p->bad ? 0 : 1;  // out_point is never set (Q7)
+      }
+    };
+    int max_olen = 0;
     for (int k = 0; k < npairs; k++) {
-      h_meta[k] = doff[pairs[k].first];
-      h_meta[npairs + k] = (int)pairs[k].first->pts.size();
-      h_meta[2 * npairs + k] = ooff[pairs[k].second];
-      h_meta[3 * npairs + k] = (int)pairs[k].second->pts.size();
-      if (h_meta[3 * npairs + k] > NP_MAXN) {
+      const auto& pr = pairs[k];
+      meta[k] = offs[pr.first];
+      meta[npairs + k] = (int)pr.first->pts.size();
+      meta[2 * npairs + k] = offs[pr.second];
+      meta[3 * npairs + k] = (int)pr.second->pts.size();
+      if (meta[3 * npairs + k] > NP_MAXN) {
         set_error("replay: object exceeds the NP kernel capacity");
         return EAO_E_CAPACITY;
       }
+      max_olen = std::max(max_olen, meta[3 * npairs + k]);
     }
-    EAO_HIP_CHECK(hipMemcpyAsync(d_pts, h_pts.data(), sizeof(float) * 3 * np, hipMemcpyHostToDevice, A->stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(d_valid, h_valid.data(), np, hipMemcpyHostToDevice, A->stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(d_meta, h_meta.data(), sizeof(int) * 4 * npairs, hipMemcpyHostToDevice, A->stream));
-    rc = A->np_batch(npairs, d_pts, d_valid, d_meta, d_meta + npairs, d_pts, d_valid, d_meta + 2 * npairs,
-                     d_meta + 3 * npairs, d_np, A->stream);
+    {
+      std::unordered_set<const void*> written;
+      for (auto& pr : pairs) {
+        if (written.insert(pr.first).second) put(pr.first, pr.first->pts);
+        if (written.insert(pr.second).second) put(pr.second, pr.second->pts);
+      }
+    }
+    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
+    const int* dmeta = (const int*)d_in;
+    const float* dpts = (const float*)(d_in + o_pts);
+    const uint8_t* dval = d_in + o_val;
+    rc = A->np_batch(npairs, dpts, dval, dmeta, dmeta + npairs, dpts, dval, dmeta + 2 * npairs,
+                     dmeta + 3 * npairs, (eao_np_stats*)d_out, A->stream, max_olen);
     if (rc) return rc;
-    std::vector<eao_np_stats> out(npairs);
-    EAO_HIP_CHECK(hipMemcpyAsync(out.data(), d_np, sizeof(eao_np_stats) * npairs, hipMemcpyDeviceToHost, A->stream));
+    EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(eao_np_stats) * npairs, hipMemcpyDeviceToHost, A->stream));
     EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    const eao_np_stats* out = (const eao_np_stats*)h_out;
     for (int k = 0; k < npairs; k++) np_cache[{di[k], oi[k]}] = out[k];
     return EAO_OK;
   }
@@ -570,9 +676,9 @@ class ReplayEngine {
   }
 
   static void vote(MapPt* p, int id) {
-    auto it = p->votes.find(id);
-    if (it != p->votes.end()) it->second += 1;
-    else p->votes[id] = 1;
+    int* v = p->vote_of(id);
+    if (v) *v += 1;
+    else p->votes.push_back({id, 1});
   }
   static void reobj(Obj* o, int id) {
     auto it = o->reobj.find(id);
@@ -596,7 +702,7 @@ class ReplayEngine {
       float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
       auto acc = [&](MapPt* p) {
         float u, v;
-        pz.proj(p->pos, u, v);
+        proj_pt(p, u, v);
         xmn = std::min(xmn, u);
         xmx = std::max(xmx, u);
         ymn = std::min(ymn, v);
@@ -622,8 +728,10 @@ class ReplayEngine {
       return false;
     mark_dirty(o);
     f->mnId = o->id;
-    std::unordered_set<PosKey, PosHash> have;
-    have.reserve(o->pts.size() * 2 + f->pts.size());
+    double qi[4], ti[3];  // cuboid pose inverse, the same for every point
+    se3_inverse(o->q, o->t, qi, ti);
+    PosSet& have = posset;
+    have.reset(o->pts.size() + f->pts.size());
     for (MapPt* q : o->pts) {
       PosKey k;
       if (pos_key(q->pos, k)) have.insert(k);
@@ -637,7 +745,7 @@ class ReplayEngine {
       if (o->frames.size() >= 10 && (o->cls == 56 || o->cls == 77)) {
         const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
         double s[3];
-        se3_inv_apply(o->q, o->t, v, s);
+        se3_apply(qi, ti, v, s);
         if (std::fabs(s[0]) > 1.2 * o->lenth / 2 || std::fabs(s[1]) > 1.2 * o->width / 2 ||
             std::fabs(s[2]) > 1.2 * o->height / 2)
           continue;
@@ -645,7 +753,7 @@ class ReplayEngine {
       vote(p, o->id);
       PosKey k;
       const bool finite = pos_key(p->pos, k);
-      if (!finite || !have.count(k)) {
+      if (!finite || !have.contains(k)) {
         o->pts.push_back(p);
         for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
         if (finite) have.insert(k);
@@ -656,13 +764,12 @@ class ReplayEngine {
       const size_t n = o->pts.size();
       for (size_t i = 0; i < n; i++) {
         MapPt* p = o->pts[i];
-        int votes = 0;
-        auto it = p->votes.find(o->id);
-        if (it != p->votes.end()) votes = it->second;
+        const int* vp = p->vote_of(o->id);
+        const int votes = vp ? *vp : 0;
         bool erase = false;
         if (votes <= 8) {
           float u, v;
-          pz.proj(p->pos, u, v);
+          proj_pt(p, u, v);
           if ((u > 0 && u < pz.cols) && (v > 0 && v < pz.rows) && !f->box.contains_f(u, v)) erase = true;
         }
         if (erase) {
@@ -888,7 +995,7 @@ class ReplayEngine {
       o->center[a] = f->pos[a];
     }
     for (MapPt* p : f->pts) {
-      p->votes.insert(std::make_pair(o->id, 1));
+      p->vote_insert(o->id, 1);
       o->pts.push_back(p);
     }
     f->mnId = o->id;
@@ -945,8 +1052,11 @@ class ReplayEngine {
 
   int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
             const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
+    Tick tk(&prof[0]);
+    prof[8] += 1;
     cur = fid;
     std::memcpy(pz.T, Tcw, sizeof(pz.T));
+    epoch++;
     np_cache.clear();
     std::vector<Det*> o2;
     int maxcls = 0;
@@ -964,17 +1074,12 @@ class ReplayEngine {
       dets.push_back(std::move(f));
     }
     odirty.assign(objs.size(), 0);
+    double tA = now_us();
     std::vector<MapPt*> tr(npts);
     for (int i = 0; i < npts; i++) {
-      auto it = mps.find(ids[i]);
-      MapPt* p;
-      if (it == mps.end()) {
-        p = new MapPt();
-        p->id = ids[i];
-        mps[ids[i]].reset(p);
-      } else
-        p = it->second.get();
+      MapPt* p = mappoint(ids[i]);
       for (int a = 0; a < 3; a++) p->pos[a] = pos[3 * i + a];
+      p->proj_epoch = 0;
       p->bad = bad ? bad[i] != 0 : false;
       tr[i] = p;
     }
@@ -982,14 +1087,17 @@ class ReplayEngine {
     for (int i = 0; i < npts; i++) {
       MapPt* p = tr[i];
       if (p->bad) continue;
+      const int px = (int)lrintf(uv[2 * i]), py = (int)lrintf(uv[2 * i + 1]);
       for (Det* f : o2)
-        if (f->box.contains_f(uv[2 * i], uv[2 * i + 1])) {
+        if (f->box.contains_i(px, py)) {
           p->fu = uv[2 * i];
           p->fv = uv[2 * i + 1];
           f->pts.push_back(p);
           for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
         }
     }
+    prof[12] += now_us() - tA;
+    tA = now_us();
     for (Det* f : o2) {  // STEP 4
       frame_mean(f);
       if (f->pts.size() >= 8) boxplot(f);
@@ -1069,7 +1177,7 @@ class ReplayEngine {
           o->center[a] = f->pos[a];
         }
         for (MapPt* p : f->pts) {
-          p->votes.insert(std::make_pair(o->id, 1));
+          p->vote_insert(o->id, 1);
           o->pts.push_back(p);
         }
         f->mnId = o->id;
@@ -1079,6 +1187,8 @@ class ReplayEngine {
         objs.push_back(std::move(o));
       }
     }
+    prof[13] += now_us() - tA;
+    tA = now_us();
     // STEP 10
     if ((long)fid > ini_frame && ini) {
       std::vector<Obj*> recent;
@@ -1112,6 +1222,8 @@ class ReplayEngine {
           if (rc) return rc;
         }
       }
+      prof[14] += now_us() - tA;
+      tA = now_us();
       for (Det* f : kept) {
         if (f->pts.size() < 5) {
           f->method = 6;
@@ -1120,6 +1232,8 @@ class ReplayEngine {
         rc = associate(f);
         if (rc) return rc;
       }
+      prof[15] += now_us() - tA;
+      tA = now_us();
       rc = flush(-1);
       if (rc) return rc;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
@@ -1181,22 +1295,25 @@ class ReplayEngine {
   }
 
   void merge(Obj* a, Obj* b) {  // Object_Map::MergeTwoMapObjs, Object.cc:1716-1902
-    std::unordered_set<PosKey, PosHash> have;
+    PosSet& have = posset;
+    have.reset(a->pts.size() + b->pts.size());
     for (MapPt* q : a->pts) {
       PosKey k;
       if (pos_key(q->pos, k)) have.insert(k);
     }
+    double qi[4], ti[3];
+    se3_inverse(a->q, a->t, qi, ti);
     for (MapPt* p : b->pts) {
       const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
       double s[3];
-      se3_inv_apply(a->q, a->t, v, s);
+      se3_apply(qi, ti, v, s);
       if (std::fabs(s[0]) > 1.1 * a->lenth / 2 || std::fabs(s[1]) > 1.1 * a->width / 2 ||
           std::fabs(s[2]) > 1.1 * a->height / 2)
         continue;
       vote(p, a->id);
       PosKey k;
       const bool finite = pos_key(p->pos, k);
-      if (!finite || !have.count(k)) {
+      if (!finite || !have.contains(k)) {
         a->pts.push_back(p);
         for (int c = 0; c < 3; c++) a->sum[c] += p->pos[c];
         if (finite) have.insert(k);
@@ -1330,6 +1447,7 @@ class ReplayEngine {
   }
 
   int local_mapping() {
+    Tick tk(&prof[1]);
     int rc = flush(-1);
     if (rc) return rc;
     for (auto& up : objs) {
@@ -1414,6 +1532,12 @@ int eao_replay_local_mapping(eao_replay* r) {
   if (!r) return EAO_E_ARG;
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   return r->r.local_mapping();
+}
+
+int eao_replay_profile(eao_replay* r, double* out12) {
+  if (!r || !out12) return EAO_E_ARG;
+  std::memcpy(out12, r->r.prof, sizeof(double) * 24);
+  return EAO_OK;
 }
 
 int eao_replay_num_objects(eao_replay* r) { return r ? (int)r->r.objs.size() : EAO_E_ARG; }

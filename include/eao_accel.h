@@ -209,6 +209,14 @@ int eao_replay_num_objects(eao_replay* r);
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats);
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
 
+/* development instrumentation: s_memtime stamps of the last isolation-forest
+   tree launch (workgroup (0,0)): [0..7] phase boundaries, [10] node count. */
+int eao_debug_iforest_stamps(uint64_t* out12);
+/* wall-clock profile of a replay (us): [0] frame total, [1] local mapping,
+   [2]/[3] iForest launches / time, [4]/[5] NP launches / time,
+   [6]/[7] rect launches / time, [8] frames, [12..15] frame sections. */
+int eao_replay_profile(eao_replay* r, double* out24);
+
 #ifdef __cplusplus
 }
 #endif

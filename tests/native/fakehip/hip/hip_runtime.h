@@ -20,6 +20,8 @@ inline const char* hipGetErrorString(hipError_t) { return "fake"; }
 inline hipError_t hipSetDevice(int) { return 0; }
 inline hipError_t hipMalloc(void* p, size_t n) { *(void**)p = std::malloc(n ? n : 1); return 0; }
 inline hipError_t hipFree(void* p) { std::free(p); return 0; }
+inline hipError_t hipHostMalloc(void** p, size_t n, unsigned) { *p = std::malloc(n ? n : 1); return 0; }
+inline hipError_t hipHostFree(void* p) { std::free(p); return 0; }
 inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, int, hipStream_t) { if (n) std::memmove(d, s, n); return 0; }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return 0; }
 inline hipError_t hipGetLastError() { return 0; }

@@ -20,7 +20,7 @@ CamDev make_cam(const eao_camera& c) {
 }
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
-                          eao_np_stats* out, hipStream_t) {
+                          eao_np_stats* out, hipStream_t, int) {
   for (int p = 0; p < npairs; p++) {
     orc_np_stats s;
     orc_np_test(flen[p], fp + 3 * foff[p], fv + foff[p], olen[p], op + 3 * ooff[p], ov + ooff[p], &s);

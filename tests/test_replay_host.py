@@ -62,7 +62,11 @@ class _HostReplay(ea.Replay):
         return self._with(super().objects)
 
     def close(self):
-        pass
+        if self.h:
+            self.H.eao_replay_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
 
 
 @pytest.mark.parametrize("flag", ["iForest", "None", "NP", "IoU", "NA"])
