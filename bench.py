@@ -46,6 +46,7 @@ import torch  # noqa: E402  (device memory, streams, torch.distributed: plumbing
 import torch.distributed as dist  # noqa: E402
 
 import eao_accel as ea  # noqa: E402
+import eao_dist  # noqa: E402
 from tools import synth  # noqa: E402
 
 W, H = 640, 480
@@ -106,9 +107,7 @@ def main():
     ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world, local = eao_dist.env_rank()
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -215,20 +214,14 @@ def main():
         step(None)
 
     rec = {"stage_ms": [], "match_ms": []}
-    if world > 1:
-        dist.barrier()
+    eao_dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step(rec)
-    if world > 1:
-        dist.barrier()
+    eao_dist.barrier()
     torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = eao_dist.max_over_ranks(time.perf_counter() - t0, dev)
 
     total_frames = F * args.steps * world
     ms_per_step = 1000.0 * elapsed / args.steps
