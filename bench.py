@@ -92,7 +92,7 @@ class Stream:
         self.poses = np.stack(poses).astype(np.float32)
         self.host_frames = frames
         self.d_frames = torch.from_numpy(np.stack(frames)).to(dev)
-        self.assoc = synth.assoc_stream(nframes, seed=0xEA1 + (seed - 0xEA0))
+        self.assoc = synth.assoc_stream_fr3(nframes, seed=0xEA1 + (seed - 0xEA0))
         self.n = nframes
 
 
@@ -255,8 +255,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (procedural textured plane along a smooth camera path + seeded object clouds / "
-                    "YOLO-shaped boxes; SURVEY.md §8d input 2)",
+            "data": "synthetic (procedural textured plane along a smooth camera path; seeded object clouds "
+                    "observed as ~8 YOLO-shaped boxes and ~800 tracked map points per frame; SURVEY.md §8d input 2)",
             "config": {"workload": "mono_tum EAO fr3_long_office 640x480 (synthetic, %d frames/rank/step, "
                                    "%d ORB features, 8 levels, assoc flag EAO=iForest ensemble)" % (F, NFEAT),
                        "frames_per_step": F, "features": NFEAT, "levels": NLEV, "parallelism": "frames%d" % world},

@@ -46,3 +46,8 @@ def test_replay_long_bad_points():
     for f in frames:
         f["bad"] = (rng.random(len(f["ids"])) < 0.01).astype(np.uint8)
     _run("iForest", frames, start=40)
+
+
+def test_replay_bench_stream_full():
+    """The benchmark's 405-frame fr3-shaped stream, EAO flag, end to end."""
+    _run("EAO", synth.assoc_stream_fr3(405))

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.join(ROOT, "eao-slam_amd", "python"))
 import eao_accel as ea  # noqa: E402
 from tools import synth  # noqa: E402
 
-frames = synth.assoc_stream(405)
+frames = synth.assoc_stream_fr3(405) if "dense" not in sys.argv else synth.assoc_stream(405)
 a = ea.Assoc()
 for rep in range(2):
     rp = ea.Replay(a, "EAO")

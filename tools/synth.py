@@ -121,6 +121,10 @@ def frame_stream(n, w=640, h=480, seed=0xEA0, step=0.004):
 # Class mix follows the reference's data/yolo_txts (39 bottle, 56 chair,
 # 73 book, 62 tv, 41 cup, 66 keyboard, 64 mouse, 77 teddy bear, 0 person).
 OFFICE_CLASSES = [39, 39, 39, 56, 56, 73, 73, 62, 41, 66, 64, 77, 0, 72]
+# the fr3_long_office shape of SURVEY.md §8d input 2: about 7 boxes per frame
+# (17,181 YOLO boxes over 2,585 frames), m = 5-300 points per box, about a
+# thousand tracked map points per frame (1000 ORB features)
+FR3_CLASSES = [39, 39, 56, 56, 73, 62, 41, 66, 64]
 CLASS_EXTENT = {39: (0.07, 0.07, 0.22), 56: (0.45, 0.45, 0.8), 73: (0.2, 0.05, 0.25),
                 62: (0.5, 0.08, 0.35), 41: (0.08, 0.08, 0.1), 66: (0.45, 0.15, 0.03),
                 64: (0.06, 0.1, 0.04), 77: (0.25, 0.2, 0.3), 0: (0.5, 0.3, 1.6), 72: (0.4, 0.3, 0.6)}
@@ -168,11 +172,11 @@ def assoc_scene(seed=0xEA1, classes=None, pts_range=(150, 600), n_background=800
 
 
 def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None, obs_frac=0.7,
-                 kf_every=5, pts_range=(150, 600)):
+                 kf_every=5, pts_range=(150, 600), n_background=800):
     """Per-frame replay inputs for the association path."""
     fx, fy, cx, cy = K
     rng = np.random.Generator(np.random.PCG64(seed + 1))
-    objs, P, owner = assoc_scene(seed, classes, pts_range)
+    objs, P, owner = assoc_scene(seed, classes, pts_range, n_background)
     frames = []
     for t in range(n_frames):
         a = -0.6 + 1.6 * t / max(1, n_frames - 1)
@@ -208,3 +212,9 @@ def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None,
         frames.append(dict(T=T, boxes=boxes, ids=obs.astype(np.int32), pos=P[obs],
                            uv=uv, bad=np.zeros(len(obs), np.uint8), kf=(t % kf_every == kf_every - 1)))
     return frames
+
+
+def assoc_stream_fr3(n_frames=405, seed=0xEA1):
+    """The benchmark's association workload (BASELINE configs[1], SURVEY §8d input 2)."""
+    return assoc_stream(n_frames, seed=seed, classes=FR3_CLASSES, obs_frac=0.5, pts_range=(80, 400),
+                        n_background=400)
