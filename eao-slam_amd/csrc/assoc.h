@@ -39,10 +39,13 @@ class AssocEngine {
   // device-level entry points (inputs already on device, stream s)
   int np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                const int* d_flen, const float* d_op, const uint8_t* d_ov, const int* d_ooff,
-               const int* d_olen, eao_np_stats* d_out, hipStream_t s, int max_olen);
+               const int* d_olen, eao_np_stats* d_out, hipStream_t s, int max_olen,
+               const double* d_oscore = nullptr, const float* d_oth = nullptr);
   int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
-                    hipStream_t s, int max_len, int max_sample, int npts_total);
+                    hipStream_t s, int max_len, int max_sample, int npts_total,
+                    double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
+                    double* scores2 = nullptr);  // optional second copy of the scores
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
 };

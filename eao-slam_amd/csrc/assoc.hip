@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <vector>
 
@@ -111,37 +112,46 @@ __device__ void block_sort3(float* S0, float* S1, float* S2, int P) {
   }
 }
 
-__device__ int block_sum_int(int v, int* red) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  int t = 0;
-  for (int i = 0; i < (int)(blockDim.x >> 6); i++) t += red[i];
-  __syncthreads();
-  return t;
-}
 
-// lower_bound / upper_bound in an ascending LDS array
-__device__ __forceinline__ void bounds(const float* S, int n, float x, int& lo, int& hi) {
+// lower_bound / upper_bound of x in the ascending virtual array S[0], S[step],
+// ..., S[(n-1)*step] (the NP subsample is never materialised)
+__device__ __forceinline__ void bounds(const float* S, int n, int step, float x, int& lo, int& hi) {
   int a = 0, b = n;
   while (a < b) {
     const int mid = (a + b) >> 1;
-    if (S[mid] < x) a = mid + 1;
+    if (S[mid * step] < x) a = mid + 1;
     else b = mid;
   }
   lo = a;
   b = n;
   while (a < b) {
     const int mid = (a + b) >> 1;
-    if (S[mid] <= x) a = mid + 1;
+    if (S[mid * step] <= x) a = mid + 1;
     else b = mid;
   }
   hi = a;
 }
 
-// dynamic LDS: 4 arrays of P floats (3 sorted axes + the subsample)
+// block-wide sums of K ints (result valid in every thread); red: >= K*16 ints
+template <int K>
+__device__ __forceinline__ void block_sum_n(int (&v)[K], int* red) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = wave_sum(v[k]);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < K; k++) red[k * 16 + w] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    int t = 0;
+    for (int i = 0; i < nw; i++) t += red[k * 16 + i];
+    v[k] = t;
+  }
+  __syncthreads();
+}
+
+// dynamic LDS: the 3 sorted axes, P floats each
 __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
@@ -150,9 +160,11 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ ov,
                                                   const int* __restrict__ ooff,
                                                   const int* __restrict__ olen, int Pmax,
+                                                  const double* __restrict__ oscore,
+                                                  const float* __restrict__ oth,
                                                   eao_np_stats* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
-  __shared__ int red[8];
+  __shared__ int red[9 * 16];
   __shared__ int wpos[4];
   const int p = blockIdx.x, t = threadIdx.x;
   const float* F = fp + 3 * (long long)foff[p];
@@ -160,12 +172,23 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   const int mt = flen[p];
   const float* O = op + 3 * (long long)ooff[p];
   const uint8_t* OV = ov + ooff[p];
-  const int nt = olen[p];
-  int mloc = 0, nloc = 0;
-  for (int i = t; i < mt; i += 256) mloc += FV[i] ? 1 : 0;
-  for (int i = t; i < nt; i += 256) nloc += OV[i] ? 1 : 0;
-  const int m = block_sum_int(mloc, red);
-  const int nvalid = block_sum_int(nloc, red);
+  const int ntot = olen[p];
+  // optional isolation-forest erasure applied on the fly (points with score >
+  // th leave the object, Object.cc:1284-1300): the pair is then evaluated on
+  // the object exactly as it stands after IsolationForestDeleteOutliers
+  const double* OS = oscore ? oscore + ooff[p] : nullptr;
+  const float th = oscore ? oth[p] : 0.f;
+  auto kept = [&](int i) { return !OS || !(OS[i] > (double)th); };
+  int cnt3[3] = {0, 0, 0};
+  for (int i = t; i < mt; i += 256) cnt3[0] += FV[i] ? 1 : 0;
+  for (int i = t; i < ntot; i += 256)
+    if (kept(i)) {
+      cnt3[1] += OV[i] ? 1 : 0;
+      cnt3[2] += 1;
+    }
+  if (t == 0) wpos[0] = 0;
+  block_sum_n<3>(cnt3, red);
+  const int m = cnt3[0], nvalid = cnt3[1], nt = cnt3[2];
   eao_np_stats r;
   r.m = m;
   r.n = nvalid;
@@ -181,15 +204,12 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
     return;
   }
   float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
-  float* T = dsm + 3 * Pmax;
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
   // compact the valid object points (order irrelevant: sorted next)
-  if (t == 0) wpos[0] = 0;
-  __syncthreads();
-  for (int i = t; i < nt; i += 256)
-    if (OV[i]) {
+  for (int i = t; i < ntot; i += 256)
+    if (OV[i] && kept(i)) {
       const int d = atomicAdd(&wpos[0], 1);
       S[0][d] = O[3 * i];
       S[1][d] = O[3 * i + 1];
@@ -198,28 +218,24 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   for (int i = nvalid + t; i < P; i += 256) S[0][i] = S[1][i] = S[2][i] = INFINITY;
   __syncthreads();
   block_sort3(S[0], S[1], S[2], P);
-  for (int a = 0; a < 3; a++) {
-    const float* srt = S[a];
-    if (sub) {  // x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-794)
-      for (int k = t; k < nsamp; k += 256) T[k] = S[a][k * step];
-      __syncthreads();
-      srt = T;
-    }
-    int gt = 0, lt = 0, eq = 0;
-    for (int i = t; i < mt; i += 256) {
-      if (!FV[i]) continue;
+  // rank counts against x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-830)
+  int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = t; i < mt; i += 256) {
+    if (!FV[i]) continue;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
       int lo, hi;
-      bounds(srt, nsamp, F[3 * i + a], lo, hi);
-      gt += lo;
-      eq += hi - lo;
-      lt += nsamp - hi;
+      bounds(S[a], nsamp, step, F[3 * i + a], lo, hi);
+      c9[3 * a] += lo;
+      c9[3 * a + 2] += hi - lo;
+      c9[3 * a + 1] += nsamp - hi;
     }
-    gt = block_sum_int(gt, red);
-    lt = block_sum_int(lt, red);
-    eq = block_sum_int(eq, red);
-    r.cnt_gt[a] = (float)gt;
-    r.cnt_lt[a] = (float)lt;
-    r.cnt_eq[a] = (float)eq;
+  }
+  block_sum_n<9>(c9, red);
+  for (int a = 0; a < 3; a++) {
+    r.cnt_gt[a] = (float)c9[3 * a];
+    r.cnt_lt[a] = (float)c9[3 * a + 1];
+    r.cnt_eq[a] = (float)c9[3 * a + 2];
   }
   if (t == 0) {
     const int n = nsamp;
@@ -322,7 +338,16 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 
 // in-kernel phase stamps of k_iforest_tree (workgroup (0,0)), read through
 // eao_debug_iforest_stamps: development instrumentation, a few SALU ops
-__device__ unsigned long long g_if_stamp[12];
+__device__ unsigned long long g_if_stamp[24];
+// EAO_IF_PROF builds only (tools/micro): cycles of the register-path node
+// sub-steps of workgroup (0,0) accumulated in g_if_stamp[12..17]
+#ifdef EAO_IF_PROF
+#define IFP_T(var) unsigned long long var; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+#define IFP_ACC(k, a, b) if (blockIdx.x == 0 && blockIdx.y == 0 && lane == 0) g_if_stamp[k] += (b) - (a)
+#else
+#define IFP_T(var)
+#define IFP_ACC(k, a, b)
+#endif
 __device__ __forceinline__ void if_stamp(int k) {
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     unsigned long long t;
@@ -407,7 +432,7 @@ struct WaveRng {
   }
   // uniform_real_distribution<float>(a, b): generate_canonical<float, 24>
   __device__ float uniform_real(float a, float b) {
-    float ret = fdiv(fmul((float)next(), 1.0f), 4294967296.0f);
+    float ret = fmul((float)next(), 0x1p-32f);  // == x / 2^32 exactly (power-of-two scale)
     if (ret >= 1.0f) ret = __uint_as_float(0x3f7fffffu);  // nextafter(1, 0)
     return fadd(fmul(ret, fsub(b, a)), a);
   }
@@ -422,31 +447,34 @@ __device__ __forceinline__ double iforest_c(uint32_t n) {  // CalculateC, isolat
   return 0.0;
 }
 
-template <int C>
-__device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), C, 0xF, 0xF, false));
+// order-preserving int key of a finite float (-0 folded onto +0, so key
+// order and equality are exactly the float comparisons); kfloat inverts it
+__device__ __forceinline__ int fkey(float f) {
+  int b = __float_as_int(f);
+  b = b == (int)0x80000000 ? 0 : b;
+  return b ^ ((b >> 31) & 0x7fffffff);
 }
-// wave-wide min and max (uniform results): DPP within rows of 16, then the
-// four row results through v_readlane -- no LDS round trips
-__device__ __forceinline__ void wave_minmax(float& mn, float& mx) {
-  mn = fminf(mn, dppf<0xB1>(mn));  // quad_perm [1,0,3,2]
-  mx = fmaxf(mx, dppf<0xB1>(mx));
-  mn = fminf(mn, dppf<0x4E>(mn));  // quad_perm [2,3,0,1]
-  mx = fmaxf(mx, dppf<0x4E>(mx));
-  mn = fminf(mn, dppf<0x141>(mn));  // row_half_mirror
-  mx = fmaxf(mx, dppf<0x141>(mx));
-  mn = fminf(mn, dppf<0x140>(mn));  // row_mirror
-  mx = fmaxf(mx, dppf<0x140>(mx));
-  const float a0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 0));
-  const float a1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 16));
-  const float a2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 32));
-  const float a3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mn), 48));
-  const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 0));
-  const float b1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 16));
-  const float b2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 32));
-  const float b3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mx), 48));
-  mn = fminf(fminf(a0, a1), fminf(a2, a3));
-  mx = fmaxf(fmaxf(b0, b1), fmaxf(b2, b3));
+__device__ __forceinline__ float kfloat(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+
+// wave-wide min and max of int keys, uniform results: DPP-fused min/max
+// within rows, then permlane16/32 swaps across rows (gfx950)
+__device__ __forceinline__ void wave_minmax_key(int& mn, int& mx) {
+  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));
+  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));
+  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x141, 0xF, 0xF, false));
+  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x140, 0xF, 0xF, false));  // row_mirror
+  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x140, 0xF, 0xF, false));
+  auto a = __builtin_amdgcn_permlane16_swap(mn, mn, false, false);
+  auto b = __builtin_amdgcn_permlane16_swap(mx, mx, false, false);
+  mn = min((int)a[0], (int)a[1]);
+  mx = max((int)b[0], (int)b[1]);
+  a = __builtin_amdgcn_permlane32_swap(mn, mn, false, false);
+  b = __builtin_amdgcn_permlane32_swap(mx, mx, false, false);
+  mn = __builtin_amdgcn_readfirstlane(min((int)a[0], (int)a[1]));
+  mx = __builtin_amdgcn_readfirstlane(max((int)b[0], (int)b[1]));
 }
 
 __host__ __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -471,11 +499,11 @@ struct IfLds {
 
 #define IF_END 0xffffu
 
-// One workgroup (4 waves) per (tree, cloud): IsolationTree::Build of
+// One workgroup (16 waves) per (tree, cloud): IsolationTree::Build of
 // isolation_forest.h:165-224,300-345 by wave 0 -- the libstdc++-11 draw stream
 // replicated exactly -- then every wave walks the cloud's points through the
-// tree (GetAnomalyScores' PathLength, :499-530); the per-(tree, point) path
-// length is summed in tree order by k_iforest_sum.
+// tree (GetAnomalyScores' PathLength, :499-530); k_iforest_sum adds the
+// per-(tree, point) path lengths in tree order.
 //
 // Sampling: std::shuffle of ids [0, n) (paired Lemire draws, stl_algo.h) is a
 // Fisher-Yates sequence of positions p_j <= j.  The draws are taken 64 at a
@@ -491,7 +519,7 @@ struct IfLds {
 //
 // mt_init: per tree, the mt19937 state after seeding and the first twist
 // (the seeds are fixed per forest, so it is computed once on the host).
-__global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ pts,
+__global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__ pts,
                                                       const int* __restrict__ off,
                                                       const int* __restrict__ len,
                                                       const uint32_t* __restrict__ mt_init,
@@ -513,10 +541,9 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
   const int psi = (int)sample[c];
   const float* P = pts + 3 * (long long)off[c];
   double* out = contrib + (long long)tr * npts_total + off[c];
-  if (n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe) {
-    for (int i = tid; i < n; i += nb) out[i] = __longlong_as_double(0x7ff8000000000000ll);
-    return;
-  }
+  const bool valid = !(n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe);
+  if (tid == 0) s_nodes_bad = valid ? 0 : 1;
+  if (valid) {
   uint16_t* p = (uint16_t*)(smem + L.shuf);
   uint32_t* head = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
   uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
@@ -612,22 +639,25 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        B0[k + u * nb] = v[u][0];
-        B0[psi + k + u * nb] = v[u][1];
-        B0[2 * psi + k + u * nb] = v[u][2];
+        ((int*)B0)[k + u * nb] = fkey(v[u][0]);
+        ((int*)B0)[psi + k + u * nb] = fkey(v[u][1]);
+        ((int*)B0)[2 * psi + k + u * nb] = fkey(v[u][2]);
       }
     }
     for (; k < psi; k += nb) {
       const float* q = P + 3 * (size_t)ids[k];
-      B0[k] = q[0];
-      B0[psi + k] = q[1];
-      B0[2 * psi + k] = q[2];
+      ((int*)B0)[k] = fkey(q[0]);
+      ((int*)B0)[psi + k] = fkey(q[1]);
+      ((int*)B0)[2 * psi + k] = fkey(q[2]);
     }
   }
   __syncthreads();
   if_stamp(5);
   if (wave == 0) {
-    // ---- Node::Build in DFS pre-order; stack entry e lives in lane e
+    // ---- Node::Build in DFS pre-order; stack entry e lives in lane e.
+    // Coordinates are order-preserving int keys (fkey): min / max / < are
+    // integer ops with DPP + permlane reductions; floats only for the split.
+    const int* K0 = (const int*)B0;
     const int maxDepth = (int)ceil(log2((double)psi));
     int sf = 0, sl = psi - 1, sd = 0, spar = -1;  // lane 0 = root
     int sp = 1, nn = 0, bad = 0;
@@ -644,31 +674,40 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
       }
-      const float* src = (depth & 1) ? B1 : B0;
+      const int* src = (depth & 1) ? (const int*)B1 : K0;
       if (cnt <= 64) {
         // whole subtree in registers: item per lane, node sets as lane masks,
         // pending right children on a lane-resident stack
         const bool has = lane < cnt;
-        const float x = has ? src[first + lane] : 0.f;
-        const float y = has ? src[psi + first + lane] : 0.f;
-        const float z = has ? src[2 * psi + first + lane] : 0.f;
+        const int x = has ? src[first + lane] : 0;
+        const int y = has ? src[psi + first + lane] : 0;
+        const int z = has ? src[2 * psi + first + lane] : 0;
         uint64_t mask = ballot(has);
         int d = depth, node = me, ssp = 0;
         int slo = 0, shi = 0, sdd = 0, spp = 0;
         while (true) {
+          IFP_T(t0);
           const int cn = popc64(mask);
           bool leaf = cn < 2 || d >= maxDepth;
           if (!leaf) {
             const uint32_t dim = g.lemire(3);
+            IFP_T(t1);
+            IFP_ACC(12, t0, t1);
             const bool in = (mask >> lane) & 1ull;
-            const float v = dim == 0 ? x : (dim == 1 ? y : z);
-            float mn = in ? v : INFINITY, mx = in ? v : -INFINITY;
-            wave_minmax(mn, mx);
+            const int v = dim == 0 ? x : (dim == 1 ? y : z);
+            int mn = in ? v : INT_MAX, mx = in ? v : INT_MIN;
+            wave_minmax_key(mn, mx);
+            IFP_T(t2);
+            IFP_ACC(13, t1, t2);
             if (mn == mx) {
               leaf = true;
             } else {
-              const float split = g.uniform_real(mn, mx);
-              const uint64_t lm = ballot(in && v < split);
+              const float split = g.uniform_real(kfloat(mn), kfloat(mx));
+              IFP_T(t3);
+              IFP_ACC(14, t2, t3);
+              const uint64_t lm = ballot(in && v < fkey(split));
+              IFP_T(t4);
+              IFP_ACC(15, t3, t4);
               if (lm == 0) {
                 leaf = true;
               } else {
@@ -685,11 +724,14 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
                 mask = lm;  // left child next (node + 1)
                 d++;
                 node = nn++;
+                IFP_T(t5);
+                IFP_ACC(16, t4, t5);
                 if (bad) break;
                 continue;
               }
             }
           }
+          IFP_T(t6);
           if (lane == 0) nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
           if (ssp == 0) break;
           ssp--;
@@ -699,35 +741,38 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
           const int par = __builtin_amdgcn_readlane(spp, ssp);
           node = nn++;
           if (lane == 0) right[par] = (uint16_t)node;
+          IFP_T(t7);
+          IFP_ACC(17, t6, t7);
         }
         continue;
       }
-      float* dst = (depth & 1) ? B0 : B1;
+      int* dst = (depth & 1) ? (int*)B0 : (int*)B1;
       const uint32_t dim = g.lemire(3);
-      float mn = INFINITY, mx = -INFINITY;
+      int mn = INT_MAX, mx = INT_MIN;
       for (int i = first + lane; i <= last; i += 64) {
-        const float v = src[dim * psi + i];
-        mn = fminf(mn, v);
-        mx = fmaxf(mx, v);
+        const int v = src[dim * psi + i];
+        mn = min(mn, v);
+        mx = max(mx, v);
       }
-      wave_minmax(mn, mx);
+      wave_minmax_key(mn, mx);
       if (mn == mx) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
       }
-      const float split = g.uniform_real(mn, mx);
+      const float split = g.uniform_real(kfloat(mn), kfloat(mx));
+      const int ks = fkey(split);
       int nl = 0, nr = 0;
       for (int c0 = first; c0 <= last; c0 += 64) {
         const int i = c0 + lane;
         const bool in = i <= last;
-        float x = 0.f, y = 0.f, z = 0.f;
+        int x = 0, y = 0, z = 0;
         if (in) {
           x = src[i];
           y = src[psi + i];
           z = src[2 * psi + i];
         }
-        const float v = dim == 0 ? x : (dim == 1 ? y : z);
-        const bool lft = in && v < split;
+        const int v = dim == 0 ? x : (dim == 1 ? y : z);
+        const bool lft = in && v < ks;
         const uint64_t ml = ballot(lft), mr = ballot(in && !lft);
         if (in) {
           const int dd = lft ? first + nl + popc64(ml & lanes_below())
@@ -765,13 +810,14 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
     if (lane == 0) s_nodes_bad = bad;
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
   }
+  }  // valid
   __syncthreads();
   if_stamp(6);
   // ---- path length of every point of the cloud through this tree
   if (s_nodes_bad) {
     for (int i = tid; i < n; i += nb) out[i] = __longlong_as_double(0x7ff8000000000000ll);
-    return;
-  }
+  } else
+
   // four independent walks per thread in flight (LDS latency-bound chains)
   for (int i0 = tid; i0 < n; i0 += 4 * nb) {
     float x[4][3];
@@ -815,7 +861,6 @@ __global__ __launch_bounds__(256) void k_iforest_tree(const float* __restrict__ 
       if (i < n) out[i] = (double)depth[u] + iforest_c(nd[u].x >> 2);
     }
   }
-  __syncthreads();
   if_stamp(7);
 }
 
@@ -825,7 +870,8 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
                                                      const uint32_t* __restrict__ sample,
                                                      int ntrees, int npts_total,
                                                      const double* __restrict__ contrib,
-                                                     double* __restrict__ scores) {
+                                                     double* __restrict__ scores,
+                                                     double* __restrict__ scores2) {
   const int c = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len[c]) return;
@@ -834,8 +880,11 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
 #pragma unroll 10
   for (int t = 0; t < ntrees; t++) total += contrib[(long long)t * npts_total + g];
   const double avg = total / (double)ntrees;
-  scores[g] = pow(2.0, -avg / iforest_c(sample[c]));
+  const double sc = pow(2.0, -avg / iforest_c(sample[c]));
+  scores[g] = sc;
+  if (scores2) scores2[g] = sc;
 }
+
 
 // ================================================================ host
 int AssocEngine::init(int device, int mp) {
@@ -873,12 +922,12 @@ AssocEngine::~AssocEngine() {
 int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                           const int* d_flen, const float* d_op, const uint8_t* d_ov,
                           const int* d_ooff, const int* d_olen, eao_np_stats* d_out,
-                          hipStream_t s, int max_olen) {
+                          hipStream_t s, int max_olen, const double* d_oscore, const float* d_oth) {
   if (npairs <= 0) return EAO_OK;
   int P = 8;
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), sizeof(float) * 4 * P, s, d_fp, d_fv, d_foff,
-                     d_flen, d_op, d_ov, d_ooff, d_olen, P, d_out);
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), sizeof(float) * 3 * P, s, d_fp, d_fv, d_foff,
+                     d_flen, d_op, d_ov, d_ooff, d_olen, P, d_oscore, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -919,9 +968,11 @@ static void forest_states(uint32_t seed, uint32_t trees, std::vector<uint32_t>& 
 
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len,
                                uint32_t trees, uint32_t seed, const uint32_t* d_sample,
-                               double* scores, hipStream_t s, int maxN, int maxS, int npts_total) {
+                               double* scores, hipStream_t s, int maxN, int maxS, int npts_total,
+                               double* contrib, double* scores2) {
+  if (!contrib) contrib = d_contrib;
   if (nclouds <= 0) return EAO_OK;
-  if ((int)trees > max_trees || nclouds > max_clouds || npts_total > max_points) {
+  if ((int)trees > max_trees || nclouds > max_clouds || (contrib == d_contrib && npts_total > max_points)) {
     set_error("iforest: too many trees, clouds or points per call");
     return EAO_E_CAPACITY;
   }
@@ -938,11 +989,11 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     cached_seed = seed;
     cached_trees = trees;
   }
-  hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(256), L.total, s, pts, off, len,
-                     d_mtinit, d_sample, maxN, maxS, npts_total, d_contrib);
+  hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(1024), L.total, s, pts, off, len,
+                     d_mtinit, d_sample, maxN, maxS, npts_total, contrib);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
-                     d_sample, (int)trees, npts_total, (const double*)d_contrib, scores);
+                     d_sample, (int)trees, npts_total, (const double*)contrib, scores, scores2);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -1089,7 +1140,7 @@ int eao_project_rects(eao_assoc* a, const eao_camera* cam, const float* Tcw, int
 
 int eao_debug_iforest_stamps(uint64_t* out12) {
   if (!out12) return EAO_E_ARG;
-  EAO_HIP_CHECK(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_if_stamp), sizeof(uint64_t) * 12));
+  EAO_HIP_CHECK(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_if_stamp), sizeof(uint64_t) * 24));
   return EAO_OK;
 }
 

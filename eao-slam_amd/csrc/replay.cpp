@@ -135,6 +135,7 @@ struct Obj {  // Object_Map
   double q[4] = {1, 0, 0, 0}, t[3] = {0, 0, 0}, qn[4] = {1, 0, 0, 0}, tn[3] = {0, 0, 0};
   float rotY = 0, rotP = 0, rotR = 0, rmax = 0;
   int pending = 0;  // 0 none, 1 iForest, 2 iForest then ComputeMeanAndStandard
+  int slot = -1;    // in-flight isolation-forest slot, -1 if not launched
 };
 const float* Det::P() const { return alias ? alias->center : pos; }
 
@@ -312,9 +313,17 @@ class ReplayEngine {
   // one packed upload + one download on the association stream
   unsigned char *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
   size_t cap_in = 0, cap_out = 0;
-  // per frame NP results: (det index, object index) -> stats
-  std::map<std::pair<int, int>, eao_np_stats> np_cache;
-  std::vector<char> odirty;  // objects modified in this frame (NP cache invalid)
+  // per frame NP results: (det index, object index) -> stats at an object
+  // version; an object's version is bumped each time it is modified
+  struct NpEntry {
+    eao_np_stats st;
+    int ver;
+  };
+  std::map<std::pair<int, int>, NpEntry> np_cache;
+  std::vector<int> over;          // object version within this frame
+  std::vector<Det*> kept_cur;     // this frame's kept detections, in association order
+  int kept_pos = -1;              // the detection being associated
+  bool cur_np_done = false;       // ... and whether its NP step has read the cache
   // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
   double prof[24] = {0};
   static double now_us() {
@@ -327,7 +336,42 @@ class ReplayEngine {
     ~Tick() { *acc += now_us() - t0; }
   };
 
+  // isolation forests run asynchronously in batches: every pending object not
+  // yet launched is launched together (kick) before the host blocks on any
+  // other GPU result and whenever a pending object's points are needed; an
+  // object's outliers are erased (complete) the first time its points are read
+  static constexpr int kIfBatches = 8, kIfStreams = 4;
+  struct IfBatch {
+    std::vector<Obj*> objs;
+    std::vector<int> off;
+    int left = 0;  // objects not yet completed
+    // speculative NP pairs evaluated right behind the forest, on the object as
+    // it will stand after the erasure: (det index, object index, version)
+    std::vector<int> sp_det, sp_obj, sp_ver;
+    size_t sp_out = 0;  // byte offset of their stats in h_out
+    hipEvent_t ev = nullptr;
+    unsigned char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+    size_t cap_in = 0, cap_out = 0;
+    double* contrib = nullptr;  // [50][max_points]
+  };
+  std::vector<IfBatch> ifb;
+  hipStream_t if_stream[kIfStreams] = {};
+  int if_next = 0;
+  int pend_err = 0;
+
   ~ReplayEngine() {
+    for (hipStream_t st : if_stream)
+      if (st) (void)hipStreamSynchronize(st);
+    for (IfBatch& sl : ifb) {
+      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      if (sl.h_in) (void)hipHostFree(sl.h_in);
+      if (sl.h_out) (void)hipHostFree(sl.h_out);
+      if (sl.d_in) (void)hipFree(sl.d_in);
+      if (sl.d_out) (void)hipFree(sl.d_out);
+      if (sl.contrib) (void)hipFree(sl.contrib);
+    }
+    for (hipStream_t st : if_stream)
+      if (st) (void)hipStreamDestroy(st);
     if (h_in) (void)hipHostFree(h_in);
     if (h_out) (void)hipHostFree(h_out);
     if (d_in) (void)hipFree(d_in);
@@ -462,84 +506,245 @@ class ReplayEngine {
     return biForest && !(o->cls == 75 || o->cls == 64 || o->cls == 65) && o->pts.size() >= 30;
   }
 
-  // run the pending isolation forests (Object.cc:1202-1309) of the selected
-  // objects in one batched launch; erase outliers in list order (Q8).
-  int flush(int cls) {
-    std::vector<Obj*> todo;
-    for (auto& up : objs)
-      if (up->pending && (cls < 0 || up->cls == cls)) todo.push_back(up.get());
-    return flush_list(todo);
+  // Object_Map::IsolationForestDeleteOutliers (Object.cc:1202-1309), split in
+  // a batched launch and a per-object completion (erase the outliers in list
+  // order, Q8, then ComputeMeanAndStandard for pending 2)
+  int if_init() {
+    ifb.resize(kIfBatches);
+    for (int k = 0; k < kIfStreams; k++) EAO_HIP_CHECK(hipStreamCreateWithFlags(&if_stream[k], hipStreamNonBlocking));
+    for (IfBatch& b : ifb) {
+      EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+      EAO_HIP_CHECK(hipMalloc((void**)&b.contrib, sizeof(double) * 50 * (size_t)A->max_points));
+    }
+    return EAO_OK;
   }
-  // an object's points are about to be read: run its deferred forest first
-  int touch(Obj* o) { return o->pending ? flush_list({o}) : EAO_OK; }
-
-  int flush_list(const std::vector<Obj*>& todo) {
-    Tick tk(&prof[3]);
+  int resolve_trivial(Obj* o) {  // pending objects the forest does not apply to
+    if (o->pending == 2) mean_std(o);
+    o->pending = 0;
+    return EAO_OK;
+  }
+  // launch every pending, not yet launched object (one or more batches)
+  int kick() {
+    std::vector<Obj*> todo;
+    for (auto& up : objs) {
+      Obj* o = up.get();
+      if (!o->pending || o->slot >= 0) continue;
+      if (!iforest_applies(o)) {
+        resolve_trivial(o);
+        continue;
+      }
+      if ((int)o->pts.size() > IF_MAXN) {
+        set_error("replay: object exceeds the isolation-forest capacity");
+        return EAO_E_CAPACITY;
+      }
+      todo.push_back(o);
+    }
+    if (todo.empty()) return EAO_OK;
+    if (ifb.empty()) {
+      int rc = if_init();
+      if (rc) return rc;
+    }
     size_t i = 0;
     while (i < todo.size()) {
-      std::vector<Obj*> batch;
-      int np = 0;
-      for (; i < todo.size() && (int)batch.size() < A->max_clouds; i++) {
-        Obj* o = todo[i];
-        if (!o->pending) continue;
-        if (iforest_applies(o)) {
-          if ((int)o->pts.size() > IF_MAXN) {
-            set_error("replay: object exceeds the isolation-forest capacity");
-            return EAO_E_CAPACITY;
-          }
-          if (!batch.empty() && np + (int)o->pts.size() > A->max_points) break;  // next batch
-          batch.push_back(o);
-          np += (int)o->pts.size();
-        } else if (o->pending == 2) {
-          mean_std(o);
-          o->pending = 0;
-        } else {
-          o->pending = 0;
+      int k = -1;
+      for (int t = 0; t < kIfBatches; t++) {
+        const int c = (if_next + t) % kIfBatches;
+        if (ifb[c].left == 0) {
+          k = c;
+          break;
         }
       }
-      if (batch.empty()) continue;
-      const int nb = (int)batch.size();
+      if (k < 0) {  // every batch in flight: retire the oldest
+        k = if_next;
+        std::vector<Obj*> os = ifb[k].objs;
+        for (Obj* o : os)
+          if (o->slot == k) {
+            int rc = complete_forest(o);
+            if (rc) return rc;
+          }
+      }
+      if_next = (k + 1) % kIfBatches;
+      IfBatch& b = ifb[k];
+      b.objs.clear();
+      b.off.clear();
+      b.sp_det.clear();
+      b.sp_obj.clear();
+      b.sp_ver.clear();
+      int np = 0, maxN = 0;
+      for (; i < todo.size() && (int)b.objs.size() < A->max_clouds; i++) {
+        const int n = (int)todo[i]->pts.size();
+        if (!b.objs.empty() && np + n > A->max_points) break;
+        b.objs.push_back(todo[i]);
+        b.off.push_back(np);
+        np += n;
+        maxN = std::max(maxN, n);
+      }
+      const int nb = (int)b.objs.size();
+      // speculative NP: every later detection of this frame that will run the
+      // NP test against these objects (same class, >= 20 points, Object.cc:255-339)
+      std::vector<Det*> sdets;
+      std::vector<int> sdoff;
+      int nfp = 0, max_olen = 0;
+      for (int c = 0; c < nb; c++) {
+        Obj* o = b.objs[c];
+        if (flag == "NA" || flag == "IoU" || o->bad) continue;
+        const int q0 = std::max(kept_pos + (cur_np_done ? 1 : 0), 0);
+        for (size_t q = (size_t)q0; q < kept_cur.size(); q++) {
+          Det* f = kept_cur[q];
+          if (f->cls != o->cls || f->pts.size() < 20) continue;
+          int di = -1;
+          for (size_t z = 0; z < sdets.size(); z++)
+            if (sdets[z] == f) di = (int)z;
+          if (di < 0) {
+            di = (int)sdets.size();
+            sdets.push_back(f);
+            sdoff.push_back(nfp);
+            nfp += (int)f->pts.size();
+          }
+          b.sp_det.push_back(di);  // remapped to f->index below
+          b.sp_obj.push_back(c);
+          b.sp_ver.push_back(over[o->id]);
+          max_olen = std::max(max_olen, (int)o->pts.size());
+        }
+      }
+      const int ns = (int)b.sp_det.size();
+      // in: forest meta [3 nb] | object points [3 np] | object valid [np] | NP meta [4 ns] | th [ns] |
+      //     frame points [3 nfp] | frame valid [nfp]
+      // out (host): scores [np] doubles | NP stats [ns]; device: scores [np] for the NP kernel
       const size_t o_pts = al16(sizeof(int) * 3 * nb);
-      int rc = stage(o_pts + sizeof(float) * 3 * (size_t)np, sizeof(double) * (size_t)np);
-      if (rc) return rc;
-      int* meta = (int*)h_in;
-      float* pts = (float*)(h_in + o_pts);
-      int off = 0, maxN = 0;
-      for (int b = 0; b < nb; b++) {
-        Obj* o = batch[b];
-        meta[b] = off;
-        meta[nb + b] = (int)o->pts.size();
-        meta[2 * nb + b] = (int)((int)o->pts.size() / 2);
-        maxN = std::max(maxN, (int)o->pts.size());
-        for (MapPt* p : o->pts) std::memcpy(&pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
+      const size_t o_oval = o_pts + sizeof(float) * 3 * (size_t)np;
+      const size_t o_spm = al16(o_oval + np);
+      const size_t o_th = o_spm + sizeof(int) * 4 * ns;
+      const size_t o_fp = al16(o_th + sizeof(float) * ns);
+      const size_t o_fval = o_fp + sizeof(float) * 3 * (size_t)nfp;
+      const size_t in_bytes = ns ? o_fval + nfp : o_pts + sizeof(float) * 3 * (size_t)np;
+      b.sp_out = al16(sizeof(double) * np);
+      const size_t out_bytes = b.sp_out + sizeof(eao_np_stats) * ns;
+      if (in_bytes > b.cap_in) {
+        if (b.h_in) (void)hipHostFree(b.h_in);
+        if (b.d_in) (void)hipFree(b.d_in);
+        b.cap_in = std::max(in_bytes, 2 * b.cap_in);
+        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_in, b.cap_in, 0));
+        EAO_HIP_CHECK(hipMalloc((void**)&b.d_in, b.cap_in));
       }
-      prof[2] += 1;
-      EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, o_pts + sizeof(float) * 3 * (size_t)np, hipMemcpyHostToDevice,
-                                   A->stream));
-      const int* dmeta = (const int*)d_in;
-      rc = A->iforest_batch(nb, (const float*)(d_in + o_pts), dmeta, dmeta + nb, 50, 12345,
-                            (const uint32_t*)(dmeta + 2 * nb), (double*)d_out, A->stream, maxN, maxN / 2, np);
-      if (rc) return rc;
-      EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(double) * np, hipMemcpyDeviceToHost, A->stream));
-      EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
-      const double* sc = (const double*)h_out;
-      for (size_t b = 0; b < batch.size(); b++) {
-        Obj* o = batch[b];
-        const float th = o->cls == 62 ? 0.65f : 0.6f;
-        const double* s = sc + meta[b];
-        size_t w = 0;
-        const size_t n = o->pts.size();
-        for (size_t k = 0; k < n; k++) {
-          if (s[k] > th) {
-            for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
-          } else {
-            o->pts[w++] = o->pts[k];
+      if (out_bytes > b.cap_out) {
+        if (b.h_out) (void)hipHostFree(b.h_out);
+        if (b.d_out) (void)hipFree(b.d_out);
+        b.cap_out = std::max(out_bytes, 2 * b.cap_out);
+        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_out, b.cap_out, 0));
+        EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, b.cap_out));
+      }
+      int* meta = (int*)b.h_in;
+      float* pts = (float*)(b.h_in + o_pts);
+      for (int c = 0; c < nb; c++) {
+        Obj* o = b.objs[c];
+        meta[c] = b.off[c];
+        meta[nb + c] = (int)o->pts.size();
+        meta[2 * nb + c] = (int)o->pts.size() / 2;
+        int w = b.off[c];
+        for (MapPt* p : o->pts) {
+          std::memcpy(&pts[3 * (size_t)w], p->pos, sizeof(float) * 3);
+          if (ns) b.h_in[o_oval + w] = p->bad ? 0 : 1;  // out_point is never set (Q7)
+          w++;
+        }
+        o->slot = k;
+      }
+      if (ns) {
+        int* spm = (int*)(b.h_in + o_spm);
+        float* th = (float*)(b.h_in + o_th);
+        float* fpt = (float*)(b.h_in + o_fp);
+        uint8_t* fval = b.h_in + o_fval;
+        for (size_t z = 0; z < sdets.size(); z++) {
+          int w = sdoff[z];
+          for (MapPt* p : sdets[z]->pts) {
+            std::memcpy(&fpt[3 * (size_t)w], p->pos, sizeof(float) * 3);
+            fval[w++] = p->bad ? 0 : 1;
           }
         }
-        o->pts.resize(w);
-        if (o->pending == 2) mean_std(o);
-        o->pending = 0;
+        for (int q = 0; q < ns; q++) {
+          const int z = b.sp_det[q], c = b.sp_obj[q];
+          Obj* o = b.objs[c];
+          spm[q] = sdoff[z];
+          spm[ns + q] = (int)sdets[z]->pts.size();
+          spm[2 * ns + q] = b.off[c];
+          spm[3 * ns + q] = (int)o->pts.size();
+          th[q] = o->cls == 62 ? 0.65f : 0.6f;
+          b.sp_det[q] = sdets[z]->index;
+          b.sp_obj[q] = o->id;
+        }
       }
+      b.left = nb;
+      hipStream_t st = if_stream[k % kIfStreams];
+      prof[2] += 1;
+      EAO_HIP_CHECK(hipMemcpyAsync(b.d_in, b.h_in, in_bytes, hipMemcpyHostToDevice, st));
+      const int* dm = (const int*)b.d_in;
+      // scores go straight to pinned host memory (a device-to-host copy costs
+      // ~35 us of round trip per launch on this box) and, for the speculative
+      // NP pairs, to device memory too
+      int rc = A->iforest_batch(nb, (const float*)(b.d_in + o_pts), dm, dm + nb, 50, 12345,
+                                (const uint32_t*)(dm + 2 * nb), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
+                                ns ? (double*)b.d_out : nullptr);
+      if (rc) return rc;
+      if (ns) {
+        const int* spm = (const int*)(b.d_in + o_spm);
+        const float* dfp = (const float*)(b.d_in + o_fp);
+        rc = A->np_batch(ns, dfp, b.d_in + o_fval, spm, spm + ns, (const float*)(b.d_in + o_pts), b.d_in + o_oval,
+                         spm + 2 * ns, spm + 3 * ns, (eao_np_stats*)(b.h_out + b.sp_out), st, max_olen,
+                         (const double*)b.d_out, (const float*)(b.d_in + o_th));
+        if (rc) return rc;
+        prof[9] += ns;
+      }
+      EAO_HIP_CHECK(hipEventRecord(b.ev, st));
+    }
+    return EAO_OK;
+  }
+  int complete_forest(Obj* o) {
+    if (!o->pending) return EAO_OK;
+    if (o->slot < 0) {
+      int rc = kick();
+      if (rc) return rc;
+      if (!o->pending) return EAO_OK;
+    }
+    Tick tk(&prof[3]);
+    IfBatch& b = ifb[o->slot];
+    EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+    int c = 0;
+    while (b.objs[c] != o) c++;
+    const float th = o->cls == 62 ? 0.65f : 0.6f;
+    const double* sc = (const double*)b.h_out + b.off[c];
+    size_t w = 0;
+    const size_t n = o->pts.size();
+    for (size_t k = 0; k < n; k++) {
+      if (sc[k] > th) {
+        for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
+      } else {
+        o->pts[w++] = o->pts[k];
+      }
+    }
+    o->pts.resize(w);
+    if (o->pending == 2) mean_std(o);
+    const eao_np_stats* sps = (const eao_np_stats*)(b.h_out + b.sp_out);
+    for (size_t q = 0; q < b.sp_obj.size(); q++)
+      if (b.sp_obj[q] == o->id) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
+    o->pending = 0;
+    o->slot = -1;
+    b.left--;
+    return EAO_OK;
+  }
+  int flush(int cls) {
+    for (auto& up : objs)
+      if (up->pending && (cls < 0 || up->cls == cls)) {
+        int rc = complete_forest(up.get());
+        if (rc) return rc;
+      }
+    return EAO_OK;
+  }
+  // an object's points are about to be read: finish its forest first
+  int touch(Obj* o) { return o->pending ? complete_forest(o) : EAO_OK; }
+  int flush_list(const std::vector<Obj*>& todo) {
+    for (Obj* o : todo) {
+      int rc = touch(o);
+      if (rc) return rc;
     }
     return EAO_OK;
   }
@@ -566,6 +771,7 @@ class ReplayEngine {
   // step 10.1 for all recent objects: one k_rects launch
   int project_rects_gpu(const std::vector<Obj*>& list) {
     if (list.empty()) return EAO_OK;
+    if (int rc = kick()) return rc;  // pending forests overlap this launch
     Tick tk(&prof[7]);
     prof[6] += 1;
     const int nb = (int)list.size();
@@ -588,9 +794,8 @@ class ReplayEngine {
     EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
     const int* dmeta = (const int*)d_in;
     rc = A->rects(camdev, (const float*)(d_in + o_T), nb, (const float*)(d_in + o_pts), dmeta, dmeta + nb,
-                  (int*)d_out, d_out + sizeof(int) * 4 * nb, A->stream);
+                  (int*)h_out, h_out + sizeof(int) * 4 * nb, A->stream);  // results into pinned host memory
     if (rc) return rc;
-    EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(int) * 4 * nb + nb, hipMemcpyDeviceToHost, A->stream));
     EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
     const int* r = (const int*)h_out;
     const uint8_t* ok = h_out + sizeof(int) * 4 * nb;
@@ -603,6 +808,7 @@ class ReplayEngine {
   int np_pairs(const std::vector<std::pair<Det*, Obj*>>& pairs, const std::vector<int>& di,
                const std::vector<int>& oi) {
     if (pairs.empty()) return EAO_OK;
+    if (int rc = kick()) return rc;  // pending forests overlap this launch
     Tick tk(&prof[5]);
     prof[4] += 1;
     const int npairs = (int)pairs.size();
@@ -653,12 +859,11 @@ class ReplayEngine {
     const float* dpts = (const float*)(d_in + o_pts);
     const uint8_t* dval = d_in + o_val;
     rc = A->np_batch(npairs, dpts, dval, dmeta, dmeta + npairs, dpts, dval, dmeta + 2 * npairs,
-                     dmeta + 3 * npairs, (eao_np_stats*)d_out, A->stream, max_olen);
+                     dmeta + 3 * npairs, (eao_np_stats*)h_out, A->stream, max_olen);  // into pinned host memory
     if (rc) return rc;
-    EAO_HIP_CHECK(hipMemcpyAsync(h_out, d_out, sizeof(eao_np_stats) * npairs, hipMemcpyDeviceToHost, A->stream));
     EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
     const eao_np_stats* out = (const eao_np_stats*)h_out;
-    for (int k = 0; k < npairs; k++) np_cache[{di[k], oi[k]}] = out[k];
+    for (int k = 0; k < npairs; k++) np_cache[{di[k], oi[k]}] = NpEntry{out[k], over[oi[k]]};
     return EAO_OK;
   }
 
@@ -687,10 +892,13 @@ class ReplayEngine {
   }
 
   void mark_dirty(Obj* o) {
-    if ((size_t)o->id >= odirty.size()) odirty.resize(o->id + 1, 0);
-    odirty[o->id] = 1;
+    if ((size_t)o->id >= over.size()) over.resize(o->id + 1, 0);
+    over[o->id]++;
   }
-  bool is_dirty(int i) const { return (size_t)i < odirty.size() && odirty[i]; }
+  bool np_fresh(int det, int i) const {
+    auto it = np_cache.find({det, i});
+    return it != np_cache.end() && (size_t)i < over.size() && it->second.ver == over[i];
+  }
 
   // Object_Map::DataAssociateUpdate, Object.cc:1313-1554
   bool update(Obj* o, Det* f, int Flag) {
@@ -781,13 +989,14 @@ class ReplayEngine {
       o->pts.resize(w);
     }
     mean_std(o);
-    o->pending = std::max(o->pending, 1);  // isolation forest deferred (flush)
+    o->pending = std::max(o->pending, 1);  // isolation forest: batched launch, applied on next read
     return true;
   }
 
   // Object_2D::ObjectDataAssociation, Object.cc:162-710
   int associate(Det* f) {
     if (flag == "None") biForest = false;
+    cur_np_done = false;
     int rc = flush(f->cls);
     if (rc) return rc;
     const IRect RC = f->box;
@@ -840,14 +1049,20 @@ class ReplayEngine {
           Obj* o = objs[i].get();
           if (f->cls != o->cls || o->bad) continue;
           if (byIou && i == iouId) continue;  // its verdict is never used (Object.cc:283-284)
-          if (is_dirty(i) || !np_cache.count({f->index, i})) need.push_back(i);
+          if (!np_fresh(f->index, i)) need.push_back(i);
         }
       }
       if (!need.empty()) {
         std::vector<Obj*> tl;
         for (int i : need) tl.push_back(objs[i].get());
-        rc = flush_list(tl);
+        rc = flush_list(tl);  // completing a forest publishes its speculative NP pairs
         if (rc) return rc;
+        std::vector<int> still;
+        for (int i : need)
+          if (!np_fresh(f->index, i)) still.push_back(i);
+        need.swap(still);
+      }
+      if (!need.empty()) {
         std::vector<std::pair<Det*, Obj*>> pairs;
         std::vector<int> di;
         for (int i : need) {
@@ -857,12 +1072,13 @@ class ReplayEngine {
         rc = np_pairs(pairs, di, need);
         if (rc) return rc;
       }
+      cur_np_done = true;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {
         Obj* o = objs[i].get();
         if (f->cls != o->cls || o->bad) continue;
         if (m_small) break;  // verdict 0
         if (byIou && i == iouId) continue;
-        const int v = np_cache[{f->index, i}].verdict;
+        const int v = np_cache[{f->index, i}].st.verdict;
         if (v < 0) {
           set_error("replay: NP pair outside kernel capacity");
           return EAO_E_CAPACITY;
@@ -1057,6 +1273,9 @@ class ReplayEngine {
     cur = fid;
     std::memcpy(pz.T, Tcw, sizeof(pz.T));
     epoch++;
+    kept_cur.clear();
+    kept_pos = -1;
+    cur_np_done = true;
     np_cache.clear();
     std::vector<Det*> o2;
     int maxcls = 0;
@@ -1073,7 +1292,7 @@ class ReplayEngine {
       o2.push_back(f.get());
       dets.push_back(std::move(f));
     }
-    odirty.assign(objs.size(), 0);
+    over.assign(objs.size(), 0);
     double tA = now_us();
     std::vector<MapPt*> tr(npts);
     for (int i = 0; i < npts; i++) {
@@ -1224,7 +1443,10 @@ class ReplayEngine {
       }
       prof[14] += now_us() - tA;
       tA = now_us();
-      for (Det* f : kept) {
+      kept_cur = kept;
+      for (size_t q = 0; q < kept.size(); q++) {
+        Det* f = kept[q];
+        kept_pos = (int)q;
         if (f->pts.size() < 5) {
           f->method = 6;
           continue;
@@ -1232,6 +1454,8 @@ class ReplayEngine {
         rc = associate(f);
         if (rc) return rc;
       }
+      kept_pos = (int)kept.size();
+      cur_np_done = true;
       prof[15] += now_us() - tA;
       tA = now_us();
       rc = flush(-1);
@@ -1276,6 +1500,11 @@ class ReplayEngine {
       out[4 * k + 1] = f->mnId;
       out[4 * k + 2] = f->cls;
       out[4 * k + 3] = (int)f->pts.size();
+    }
+    if (pend_err) {
+      const int e = pend_err;
+      pend_err = 0;
+      return e;
     }
     return EAO_OK;
   }
@@ -1351,7 +1580,7 @@ class ReplayEngine {
 
   int iforest_now(Obj* o) {  // synchronous forest (LocalMapping merge path)
     o->pending = std::max(o->pending, 1);
-    return flush_list({o});
+    return complete_forest(o);
   }
 
   int whether_merge(Obj* o) {  // Object_Map::WhetherMergeTwoMapObjs, Object.cc:1607-1655
@@ -1526,6 +1755,28 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
   const int rc = r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv,
                             mp_bad, det_out);
   return rc ? rc : (int)r->r.objs.size();
+}
+
+int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                   const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                   const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                   const uint8_t* mp_bad, const uint8_t* keyframe, int32_t* det_out) {
+  if (!r || n_frames < 0 || (n_frames && (!frame_ids || !Tcw || !n_boxes || !n_pts || !keyframe)))
+    return EAO_E_ARG;
+  size_t ob = 0, op = 0;
+  for (int t = 0; t < n_frames; t++) {
+    const int rc = eao_replay_frame(r, frame_ids[t], Tcw + 16 * (size_t)t, n_boxes[t], boxes + 5 * ob, n_pts[t],
+                                    mp_ids + op, mp_pos + 3 * op, kp_uv + 2 * op, mp_bad ? mp_bad + op : nullptr,
+                                    det_out + 4 * ob);
+    if (rc < 0) return rc;
+    if (keyframe[t]) {
+      const int rl = eao_replay_local_mapping(r);
+      if (rl < 0) return rl;
+    }
+    ob += (size_t)n_boxes[t];
+    op += (size_t)n_pts[t];
+  }
+  return (int)r->r.objs.size();
 }
 
 int eao_replay_local_mapping(eao_replay* r) {

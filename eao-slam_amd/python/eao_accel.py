@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libeao_accel.so")
+LIB_PATH = os.environ.get("EAO_ACCEL_LIB") or os.path.join(os.path.dirname(HERE), "lib", "libeao_accel.so")
 
 EAO_OK, EAO_E_ARG, EAO_E_NODEVICE, EAO_E_HIP, EAO_E_CAPACITY, EAO_E_STATE = 0, -1, -2, -3, -4, -5
 
@@ -315,6 +315,30 @@ class Replay:
 
     def local_mapping(self):
         check(lib().eao_replay_local_mapping(self.h), "eao_replay_local_mapping")
+
+    @staticmethod
+    def pack(frames, first_id=1):
+        """Concatenate a list of per-frame dicts (T, boxes, ids, pos, uv, bad, kf) for run()."""
+        n = len(frames)
+        return dict(
+            n=n, ids=np.arange(first_id, first_id + n, dtype=np.int32),
+            T=np.ascontiguousarray(np.stack([f["T"] for f in frames]), np.float32).reshape(n, 16),
+            nb=np.array([len(f["boxes"]) for f in frames], np.int32),
+            boxes=np.ascontiguousarray(np.concatenate([np.asarray(f["boxes"], np.int32).reshape(-1, 5) for f in frames])),
+            npt=np.array([len(f["ids"]) for f in frames], np.int32),
+            mp=np.ascontiguousarray(np.concatenate([f["ids"] for f in frames]), np.int32),
+            pos=np.ascontiguousarray(np.concatenate([f["pos"] for f in frames]), np.float32),
+            uv=np.ascontiguousarray(np.concatenate([f["uv"] for f in frames]), np.float32),
+            bad=np.ascontiguousarray(np.concatenate([f["bad"] for f in frames]), np.uint8),
+            kf=np.array([1 if f["kf"] else 0 for f in frames], np.uint8))
+
+    def run(self, pk):
+        """eao_replay_run over a packed stream; returns det_out (total boxes x 4)."""
+        out = np.zeros((int(pk["nb"].sum()), 4), np.int32)
+        check(lib().eao_replay_run(self.h, pk["n"], P(pk["ids"]), P(pk["T"]), P(pk["nb"]), P(pk["boxes"]),
+                                   P(pk["npt"]), P(pk["mp"]), P(pk["pos"]), P(pk["uv"]), P(pk["bad"]), P(pk["kf"]),
+                                   P(out)), "eao_replay_run")
+        return out
 
     def objects(self):
         n = check(lib().eao_replay_num_objects(self.h), "eao_replay_num_objects")

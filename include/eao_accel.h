@@ -205,6 +205,14 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
                      const int32_t* boxes, int n_pts, const int32_t* mp_ids, const float* mp_pos,
                      const float* kp_uv, const uint8_t* mp_bad, int32_t* det_out);
 int eao_replay_local_mapping(eao_replay* r);
+/* a recorded stream in one call: frame t is eao_replay_frame on the t-th
+   slices of the packed arrays (boxes / points concatenated over frames),
+   followed by eao_replay_local_mapping when keyframe[t]. det_out receives 4
+   ints per box in the same concatenated order. Returns #objects or < 0. */
+int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                   const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                   const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                   const uint8_t* mp_bad, const uint8_t* keyframe, int32_t* det_out);
 int eao_replay_num_objects(eao_replay* r);
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats);
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);

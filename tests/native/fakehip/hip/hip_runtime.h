@@ -37,3 +37,11 @@ static struct { unsigned x; } threadIdx;
 template <typename T> T __shfl_xor(T v, int, int) { return v; }
 inline unsigned long long __ballot(bool p) { return p; }
 inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }
+enum { hipEventDisableTiming = 2 };
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hipStream_t)1; return 0; }
+inline hipError_t hipStreamDestroy(hipStream_t) { return 0; }
+inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = (hipEvent_t)1; return 0; }
+inline hipError_t hipEventDestroy(hipEvent_t) { return 0; }
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return 0; }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return 0; }
+inline hipError_t hipMemset(void* p, int v, size_t n) { std::memset(p, v, n); return 0; }

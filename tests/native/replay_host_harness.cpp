@@ -20,10 +20,17 @@ CamDev make_cam(const eao_camera& c) {
 }
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
-                          eao_np_stats* out, hipStream_t, int) {
+                          eao_np_stats* out, hipStream_t, int, const double* oscore, const float* oth) {
   for (int p = 0; p < npairs; p++) {
+    std::vector<float> pts;
+    std::vector<uint8_t> val;
+    for (int i = 0; i < olen[p]; i++) {  // the forest's erasure, as the kernel applies it
+      if (oscore && oscore[ooff[p] + i] > (double)oth[p]) continue;
+      pts.insert(pts.end(), op + 3 * (ooff[p] + i), op + 3 * (ooff[p] + i) + 3);
+      val.push_back(ov[ooff[p] + i]);
+    }
     orc_np_stats s;
-    orc_np_test(flen[p], fp + 3 * foff[p], fv + foff[p], olen[p], op + 3 * ooff[p], ov + ooff[p], &s);
+    orc_np_test(flen[p], fp + 3 * foff[p], fv + foff[p], (int)val.size(), pts.data(), val.data(), &s);
     static_assert(sizeof(s) == sizeof(eao_np_stats), "layout");
     std::memcpy(&out[p], &s, sizeof(s));
   }
@@ -31,13 +38,15 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
 }
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
                                uint32_t seed, const uint32_t* sample, double* scores, hipStream_t, int, int,
-                               int) {
-  for (int c = 0; c < nclouds; c++)
+                               int, double*, double* scores2) {
+  for (int c = 0; c < nclouds; c++) {
     if (orc_iforest_scores(pts + 3 * off[c], len[c], trees, seed, sample[c], scores + off[c]))
       for (int i = 0; i < len[c]; i++) scores[off[c] + i] = NAN;  // Build() failed: nothing erased
+    if (scores2)
+      for (int i = 0; i < len[c]; i++) scores2[off[c] + i] = scores[off[c] + i];
+  }
   return 0;
 }
-
 int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const float* pts, const int* off,
                        const int* len, int* rect, uint8_t* ok, hipStream_t) {
   orc_camera c{(int)cam.maxX, (int)cam.maxY, cam.fx, cam.fy, cam.cx, cam.cy};

@@ -51,3 +51,22 @@ def test_replay_long_bad_points():
 def test_replay_bench_stream_full():
     """The benchmark's 405-frame fr3-shaped stream, EAO flag, end to end."""
     _run("EAO", synth.assoc_stream_fr3(405))
+
+
+def test_replay_run_stream_matches_per_frame_oracle():
+    """eao_replay_run (packed stream, one call) == the oracle frame by frame."""
+    frames = synth.assoc_stream_fr3(120, seed=0xEA5)
+    a = ea.Assoc()
+    g = ea.Replay(a, "EAO")
+    det = g.run(ea.Replay.pack(frames))
+    o = orc.Replay("EAO")
+    ref = []
+    for i, f in enumerate(frames):
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            o.local_mapping()
+    assert np.array_equal(det, np.concatenate(ref))
+    gi, gf, gp = g.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi)
+    assert np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)

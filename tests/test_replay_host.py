@@ -86,3 +86,16 @@ def test_host_orchestration_matches_oracle(harness, flag):
     assert np.array_equal(gi, oi)
     assert np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
     assert all(np.array_equal(x, y) for x, y in zip(gp, op))
+
+
+def test_host_run_stream_matches_oracle(harness):
+    frames = synth.assoc_stream_fr3(50, seed=0xEA6)
+    g = _HostReplay(harness, "EAO")
+    det = g._with(ea.Replay.run, g, ea.Replay.pack(frames))
+    o = orc.Replay("EAO")
+    ref = []
+    for i, f in enumerate(frames):
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            o.local_mapping()
+    assert np.array_equal(det, np.concatenate(ref))
