@@ -66,7 +66,8 @@ def level_sizes():
 
 
 def algorithmic_bytes(n_kps):
-    """Per-frame algorithmic bytes of each extraction stage."""
+    """Per-frame algorithmic bytes of each extraction stage:
+    every input byte read once, every output byte written once."""
     lv = [w * h for w, h in level_sizes()]
     l0, upper = lv[0], sum(lv[1:])
     return {
@@ -74,15 +75,17 @@ def algorithmic_bytes(n_kps):
         "pyramid": sum(lv[:-1]) + upper,
         # FAST: every level plane read once
         "fast": l0 + upper,
-        # orient+describe: every level plane read once, outputs 28 B kp + 32 B desc
-        "describe": l0 + upper + n_kps * 60,
+        # blur: every level read once and its blurred copy written once
+        "blur": 2 * (l0 + upper),
+        # orient (raw level) + describe (blurred level), outputs 28 B kp + 32 B desc
+        "describe": 2 * (l0 + upper) + n_kps * 60,
         # SURVEY §8d per-frame figure for the whole extraction
         "extract": l0 + 2 * upper + n_kps * 60,
     }
 
 
 def stage_names():
-    return ["pyramid", "fast", "distribute", "describe"]
+    return ["pyramid", "fast", "distribute", "blur", "describe"]
 
 
 class Stream:
@@ -109,10 +112,21 @@ def main():
     args = ap.parse_args()
 
     rank, world, local = eao_dist.env_rank()
+    # one process per GPU; ranks beyond the visible devices (a rehearsal of
+    # several ranks on one card) share devices round-robin
+    ndev = torch.cuda.device_count()
+    if ndev < 1:
+        raise RuntimeError("no GPU visible: the engine has no CPU fallback")
+    gpu = local % ndev
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        backend = os.environ.get("EAO_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    local = gpu
     if not ea.device_ok(local):
         raise RuntimeError("no gfx950 device: the engine has no CPU fallback")
 
@@ -232,7 +246,7 @@ def main():
     names = stage_names()
     dom = int(np.argmax(stage))
     dom_name = names[dom]
-    kernels = {"pyramid": "k_resize (x7)", "fast": "k_fast", "distribute": "k_distribute",
+    kernels = {"pyramid": "k_resize (x7)", "fast": "k_fast", "distribute": "k_distribute", "blur": "k_blur",
                "describe": "k_describe"}
 
     result = None

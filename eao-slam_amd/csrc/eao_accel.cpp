@@ -131,11 +131,12 @@ int eao_orb_set_timing(eao_orb* h, int on) {
   return EAO_OK;
 }
 
-int eao_orb_stage_ms(eao_orb* h, float* ms4) {
-  if (!h || !ms4 || !h->e.timing) return EAO_E_STATE;
-  EAO_HIP_CHECK(hipEventSynchronize(h->e.ev[4]));
-  for (int i = 0; i < 4; i++) EAO_HIP_CHECK(hipEventElapsedTime(&ms4[i], h->e.ev[i], h->e.ev[i + 1]));
-  return EAO_OK;
+int eao_orb_stage_ms(eao_orb* h, float* ms, int n) {
+  if (!h || !ms || !h->e.timing) return EAO_E_STATE;
+  const int k = OrbEngine::kStages;
+  EAO_HIP_CHECK(hipEventSynchronize(h->e.ev[k]));
+  for (int i = 0; i < k && i < n; i++) EAO_HIP_CHECK(hipEventElapsedTime(&ms[i], h->e.ev[i], h->e.ev[i + 1]));
+  return k;
 }
 
 int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out) {

@@ -31,6 +31,13 @@ struct LevelDev {
   float hX;
   float scale, size;          // mvScaleFactor[l], PATCH_SIZE*scale truncated
   int tab_x, tab_y, xmax;     // resize tables
+  int pad1;
+  long long blur_off;         // byte offset of the blurred level plane in a frame's blur area
+};
+
+struct BlurTile {             // 64 x 16 output tile of one level
+  int16_t level, pad;
+  int16_t x0, y0;
 };
 
 struct CellDev {
@@ -51,11 +58,13 @@ class OrbEngine {
   std::vector<int> resize_xofs, resize_yrows;
   std::vector<short> resize_ia, resize_ib;
   std::vector<int2> slot_map;
-  long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;
+  long long pyr_bytes = 0, blur_bytes = 0, cand_stride = 0, sel_stride = 0;
+  std::vector<BlurTile> btiles;
   int cap = 0, roi_stride = 0, roi_rows = 0;
-  // optional per-stage timing: events around resize / fast / distribute / describe
+  // optional per-stage timing: events around resize / fast / distribute / blur / describe
+  static constexpr int kStages = 5;
   bool timing = false;
-  hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[kStages + 1] = {};
 
   hipStream_t stream = nullptr;
   LevelDev* d_levels = nullptr;
@@ -64,6 +73,8 @@ class OrbEngine {
   short *d_ia = nullptr, *d_ib = nullptr;
   int2* d_slot_map = nullptr;
   uint8_t* d_pyr = nullptr;
+  uint8_t* d_blur = nullptr;  // per frame: the 7x7 sigma-2 blur of every level (ORBextractor.cc:1085-1086)
+  BlurTile* d_btiles = nullptr;
   uint32_t *d_cand = nullptr, *d_qbuf = nullptr, *d_sel = nullptr;
   int *d_cell_cnt = nullptr, *d_sel_cnt = nullptr;
   uint8_t* d_img = nullptr;

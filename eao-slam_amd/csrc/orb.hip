@@ -9,8 +9,10 @@
 //                     minTh retry for empty cells (ORBextractor.cc:789-829)
 //   k_distribute  x1  one wave per (level, frame): DistributeOctTree with
 //                     the reference's list order (ORBextractor.cc:539-763)
+//   k_blur        x1  7x7 sigma-2 Gaussian of every level (separable, fixed
+//                     point, REFLECT_101), 64x16 tiles (:1085-1086)
 //   k_describe    x1  one wave per selected keypoint: IC_Angle on the level,
-//                     7x7 Gaussian evaluated in LDS at the 512 rBRIEF taps,
+//                     the 512 rBRIEF taps gathered from the blurred level,
 //                     256-bit descriptor, final scaling (:77-147, :1076-1104)
 // Bit-exactness: integer paths are exact; float paths use __f*_rn intrinsics
 // and -ffp-contract=off so every rounding matches the oracle.
@@ -501,15 +503,7 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
   if (lane == 0) sel_cnt[f * nlevels + l] = overflow ? -1 : min(outn, L.sel_cap);
 }
 
-// ---------------------------------------------------------------- describe
-__device__ __forceinline__ int reflect101(int p, int len) {
-  if (len == 1) return 0;
-  while (p < 0 || p >= len) {
-    if (p < 0) p = -p;
-    if (p >= len) p = 2 * len - 2 - p;
-  }
-  return p;
-}
+// ---------------------------------------------------------------- orientation
 
 // fastAtan2 (OpenCV 3.2), fp32, no contraction
 __device__ float fast_atan2(float y, float x) {
@@ -533,16 +527,118 @@ __device__ float fast_atan2(float y, float x) {
   return a;
 }
 
-constexpr int PATCH = 43;  // 2*(18+3)+1: rBRIEF reach 18 px + 3-px blur taps
+// ---------------------------------------------------------------- blur
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level, the clone
+// ORBextractor::operator() blurs before computeDescriptors (:1085-1086): 8U
+// fixed point, separable (exact in integers): horizontal sums of 8-bit
+// pixels x 8-bit taps stay below 2^16, then (sum_v + 2^15) >> 16, saturated.
+// One workgroup per 64 x 16 output tile.
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, int fpitch,
+                                              long long fstride, const uint8_t* __restrict__ pyr,
+                                              long long pstride, const LevelDev* __restrict__ levels,
+                                              const BlurTile* __restrict__ tiles,
+                                              const int* __restrict__ gk, uint8_t* __restrict__ blur,
+                                              long long bstride) {
+  // in: 22 rows x 72 cols (x0-4 .. x0+67), word aligned; hs: horizontal sums
+  // (< 2^16) packed two per word, 22 rows x 64 cols
+  __shared__ uint32_t in[22][18];
+  __shared__ uint32_t hs[22][32];
+  const BlurTile T = tiles[blockIdx.x];
+  const int f = blockIdx.y, t = threadIdx.x;
+  const LevelDev& L = levels[T.level];
+  const uint8_t* img;
+  int pitch;
+  if (T.level == 0) {
+    img = frames + f * fstride;
+    pitch = fpitch;
+  } else {
+    img = pyr + f * pstride + L.plane_off;
+    pitch = L.pitch;
+  }
+  const bool interior = T.x0 >= 4 && T.x0 + 68 <= L.w && T.y0 >= 3 && T.y0 + 19 <= L.h && (pitch & 3) == 0;
+  if (interior) {
+    for (int i = t; i < 22 * 18; i += 256) {
+      const int r = i / 18, c = i - r * 18;
+      in[r][c] = *(const uint32_t*)(img + (long long)(T.y0 - 3 + r) * pitch + T.x0 - 4 + 4 * c);
+    }
+  } else {
+    uint8_t* inb = (uint8_t*)&in[0][0];
+    for (int i = t; i < 22 * 72; i += 256) {
+      const int r = i / 72, c = i - r * 72;
+      int yy = T.y0 - 3 + r, xx = T.x0 - 4 + c;
+      // REFLECT_101 on the isolated level (gfedcb|abcdefgh|gfedcba)
+      if (L.h == 1) yy = 0;
+      while (yy < 0 || yy >= L.h) yy = yy < 0 ? -yy : 2 * L.h - 2 - yy;
+      if (L.w == 1) xx = 0;
+      while (xx < 0 || xx >= L.w) xx = xx < 0 ? -xx : 2 * L.w - 2 - xx;
+      inb[r * 72 + c] = img[(long long)yy * pitch + xx];
+    }
+  }
+  __syncthreads();
+  int k[7];
+#pragma unroll
+  for (int i = 0; i < 7; i++) k[i] = gk[i];
+  // horizontal: item (row, group of 4 columns): columns 4g..4g+3 use input
+  // bytes 4g+1 .. 4g+10 (input column 0 is x0-4)
+  for (int i = t; i < 22 * 16; i += 256) {
+    const int r = i >> 4, g = i & 15;
+    const uint32_t w0 = in[r][g], w1 = in[r][g + 1], w2 = in[r][g + 2];
+    int px[12];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      px[q] = (w0 >> (8 * q)) & 255;
+      px[4 + q] = (w1 >> (8 * q)) & 255;
+      px[8 + q] = (w2 >> (8 * q)) & 255;
+    }
+    uint32_t h[4];
+#pragma unroll
+    for (int o = 0; o < 4; o++) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < 7; j++) v += (uint32_t)(k[j] * px[o + 1 + j]);
+      h[o] = v;
+    }
+    hs[r][2 * g] = h[0] | (h[1] << 16);
+    hs[r][2 * g + 1] = h[2] | (h[3] << 16);
+  }
+  __syncthreads();
+  // vertical: thread -> (row, 4 columns)
+  const int r = t >> 4, g = t & 15;
+  const int x = T.x0 + 4 * g, y = T.y0 + r;
+  if (y >= L.h || x >= L.w) return;
+  uint32_t acc[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 7; j++) {
+    const uint32_t a0 = hs[r + j][2 * g], a1 = hs[r + j][2 * g + 1];
+    acc[0] += (uint32_t)k[j] * (a0 & 0xffffu);
+    acc[1] += (uint32_t)k[j] * (a0 >> 16);
+    acc[2] += (uint32_t)k[j] * (a1 & 0xffffu);
+    acc[3] += (uint32_t)k[j] * (a1 >> 16);
+  }
+  uint32_t ow = 0;
+#pragma unroll
+  for (int o = 0; o < 4; o++) ow |= min((acc[o] + (1u << 15)) >> 16, 255u) << (8 * o);
+  uint8_t* out = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
+  if (x + 4 <= L.w) {
+    *(uint32_t*)out = ow;  // pitch and x are multiples of 4
+  } else {
+    for (int o = 0; o < 4 && x + o < L.w; o++) out[o] = (uint8_t)(ow >> (8 * o));
+  }
+}
 
+// ---------------------------------------------------------------- describe
+// One wave per selected keypoint: IC_Angle on the raw level, then the 256
+// rBRIEF tests (4 per lane) gathered from the blurred level. Keypoints lie
+// >= 19 px inside the level (minBorder 16 + FAST 3) and the rotated pattern
+// reaches <= 18 px, so no border handling is needed here.
 __global__ __launch_bounds__(256) void k_describe(
     const uint8_t* __restrict__ frames, int fpitch, long long fstride,
-    const uint8_t* __restrict__ pyr, long long pstride, const LevelDev* __restrict__ levels,
+    const uint8_t* __restrict__ pyr, long long pstride, const uint8_t* __restrict__ blur,
+    long long bstride, const LevelDev* __restrict__ levels,
     const uint32_t* __restrict__ sel, long long sel_stride, const int* __restrict__ sel_cnt,
     const int2* __restrict__ slot_map, int nslots, int nlevels, const int* __restrict__ umax,
-    const int* __restrict__ gk, eao_keypoint_dev* __restrict__ out_kps,
-    uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt, int cap) {
-  __shared__ uint8_t patch[4][PATCH * PATCH];
+    eao_keypoint_dev* __restrict__ out_kps, uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt,
+    int cap) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int slot = blockIdx.x * 4 + w;
   const int f = blockIdx.y;
@@ -552,19 +648,14 @@ __global__ __launch_bounds__(256) void k_describe(
     for (int i = 0; i < nlevels; i++) tot += max(cnts[i], 0);
     out_cnt[f] = tot;
   }
-  int l = 0, k = 0;
-  bool active = slot < nslots;
-  if (active) {
-    const int2 sm = slot_map[slot];  // (level, index within level)
-    l = sm.x;
-    k = sm.y;
-    active = k < cnts[l];
-  }
+  if (slot >= nslots) return;
+  const int2 sm = slot_map[slot];  // (level, index within level)
+  const int l = sm.x, k = sm.y;
+  if (k >= cnts[l]) return;
   int off = 0;
   for (int i = 0; i < l; i++) off += max(cnts[i], 0);
   const LevelDev& L = levels[l];
-  uint32_t pk = 0;
-  if (active) pk = sel[f * sel_stride + L.sel_off + k];
+  const uint32_t pk = sel[f * sel_stride + L.sel_off + k];
   const int x = kp_x(pk) + L.minBX, y = kp_y(pk) + L.minBY;
   const uint8_t* img;
   int pitch;
@@ -575,61 +666,40 @@ __global__ __launch_bounds__(256) void k_describe(
     img = pyr + f * pstride + L.plane_off;
     pitch = L.pitch;
   }
-  float angle = 0.f;
-  uint8_t* P = patch[w];
-  if (active) {
-    // ---- IC_Angle (ORBextractor.cc:77-104): integer moments, wave reduction
-    int m10 = 0, m01 = 0;
-    const uint8_t* center = img + (long long)y * pitch + x;
-    if (lane < 31) m10 += (lane - 15) * center[lane - 15];
-    for (int v = 1 + (lane >> 5); v <= 15; v += 2) {
-      const int d = umax[v];
-      const int u = (lane & 31) - d;
-      if (u <= d) {
-        const int vp = center[u + v * pitch], vm = center[u - v * pitch];
-        m10 += u * (vp + vm);
-        m01 += v * (vp - vm);
-      }
-    }
-    m10 = wave_sum(m10);
-    m01 = wave_sum(m01);
-    angle = fast_atan2((float)m01, (float)m10);
-    // ---- stage the 43x43 raw patch (REFLECT_101 at the level border)
-    for (int i = lane; i < PATCH * PATCH; i += 64) {
-      const int r = i / PATCH, c = i - r * PATCH;
-      const int yy = reflect101(y - 21 + r, L.h), xx = reflect101(x - 21 + c, L.w);
-      P[i] = img[(long long)yy * pitch + xx];
+  // ---- IC_Angle (ORBextractor.cc:77-104): integer moments, wave reduction
+  int m10 = 0, m01 = 0;
+  const uint8_t* center = img + (long long)y * pitch + x;
+  if (lane < 31) m10 += (lane - 15) * center[lane - 15];
+  for (int v = 1 + (lane >> 5); v <= 15; v += 2) {
+    const int d = umax[v];
+    const int u = (lane & 31) - d;
+    if (u <= d) {
+      const int vp = center[u + v * pitch], vm = center[u - v * pitch];
+      m10 += u * (vp + vm);
+      m01 += v * (vp - vm);
     }
   }
-  __syncthreads();
-  if (!active) return;
-  // ---- rBRIEF (ORBextractor.cc:108-147) on the 7x7 sigma-2 blur (:1086)
+  m10 = wave_sum(m10);
+  m01 = wave_sum(m01);
+  const float angle = fast_atan2((float)m01, (float)m10);
+  // ---- rBRIEF (ORBextractor.cc:108-147) on the blurred level
   const float factorPI = (float)(M_PI / 180.f);
   const float ang = fmul(angle, factorPI);
   const float a = (float)cos((double)ang), b = (float)sin((double)ang);
+  const uint8_t* bc = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
   const int byte = lane >> 1, half = lane & 1;
-  int nib = 0;
-  for (int t = 0; t < 4; t++) {
-    int val[2];
-    for (int e = 0; e < 2; e++) {
-      const int pi = 16 * byte + 8 * half + 2 * t + e;
-      const float px = (float)c_pattern[2 * pi], py = (float)c_pattern[2 * pi + 1];
-      const int dy = dev_round(fadd(fmul(px, b), fmul(py, a)));
-      const int dx = dev_round(fsub(fmul(px, a), fmul(py, b)));
-      const int cy = 21 + dy, cx = 21 + dx;
-      int s = 0;
+  int px[8];
 #pragma unroll
-      for (int j = 0; j < 7; j++) {
-        const uint8_t* row = P + (cy + j - 3) * PATCH + cx - 3;
-        int rs = 0;
-#pragma unroll
-        for (int i = 0; i < 7; i++) rs += gk[i] * row[i];
-        s += gk[j] * rs;
-      }
-      val[e] = min(max((s + (1 << 15)) >> 16, 0), 255);
-    }
-    nib |= (val[0] < val[1]) << t;
+  for (int e = 0; e < 8; e++) {
+    const int pi = 16 * byte + 8 * half + e;
+    const float fx = (float)c_pattern[2 * pi], fy = (float)c_pattern[2 * pi + 1];
+    const int dy = dev_round(fadd(fmul(fx, b), fmul(fy, a)));
+    const int dx = dev_round(fsub(fmul(fx, a), fmul(fy, b)));
+    px[e] = bc[dy * L.pitch + dx];
   }
+  int nib = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) nib |= (px[2 * t] < px[2 * t + 1]) << t;
   const int other = __shfl_xor(nib, 1, 64);
   const long long oi = (long long)f * cap + off + k;
   if (half == 0) out_desc[oi * 32 + byte] = (uint8_t)(nib | (other << 4));
@@ -838,6 +908,18 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
     }
   }
   pyr_bytes = (long long)((poff + 255) & ~255LL);
+  {
+    // blur area: level 0 plane then levels 1.. in the pyramid layout
+    const long long l0 = (long long)levels[0].pitch * levels[0].h;
+    btiles.clear();
+    for (int l = 0; l < nl; l++) {
+      LevelDev& L = levels[l];
+      L.blur_off = l == 0 ? 0 : l0 + L.plane_off;
+      for (int y = 0; y < L.h; y += 16)
+        for (int x = 0; x < L.w; x += 64) btiles.push_back(BlurTile{(int16_t)l, 0, (int16_t)x, (int16_t)y});
+    }
+    blur_bytes = (l0 + poff + 255) & ~255LL;
+  }
   cand_stride = ((long long)cand_total + 63) & ~63LL;
   sel_stride = ((long long)sel_total + 63) & ~63LL;
   cap = sel_total;
@@ -869,6 +951,8 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
   if ((rc = up((void**)&d_umax, umax.data(), umax.size() * sizeof(int)))) return rc;
   if ((rc = up((void**)&d_gk, gk.data(), gk.size() * sizeof(int)))) return rc;
   if ((rc = up((void**)&d_slot_map, slot_map.data(), slot_map.size() * sizeof(int2)))) return rc;
+  if ((rc = up((void**)&d_btiles, btiles.data(), btiles.size() * sizeof(BlurTile)))) return rc;
+  EAO_HIP_CHECK(hipMalloc(&d_blur, blur_bytes * B));
   EAO_HIP_CHECK(hipMalloc(&d_pyr, std::max<long long>(pyr_bytes, 256) * B));
   EAO_HIP_CHECK(hipMalloc(&d_cand, cand_stride * sizeof(uint32_t) * B));
   EAO_HIP_CHECK(hipMalloc(&d_qbuf, 2 * cand_stride * sizeof(uint32_t) * B));
@@ -885,7 +969,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
 
 OrbEngine::~OrbEngine() {
   void* ptrs[] = {d_levels, d_cells, d_xofs, d_ia, d_yrows, d_ib, d_umax, d_gk, d_slot_map,
-                  d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
+                  d_btiles, d_blur, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
                   d_out_desc, d_out_cnt};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -934,15 +1018,22 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        sel_stride, d_sel_cnt, nl);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[3], s));
+  // blurred levels
+  {
+    dim3 g((unsigned)btiles.size(), nframes);
+    hipLaunchKernelGGL(k_blur, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels,
+                       d_btiles, d_gk, d_blur, blur_bytes);
+  }
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
   // orientation + descriptors
   {
     const int nslots = (int)slot_map.size();
     dim3 g((nslots + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
-                       d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax,
-                       d_gk, d_kps, d_desc, d_counts, out_cap);
+    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_blur,
+                       blur_bytes, d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax,
+                       d_kps, d_desc, d_counts, out_cap);
   }
-  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[5], s));
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }

@@ -134,9 +134,9 @@ class Orb:
         check(lib().eao_orb_set_timing(self.h, int(on)), "eao_orb_set_timing")
 
     def stage_ms(self):
-        ms = np.zeros(4, np.float32)
-        check(lib().eao_orb_stage_ms(self.h, P(ms)), "eao_orb_stage_ms")
-        return ms
+        ms = np.zeros(8, np.float32)
+        n = check(lib().eao_orb_stage_ms(self.h, P(ms), len(ms)), "eao_orb_stage_ms")
+        return ms[:n]
 
     def extract_batch_device(self, frames_ptr, nframes, pitch, kps_ptr, desc_ptr, counts_ptr, cap, stream=None):
         check(lib().eao_orb_extract_batch_device(self.h, ctypes.c_void_p(frames_ptr), nframes, pitch,

@@ -84,10 +84,11 @@ int eao_orb_extract_batch_device(eao_orb* h, const uint8_t* d_frames, int nframe
                                  eao_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap,
                                  void* stream);
 /* per-stage timing of the batched path (HIP events on the launch stream):
-   enable once, then after a run eao_orb_stage_ms returns 4 values in ms:
-   pyramid (7 resizes), FAST cells, quadtree distribution, orient+describe. */
+   enable once, then after a run eao_orb_stage_ms writes min(n, 5) values in
+   ms -- pyramid (7 resizes), FAST cells, quadtree distribution, level blur,
+   orient+describe -- and returns the number of stages (5). */
 int eao_orb_set_timing(eao_orb* h, int on);
-int eao_orb_stage_ms(eao_orb* h, float* ms4);
+int eao_orb_stage_ms(eao_orb* h, float* ms, int n);
 /* debug taps for parity tests (device work, host results) */
 int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out /* concatenated levels */);
 

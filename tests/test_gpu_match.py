@@ -102,3 +102,48 @@ def test_initialization(frames):
     no, mo, po = orc.match_init(orc.cam(), 0.9, 1, k1, d1, k2, d2, prev, 100)
     assert ng == no and np.array_equal(mg, mo) and np.array_equal(pg, po)
     assert no > 100
+
+
+def test_motion_batch_device_exact():
+    """Batched HBM-resident extraction + motion matching (the bench path) vs the
+    oracle frame by frame: keypoints, descriptors and match ids bit-exact."""
+    import torch
+    F = 6
+    fr, poses = synth.frame_stream(F, seed=0xEA7)
+    dev = torch.device("cuda", 0)
+    orb = ea.Orb(max_batch=F)
+    cap = orb.cap
+    d_fr = torch.from_numpy(np.stack(fr)).to(dev)
+    kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    s = torch.cuda.Stream(dev)
+    orb.extract_batch_device(d_fr.data_ptr(), F, 640, kps.data_ptr(), desc.data_ptr(), cnt.data_ptr(), cap,
+                             s.cuda_stream)
+    torch.cuda.synchronize()
+    n = cnt.cpu().numpy()
+    hk = kps.cpu().numpy().view(ea.KP_DTYPE).reshape(F, cap)
+    hd = desc.cpu().numpy()
+    ok, od = zip(*[orc.extract(f) for f in fr])
+    for t in range(F):
+        assert n[t] == len(ok[t]) and np.array_equal(hk[t, :n[t]], ok[t]) and np.array_equal(hd[t, :n[t]], od[t])
+    rng = np.random.default_rng(5)
+    has = np.zeros((F, cap), np.uint8)
+    pos = np.zeros((F, cap, 3), np.float32)
+    for t in range(F):
+        has[t, :n[t]] = rng.random(n[t]) < 0.9
+        pos[t, :n[t]] = synth.backproject(poses[t], ok[t]["x"], ok[t]["y"])
+    T = torch.from_numpy(np.stack(poses).astype(np.float32).reshape(F, 16)).to(dev)
+    d_has = torch.from_numpy(has).to(dev)
+    d_pos = torch.from_numpy(pos).to(dev)
+    match = torch.full((F, cap), -1, dtype=torch.int32, device=dev)
+    nm = torch.zeros(F, dtype=torch.int32, device=dev)
+    ea.Matcher(max_kps=cap, max_batch=F).motion_batch_device(
+        ea.camera(), F, cap, T.data_ptr(), 15, 1, kps.data_ptr(), desc.data_ptr(), cnt.data_ptr(), d_has.data_ptr(),
+        d_pos.data_ptr(), desc.data_ptr(), SC, match.data_ptr(), nm.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    hm, hn = match.cpu().numpy(), nm.cpu().numpy()
+    for t in range(1, F):
+        no, mo = orc.match_motion(orc.cam(), poses[t], 15, 1, ok[t - 1], has[t - 1, :n[t - 1]],
+                                  pos[t - 1, :n[t - 1]], od[t - 1], ok[t], od[t], SC)
+        assert hn[t] == no and np.array_equal(hm[t, :n[t]], mo), t
