@@ -181,6 +181,114 @@ __global__ __launch_bounds__(64) void k_fast(const uint8_t* __restrict__ frames,
   if (lane == 0) cell_cnt[f * ncells + ci] = n;
 }
 
+// FAST corner strength of a pixel: S = max over the 16 arcs of 9 of
+// max(min d, min -d), d = centre - ring. The pixel is a FAST-9 corner at
+// threshold th iff S > th, and OpenCV's cornerScore<16> at that threshold is
+// then S - 1 (its a0 starts at th < S), so one strength map serves both the
+// iniTh pass and the minTh retry.
+__device__ __forceinline__ int fast_strength(const uint8_t* roi, int RS, int r, int c) {
+  const int v = roi[r * RS + c];
+  int d[25];
+#pragma unroll
+  for (int k = 0; k < 16; k++) d[k] = v - (int)roi[(r + c_off16[k][1]) * RS + c + c_off16[k][0]];
+#pragma unroll
+  for (int k = 16; k < 25; k++) d[k] = d[k - 16];
+  int u = -256, w = 256;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    int a = min(d[k + 1], d[k + 2]), b = max(d[k + 1], d[k + 2]);
+#pragma unroll
+    for (int q = 3; q <= 8; q++) {
+      a = min(a, d[k + q]);
+      b = max(b, d[k + q]);
+    }
+    u = max(u, max(min(a, d[k]), min(a, d[k + 9])));
+    w = min(w, min(max(b, d[k]), max(b, d[k + 9])));
+  }
+  return max(0, max(u, -w));
+}
+
+// One workgroup per (row of cells, frame): the band's ROI staged in LDS,
+// the strength of every detection pixel computed once, then one wave per
+// cell applies ORBextractor.cc:789-829 -- FAST at iniTh with in-cell 3x3
+// non-max suppression (neighbours outside the cell's detection window count
+// as 0, Q15), retry at minTh only when the cell found nothing -- and emits
+// the corners row-major.
+__global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ frames, int fpitch,
+                                                   long long fstride, const uint8_t* __restrict__ pyr,
+                                                   long long pstride, const LevelDev* __restrict__ levels,
+                                                   const BandDev* __restrict__ bands,
+                                                   const CellDev* __restrict__ cells, int iniTh, int minTh,
+                                                   int RS, uint32_t* __restrict__ cand, long long cand_stride,
+                                                   int* __restrict__ cell_cnt, int ncells) {
+  extern __shared__ uint8_t smem[];
+  const BandDev B = bands[blockIdx.x];
+  const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const LevelDev& L = levels[B.level];
+  const uint8_t* img;
+  int pitch;
+  if (B.level == 0) {
+    img = frames + f * fstride;
+    pitch = fpitch;
+  } else {
+    img = pyr + f * pstride + L.plane_off;
+    pitch = L.pitch;
+  }
+  const int bw = B.x1 - B.x0, bh = B.y1 - B.y0;
+  uint8_t* roi = smem;
+  uint8_t* S = smem + RS * bh;
+  for (int r = t >> 6; r < bh; r += 4)
+    for (int c = lane; c < bw; c += 64) roi[r * RS + c] = img[(long long)(B.y0 + r) * pitch + B.x0 + c];
+  __syncthreads();
+  // strength of every detection pixel (roi [3, bw-3) x [3, bh-3)), computed once
+  for (int r = 3 + (t >> 6); r < bh - 3; r += 4)
+    for (int c = 3 + lane; c < bw - 3; c += 64) {
+      const int sv = fast_strength(roi, RS, r, c);
+      S[r * RS + c] = (uint8_t)(sv > minTh ? sv : 0);
+    }
+  __syncthreads();
+  for (int cc = wv; cc < B.ncells; cc += 4) {
+    const int ci = B.cell_begin + cc;
+    const CellDev c = cells[ci];
+    // the cell's detection window in band ROI coordinates
+    const int wx0 = c.x0 + 3 - B.x0, wx1 = c.x1 - 3 - B.x0, wy0 = 3, wy1 = c.y1 - c.y0 - 3;
+    const int ww = wx1 - wx0;
+    uint32_t* out = cand + f * cand_stride + c.slot;
+    int n = 0;
+    for (int pass = 0; pass < 2; pass++) {
+      const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
+      n = 0;
+      for (int r = wy0; r < wy1; r++) {
+        for (int c0 = 0; c0 < ww; c0 += 64) {
+          const int x = wx0 + c0 + lane;
+          bool keep = false;
+          int sc = 0;
+          if (c0 + lane < ww) {
+            auto score = [&](int rr, int xx) -> int {
+              if (rr < wy0 || rr >= wy1 || xx < wx0 || xx >= wx1) return 0;
+              const int v = S[rr * RS + xx];
+              return v > th ? v - 1 : 0;
+            };
+            sc = score(r, x);
+            keep = sc > 0 && sc > score(r, x + 1) && sc > score(r, x - 1) && sc > score(r - 1, x - 1) &&
+                   sc > score(r - 1, x) && sc > score(r - 1, x + 1) && sc > score(r + 1, x - 1) &&
+                   sc > score(r + 1, x) && sc > score(r + 1, x + 1);
+          }
+          const uint64_t m = ballot(keep);
+          if (keep) {
+            const int pos = n + popc64(m & lanes_below());
+            // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
+            if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, sc);
+          }
+          n += popc64(m);
+        }
+      }
+      if (n > 0) break;  // ORBextractor.cc:812 -- retry with minTh only when empty
+    }
+    if (lane == 0) cell_cnt[f * ncells + ci] = n;
+  }
+}
+
 // ---------------------------------------------------------------- quadtree
 // One wave per (level, frame). Node list order is kept explicitly in an
 // ordered slot array with push-front semantics; ties in the final-phase sort
@@ -909,6 +1017,30 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
   }
   pyr_bytes = (long long)((poff + 255) & ~255LL);
   {
+    // FAST bands: the cells of a level row share their ROI rows
+    bands.clear();
+    band_w = band_h = 0;
+    for (size_t c = 0; c < cells.size();) {
+      size_t e = c;
+      // split long rows: the band ROI stays <= 512 px wide (LDS budget, u16 queue)
+      while (e < cells.size() && cells[e].level == cells[c].level && cells[e].i == cells[c].i &&
+             (e == c || cells[e].x1 - cells[c].x0 <= 512))
+        e++;
+      BandDev b{};
+      b.level = cells[c].level;
+      b.ncells = (int16_t)(e - c);
+      b.x0 = cells[c].x0;
+      b.x1 = cells[e - 1].x1;
+      b.y0 = cells[c].y0;
+      b.y1 = cells[c].y1;
+      b.cell_begin = (int)c;
+      band_w = std::max(band_w, b.x1 - b.x0);
+      band_h = std::max(band_h, b.y1 - b.y0);
+      bands.push_back(b);
+      c = e;
+    }
+  }
+  {
     // blur area: level 0 plane then levels 1.. in the pyramid layout
     const long long l0 = (long long)levels[0].pitch * levels[0].h;
     btiles.clear();
@@ -952,6 +1084,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
   if ((rc = up((void**)&d_gk, gk.data(), gk.size() * sizeof(int)))) return rc;
   if ((rc = up((void**)&d_slot_map, slot_map.data(), slot_map.size() * sizeof(int2)))) return rc;
   if ((rc = up((void**)&d_btiles, btiles.data(), btiles.size() * sizeof(BlurTile)))) return rc;
+  if ((rc = up((void**)&d_bands, bands.data(), bands.size() * sizeof(BandDev)))) return rc;
   EAO_HIP_CHECK(hipMalloc(&d_blur, blur_bytes * B));
   EAO_HIP_CHECK(hipMalloc(&d_pyr, std::max<long long>(pyr_bytes, 256) * B));
   EAO_HIP_CHECK(hipMalloc(&d_cand, cand_stride * sizeof(uint32_t) * B));
@@ -969,7 +1102,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
 
 OrbEngine::~OrbEngine() {
   void* ptrs[] = {d_levels, d_cells, d_xofs, d_ia, d_yrows, d_ib, d_umax, d_gk, d_slot_map,
-                  d_btiles, d_blur, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
+                  d_btiles, d_bands, d_blur, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
                   d_out_desc, d_out_cnt};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -1001,13 +1134,14 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[1], s));
-  // FAST per cell
+  // FAST per band of cells
   {
-    dim3 g((unsigned)cells.size(), nframes);
-    size_t lds = (size_t)roi_stride * roi_rows * 2;
-    hipLaunchKernelGGL(k_fast, g, dim3(64), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
-                       d_levels, d_cells, p.ini_th_fast, p.min_th_fast, roi_stride, roi_rows,
-                       d_cand, cand_stride, d_cell_cnt, (int)cells.size());
+    const int RS = (band_w + 3) & ~3;
+    dim3 g((unsigned)bands.size(), nframes);
+    size_t lds = (size_t)RS * band_h * 2;  // roi, strength
+    hipLaunchKernelGGL(k_fast_band, g, dim3(256), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
+                       d_levels, d_bands, d_cells, p.ini_th_fast, p.min_th_fast, RS, d_cand, cand_stride,
+                       d_cell_cnt, (int)cells.size());
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[2], s));
   // quadtree distribution
