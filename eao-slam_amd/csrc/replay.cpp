@@ -33,6 +33,7 @@
 #include "../../include/eao_accel.h"
 #include "assoc.h"
 #include "common.h"
+#include "shard.h"
 
 namespace eao {
 
@@ -343,12 +344,20 @@ class ReplayEngine {
   static constexpr int kIfBatches = 8, kIfStreams = 4;
   struct IfBatch {
     std::vector<Obj*> objs;
-    std::vector<int> off;
     int left = 0;  // objects not yet completed
     // speculative NP pairs evaluated right behind the forest, on the object as
     // it will stand after the erasure: (det index, object index, version)
-    std::vector<int> sp_det, sp_obj, sp_ver;
+    std::vector<int> sp_det, sp_obj, sp_ver;  // sp_obj: position in objs
     size_t sp_out = 0;  // byte offset of their stats in h_out
+    // launch list (the owned objects), their offsets in the packed clouds
+    std::vector<int> lc, loff;
+    bool launched = false;
+    // sharded: the all-gathered outcome, an outlier bit mask per object
+    // (mask_off into xres) and the speculative NP stats in sp_* order
+    bool xdone = true;
+    std::vector<unsigned char> xres;
+    std::vector<size_t> mask_off;
+    std::vector<eao_np_stats> spst;
     hipEvent_t ev = nullptr;
     unsigned char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
@@ -358,6 +367,27 @@ class ReplayEngine {
   hipStream_t if_stream[kIfStreams] = {};
   int if_next = 0;
   int pend_err = 0;
+
+  // object sharding (shard.h): the GPU work of object o runs on
+  // rank o->id % sworld and its result records are all-gathered
+  std::unique_ptr<Exchanger> ex;
+  int srank = 0, sworld = 1;
+  double xstat[4] = {0};  // exchanges, bytes per rank, us in the exchange
+  std::vector<unsigned char> xsend, xrecv;
+  int owner(const Obj* o) const { return o->id % sworld; }
+  bool mine(const Obj* o) const { return sworld == 1 || owner(o) == srank; }
+  // all-gather xsend (padded to `bytes`) into xrecv [sworld][bytes]
+  int exchange(size_t bytes) {
+    const double t0 = now_us();
+    bytes = std::max<size_t>(al16(bytes), 16);
+    xsend.resize(bytes, 0);
+    xrecv.resize(bytes * sworld);
+    int rc = ex->allgather(xsend.data(), xrecv.data(), bytes);
+    xstat[0] += 1;
+    xstat[1] += (double)bytes;
+    xstat[2] += now_us() - t0;
+    return rc;
+  }
 
   ~ReplayEngine() {
     for (hipStream_t st : if_stream)
@@ -566,25 +596,21 @@ class ReplayEngine {
       if_next = (k + 1) % kIfBatches;
       IfBatch& b = ifb[k];
       b.objs.clear();
-      b.off.clear();
       b.sp_det.clear();
       b.sp_obj.clear();
       b.sp_ver.clear();
-      int np = 0, maxN = 0;
+      int tot = 0;
       for (; i < todo.size() && (int)b.objs.size() < A->max_clouds; i++) {
         const int n = (int)todo[i]->pts.size();
-        if (!b.objs.empty() && np + n > A->max_points) break;
+        if (!b.objs.empty() && tot + n > A->max_points) break;
         b.objs.push_back(todo[i]);
-        b.off.push_back(np);
-        np += n;
-        maxN = std::max(maxN, n);
+        tot += n;
       }
       const int nb = (int)b.objs.size();
       // speculative NP: every later detection of this frame that will run the
       // NP test against these objects (same class, >= 20 points, Object.cc:255-339)
       std::vector<Det*> sdets;
-      std::vector<int> sdoff;
-      int nfp = 0, max_olen = 0;
+      std::vector<int> sdoff, sdz;
       for (int c = 0; c < nb; c++) {
         Obj* o = b.objs[c];
         if (flag == "NA" || flag == "IoU" || o->bad) continue;
@@ -592,26 +618,52 @@ class ReplayEngine {
         for (size_t q = (size_t)q0; q < kept_cur.size(); q++) {
           Det* f = kept_cur[q];
           if (f->cls != o->cls || f->pts.size() < 20) continue;
-          int di = -1;
-          for (size_t z = 0; z < sdets.size(); z++)
-            if (sdets[z] == f) di = (int)z;
-          if (di < 0) {
-            di = (int)sdets.size();
-            sdets.push_back(f);
-            sdoff.push_back(nfp);
-            nfp += (int)f->pts.size();
-          }
-          b.sp_det.push_back(di);  // remapped to f->index below
-          b.sp_obj.push_back(c);
+          b.sp_det.push_back(f->index);
+          b.sp_obj.push_back(c);  // batch position until the launch list is known
           b.sp_ver.push_back(over[o->id]);
-          max_olen = std::max(max_olen, (int)o->pts.size());
+          sdz.push_back((int)q);
         }
       }
-      const int ns = (int)b.sp_det.size();
-      // in: forest meta [3 nb] | object points [3 np] | object valid [np] | NP meta [4 ns] | th [ns] |
+      // launch list: the batch's objects this rank owns (all of them unsharded),
+      // packed at their own offsets; the speculative pairs of those objects
+      b.lc.clear();
+      b.loff.assign(nb, -1);
+      int np = 0, maxN = 0;
+      for (int c = 0; c < nb; c++) {
+        if (!mine(b.objs[c])) continue;
+        b.lc.push_back(c);
+        b.loff[c] = np;
+        np += (int)b.objs[c]->pts.size();
+        maxN = std::max(maxN, (int)b.objs[c]->pts.size());
+      }
+      std::vector<int> lsp;
+      int nfp = 0, max_olen = 0;
+      for (size_t q = 0; q < b.sp_obj.size(); q++) {
+        if (!mine(b.objs[b.sp_obj[q]])) continue;
+        lsp.push_back((int)q);
+        Det* f = kept_cur[sdz[q]];
+        int di = -1;
+        for (size_t z = 0; z < sdets.size(); z++)
+          if (sdets[z] == f) di = (int)z;
+        if (di < 0) {
+          di = (int)sdets.size();
+          sdets.push_back(f);
+          sdoff.push_back(nfp);
+          nfp += (int)f->pts.size();
+        }
+        sdz[q] = di;
+        max_olen = std::max(max_olen, (int)b.objs[b.sp_obj[q]]->pts.size());
+      }
+      const int nl = (int)b.lc.size(), ns = (int)lsp.size();
+      for (int c = 0; c < nb; c++) b.objs[c]->slot = k;
+      b.left = nb;
+      b.xdone = sworld == 1;
+      b.launched = nl > 0;
+      if (!b.launched) continue;
+      // in: forest meta [3 nl] | object points [3 np] | object valid [np] | NP meta [4 ns] | th [ns] |
       //     frame points [3 nfp] | frame valid [nfp]
       // out (host): scores [np] doubles | NP stats [ns]; device: scores [np] for the NP kernel
-      const size_t o_pts = al16(sizeof(int) * 3 * nb);
+      const size_t o_pts = al16(sizeof(int) * 3 * nl);
       const size_t o_oval = o_pts + sizeof(float) * 3 * (size_t)np;
       const size_t o_spm = al16(o_oval + np);
       const size_t o_th = o_spm + sizeof(int) * 4 * ns;
@@ -636,18 +688,17 @@ class ReplayEngine {
       }
       int* meta = (int*)b.h_in;
       float* pts = (float*)(b.h_in + o_pts);
-      for (int c = 0; c < nb; c++) {
-        Obj* o = b.objs[c];
-        meta[c] = b.off[c];
-        meta[nb + c] = (int)o->pts.size();
-        meta[2 * nb + c] = (int)o->pts.size() / 2;
-        int w = b.off[c];
+      for (int j = 0; j < nl; j++) {
+        Obj* o = b.objs[b.lc[j]];
+        meta[j] = b.loff[b.lc[j]];
+        meta[nl + j] = (int)o->pts.size();
+        meta[2 * nl + j] = (int)o->pts.size() / 2;
+        int w = meta[j];
         for (MapPt* p : o->pts) {
           std::memcpy(&pts[3 * (size_t)w], p->pos, sizeof(float) * 3);
           if (ns) b.h_in[o_oval + w] = p->bad ? 0 : 1;  // out_point is never set (Q7)
           w++;
         }
-        o->slot = k;
       }
       if (ns) {
         int* spm = (int*)(b.h_in + o_spm);
@@ -661,19 +712,16 @@ class ReplayEngine {
             fval[w++] = p->bad ? 0 : 1;
           }
         }
-        for (int q = 0; q < ns; q++) {
-          const int z = b.sp_det[q], c = b.sp_obj[q];
+        for (int j = 0; j < ns; j++) {
+          const int q = lsp[j], z = sdz[q], c = b.sp_obj[q];
           Obj* o = b.objs[c];
-          spm[q] = sdoff[z];
-          spm[ns + q] = (int)sdets[z]->pts.size();
-          spm[2 * ns + q] = b.off[c];
-          spm[3 * ns + q] = (int)o->pts.size();
-          th[q] = o->cls == 62 ? 0.65f : 0.6f;
-          b.sp_det[q] = sdets[z]->index;
-          b.sp_obj[q] = o->id;
+          spm[j] = sdoff[z];
+          spm[ns + j] = (int)sdets[z]->pts.size();
+          spm[2 * ns + j] = b.loff[c];
+          spm[3 * ns + j] = (int)o->pts.size();
+          th[j] = o->cls == 62 ? 0.65f : 0.6f;
         }
       }
-      b.left = nb;
       hipStream_t st = if_stream[k % kIfStreams];
       prof[2] += 1;
       EAO_HIP_CHECK(hipMemcpyAsync(b.d_in, b.h_in, in_bytes, hipMemcpyHostToDevice, st));
@@ -681,8 +729,8 @@ class ReplayEngine {
       // scores go straight to pinned host memory (a device-to-host copy costs
       // ~35 us of round trip per launch on this box) and, for the speculative
       // NP pairs, to device memory too
-      int rc = A->iforest_batch(nb, (const float*)(b.d_in + o_pts), dm, dm + nb, 50, 12345,
-                                (const uint32_t*)(dm + 2 * nb), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
+      int rc = A->iforest_batch(nl, (const float*)(b.d_in + o_pts), dm, dm + nl, 50, 12345,
+                                (const uint32_t*)(dm + 2 * nl), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
                                 ns ? (double*)b.d_out : nullptr);
       if (rc) return rc;
       if (ns) {
@@ -698,6 +746,53 @@ class ReplayEngine {
     }
     return EAO_OK;
   }
+  // sharded: all-gather every rank's outcome of batch b, once, at its first
+  // completion (no object of the batch has changed since the launch): per
+  // owned object an outlier bit mask, then the owned speculative NP stats
+  int exchange_batch(IfBatch& b) {
+    if (b.launched) EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+    const int nb = (int)b.objs.size();
+    const size_t sb = sizeof(eao_np_stats);
+    std::vector<size_t> mb(sworld, 0), nsr(sworld, 0);
+    for (int c = 0; c < nb; c++) mb[owner(b.objs[c])] += (b.objs[c]->pts.size() + 7) / 8;
+    for (size_t q = 0; q < b.sp_obj.size(); q++) nsr[owner(b.objs[b.sp_obj[q]])]++;
+    size_t bytes = 0;
+    for (int r = 0; r < sworld; r++) bytes = std::max(bytes, mb[r] + sb * nsr[r]);
+    xsend.assign(bytes, 0);
+    size_t w = 0;
+    for (int c : b.lc) {
+      const Obj* o = b.objs[c];
+      const float th = o->cls == 62 ? 0.65f : 0.6f;
+      const double* sc = (const double*)b.h_out + b.loff[c];
+      const size_t n = o->pts.size();
+      for (size_t k = 0; k < n; k++)
+        if (sc[k] > th) xsend[w + k / 8] |= (unsigned char)(1u << (k % 8));
+      w += (n + 7) / 8;
+    }
+    size_t j = 0;
+    for (size_t q = 0; q < b.sp_obj.size(); q++)
+      if (mine(b.objs[b.sp_obj[q]])) {  // launch order = sp_* order restricted to this rank
+        std::memcpy(xsend.data() + w + sb * j, b.h_out + b.sp_out + sb * j, sb);
+        j++;
+      }
+    if (int rc = exchange(bytes)) return rc;
+    const size_t stride = xrecv.size() / sworld;
+    b.xres = xrecv;
+    b.mask_off.assign(nb, 0);
+    b.spst.resize(b.sp_obj.size());
+    std::vector<size_t> cm(sworld, 0), cs(sworld, 0);
+    for (int c = 0; c < nb; c++) {
+      const int r = owner(b.objs[c]);
+      b.mask_off[c] = stride * r + cm[r];
+      cm[r] += (b.objs[c]->pts.size() + 7) / 8;
+    }
+    for (size_t q = 0; q < b.sp_obj.size(); q++) {
+      const int r = owner(b.objs[b.sp_obj[q]]);
+      std::memcpy(&b.spst[q], b.xres.data() + stride * r + mb[r] + sb * cs[r]++, sb);
+    }
+    b.xdone = true;
+    return EAO_OK;
+  }
   int complete_forest(Obj* o) {
     if (!o->pending) return EAO_OK;
     if (o->slot < 0) {
@@ -707,25 +802,41 @@ class ReplayEngine {
     }
     Tick tk(&prof[3]);
     IfBatch& b = ifb[o->slot];
-    EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+    if (!b.xdone) {
+      int rc = exchange_batch(b);
+      if (rc) return rc;
+    } else if (b.launched) {
+      EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+    }
     int c = 0;
     while (b.objs[c] != o) c++;
-    const float th = o->cls == 62 ? 0.65f : 0.6f;
-    const double* sc = (const double*)b.h_out + b.off[c];
-    size_t w = 0;
     const size_t n = o->pts.size();
-    for (size_t k = 0; k < n; k++) {
-      if (sc[k] > th) {
-        for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
-      } else {
-        o->pts[w++] = o->pts[k];
+    size_t w = 0;
+    if (sworld > 1) {
+      const unsigned char* m = b.xres.data() + b.mask_off[c];
+      for (size_t k = 0; k < n; k++) {
+        if (m[k / 8] >> (k % 8) & 1) {
+          for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
+        } else {
+          o->pts[w++] = o->pts[k];
+        }
+      }
+    } else {
+      const float th = o->cls == 62 ? 0.65f : 0.6f;
+      const double* sc = (const double*)b.h_out + b.loff[c];
+      for (size_t k = 0; k < n; k++) {
+        if (sc[k] > th) {
+          for (int a = 0; a < 3; a++) o->sum[a] -= o->pts[k]->pos[a];
+        } else {
+          o->pts[w++] = o->pts[k];
+        }
       }
     }
     o->pts.resize(w);
     if (o->pending == 2) mean_std(o);
-    const eao_np_stats* sps = (const eao_np_stats*)(b.h_out + b.sp_out);
+    const eao_np_stats* sps = sworld > 1 ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
     for (size_t q = 0; q < b.sp_obj.size(); q++)
-      if (b.sp_obj[q] == o->id) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
+      if (b.sp_obj[q] == c) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
     o->pending = 0;
     o->slot = -1;
     b.left--;
@@ -768,39 +879,148 @@ class ReplayEngine {
     o->proj = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
   }
 
-  // step 10.1 for all recent objects: one k_rects launch
-  int project_rects_gpu(const std::vector<Obj*>& list) {
-    if (list.empty()) return EAO_OK;
+  // projected rects (step 10.1, Object_Map::ComputeProjectRectFrame) of `list`
+  // and NoParaDataAssociation statistics of the (det, obj) `pairs`: one packed
+  // upload of the points they read, two launches and one synchronisation.
+  // Results: rects [5 per object: x, y, w, h, ok], stats [per pair].
+  int rects_np_launch(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
+                      std::vector<int>& rects, std::vector<eao_np_stats>& stats) {
+    const int nb = (int)list.size(), npairs = (int)pairs.size();
+    rects.assign(5 * (size_t)nb, 0);
+    stats.resize(npairs);
+    if (nb == 0 && npairs == 0) return EAO_OK;
+    std::unordered_map<const void*, int> offs;
+    std::vector<const std::vector<MapPt*>*> srcs;  // point lists in upload order
+    size_t total = 0;
+    auto add = [&](const void* key, const std::vector<MapPt*>& v) {
+      if (offs.emplace(key, (int)total).second) {
+        srcs.push_back(&v);
+        total += v.size();
+      }
+    };
+    for (Obj* o : list) add(o, o->pts);
+    for (auto& pr : pairs) {
+      add(pr.first, pr.first->pts);
+      add(pr.second, pr.second->pts);
+    }
+    // in: rect meta [2 nb] | pair meta [4 npairs] | Tcw [16] | points [3 total] | valid [total]
+    // out: stats [npairs] | rects [4 nb] | ok [nb]
+    const size_t o_pm = sizeof(int) * 2 * (size_t)nb, o_T = al16(o_pm + sizeof(int) * 4 * (size_t)npairs);
+    const size_t o_pts = o_T + sizeof(float) * 16, o_val = o_pts + sizeof(float) * 3 * total;
+    const size_t in_bytes = o_val + total;
+    const size_t o_r = sizeof(eao_np_stats) * (size_t)npairs, o_ok = o_r + sizeof(int) * 4 * (size_t)nb;
+    int rc = stage(in_bytes, o_ok + nb);
+    if (rc) return rc;
+    int* rmeta = (int*)h_in;
+    int* pmeta = (int*)(h_in + o_pm);
+    float* pts = (float*)(h_in + o_pts);
+    uint8_t* valid = h_in + o_val;
+    std::memcpy(h_in + o_T, pz.T, sizeof(float) * 16);
+    {
+      size_t o = 0;
+      for (const std::vector<MapPt*>* v : srcs)
+        for (MapPt* p : *v) {
+          std::memcpy(&pts[3 * o], p->pos, sizeof(float) * 3);
+          valid[o++] = p->bad ? 0 : 1;  // out_point is never set (Q7)
+        }
+    }
+    for (int b = 0; b < nb; b++) {
+      rmeta[b] = offs[list[b]];
+      rmeta[nb + b] = (int)list[b]->pts.size();
+    }
+    int max_olen = 0;
+    for (int k = 0; k < npairs; k++) {
+      const auto& pr = pairs[k];
+      pmeta[k] = offs[pr.first];
+      pmeta[npairs + k] = (int)pr.first->pts.size();
+      pmeta[2 * npairs + k] = offs[pr.second];
+      pmeta[3 * npairs + k] = (int)pr.second->pts.size();
+      if (pmeta[3 * npairs + k] > NP_MAXN) {
+        set_error("replay: object exceeds the NP kernel capacity");
+        return EAO_E_CAPACITY;
+      }
+      max_olen = std::max(max_olen, pmeta[3 * npairs + k]);
+    }
+    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
+    const int* drm = (const int*)d_in;
+    const int* dpm = (const int*)(d_in + o_pm);
+    const float* dpts = (const float*)(d_in + o_pts);
+    const uint8_t* dval = d_in + o_val;
+    // results go straight into pinned host memory
+    rc = A->rects(camdev, (const float*)(d_in + o_T), nb, dpts, drm, drm + nb, (int*)(h_out + o_r), h_out + o_ok,
+                  A->stream);
+    if (rc) return rc;
+    rc = A->np_batch(npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
+                     (eao_np_stats*)h_out, A->stream, max_olen);
+    if (rc) return rc;
+    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    const int* r = (const int*)(h_out + o_r);
+    const uint8_t* ok = h_out + o_ok;
+    for (int b = 0; b < nb; b++) {
+      for (int q = 0; q < 4; q++) rects[5 * b + q] = r[4 * b + q];
+      rects[5 * b + 4] = ok[b];
+    }
+    if (npairs) std::memcpy(stats.data(), h_out, sizeof(eao_np_stats) * npairs);
+    return EAO_OK;
+  }
+
+  // sharded form: each rank launches the objects (and pairs of objects) it
+  // owns, then the records are all-gathered and re-assembled in list order
+  int rects_np(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
+               std::vector<int>& rects, std::vector<eao_np_stats>& stats) {
+    if (sworld == 1) return rects_np_launch(list, pairs, rects, stats);
+    std::vector<Obj*> L;
+    std::vector<std::pair<Det*, Obj*>> P;
+    std::vector<int> nl(sworld, 0), npr(sworld, 0);
+    for (Obj* o : list) {
+      nl[owner(o)]++;
+      if (mine(o)) L.push_back(o);
+    }
+    for (auto& pr : pairs) {
+      npr[owner(pr.second)]++;
+      if (mine(pr.second)) P.push_back(pr);
+    }
+    std::vector<int> R;
+    std::vector<eao_np_stats> S;
+    int rc = rects_np_launch(L, P, R, S);
+    if (rc) return rc;
+    const size_t rb = sizeof(int) * 5, sb = sizeof(eao_np_stats);
+    size_t bytes = 0;
+    for (int q = 0; q < sworld; q++) bytes = std::max(bytes, rb * nl[q] + sb * npr[q]);
+    xsend.assign(bytes, 0);
+    if (!R.empty()) std::memcpy(xsend.data(), R.data(), rb * L.size());
+    if (!S.empty()) std::memcpy(xsend.data() + rb * L.size(), S.data(), sb * P.size());
+    if ((rc = exchange(bytes))) return rc;
+    const size_t stride = xrecv.size() / sworld;
+    std::vector<int> il(sworld, 0), ip(sworld, 0);
+    rects.assign(5 * list.size(), 0);
+    stats.resize(pairs.size());
+    for (size_t b = 0; b < list.size(); b++) {
+      const int q = owner(list[b]);
+      std::memcpy(&rects[5 * b], xrecv.data() + stride * q + rb * il[q]++, rb);
+    }
+    for (size_t k = 0; k < pairs.size(); k++) {
+      const int q = owner(pairs[k].second);
+      std::memcpy(&stats[k], xrecv.data() + stride * q + rb * nl[q] + sb * ip[q]++, sb);
+    }
+    return EAO_OK;
+  }
+
+  // frame start: step 10.1 for the recent objects and the NP statistics of
+  // every (kept detection, same-class object) pair, together
+  int frame_start_gpu(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
+                      const std::vector<int>& di, const std::vector<int>& oi) {
+    if (list.empty() && pairs.empty()) return EAO_OK;
     if (int rc = kick()) return rc;  // pending forests overlap this launch
     Tick tk(&prof[7]);
     prof[6] += 1;
-    const int nb = (int)list.size();
-    int np = 0;
-    for (Obj* o : list) np += (int)o->pts.size();
-    // in: meta [2 nb] | Tcw [16] | points; out: rects [4 nb] | ok [nb]
-    const size_t o_T = al16(sizeof(int) * 2 * nb), o_pts = o_T + sizeof(float) * 16;
-    const size_t in_bytes = o_pts + sizeof(float) * 3 * (size_t)np;
-    int rc = stage(in_bytes, sizeof(int) * 4 * nb + nb);
+    std::vector<int> rects;
+    std::vector<eao_np_stats> st;
+    int rc = rects_np(list, pairs, rects, st);
     if (rc) return rc;
-    int* meta = (int*)h_in;
-    float* pts = (float*)(h_in + o_pts);
-    std::memcpy(h_in + o_T, pz.T, sizeof(float) * 16);
-    int off = 0;
-    for (int b = 0; b < nb; b++) {
-      meta[b] = off;
-      meta[nb + b] = (int)list[b]->pts.size();
-      for (MapPt* p : list[b]->pts) std::memcpy(&pts[3 * (size_t)off++], p->pos, sizeof(float) * 3);
-    }
-    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
-    const int* dmeta = (const int*)d_in;
-    rc = A->rects(camdev, (const float*)(d_in + o_T), nb, (const float*)(d_in + o_pts), dmeta, dmeta + nb,
-                  (int*)h_out, h_out + sizeof(int) * 4 * nb, A->stream);  // results into pinned host memory
-    if (rc) return rc;
-    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
-    const int* r = (const int*)h_out;
-    const uint8_t* ok = h_out + sizeof(int) * 4 * nb;
-    for (int b = 0; b < nb; b++)
-      if (ok[b]) list[b]->proj = IRect(r[4 * b], r[4 * b + 1], r[4 * b + 2], r[4 * b + 3]);
+    for (size_t b = 0; b < list.size(); b++)
+      if (rects[5 * b + 4]) list[b]->proj = IRect(rects[5 * b], rects[5 * b + 1], rects[5 * b + 2], rects[5 * b + 3]);
+    for (size_t k = 0; k < pairs.size(); k++) np_cache[{di[k], oi[k]}] = NpEntry{st[k], over[oi[k]]};
     return EAO_OK;
   }
 
@@ -811,59 +1031,11 @@ class ReplayEngine {
     if (int rc = kick()) return rc;  // pending forests overlap this launch
     Tick tk(&prof[5]);
     prof[4] += 1;
-    const int npairs = (int)pairs.size();
-    // distinct detections / objects are uploaded once
-    std::unordered_map<const void*, int> offs;
-    size_t total = 0;
-    for (auto& pr : pairs) {
-      if (offs.emplace(pr.first, (int)total).second) total += pr.first->pts.size();
-      if (offs.emplace(pr.second, (int)total).second) total += pr.second->pts.size();
-    }
-    // in: meta [4 npairs] | points [3 total] | valid [total]; out: stats [npairs]
-    const size_t o_pts = al16(sizeof(int) * 4 * npairs), o_val = o_pts + sizeof(float) * 3 * total;
-    const size_t in_bytes = o_val + total;
-    int rc = stage(in_bytes, sizeof(eao_np_stats) * npairs);
+    std::vector<int> rects;
+    std::vector<eao_np_stats> st;
+    int rc = rects_np({}, pairs, rects, st);
     if (rc) return rc;
-    int* meta = (int*)h_in;
-    float* pts = (float*)(h_in + o_pts);
-    uint8_t* valid = h_in + o_val;
-    auto put = [&](const void* key, const std::vector<MapPt*>& v) {
-      int o = offs[key];
-      for (MapPt* p : v) {
-        std::memcpy(&pts[3 * (size_t)o], p->pos, sizeof(float) * 3);
-        valid[o++] = p->bad ? 0 : 1;  // out_point is never set (Q7)
-      }
-    };
-    int max_olen = 0;
-    for (int k = 0; k < npairs; k++) {
-      const auto& pr = pairs[k];
-      meta[k] = offs[pr.first];
-      meta[npairs + k] = (int)pr.first->pts.size();
-      meta[2 * npairs + k] = offs[pr.second];
-      meta[3 * npairs + k] = (int)pr.second->pts.size();
-      if (meta[3 * npairs + k] > NP_MAXN) {
-        set_error("replay: object exceeds the NP kernel capacity");
-        return EAO_E_CAPACITY;
-      }
-      max_olen = std::max(max_olen, meta[3 * npairs + k]);
-    }
-    {
-      std::unordered_set<const void*> written;
-      for (auto& pr : pairs) {
-        if (written.insert(pr.first).second) put(pr.first, pr.first->pts);
-        if (written.insert(pr.second).second) put(pr.second, pr.second->pts);
-      }
-    }
-    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
-    const int* dmeta = (const int*)d_in;
-    const float* dpts = (const float*)(d_in + o_pts);
-    const uint8_t* dval = d_in + o_val;
-    rc = A->np_batch(npairs, dpts, dval, dmeta, dmeta + npairs, dpts, dval, dmeta + 2 * npairs,
-                     dmeta + 3 * npairs, (eao_np_stats*)h_out, A->stream, max_olen);  // into pinned host memory
-    if (rc) return rc;
-    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
-    const eao_np_stats* out = (const eao_np_stats*)h_out;
-    for (int k = 0; k < npairs; k++) np_cache[{di[k], oi[k]}] = NpEntry{out[k], over[oi[k]]};
+    for (size_t k = 0; k < pairs.size(); k++) np_cache[{di[k], oi[k]}] = NpEntry{st[k], over[oi[k]]};
     return EAO_OK;
   }
 
@@ -1417,12 +1589,10 @@ class ReplayEngine {
         if ((unsigned long)(long)o->last_add > fid - 30) recent.push_back(o);
         else o->proj = IRect(0, 0, 0, 0);
       }
-      int rc = project_rects_gpu(recent);
-      if (rc) return rc;
-      // NP statistics of every (kept detection, same-class object) pair: one launch
+      // with the NP statistics of every (kept detection, same-class object) pair
+      std::vector<std::pair<Det*, Obj*>> pairs;
+      std::vector<int> di, oi;
       if (flag != "NA" && flag != "IoU") {
-        std::vector<std::pair<Det*, Obj*>> pairs;
-        std::vector<int> di, oi;
         for (Det* f : kept) {
           if (f->pts.size() < 5) continue;
           for (size_t i = 0; i < objs.size(); i++) {
@@ -1433,14 +1603,9 @@ class ReplayEngine {
             oi.push_back((int)i);
           }
         }
-        for (size_t s = 0; s < pairs.size(); s += 4096) {
-          const size_t e = std::min(pairs.size(), s + 4096);
-          std::vector<std::pair<Det*, Obj*>> pp(pairs.begin() + s, pairs.begin() + e);
-          std::vector<int> dd(di.begin() + s, di.begin() + e), ooi(oi.begin() + s, oi.begin() + e);
-          rc = np_pairs(pp, dd, ooi);
-          if (rc) return rc;
-        }
       }
+      int rc = frame_start_gpu(recent, pairs, di, oi);
+      if (rc) return rc;
       prof[14] += now_us() - tA;
       tA = now_us();
       kept_cur = kept;
@@ -1788,6 +1953,58 @@ int eao_replay_local_mapping(eao_replay* r) {
 int eao_replay_profile(eao_replay* r, double* out12) {
   if (!r || !out12) return EAO_E_ARG;
   std::memcpy(out12, r->r.prof, sizeof(double) * 24);
+  return EAO_OK;
+}
+
+}  // extern "C"
+
+namespace {
+struct CallbackExchanger : eao::Exchanger {
+  eao_allgather_fn fn;
+  void* ctx;
+  CallbackExchanger(eao_allgather_fn f, void* c) : fn(f), ctx(c) {}
+  int allgather(const void* send, void* recv, size_t bytes) override {
+    const int rc = fn(ctx, send, recv, bytes);
+    if (rc) eao::set_error("replay: all-gather callback failed");
+    return rc ? EAO_E_ARG : EAO_OK;
+  }
+};
+int shard_check(eao_replay* r, int rank, int world) {
+  if (!r || world < 1 || rank < 0 || rank >= world) return EAO_E_ARG;
+  if (!r->r.objs.empty() || r->r.ini) {
+    eao::set_error("replay: sharding must be set before the first frame");
+    return EAO_E_ARG;
+  }
+  return EAO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx) {
+  if (int rc = shard_check(r, rank, world)) return rc;
+  if (world > 1 && !fn) return EAO_E_ARG;
+  r->r.ex.reset(world > 1 ? new CallbackExchanger(fn, ctx) : nullptr);
+  r->r.srank = rank;
+  r->r.sworld = world;
+  return EAO_OK;
+}
+
+int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* unique_id) {
+  if (int rc = shard_check(r, rank, world)) return rc;
+  if (!unique_id) return EAO_E_ARG;
+  int rc = EAO_OK;
+  eao::Exchanger* x = eao::make_rccl_exchanger(r->r.A->dev, rank, world, unique_id, &rc);
+  if (!x) return rc ? rc : EAO_E_HIP;
+  r->r.ex.reset(x);
+  r->r.srank = rank;
+  r->r.sworld = world;
+  return EAO_OK;
+}
+
+int eao_replay_shard_stats(eao_replay* r, double* out3) {
+  if (!r || !out3) return EAO_E_ARG;
+  std::memcpy(out3, r->r.xstat, sizeof(double) * 3);
   return EAO_OK;
 }
 

@@ -63,6 +63,13 @@ def check(rc, what):
     return rc
 
 
+def rccl_unique_id():
+    """eao_rccl_unique_id: 128-byte RCCL communicator id (one rank creates it)."""
+    out = np.zeros(128, np.uint8)
+    check(lib().eao_rccl_unique_id(P(out)), "eao_rccl_unique_id")
+    return out.tobytes()
+
+
 def device_ok(dev=0):
     return bool(lib().eao_device_ok(dev))
 
@@ -315,6 +322,36 @@ class Replay:
 
     def local_mapping(self):
         check(lib().eao_replay_local_mapping(self.h), "eao_replay_local_mapping")
+
+    ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+    def shard(self, rank, world, allgather=None, unique_id=None):
+        """Object-sharded association (eao_replay_shard_*): call
+        before the first frame on every rank with the same stream.
+        allgather(bytes) -> bytes (world x len, rank order) selects the callback
+        exchanger (e.g. gloo); otherwise unique_id (128 bytes, eao_rccl_unique_id
+        on one rank, broadcast) selects RCCL."""
+        if allgather is not None:
+            def cb(ctx, send, recv, nbytes):
+                try:
+                    data = allgather(ctypes.string_at(send, nbytes))
+                    if len(data) != nbytes * world:
+                        return -1
+                    ctypes.memmove(recv, data, len(data))
+                    return 0
+                except Exception:  # noqa: BLE001 -- reported through the C status
+                    return -1
+            self._cb = Replay.ALLGATHER(cb)
+            check(lib().eao_replay_shard_callback(self.h, rank, world, self._cb, None), "eao_replay_shard_callback")
+        else:
+            uid = np.frombuffer(bytes(unique_id), np.uint8).copy()
+            assert uid.size == 128
+            check(lib().eao_replay_shard_rccl(self.h, rank, world, P(uid)), "eao_replay_shard_rccl")
+
+    def shard_stats(self):
+        out = np.zeros(3, np.float64)
+        check(lib().eao_replay_shard_stats(self.h, P(out)), "eao_replay_shard_stats")
+        return dict(exchanges=int(out[0]), bytes_per_rank=float(out[1]), exchange_us=float(out[2]))
 
     @staticmethod
     def pack(frames, first_id=1):

@@ -51,3 +51,27 @@ def sum_over_ranks(value, device=None):
 def barrier():
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
+
+
+# ---------------------------------------------------------------- Config C
+# Object-sharded association: objects are owned by id mod
+# world; every rank replays the same stream and the owners' result records are
+# all-gathered once per exchange step (eao_replay_shard_*).
+
+def allgather_bytes_gloo(group=None):
+    """An allgather(bytes) -> bytes over a CPU (gloo) process group, for
+    Replay.shard(..., allgather=...). World order, equal lengths."""
+    def ag(data):
+        world = dist.get_world_size(group)
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t, group=group)
+        return b"".join(o.numpy().tobytes() for o in out)
+    return ag
+
+
+def broadcast_bytes(data, src=0, group=None):
+    """Broadcast a small byte string (e.g. the 128-byte RCCL id) from `src`."""
+    obj = [data]
+    dist.broadcast_object_list(obj, src=src, group=group)
+    return obj[0]

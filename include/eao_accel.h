@@ -18,6 +18,7 @@
  */
 #ifndef EAO_ACCEL_H
 #define EAO_ACCEL_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -217,6 +218,22 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
 int eao_replay_num_objects(eao_replay* r);
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats);
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
+
+/* Object-sharded association (Config C; replaces nothing in the
+   reference, which is single-threaded here -- the sharded replay returns the
+   same ids as eao_replay_frame). Every rank replays the same stream; the GPU
+   work of object o (its NP pairs, projected rect, isolation forest) runs on
+   rank o.id % world and the result records are all-gathered. Call before the
+   first frame.
+   eao_replay_shard_rccl: RCCL communicator (one device per rank, xGMI);
+     unique_id = 128 bytes from eao_rccl_unique_id on one rank, broadcast.
+   eao_replay_shard_callback: the all-gather is the caller's (e.g. gloo). */
+typedef int (*eao_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes_per_rank);
+int eao_rccl_unique_id(uint8_t* out128);
+int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* unique_id128);
+int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx);
+/* [0] exchanges, [1] bytes per rank, [2] us spent in the exchange */
+int eao_replay_shard_stats(eao_replay* r, double* out3);
 
 /* development instrumentation: s_memtime stamps of the last isolation-forest
    tree launch (workgroup (0,0)): [0..7] phase boundaries, [10] node count. */

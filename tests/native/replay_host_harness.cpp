@@ -4,6 +4,7 @@
 // infrastructure only -- never part of the product.
 #include <cmath>
 #include "../../eao-slam_amd/csrc/assoc.h"
+#include "../../eao-slam_amd/csrc/shard.h"
 #include "../../oracle/oracle.h"
 #include <string>
 #include <vector>
@@ -59,3 +60,12 @@ AssocEngine::~AssocEngine() {}
 struct eao_assoc { eao::AssocEngine e; };
 namespace eao { AssocEngine* assoc_engine(eao_assoc* a) { return &a->e; } }
 extern "C" eao_assoc* harness_assoc_create() { auto* a = new eao_assoc(); a->e.dev = 0; return a; }
+// the RCCL exchanger is product-only; the harness shards through
+// eao_replay_shard_callback (gloo from Python)
+namespace eao {
+Exchanger* make_rccl_exchanger(int, int, int, const void*, int* rc) {
+  set_error("harness: no RCCL");
+  *rc = -3;
+  return nullptr;
+}
+}  // namespace eao

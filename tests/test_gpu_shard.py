@@ -1,0 +1,122 @@
+"""Object-sharded association on the GPU (Config C).
+
+Unsharded: the Config C stream through the engine == the oracle (ids every
+frame, object points, statistics within 1e-5).
+Sharded, world 2 on the one GPU of the box: two processes, each running the
+engine's kernels for the objects it owns (id mod 2), with the result records
+all-gathered through gloo (eao_replay_shard_callback) and through RCCL
+(eao_replay_shard_rccl, when the RCCL build accepts two ranks on one device).
+Every rank must reproduce the oracle's ids and statistics."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import eao_accel as ea
+import eao_dist
+import pyoracle as orc
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+
+N_FRAMES = 60
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle(frames, flag="EAO"):
+    o = orc.Replay(flag)
+    outs = []
+    for i, f in enumerate(frames):
+        outs.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            o.local_mapping()
+    return outs, o.objects()
+
+
+def _check(outs, objs, ref):
+    ref_outs, (ri, rf, rp) = ref
+    for t, (a, b) in enumerate(zip(outs, ref_outs)):
+        assert np.array_equal(a, b), (t, a.tolist(), b.tolist())
+    gi, gf, gp = objs
+    assert np.array_equal(gi, ri)
+    assert np.allclose(gf, rf, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert len(gp) == len(rp) and all(np.array_equal(np.asarray(a), b) for a, b in zip(gp, rp))
+
+
+def test_config_c_unsharded_matches_oracle():
+    frames = synth.assoc_stream_config_c(N_FRAMES)
+    g = ea.Replay(ea.Assoc(), "EAO")
+    outs = []
+    for i, f in enumerate(frames):
+        outs.append(g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            g.local_mapping()
+    _check(outs, g.objects(), _oracle(frames))
+
+
+def _worker(rank, world, port, mode, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        g = ea.Replay(ea.Assoc(), "EAO")
+        if mode == "gloo":
+            g.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
+        else:
+            uid = eao_dist.broadcast_bytes(ea.rccl_unique_id() if rank == 0 else None)
+            try:
+                g.shard(rank, world, unique_id=uid)
+            except ea.EaoError as e:
+                q.put((rank, None, None, None, "rccl-init: " + str(e)))
+                return
+        outs = []
+        for i, f in enumerate(synth.assoc_stream_config_c(N_FRAMES)):
+            outs.append(g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+            if f["kf"]:
+                g.local_mapping()
+        ints, fl, pts = g.objects()
+        st = g.shard_stats()
+        q.put((rank, outs, (ints, fl, [p.tolist() for p in pts]), st, None))
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, None, None, None, repr(e)))
+
+
+def _run_world2(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+@pytest.mark.parametrize("mode", ["gloo", "rccl"])
+def test_config_c_sharded_world2_matches_oracle(mode):
+    res = _run_world2(mode)
+    errs = [r[4] for r in res if r[4]]
+    if mode == "rccl" and errs and all(e.startswith("rccl-init") for e in errs):
+        pytest.skip("RCCL refused two ranks on one device: %s" % errs[0])
+    assert not errs, errs
+    ref = _oracle(synth.assoc_stream_config_c(N_FRAMES))
+    for rank, outs, objs, st, _ in res:
+        _check(outs, objs, ref)
+        assert st["exchanges"] > 0
+    assert res[0][3]["exchanges"] == res[1][3]["exchanges"]

@@ -1,0 +1,99 @@
+"""World-size-2 gloo tests of the object-sharded association (SURVEY.md §8e,
+Config C): eao_replay_shard_callback on the host harness (tests/native, the
+engine's replay.cpp with oracle-served primitives), two processes, objects
+owned by id mod 2, result records all-gathered through gloo. Every rank must
+return the association ids and object statistics of the unsharded oracle
+replay. CPU only; the RCCL exchanger is covered by tests/test_gpu_shard.py."""
+import ctypes
+import os
+import socket
+import subprocess
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import eao_accel as ea
+import eao_dist
+import pyoracle as orc
+from tools import synth
+
+NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+HARNESS = os.path.join(NATIVE, "_build", "libreplay_host.so")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stream(kind, n):
+    return synth.assoc_stream_config_c(n) if kind == "C" else synth.assoc_stream(n)
+
+
+def _worker(rank, world, port, flag, kind, n, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        H = ctypes.CDLL(HARNESS)
+        H.harness_assoc_create.restype = ctypes.c_void_p
+        ea._lib = H  # this process only talks to the harness build of the engine
+
+        class A:
+            pass
+        a = A()
+        a.h = ctypes.c_void_p(H.harness_assoc_create())
+        g = ea.Replay(a, flag)
+        g.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
+        outs = []
+        for i, f in enumerate(_stream(kind, n)):
+            outs.append(g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+            if f["kf"]:
+                g.local_mapping()
+        ints, fl, pts = g.objects()
+        st = g.shard_stats()
+        dist.destroy_process_group()
+        q.put((rank, outs, ints, fl, [p.tolist() for p in pts], st, None))
+    except Exception as e:  # noqa: BLE001 -- reported to the parent
+        q.put((rank, None, None, None, None, None, repr(e)))
+
+
+def _oracle(flag, kind, n):
+    o = orc.Replay(flag)
+    outs = []
+    for i, f in enumerate(_stream(kind, n)):
+        outs.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            o.local_mapping()
+    return outs, o.objects()
+
+
+@pytest.mark.parametrize("kind,n,flag", [("C", 40, "EAO"), ("fr3", 60, "iForest"), ("fr3", 30, "NP")])
+def test_sharded_replay_world2_matches_oracle(kind, n, flag):
+    orc.lib()
+    subprocess.check_call(["make", "-s", "-C", NATIVE])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, flag, kind, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=600) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[6] is None for r in res), [r[6] for r in res]
+    assert all(p.exitcode == 0 for p in procs)
+    ref_outs, (ri, rf, rp) = _oracle(flag, kind, n)
+    for rank, outs, ints, fl, pts, st, _ in res:
+        for t, (a, b) in enumerate(zip(outs, ref_outs)):
+            assert np.array_equal(a, b), (rank, t, a.tolist(), b.tolist())
+        assert np.array_equal(ints, ri)
+        assert np.allclose(fl, rf, rtol=1e-5, atol=1e-5, equal_nan=True)
+        assert pts == [p.tolist() for p in rp]
+        assert st["exchanges"] > 0
+    # both ranks saw the same exchanges
+    assert res[0][5]["exchanges"] == res[1][5]["exchanges"]

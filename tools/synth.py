@@ -218,3 +218,81 @@ def assoc_stream_fr3(n_frames=405, seed=0xEA1):
     """The benchmark's association workload (BASELINE configs[1], SURVEY §8d input 2)."""
     return assoc_stream(n_frames, seed=seed, classes=FR3_CLASSES, obs_frac=0.5, pts_range=(80, 400),
                         n_background=400)
+
+
+# SURVEY.md §8d input 4 (Config C): 64 objects x 2000 map points, 16 classes,
+# 8 detections per frame each observing m in [50, 300] points of one object
+CONFIG_C_CLASSES = [39, 41, 62, 66, 73, 24, 26, 28, 45, 46, 47, 58, 59, 60, 61, 72]
+
+
+def config_c_scene(seed=0xEA3, n_obj=64, n_pts=2000, spacing=1.5):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    g = int(np.ceil(np.sqrt(n_obj)))
+    objs, pos = [], []
+    for k in range(n_obj):
+        sd = rng.uniform(0.02, 0.2, 3)
+        center = np.array([(k % g) * spacing, (k // g) * spacing, 2 * sd[2]])
+        p = rng.normal(0, 1, (n_pts, 3)) * sd + center
+        n_out = n_pts // 20
+        p[:n_out] = center + rng.uniform(-1, 1, (n_out, 3)) * (2 * sd + 0.5)
+        objs.append(dict(cls=CONFIG_C_CLASSES[k % len(CONFIG_C_CLASSES)], center=center, first=len(pos), n=n_pts))
+        pos.extend(p.tolist())
+    ext = (g - 1) * spacing
+    bg = rng.uniform([-1.0, -1.0, 0.0], [ext + 1.0, ext + 1.0, 1.5], (800, 3))
+    pos.extend(bg.tolist())
+    return objs, np.asarray(pos, np.float32), ext
+
+
+def assoc_stream_config_c(n_frames=1000, seed=0xEA3, K=TUM3_K, w=640, h=480, n_det=8, m_range=(50, 300),
+                          kf_every=5):
+    """Per-frame replay inputs of Config C: the camera sweeps the 8x8 object grid
+    (serpentine), the n_det objects with the most visible points are detected,
+    and each detection observes a random m in m_range of its visible points."""
+    fx, fy, cx, cy = K
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    objs, P, ext = config_c_scene(seed)
+    frames = []
+    for t in range(n_frames):
+        s = t / max(1, n_frames - 1)
+        row = s * 3.0  # three serpentine passes over the grid
+        y = (np.floor(row) + 0.5) * ext / 3.0
+        x = (row % 1.0) if int(row) % 2 == 0 else 1.0 - (row % 1.0)
+        target = np.array([x * ext, y, 0.0])
+        eye = target + np.array([-0.3, -2.2, 3.0])
+        T = _look_at(eye, target)
+        Pc = P @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+        z = Pc[:, 2]
+        u = fx * Pc[:, 0] / z + cx
+        v = fy * Pc[:, 1] / z + cy
+        vis = (z > 0.1) & (u >= 0) & (u < w) & (v >= 0) & (v < h)
+        cand = []
+        for k, o in enumerate(objs):
+            nv = int(vis[o["first"]:o["first"] + o["n"]].sum())
+            if nv >= 0.6 * o["n"]:
+                cand.append((-nv, k))
+        chosen = [k for _, k in sorted(cand)[:n_det]]
+        boxes, obs = [], []
+        for k in chosen:
+            o = objs[k]
+            sel = np.arange(o["first"], o["first"] + o["n"])
+            sv = sel[vis[sel]]
+            core = sv[sv - o["first"] >= o["n"] // 20]
+            x0, x1 = np.percentile(u[core], [1, 99])
+            y0, y1 = np.percentile(v[core], [1, 99])
+            j = rng.integers(-3, 4, 4)
+            bx, by = int(max(0, x0 + j[0])), int(max(0, y0 + j[1]))
+            bw, bh = int(min(w - 1, x1 + j[2]) - bx), int(min(h - 1, y1 + j[3]) - by)
+            if bw > 4 and bh > 4:
+                boxes.append([o["cls"], bx, by, bw, bh])
+                m = int(rng.integers(m_range[0], m_range[1] + 1))
+                obs.append(rng.choice(sv, size=min(m, len(sv)), replace=False))
+        bg = np.arange(objs[-1]["first"] + objs[-1]["n"], len(P))
+        bgv = bg[vis[bg] & (rng.random(len(bg)) < 0.5)]
+        obs = np.concatenate(obs + [bgv]) if obs else bgv
+        obs = obs[rng.permutation(len(obs))]
+        order = rng.permutation(len(boxes))
+        boxes = np.asarray([boxes[i] for i in order], np.int32).reshape(-1, 5)
+        uv = (np.round(np.stack([u[obs], v[obs]], 1) * 10) / 10).astype(np.float32)
+        frames.append(dict(T=T, boxes=boxes, ids=obs.astype(np.int32), pos=P[obs], uv=uv,
+                           bad=np.zeros(len(obs), np.uint8), kf=(t % kf_every == kf_every - 1)))
+    return frames
