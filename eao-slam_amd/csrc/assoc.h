@@ -33,6 +33,10 @@ class AssocEngine {
   size_t lds_limit = 0;
   double* d_scores = nullptr;    // [max_points]
   int max_pairs = 256, max_clouds = 64, max_trees = 64;
+  // resources a finished association replay hands to the next one on this
+  // engine (forest batch slots, streams, pinned staging; opaque, replay.cpp)
+  void* replay_pool = nullptr;
+  void (*replay_pool_free)(void*) = nullptr;
 
   int init(int device, int max_points);
   ~AssocEngine();

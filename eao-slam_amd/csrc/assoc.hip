@@ -21,6 +21,7 @@
 
 #include "assoc.h"
 #include "common.h"
+#include "iforest_wave.h"
 
 namespace eao {
 
@@ -331,10 +332,6 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 }
 
 // ---------------------------------------------------------------- iForest
-// Compiler barrier between the phases of a one-wave algorithm: a wave's LDS
-// operations execute in program order, so only compiler reordering across
-// lanes' data dependencies has to be prevented.
-#define WAVE_FENCE() __asm__ volatile("" ::: "memory")
 
 // in-kernel phase stamps of k_iforest_tree (workgroup (0,0)), read through
 // eao_debug_iforest_stamps: development instrumentation, a few SALU ops
@@ -356,139 +353,18 @@ __device__ __forceinline__ void if_stamp(int k) {
   }
 }
 
-// std::mt19937 for one wave: state in LDS, tempered outputs buffered one per
-// lane in a VGPR and handed out in stream order with v_readlane.
-struct WaveRng {
-  uint32_t* mt;  // LDS [624]
-  int idx;       // next untempered state word (uniform)
-  uint32_t buf;  // lane j: draw number (base + j) of the current chunk
-  int bp, blen;  // uniform read position / valid length of buf
-
-  __device__ void seed(uint32_t s) {
-    if (lane_id() == 0) {
-      uint32_t x = s;
-      mt[0] = x;
-      for (int i = 1; i < 624; i++) {
-        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
-        mt[i] = x;
-      }
-    }
-    idx = 624;
-    bp = blen = 0;
-    WAVE_FENCE();
-  }
-  // libstdc++ _M_gen_rand in chunks of 64 words in increasing order: word k
-  // reads k+1 (old) and (k+397)%624 (new for k >= 227, written by an earlier
-  // chunk), exactly the in-place order of the sequential recurrence.
-  __device__ void twist() {
-    const int l = lane_id();
-    for (int c0 = 0; c0 < 623; c0 += 64) {
-      const int k = c0 + l;
-      uint32_t nv = 0;
-      if (k < 623) {
-        const uint32_t y = (mt[k] & 0x80000000u) | (mt[k + 1] & 0x7fffffffu);
-        nv = mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-      }
-      WAVE_FENCE();
-      if (k < 623) mt[k] = nv;
-      WAVE_FENCE();
-    }
-    if (l == 0) {
-      const uint32_t y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
-      mt[623] = mt[396] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
-    }
-    WAVE_FENCE();
-    idx = 0;
-  }
-  __device__ void refill() {
-    if (idx >= 624) twist();
-    blen = min(64, 624 - idx);
-    const int l = lane_id();
-    uint32_t y = l < blen ? mt[idx + l] : 0u;
-    y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= (y >> 18);
-    buf = y;
-    idx += blen;
-    bp = 0;
-  }
-  __device__ uint32_t next() {
-    if (bp >= blen) refill();
-    return (uint32_t)__builtin_amdgcn_readlane((int)buf, bp++);
-  }
-  // uniform_int_distribution<uint32_t>(0, range-1) with a 32-bit URNG (Lemire)
-  __device__ uint32_t lemire(uint32_t range) {
-    uint64_t product = (uint64_t)next() * (uint64_t)range;
-    uint32_t low = (uint32_t)product;
-    if (low < range) {
-      const uint32_t threshold = (uint32_t)(0u - range) % range;
-      while (low < threshold) {
-        product = (uint64_t)next() * (uint64_t)range;
-        low = (uint32_t)product;
-      }
-    }
-    return (uint32_t)(product >> 32);
-  }
-  // uniform_real_distribution<float>(a, b): generate_canonical<float, 24>
-  __device__ float uniform_real(float a, float b) {
-    float ret = fmul((float)next(), 0x1p-32f);  // == x / 2^32 exactly (power-of-two scale)
-    if (ret >= 1.0f) ret = __uint_as_float(0x3f7fffffu);  // nextafter(1, 0)
-    return fadd(fmul(ret, fsub(b, a)), a);
-  }
-};
-
-__device__ __forceinline__ double iforest_c(uint32_t n) {  // CalculateC, isolation_forest.h:97-118
-  if (n > 2) {
-    const double h = log((double)(n - 1)) + 0.5772156649;
-    return __dsub_rn(2.0 * h, (2.0 * (double)(n - 1)) / (double)n);
-  } else if (n == 2)
-    return 1.0;
-  return 0.0;
-}
-
-// order-preserving int key of a finite float (-0 folded onto +0, so key
-// order and equality are exactly the float comparisons); kfloat inverts it
-__device__ __forceinline__ int fkey(float f) {
-  int b = __float_as_int(f);
-  b = b == (int)0x80000000 ? 0 : b;
-  return b ^ ((b >> 31) & 0x7fffffff);
-}
-__device__ __forceinline__ float kfloat(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
-
-// wave-wide min and max of int keys, uniform results: DPP-fused min/max
-// within rows, then permlane16/32 swaps across rows (gfx950)
-__device__ __forceinline__ void wave_minmax_key(int& mn, int& mx) {
-  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0xB1, 0xF, 0xF, false));
-  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x4E, 0xF, 0xF, false));
-  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x141, 0xF, 0xF, false));  // row_half_mirror
-  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x141, 0xF, 0xF, false));
-  mn = min(mn, __builtin_amdgcn_update_dpp(0, mn, 0x140, 0xF, 0xF, false));  // row_mirror
-  mx = max(mx, __builtin_amdgcn_update_dpp(0, mx, 0x140, 0xF, 0xF, false));
-  auto a = __builtin_amdgcn_permlane16_swap(mn, mn, false, false);
-  auto b = __builtin_amdgcn_permlane16_swap(mx, mx, false, false);
-  mn = min((int)a[0], (int)a[1]);
-  mx = max((int)b[0], (int)b[1]);
-  a = __builtin_amdgcn_permlane32_swap(mn, mn, false, false);
-  b = __builtin_amdgcn_permlane32_swap(mx, mx, false, false);
-  mn = __builtin_amdgcn_readfirstlane(min((int)a[0], (int)a[1]));
-  mx = __builtin_amdgcn_readfirstlane(max((int)b[0], (int)b[1]));
-}
-
-__host__ __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
 struct IfLds {
-  size_t mt, b0, b1, nodes, right, shuf, total;
+  size_t mt, b0, b1, nodes, right, ndep, shuf, total;
   __host__ __device__ IfLds(int N, int S) {
     mt = 0;
     b0 = al16(624 * 4);
     b1 = b0 + al16(12 * (size_t)S);
     nodes = b1 + al16(12 * (size_t)S);
     right = nodes + al16(8 * 2 * (size_t)S);
-    const size_t build_end = right + al16(2 * 2 * (size_t)S);
+    ndep = right + al16(2 * 2 * (size_t)S);
+    const size_t build_end = ndep + al16(2 * (size_t)S);
     // sampling scratch (p, head, next, ids) aliases B1 / nodes, dead until the build
     shuf = b1;
     const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
@@ -533,10 +409,15 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   float* B1 = (float*)(smem + L.b1);
   uint2* nodes = (uint2*)(smem + L.nodes);
   uint16_t* right = (uint16_t*)(smem + L.right);
+  uint8_t* ndep = (uint8_t*)(smem + L.ndep);  // node depth, preorder (right links derive from it)
+  __shared__ int s_nn;
   __shared__ int s_nodes_bad;
 
   const int tr = blockIdx.x, c = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nb = blockDim.x;
+  // the wave index is wave-uniform: readfirstlane tells the compiler, so the
+  // one-wave phases below branch on scalars and keep their state in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, nb = blockDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = len[c];
   const int psi = (int)sample[c];
   const float* P = pts + 3 * (long long)off[c];
@@ -659,22 +540,30 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     // integer ops with DPP + permlane reductions; floats only for the split.
     const int* K0 = (const int*)B0;
     const int maxDepth = (int)ceil(log2((double)psi));
-    int sf = 0, sl = psi - 1, sd = 0, spar = -1;  // lane 0 = root
+    int sf = 0, sl = psi - 1, sd = 0;  // lane 0 = root
     int sp = 1, nn = 0, bad = 0;
     while (sp > 0 && !bad) {
       sp--;
       const int first = __builtin_amdgcn_readlane(sf, sp);
       const int last = __builtin_amdgcn_readlane(sl, sp);
       const int depth = __builtin_amdgcn_readlane(sd, sp);
-      const int parent = __builtin_amdgcn_readlane(spar, sp);
       const int me = nn++;
-      if (parent >= 0 && lane == 0) right[parent] = (uint16_t)me;
       const int cnt = last - first + 1;
+      if (lane == 0) ndep[me] = (uint8_t)depth;
       if (cnt < 2 || depth >= maxDepth) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
       }
       const int* src = (depth & 1) ? (const int*)B1 : K0;
+      if (cnt >= 8 && cnt <= 64) {
+        // whole subtree in rank space (iforest_wave.h rank_subtree)
+        const bool has = lane < cnt;
+        const int kx = has ? src[first + lane] : INT_MAX;
+        const int ky = has ? src[psi + first + lane] : INT_MAX;
+        const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
+        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, ndep);
+        continue;
+      }
       if (cnt <= 64) {
         // whole subtree in registers: item per lane, node sets as lane masks,
         // pending right children on a lane-resident stack
@@ -684,9 +573,10 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const int z = has ? src[2 * psi + first + lane] : 0;
         uint64_t mask = ballot(has);
         int d = depth, node = me, ssp = 0;
-        int slo = 0, shi = 0, sdd = 0, spp = 0;
+        int slo = 0, shi = 0, sdd = 0;
         while (true) {
           IFP_T(t0);
+          IFP_ACC(20, 0ull, 1ull);
           const int cn = popc64(mask);
           bool leaf = cn < 2 || d >= maxDepth;
           if (!leaf) {
@@ -713,12 +603,14 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
               } else {
                 const uint64_t rmk = mask & ~lm;
                 if (rmk == 0) bad = 1;  // empty right range: Node::Build fails
-                if (lane == 0) nodes[node] = make_uint2(dim + 1u, __float_as_uint(split));
+                if (lane == 0) {
+                  nodes[node] = make_uint2(dim + 1u, __float_as_uint(split));
+                  ndep[node] = (uint8_t)d;
+                }
                 if (lane == ssp) {
                   slo = (int)(uint32_t)rmk;
                   shi = (int)(uint32_t)(rmk >> 32);
                   sdd = d + 1;
-                  spp = node;
                 }
                 ssp++;
                 mask = lm;  // left child next (node + 1)
@@ -732,21 +624,23 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
             }
           }
           IFP_T(t6);
-          if (lane == 0) nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
+          if (lane == 0) {
+            nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
+            ndep[node] = (uint8_t)d;
+          }
           if (ssp == 0) break;
           ssp--;
           mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(slo, ssp) |
                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(shi, ssp) << 32);
           d = __builtin_amdgcn_readlane(sdd, ssp);
-          const int par = __builtin_amdgcn_readlane(spp, ssp);
           node = nn++;
-          if (lane == 0) right[par] = (uint16_t)node;
           IFP_T(t7);
           IFP_ACC(17, t6, t7);
         }
         continue;
       }
       int* dst = (depth & 1) ? (int*)B0 : (int*)B1;
+      IFP_T(bb0);
       const uint32_t dim = g.lemire(3);
       int mn = INT_MAX, mx = INT_MIN;
       for (int i = first + lane; i <= last; i += 64) {
@@ -797,19 +691,36 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         sf = middle;
         sl = last;
         sd = depth + 1;
-        spar = me;
       }
       if (lane == sp + 1) {
         sf = first;
         sl = middle - 1;
         sd = depth + 1;
-        spar = -1;
       }
       sp += 2;
+      IFP_T(bb1);
+      IFP_ACC(18, bb0, bb1);
+      IFP_ACC(19, 0ull, 1ull);
     }
-    if (lane == 0) s_nodes_bad = bad;
+    if (lane == 0) {
+      s_nodes_bad = bad;
+      s_nn = nn;
+    }
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
   }
+  __syncthreads();
+  // ---- right links from the preorder depths: q is a right child iff the
+  // node before it is at least as deep; its parent is the last node before q
+  // one level up (everything in between is the left sibling's subtree)
+  if (!s_nodes_bad)
+    for (int q = 1 + tid; q < s_nn; q += nb) {
+      const int dq = ndep[q];
+      if (ndep[q - 1] >= dq) {
+        int p = q - 2;
+        while (ndep[p] != dq - 1) p--;
+        right[p] = (uint16_t)q;
+      }
+    }
   }  // valid
   __syncthreads();
   if_stamp(6);
@@ -913,6 +824,7 @@ int AssocEngine::init(int device, int mp) {
 }
 
 AssocEngine::~AssocEngine() {
+  if (replay_pool && replay_pool_free) replay_pool_free(replay_pool);
   void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_mtinit, d_scores, d_contrib};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);

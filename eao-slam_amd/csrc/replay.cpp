@@ -389,9 +389,65 @@ class ReplayEngine {
     return rc;
   }
 
+  // forest slots, streams and staging outlive the replay: the next replay on
+  // the same engine adopts them (allocation is not per replay)
+  struct Pool {
+    std::vector<IfBatch> ifb;
+    hipStream_t if_stream[kIfStreams] = {};
+    unsigned char *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
+    size_t cap_in = 0, cap_out = 0;
+  };
+  static void free_pool(void* v) {
+    Pool* p = (Pool*)v;
+    ReplayEngine tmp;  // its destructor releases the resources
+    tmp.ifb.swap(p->ifb);
+    for (int k = 0; k < kIfStreams; k++) tmp.if_stream[k] = p->if_stream[k];
+    tmp.h_in = p->h_in;
+    tmp.d_in = p->d_in;
+    tmp.h_out = p->h_out;
+    tmp.d_out = p->d_out;
+    delete p;
+  }
+  void adopt() {
+    if (!A || !A->replay_pool) return;
+    Pool* p = (Pool*)A->replay_pool;
+    A->replay_pool = nullptr;
+    ifb.swap(p->ifb);
+    for (IfBatch& b : ifb) {
+      b.objs.clear();
+      b.left = 0;
+      b.xdone = true;
+      b.launched = false;
+    }
+    for (int k = 0; k < kIfStreams; k++) if_stream[k] = p->if_stream[k];
+    h_in = p->h_in;
+    d_in = p->d_in;
+    h_out = p->h_out;
+    d_out = p->d_out;
+    cap_in = p->cap_in;
+    cap_out = p->cap_out;
+    delete p;
+  }
   ~ReplayEngine() {
     for (hipStream_t st : if_stream)
       if (st) (void)hipStreamSynchronize(st);
+    if (A && !A->replay_pool && !ifb.empty()) {
+      Pool* p = new Pool();
+      p->ifb.swap(ifb);
+      for (int k = 0; k < kIfStreams; k++) {
+        p->if_stream[k] = if_stream[k];
+        if_stream[k] = nullptr;
+      }
+      p->h_in = h_in;
+      p->d_in = d_in;
+      p->h_out = h_out;
+      p->d_out = d_out;
+      p->cap_in = cap_in;
+      p->cap_out = cap_out;
+      h_in = d_in = h_out = d_out = nullptr;
+      A->replay_pool = p;
+      A->replay_pool_free = &ReplayEngine::free_pool;
+    }
     for (IfBatch& sl : ifb) {
       if (sl.ev) (void)hipEventDestroy(sl.ev);
       if (sl.h_in) (void)hipHostFree(sl.h_in);
@@ -555,7 +611,9 @@ class ReplayEngine {
   }
   // launch every pending, not yet launched object (one or more batches)
   int kick() {
+    Tick tk(&prof[18]);
     std::vector<Obj*> todo;
+    double tscan = now_us();
     for (auto& up : objs) {
       Obj* o = up.get();
       if (!o->pending || o->slot >= 0) continue;
@@ -569,6 +627,7 @@ class ReplayEngine {
       }
       todo.push_back(o);
     }
+    prof[22] += now_us() - tscan;
     if (todo.empty()) return EAO_OK;
     if (ifb.empty()) {
       int rc = if_init();
@@ -585,6 +644,8 @@ class ReplayEngine {
         }
       }
       if (k < 0) {  // every batch in flight: retire the oldest
+        Tick tr(&prof[21]);
+        prof[20] += 1;
         k = if_next;
         std::vector<Obj*> os = ifb[k].objs;
         for (Obj* o : os)
@@ -607,6 +668,7 @@ class ReplayEngine {
         tot += n;
       }
       const int nb = (int)b.objs.size();
+      Tick tpk(&prof[23]);
       // speculative NP: every later detection of this frame that will run the
       // NP test against these objects (same class, >= 20 points, Object.cc:255-339)
       std::vector<Det*> sdets;
@@ -724,6 +786,7 @@ class ReplayEngine {
       }
       hipStream_t st = if_stream[k % kIfStreams];
       prof[2] += 1;
+      Tick tl(&prof[19]);
       EAO_HIP_CHECK(hipMemcpyAsync(b.d_in, b.h_in, in_bytes, hipMemcpyHostToDevice, st));
       const int* dm = (const int*)b.d_in;
       // scores go straight to pinned host memory (a device-to-host copy costs
@@ -1169,7 +1232,11 @@ class ReplayEngine {
   int associate(Det* f) {
     if (flag == "None") biForest = false;
     cur_np_done = false;
-    int rc = flush(f->cls);
+    int rc;
+    {
+      Tick tk(&prof[16]);  // waits for same-class forests
+      rc = flush(f->cls);
+    }
     if (rc) return rc;
     const IRect RC = f->box;
     float IouMax = 0;
@@ -1623,7 +1690,10 @@ class ReplayEngine {
       cur_np_done = true;
       prof[15] += now_us() - tA;
       tA = now_us();
-      rc = flush(-1);
+      {
+        Tick tk(&prof[17]);  // end-of-frame forest completion
+        rc = flush(-1);
+      }
       if (rc) return rc;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
         if (flag == "NA") continue;
@@ -1901,6 +1971,7 @@ int eao_replay_create(eao_assoc* a, const char* flag, int img_w, int img_h, cons
   r->r.pz.rows = img_h;
   eao_camera c{img_w, img_h, K4[0], K4[1], K4[2], K4[3]};
   r->r.camdev = make_cam(c);
+  r->r.adopt();
   *out = r.release();
   return EAO_OK;
 }

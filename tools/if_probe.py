@@ -28,3 +28,4 @@ for n in (100, 300, 600, 1000, 2000):
     if st[12:18].any():
         print("   register path (cycles, cumulative over calls): lemire %d minmax %d uniform %d ballot %d push %d leaf/pop %d"
               % tuple(int(v) for v in st[12:18]))
+        print("   big-node path cycles %d over %d nodes; register-path steps %d" % tuple(int(v) for v in st[18:21]))

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #define CK(x) do { if ((x) != hipSuccess) { printf("err %s line %d\n", #x, __LINE__); return 1; } } while (0)
 __global__ void k_nop(int* p) { if (threadIdx.x == 0 && p) p[blockIdx.x] = 1; }
 __global__ void k_write_host(double* h, int n) { int i = blockIdx.x * blockDim.x + threadIdx.x; if (i < n) h[i] = i * 0.5; }
@@ -47,6 +49,25 @@ int main() {
     printf("H2D async call %.2f us | launch call %.2f us (drain %.1f us/launch) | event record %.2f us | "
            "H2D+kernel+D2H+sync round trip %.1f us | kernel+sync %.1f us | H2D+kernel(write host)+sync %.1f us\n",
            (t1 - t0) / R, (t3 - t2) / R, (t4 - t2) / R, (t5 - t4) / R, rt / 200, rt2 / 200, rt3 / 200);
+  }
+  {  // CPU access cost of pinned (hipHostMalloc) vs pageable memory
+    unsigned char* pg = (unsigned char*)malloc(1 << 20);
+    float src[3] = {1.f, 2.f, 3.f};
+    for (int pass = 0; pass < 2; pass++) {
+      unsigned char* buf = pass ? pg : h;
+      double a = now();
+      for (int r = 0; r < 100; r++)
+        for (int i = 0; i < 2000; i++) memcpy(buf + 12 * i, src, 12);  // 2000 packed points
+      double b = now();
+      hipLaunchKernelGGL(k_write_host, dim3(8), dim3(256), 0, s, (double*)h, 2000);
+      CK(hipStreamSynchronize(s));
+      double c = now(), acc = 0;
+      for (int r = 0; r < 100; r++)
+        for (int i = 0; i < 2000; i++) acc += ((double*)buf)[i];
+      double e = now();
+      printf("%s: write 2000 x 12 B %.2f us | read 2000 doubles %.2f us (%g)\n", pass ? "pageable" : "hipHostMalloc",
+             (b - a) / 100, (e - c) / 100, acc);
+    }
   }
   double* hd = (double*)h;
   printf("host sees %.1f %.1f\n", hd[2], hd[1999]);

@@ -9,7 +9,9 @@ sys.path.insert(0, ROOT)
 from tools import synth  # noqa: E402
 
 out = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/stream.bin"
-fr = synth.assoc_stream_fr3(405)
+kind = sys.argv[2] if len(sys.argv) > 2 else "fr3"
+nfr = int(sys.argv[3]) if len(sys.argv) > 3 else (405 if kind == "fr3" else 1000)
+fr = synth.assoc_stream_fr3(nfr) if kind == "fr3" else synth.assoc_stream_config_c(nfr)
 with open(out, "wb") as f:
     np.array([len(fr)], np.int32).tofile(f)
     for t in fr:

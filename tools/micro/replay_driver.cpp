@@ -42,9 +42,9 @@ int main(int argc, char** argv) {
     double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     double pr[24]; eao_replay_profile(rp, pr);
     printf("rep %d: %.1f ms (%.0f us/frame) frame %.0f lm %.0f | iforest %.0f %.0f | np %.0f %.0f | rects %.0f %.0f"
-           " | sections(us/frame) pts %.0f stats %.0f gpu0 %.0f assoc %.0f | spec %.0f\n", r,
+           " | sections(us/frame) pts %.0f stats %.0f gpu0 %.0f assoc %.0f | spec %.0f | flush cls %.0f end %.0f | kick %.0f launch %.0f | retire %.0f x %.0f us | scan %.0f pack+launch %.0f\n", r,
            dt * 1e3, dt * 1e6 / n, pr[0] / 1e3, pr[1] / 1e3, pr[2], pr[3] / 1e3, pr[4], pr[5] / 1e3, pr[6], pr[7] / 1e3,
-           pr[12] / n, pr[13] / n, pr[14] / n, pr[15] / n, pr[9]);
+           pr[12] / n, pr[13] / n, pr[14] / n, pr[15] / n, pr[9], pr[16] / n, pr[17] / n, pr[18] / n, pr[19] / n, pr[20], pr[21] / n, pr[22] / n, pr[23] / n);
     eao_replay_destroy(rp);
   }
   return 0;
