@@ -17,8 +17,10 @@ over the whole 405-frame stream, everything resident in HBM before timing:
      It runs on its own host thread + HIP stream, overlapped with 1-2 the way
      the reference's Tracking thread overlaps the next frame's extraction.
 
-The EAO flag is iForest + yaw sampling; yaw sampling is out of scope (SURVEY
-§8f rank 1), so the association runs in the iForest ensemble mode.
+The EAO flag is the full ensemble: IoU / NP / projected IoU / t-test
+association, isolation forests, and the object-line association + yaw sampling
+(Tracking.cc:2472-2527, 2624-2871) over each frame's synthetic line segments
+(projected ground-truth cuboid edges, +-2 deg noise, broken edges, clutter).
 
 Multi-GPU: frames are independent units, so each rank processes
 its own 405-frame stream shard with no data-path collective ("scaling":
@@ -272,7 +274,7 @@ def main():
             "data": "synthetic (procedural textured plane along a smooth camera path; seeded object clouds "
                     "observed as ~8 YOLO-shaped boxes and ~800 tracked map points per frame; SURVEY.md §8d input 2)",
             "config": {"workload": "mono_tum EAO fr3_long_office 640x480 (synthetic, %d frames/rank/step, "
-                                   "%d ORB features, 8 levels, assoc flag EAO=iForest ensemble)" % (F, NFEAT),
+                                   "%d ORB features, 8 levels, assoc flag EAO: iForest + object lines + yaw sampling)" % (F, NFEAT),
                        "frames_per_step": F, "features": NFEAT, "levels": NLEV, "parallelism": "frames%d" % world},
             "roofline": {"bound": "hbm", "kernel": kernels[dom_name], "achieved": ach, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": None,
@@ -335,7 +337,7 @@ def cpu_baseline(args, data, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu
     rp = orc.Replay("EAO")
     ok_assoc = True
     for t, f in enumerate(data.assoc):
-        ids = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+        ids = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
         ok_assoc &= np.array_equal(ids, gpu_ids[t])
         if f["kf"]:
             rp.local_mapping()

@@ -41,6 +41,7 @@ class MatchEngine {
   int* d_out = nullptr;               // [max_kps + 16]
   float* d_T = nullptr;               // [16 * batch]
   float* d_scales = nullptr;          // [32]
+  float* d_geo = nullptr;             // [max_kps][4] per-map-point projection (keyframe search)
 
   int init(int device, int max_kps, int max_batch);
   ~MatchEngine();

@@ -347,6 +347,125 @@ __global__ __launch_bounds__(256) void k_frustum(CamDev cam, const float* __rest
   vcos[i] = viewCos;
 }
 
+// SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist), ORBmatcher.cc:1472-1599
+// (relocalisation, Tracking.cc:2295,2309). One wave. Phase 1 is lane-parallel: each lane
+// projects its map points (no depth test, as :1501-1506), applies the distance gate and
+// PredictScale (clamped, Q13) and leaves (u, v, radius, level) in geo[]. Phase 2 walks the
+// map points in order with the first-wins assignment (Q17/Q18) like k_match_motion.
+__global__ __launch_bounds__(64) void k_match_keyframe(
+    CamDev cam, const float* __restrict__ Tg, float th, int orb_dist, int check_ori, int n_kf,
+    const eao_keypoint_dev* __restrict__ KK, const uint8_t* __restrict__ valid,
+    const float* __restrict__ pos, const uint8_t* __restrict__ mdesc,
+    const float* __restrict__ mind, const float* __restrict__ maxd, float logsf, int n_cur,
+    const eao_keypoint_dev* __restrict__ CK, const uint8_t* __restrict__ CD,
+    const int* __restrict__ pre, int nlevels, const float* __restrict__ scales,
+    const int* __restrict__ GS, const int* __restrict__ GI, float4* __restrict__ geo,
+    int* __restrict__ out, int* __restrict__ nmatch_out) {
+  __shared__ int match[MAXK];
+  __shared__ signed char bins[MAXK];
+  __shared__ int hist[HISTO_LENGTH];
+  const int lane = threadIdx.x;
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tg[k];
+  float Ow[3];  // -Rcw^T tcw: transposed gemm operand, double accumulation (see k_frustum)
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    double s = (double)T[c] * (double)T[3];
+    s = __dadd_rn(s, (double)T[4 + c] * (double)T[7]);
+    s = __dadd_rn(s, (double)T[8 + c] * (double)T[11]);
+    Ow[c] = (float)(s * -1.0);
+  }
+  for (int i = lane; i < n_cur; i += 64) {
+    match[i] = pre ? pre[i] : -1;
+    bins[i] = -1;
+  }
+  for (int i = lane; i < n_kf; i += 64) {
+    float4 g = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+    if (valid[i]) {
+      const float* P = pos + 3 * i;
+      float Pc[3];
+      transform_point(T, P, Pc);
+      const float invzc = (float)(1.0 / (double)Pc[2]);
+      const float u = fadd(fmul(fmul(cam.fx, Pc[0]), invzc), cam.cx);
+      const float v = fadd(fmul(fmul(cam.fy, Pc[1]), invzc), cam.cy);
+      const float PO[3] = {fsub(P[0], Ow[0]), fsub(P[1], Ow[1]), fsub(P[2], Ow[2])};
+      double s = 0;
+      for (int k = 0; k < 3; k++) s = __dadd_rn(s, __dmul_rn((double)PO[k], (double)PO[k]));
+      const float dist3D = (float)sqrt(s);
+      const float maxDistance = fmul(1.2f, maxd[i]);
+      const float minDistance = fmul(0.8f, mind[i]);
+      if (!(u < cam.minX || u > cam.maxX || v < cam.minY || v > cam.maxY ||
+            dist3D < minDistance || dist3D > maxDistance)) {
+        const float ratio = fdiv(maxd[i], dist3D);
+        int lvl = (int)ceilf(fdiv((float)log((double)ratio), logsf));
+        lvl = min(max(lvl, 0), nlevels - 1);
+        g = make_float4(u, v, fmul(th, scales[lvl]), __int_as_float(lvl));
+      }
+    }
+    geo[i] = g;
+  }
+  __syncthreads();
+  int nmatches = 0;
+  for (int i = 0; i < n_kf; i++) {
+    const float4 g = geo[i];
+    const int lvl = __float_as_int(g.w);
+    if (lvl < 0) continue;
+    const float u = g.x, v = g.y, r = g.z;
+    const Window w = window_cells(cam, u, v, r);
+    if (w.empty) continue;
+    const int minL = lvl - 1, maxL = lvl + 1;
+    const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+    const uint8_t* d = mdesc + 32 * (long long)i;
+    unsigned long long best = KEY_NONE;
+    for (int ck = lane; ck < ncell; ck += 64) {
+      const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
+      const int cell = ix * GRID_ROWS + iy;
+      for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+        const int i2 = GI[q];
+        const eao_keypoint_dev& kp = CK[i2];
+        if (minL > 0 && kp.octave < minL) continue;  // bCheckLevels: minL > 0 || maxL >= 0
+        if (kp.octave > maxL) continue;
+        if (!(fabsf(fsub(kp.x, u)) < r && fabsf(fsub(kp.y, v)) < r)) continue;
+        if (match[i2] >= 0) continue;  // CurrentFrame.mvpMapPoints[i2]
+        const int dist = hamming256(d, CD + 32 * (long long)i2);
+        const unsigned long long key = make_key(dist, ck, i2);
+        best = key < best ? key : best;
+      }
+    }
+    best = wave_min_u64(best);
+    if (best != KEY_NONE && key_dist(best) <= orb_dist) {
+      const int i2 = key_idx(best);
+      if (lane == 0) {
+        match[i2] = i;
+        if (check_ori) bins[i2] = (signed char)rot_bin(KK[i].angle, CK[i2].angle);
+      }
+      nmatches++;
+    }
+    __syncthreads();
+  }
+  if (check_ori) {
+    for (int b = lane; b < HISTO_LENGTH; b += 64) hist[b] = 0;
+    __syncthreads();
+    for (int i2 = lane; i2 < n_cur; i2 += 64)
+      if (bins[i2] >= 0) atomicAdd(&hist[bins[i2]], 1);
+    __syncthreads();
+    int ind1, ind2, ind3;
+    three_maxima(hist, ind1, ind2, ind3);
+    int removed = 0;
+    for (int i2 = lane; i2 < n_cur; i2 += 64) {
+      const int b = bins[i2];
+      if (b >= 0 && b != ind1 && b != ind2 && b != ind3) {
+        match[i2] = -1;
+        removed++;
+      }
+    }
+    nmatches -= wave_sum(removed);
+    __syncthreads();
+  }
+  for (int i2 = lane; i2 < n_cur; i2 += 64) out[i2] = match[i2];
+  if (lane == 0) *nmatch_out = nmatches;
+}
+
 // SearchByProjection(Frame&, vector<MapPoint*>, th), ORBmatcher.cc:45-129
 __global__ __launch_bounds__(64) void k_match_local(
     CamDev cam, float th, float nnratio, int n_mp, const uint8_t* __restrict__ inview,
@@ -550,12 +669,13 @@ int MatchEngine::init(int device, int mk, int mb) {
   EAO_HIP_CHECK(hipMalloc(&d_out, sizeof(int) * (mk * 2 + 16)));
   EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16 * 2));
   EAO_HIP_CHECK(hipMalloc(&d_scales, sizeof(float) * 32));
+  EAO_HIP_CHECK(hipMalloc(&d_geo, sizeof(float) * 4 * mk));
   return EAO_OK;
 }
 
 MatchEngine::~MatchEngine() {
   void* ptrs[] = {d_gstart, d_gitems, d_kps, d_desc, d_u8, d_f, d_f2, d_f3, d_f4,
-                  d_mdesc, d_i32, d_i32b, d_out, d_T, d_scales};
+                  d_mdesc, d_i32, d_i32b, d_out, d_T, d_scales, d_geo};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -746,6 +866,52 @@ int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnrat
                      e.d_f2, e.d_mdesc, n_cur, e.d_kps, e.d_desc,
                      cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart,
                      e.d_gitems, e.d_out, e.d_out + 2 * K);
+  EAO_HIP_CHECK(hipGetLastError());
+  int nm = 0;
+  EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return nm;
+}
+
+int eao_match_keyframe(eao_matcher* m, const eao_camera* cam, const float* Tcw, float th,
+                       int orb_dist, int check_ori, int n_kf, const eao_keypoint* kf_kps,
+                       const uint8_t* kf_mp_valid, const float* kf_mp_pos,
+                       const uint8_t* kf_mp_desc, const float* kf_mp_min_dist,
+                       const float* kf_mp_max_dist, float log_scale_factor, int n_cur,
+                       const eao_keypoint* cur_kps, const uint8_t* cur_desc,
+                       const int32_t* cur_preassigned, int nlevels, const float* scale_factors,
+                       int32_t* cur_match) {
+  if (!m || !cam || !Tcw || n_kf < 0 || n_cur < 0 || nlevels < 1 || nlevels > 32) return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  const int K = e.max_kps;
+  if (n_kf > K || n_cur > K) {
+    set_error("eao_match_keyframe: more keypoints than max_kps");
+    return EAO_E_CAPACITY;
+  }
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = e.stream;
+  // slot 0 = current frame (grid), slot 1 = keyframe keypoints (angles)
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, cur_kps, sizeof(eao_keypoint) * n_cur, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, kf_kps, sizeof(eao_keypoint) * n_kf, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, cur_desc, (size_t)n_cur * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_u8, kf_mp_valid, n_kf, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, kf_mp_pos, sizeof(float) * 3 * n_kf, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_mdesc, kf_mp_desc, (size_t)n_kf * 32, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f3, kf_mp_min_dist, sizeof(float) * n_kf, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f3 + K, kf_mp_max_dist, sizeof(float) * n_kf, hipMemcpyHostToDevice, s));
+  if (cur_preassigned)
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32b, cur_preassigned, sizeof(int) * n_cur, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_T, Tcw, sizeof(float) * 16, hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  int rc = e.build_grid(cd, e.d_kps, nullptr, n_cur, K, 1, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_match_keyframe, dim3(1), dim3(64), 0, s, cd, e.d_T, th, orb_dist, check_ori,
+                     n_kf, e.d_kps + K, e.d_u8, e.d_f, e.d_mdesc, e.d_f3, e.d_f3 + K,
+                     log_scale_factor, n_cur, e.d_kps, e.d_desc,
+                     cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart,
+                     e.d_gitems, reinterpret_cast<float4*>(e.d_geo), e.d_out, e.d_out + 2 * K);
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -118,6 +119,9 @@ struct Det {  // Object_2D
   bool bad = false;
   int mnId = -1, method = 0, index = -1;
   Obj* alias = nullptr;  // _Pos shares mCenter3D's buffer (Object.cc:677, Tracking.cc:2563)
+  // mObjLinesEigen (Tracking.cc:2524): the line angles SampleObjYaw reads, in degrees
+  // as (double)(atan2f-rounded angle * 180) / pi -- only kept for yaw-sampled classes
+  std::vector<double> line_deg;
   const float* P() const;
 };
 
@@ -135,6 +139,9 @@ struct Obj {  // Object_Map
   float xmn = 0, xmx = 0, ymn = 0, ymx = 0, zmn = 0, zmx = 0, lenth = 0, width = 0, height = 0;
   double q[4] = {1, 0, 0, 0}, t[3] = {0, 0, 0}, qn[4] = {1, 0, 0, 0}, tn[3] = {0, 0, 0};
   float rotY = 0, rotP = 0, rotR = 0, rmax = 0;
+  double corner_w[8][3] = {};                  // corner_k_w (pose_without_yaw)
+  std::vector<std::array<float, 5>> angles;    // mvAngleTimesAndScore
+  float err_par = 0, err_yaw = 0;              // mfErrorParallel, mfErroeYaw
   int pending = 0;  // 0 none, 1 iForest, 2 iForest then ComputeMeanAndStandard
   int slot = -1;    // in-flight isolation-forest slot, -1 if not launched
 };
@@ -486,6 +493,207 @@ class ReplayEngine {
     return EAO_OK;
   }
 
+  // ---------------------------------------------------------------- object lines + yaw (E14)
+  std::vector<std::vector<float>> staged_lines;  // eao_replay_lines, one set per frame
+  size_t staged_next = 0;
+
+  static bool yaw_class(int c) { return c == 73 || c == 64 || c == 65 || c == 66 || c == 56; }
+  bool yaw_on() const { return flag != "None" && flag != "iForest"; }
+
+  // merge_break_lines (detect_3d_cuboid/object_3d_util.cpp:349-436; fast_RemoveRow
+  // matrix_utils.cpp:201-205), thresholds of Tracking.cc:2515-2521
+  static void merge_lines(std::vector<double>& L, std::vector<double>& ang) {
+    const double dist_th = 20, ath = 5 / 180.0 * M_PI, len_th = 30;
+    int total = (int)L.size() / 4, counter = 0;
+    bool can = true;
+    auto nrm = [](double x, double y) { return std::sqrt(x * x + y * y); };
+    while (can && counter < 500) {
+      counter++;
+      can = false;
+      ang.resize(total);
+      for (int i = 0; i < total; i++) ang[i] = std::atan2(L[4 * i + 3] - L[4 * i + 1], L[4 * i + 2] - L[4 * i]);
+      for (int s1 = 0; s1 < total - 1 && !can; s1++)
+        for (int s2 = s1 + 1; s2 < total; s2++) {
+          const double diff = std::abs(ang[s1] - ang[s2]);
+          if (!(std::min(diff, M_PI - diff) < ath)) continue;
+          const double* A = &L[4 * s1];
+          const double* B = &L[4 * s2];
+          if (!(nrm(A[2] - B[0], A[3] - B[1]) < dist_th || nrm(B[2] - A[0], B[3] - A[1]) < dist_th)) continue;
+          const double* st = A[0] < B[0] ? A : B;
+          const double* en = A[2] > B[2] ? A : B;
+          const double s0 = st[0], s1y = st[1], e0 = en[2], e1 = en[3];
+          const double t = std::abs(ang[s1] - std::atan2(e1 - s1y, e0 - s0));
+          if (!(std::min(t, M_PI - t) < ath)) continue;
+          L[4 * s1] = s0;
+          L[4 * s1 + 1] = s1y;
+          L[4 * s1 + 2] = e0;
+          L[4 * s1 + 3] = e1;
+          for (int c = 0; c < 4; c++) L[4 * s2 + c] = L[4 * (total - 1) + c];
+          total--;
+          can = true;
+          break;
+        }
+    }
+    int w = 0;
+    for (int i = 0; i < total; i++) {
+      if (!(nrm(L[4 * i + 2] - L[4 * i], L[4 * i + 3] - L[4 * i + 1]) > len_th)) continue;
+      for (int c = 0; c < 4; c++) L[4 * w + c] = L[4 * i + c];
+      w++;
+    }
+    L.resize(4 * w);
+  }
+
+  // Tracking::AssociateObjAndLines (Tracking.cc:2472-2527) for the detections whose
+  // lines SampleObjYaw can read (yaw-sampled classes); the frame's staged line set
+  void associate_lines(const std::vector<Det*>& o2) {
+    const std::vector<float>* fl = staged_next < staged_lines.size() ? &staged_lines[staged_next] : nullptr;
+    if (fl) staged_next++;
+    std::vector<double> all, in, ang;
+    if (fl && yaw_on()) {
+      all.assign(fl->begin(), fl->end());
+      for (size_t i = 0; i + 3 < all.size(); i += 4)  // align_left_right_edges
+        if (all[i + 2] < all[i]) {
+          std::swap(all[i], all[i + 2]);
+          std::swap(all[i + 1], all[i + 3]);
+        }
+      for (Det* f : o2) {
+        if (!yaw_class(f->cls)) continue;
+        const double l = std::max(0.0, f->bx - 15.0), r = (double)std::min(pz.cols, f->bx + f->bw + 15);
+        const double t = std::max(0.0, f->by - 15.0), b = (double)std::min(pz.rows, f->by + f->bh + 15);
+        in.clear();
+        for (size_t i = 0; i + 3 < all.size(); i += 4) {
+          const double* e = &all[i];
+          if (l <= e[0] && e[0] <= r && t <= e[1] && e[1] <= b && l <= e[2] && e[2] <= r && t <= e[3] && e[3] <= b)
+            in.insert(in.end(), e, e + 4);
+        }
+        merge_lines(in, ang);
+        const int n = (int)in.size() / 4;
+        f->line_deg.resize(n);
+        for (int i = 0; i < n; i++) {
+          const float a = (float)std::atan2(in[4 * i + 3] - in[4 * i + 1], in[4 * i + 2] - in[4 * i]);
+          f->line_deg[i] = (double)(a * 180) / M_PI;
+        }
+      }
+    }
+    if (staged_next == staged_lines.size() && !staged_lines.empty()) {
+      staged_lines.clear();
+      staged_next = 0;
+    }
+  }
+
+  // Tracking::SampleObjYaw (Tracking.cc:2624-2871) with WorldToImg (:2602-2620)
+  void sample_yaw(Obj* o) {
+    const std::vector<double>& L = o->frames.back()->line_deg;
+    const int nAll = (int)L.size();
+    int numMax = 0;
+    float fError = 0.0f, fErrorYaw = 0.0f, sampleYaw = 0.0f;
+    float ctr[3], rel[8][3];
+    for (int a = 0; a < 3; a++) ctr[a] = (float)o->center_c[a];
+    for (int k = 0; k < 8; k++)
+      for (int a = 0; a < 3; a++) rel[k][a] = (float)o->corner_w[k][a] - ctr[a];
+    static const int ea[3] = {4, 5, 1}, eb[3] = {5, 6, 5};  // 5->6, 6->7, 2->6 (1-based corners)
+    for (int i = 0; i < 30; i++) {
+      const float yaw = i < 15 ? (float)((0.0 - i * 3.0) / 180.0 * M_PI) : (float)((0.0 + (i - 15) * 3.0) / 180.0 * M_PI);
+      const float pitch = 0.0f, roll = 0.0f;
+      const float cp = std::cos(pitch), sp = std::sin(pitch), sr = std::sin(roll), cr = std::cos(roll);
+      // sin/cos of the sampled yaw correctly rounded via double (Q26): a constant-folded
+      // sinf and a libm sinf may differ by an ulp
+      const float sy = (float)std::sin((double)yaw), cy = (float)std::cos((double)yaw);
+      const float R[3][3] = {{cp * cy, (sr * sp * cy) - (cr * sy), (cr * sp * cy) + (sr * sy)},
+                             {cp * sy, (sr * sp * sy) + (cr * cy), (cr * sp * sy) - (sr * cy)},
+                             {-sp, sr * cp, cr * cp}};
+      float px[8], py[8];
+      for (int k = 0; k < 8; k++) {
+        if (k == 0 || k == 2 || k == 3 || k == 7) continue;  // only corners 2, 5, 6, 7 are read
+        float w[3];
+        for (int r = 0; r < 3; r++) {
+          const float d = R[r][0] * rel[k][0] + R[r][1] * rel[k][1] + R[r][2] * rel[k][2];
+          w[r] = (float)((double)d + (double)ctr[r]);
+        }
+        pz.proj(w, px[k], py[k]);
+      }
+      double adeg[3];
+      float len[3];
+      for (int e = 0; e < 3; e++) {
+        const int a = ea[e], b = eb[e];
+        const float ang = px[b] > px[a] ? std::atan2(py[b] - py[a], px[b] - px[a]) : std::atan2(py[a] - py[b], px[a] - px[b]);
+        adeg[e] = (double)(ang * 180) / M_PI;
+        len[e] = std::sqrt((py[b] - py[a]) * (py[b] - py[a]) + (px[b] - px[a]) * (px[b] - px[a]));
+      }
+      const float mn = std::min(std::min(len[0], len[1]), len[2]);
+      float error = 0.0f, errorYaw = 0.0f;
+      int num = 0;
+      const float th = 5.0f;
+      for (int li = 0; li < nAll; li++) {
+        const float d1 = (float)std::abs(L[li] - adeg[0]);
+        const float d2 = (float)std::abs(L[li] - adeg[1]);
+        const float d3 = (float)std::abs(L[li] - adeg[2]);
+        if (o->cls == 56) {
+          if ((d2 < th) || (d3 < th)) num++;
+          if (d1 < th) num += 3;
+          continue;
+        }
+        if (mn == len[0]) {
+          if ((d2 < th) || (d3 < th)) {
+            num++;
+            if (d2 < th) error += d2;
+            if (d3 < th) error += d3;
+          }
+          errorYaw += std::min(d2, d3);
+        }
+        if (mn == len[1]) {
+          if ((d1 < th) || (d3 < th)) {
+            num++;
+            if (d1 < th) error += d1;
+            if (d3 < th) error += d3;
+          }
+          errorYaw += std::min(d3, d1);
+        }
+        if (mn == len[2]) {
+          if ((d1 < th) || (d2 < th)) {
+            num++;
+            if (d1 < th) error += d1;
+            if (d2 < th) error += d2;
+          }
+          errorYaw += std::min(d2, d1);
+        }
+      }
+      if (num == 0) {
+        num = 1;
+        errorYaw = 10.0f;
+      }
+      if (num > numMax) {
+        numMax = num;
+        sampleYaw = yaw;
+        fError = error;
+        fErrorYaw = (float)((double)(errorYaw / (float)num) / 10.0);
+      }
+    }
+    float fScore = (float)((double)((float)numMax / (float)nAll) * (1.0 - 0.1 * (double)fErrorYaw));
+    if (std::isinf(fScore)) fScore = 0.0f;
+    const std::array<float, 5> v = {sampleYaw, 1.0f, fScore, fError, fErrorYaw};
+    bool fresh = true;
+    for (auto& row : o->angles)
+      if (row[0] == v[0]) {
+        row[1] += 1.0f;
+        for (int q = 2; q < 5; q++) row[q] = v[q] * (1 / row[1]) + row[q] * (1 - 1 / row[1]);
+        fresh = false;
+      }
+    if (fresh) o->angles.push_back(v);
+    std::sort(o->angles.begin(), o->angles.end(),  // VIC, index = 1 (Tracking.cc:63-68)
+              [](const std::array<float, 5>& l, const std::array<float, 5>& r) { return l[1] > r[1]; });
+    int best = 0;
+    float best_score = 0;
+    for (int i = 0; i < std::min(3, (int)o->angles.size()); i++)
+      if (o->angles[i][2] >= best_score) {
+        best_score = o->angles[i][2];
+        best = i;
+      }
+    o->rotY = o->angles[best][0];
+    o->err_par = o->angles[best][3];
+    o->err_yaw = o->angles[best][4];
+  }
+
   // ---------------------------------------------------------------- cuboid / stats
   void update_pose(Obj* o) {  // Object_Map::UpdateObjPose, Object.cc:2193-2248
     const float cp = std::cos(o->rotP), sp = std::sin(o->rotP), sr = std::sin(o->rotR),
@@ -565,6 +773,7 @@ class ReplayEngine {
     for (int k = 0; k < 8; k++) {
       const double v[3] = {cx[k] ? omx[0] : omn[0], cy[k] ? omx[1] : omn[1], cz[k] ? omx[2] : omn[2]};
       se3_apply(o->q, o->t, v, o->corner[k]);
+      se3_apply(o->qn, o->tn, v, o->corner_w[k]);
     }
     o->lenth = omx[0] - omn[0];
     o->width = omx[1] - omn[1];
@@ -1554,6 +1763,7 @@ class ReplayEngine {
           for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
         }
     }
+    associate_lines(o2);  // STEP 3 AssociateObjAndLines, Tracking.cc:1286
     prof[12] += now_us() - tA;
     tA = now_us();
     for (Det* f : o2) {  // STEP 4
@@ -1728,6 +1938,13 @@ class ReplayEngine {
           }
         }
       }
+      if (yaw_on())  // 10.6 SampleObjYaw for regular objects seen this frame (Tracking.cc:1650-1671)
+        for (int i = (int)objs.size() - 1; i >= 0; i--) {
+          Obj* o = objs[i].get();
+          if (o->bad) continue;
+          if ((unsigned long)(long)o->last_add < fid - 5) continue;
+          if (yaw_class(o->cls) && (unsigned long)(long)o->last_add == fid) sample_yaw(o);
+        }
     }
     for (Det* f : o2) {
       const int k = f->index;
@@ -1809,6 +2026,32 @@ class ReplayEngine {
       } else {
         a->lastlast_add = b->lastlast_add;
         a->lastlast = b->frames.size() >= 2 ? b->frames[b->frames.size() - 2]->box : b->frames.front()->box;
+      }
+    }
+    if (yaw_class(a->cls)) {  // step 5. orientation measurements, Object.cc:1842-1901
+      for (auto& rr : b->angles) {
+        bool fresh = true;
+        for (auto& rt : a->angles)
+          if (rr[0] == rt[0]) {
+            rt[1] += rr[1];
+            for (int q = 2; q < 5; q++) rt[q] = rt[q] * ((rt[1] - rr[1]) / rt[1]) + rr[q] * (rr[1] / rt[1]);
+            fresh = false;
+            break;
+          }
+        if (fresh) a->angles.push_back(rr);
+      }
+      if (!a->angles.empty()) {
+        int best = 0;
+        float best_score = 0.0f;
+        for (int i = 0; i < std::min(6, (int)a->angles.size()); i++)
+          if (a->angles[i][2] > best_score) {
+            best_score = a->angles[i][2];
+            best = i;
+          }
+        a->rotY = a->angles[best][0];
+        a->err_par = a->angles[best][3];
+        a->err_yaw = a->angles[best][4];
+        update_pose(a);
       }
     }
   }
@@ -2015,6 +2258,16 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
   return (int)r->r.objs.size();
 }
 
+int eao_replay_lines(eao_replay* r, int n_frames, const int32_t* n_lines, const float* lines) {
+  if (!r || n_frames < 0 || (n_frames && (!n_lines || !lines))) return EAO_E_ARG;
+  for (int t = 0; t < n_frames; t++) {
+    if (n_lines[t] < 0) return EAO_E_ARG;
+    r->r.staged_lines.emplace_back(lines, lines + 4 * (size_t)n_lines[t]);
+    lines += 4 * (size_t)n_lines[t];
+  }
+  return EAO_OK;
+}
+
 int eao_replay_local_mapping(eao_replay* r) {
   if (!r) return EAO_E_ARG;
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
@@ -2107,6 +2360,10 @@ int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
   floats[13] = o->csd_all;
   floats[14] = (float)o->proj.x;
   floats[15] = (float)o->proj.w;
+  floats[16] = o->rotY;
+  floats[17] = (float)o->angles.size();
+  floats[18] = o->err_par;
+  floats[19] = o->err_yaw;
   return EAO_OK;
 }
 

@@ -205,6 +205,20 @@ class Matcher:
                   "eao_match_local")
         return n, out
 
+    def keyframe(self, cam, Tcw, th, orb_dist, check_ori, kf_kps, valid, pos, desc, mind, maxd, logsf,
+                 cur_kps, cur_desc, pre, scales):
+        """SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1472-1599)."""
+        out = np.full(len(cur_kps), -1, np.int32)
+        n = check(lib().eao_match_keyframe(
+            self.h, ctypes.byref(cam), P(np.ascontiguousarray(Tcw, np.float32)), ctypes.c_float(th), int(orb_dist),
+            int(check_ori), len(kf_kps), P(kf_kps), P(np.ascontiguousarray(valid, np.uint8)),
+            P(np.ascontiguousarray(pos, np.float32)), P(np.ascontiguousarray(desc, np.uint8)),
+            P(np.ascontiguousarray(mind, np.float32)), P(np.ascontiguousarray(maxd, np.float32)),
+            ctypes.c_float(logsf), len(cur_kps), P(cur_kps), P(np.ascontiguousarray(cur_desc, np.uint8)),
+            P(np.ascontiguousarray(pre, np.int32)) if pre is not None else None, len(scales),
+            P(np.ascontiguousarray(scales, np.float32)), P(out)), "eao_match_keyframe")
+        return n, out
+
     def init(self, cam, nnratio, check_ori, kps1, desc1, kps2, desc2, prev_xy, window):
         m12 = np.full(len(kps1), -1, np.int32)
         prev = np.ascontiguousarray(prev_xy, np.float32).copy()
@@ -309,10 +323,19 @@ class Replay:
 
     __del__ = close
 
-    def frame(self, fid, T, boxes, ids, pos, uv, bad=None):
+    def lines(self, sets):
+        """Stage frame line segments (eao_replay_lines): a list of (L, 4) arrays, one per upcoming frame."""
+        nl = np.array([len(np.asarray(x).reshape(-1, 4)) for x in sets], np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(x, np.float32).reshape(-1, 4) for x in sets])
+                                    if len(sets) else np.zeros((0, 4), np.float32), np.float32)
+        check(lib().eao_replay_lines(self.h, len(sets), P(nl), P(flat)), "eao_replay_lines")
+
+    def frame(self, fid, T, boxes, ids, pos, uv, bad=None, lines=None):
         boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 5)
         out = np.zeros((len(boxes), 4), np.int32)
         bad = np.zeros(len(ids), np.uint8) if bad is None else np.ascontiguousarray(bad, np.uint8)
+        if lines is not None:
+            self.lines([lines])
         check(lib().eao_replay_frame(self.h, int(fid), P(np.ascontiguousarray(T, np.float32)), len(boxes),
                                      P(boxes), len(ids), P(np.ascontiguousarray(ids, np.int32)),
                                      P(np.ascontiguousarray(pos, np.float32)),
@@ -367,11 +390,14 @@ class Replay:
             pos=np.ascontiguousarray(np.concatenate([f["pos"] for f in frames]), np.float32),
             uv=np.ascontiguousarray(np.concatenate([f["uv"] for f in frames]), np.float32),
             bad=np.ascontiguousarray(np.concatenate([f["bad"] for f in frames]), np.uint8),
-            kf=np.array([1 if f["kf"] else 0 for f in frames], np.uint8))
+            kf=np.array([1 if f["kf"] else 0 for f in frames], np.uint8),
+            lines=[f["lines"] for f in frames] if all("lines" in f for f in frames) else None)
 
     def run(self, pk):
         """eao_replay_run over a packed stream; returns det_out (total boxes x 4)."""
         out = np.zeros((int(pk["nb"].sum()), 4), np.int32)
+        if pk.get("lines") is not None:
+            self.lines(pk["lines"])
         check(lib().eao_replay_run(self.h, pk["n"], P(pk["ids"]), P(pk["T"]), P(pk["nb"]), P(pk["boxes"]),
                                    P(pk["npt"]), P(pk["mp"]), P(pk["pos"]), P(pk["uv"]), P(pk["bad"]), P(pk["kf"]),
                                    P(out)), "eao_replay_run")
@@ -380,7 +406,7 @@ class Replay:
     def objects(self):
         n = check(lib().eao_replay_num_objects(self.h), "eao_replay_num_objects")
         ints = np.zeros((n, 8), np.int32)
-        fl = np.zeros((n, 16), np.float32)
+        fl = np.zeros((n, 20), np.float32)
         pts = []
         for i in range(n):
             check(lib().eao_replay_object(self.h, i, P(ints[i]), P(fl[i])), "eao_replay_object")

@@ -151,6 +151,23 @@ int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnrat
                     const uint8_t* cur_desc, const int32_t* cur_preassigned, int nlevels,
                     const float* scale_factors, int32_t* cur_match);
 
+/* SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>& sAlreadyFound, th, ORBdist)
+   (src/ORBmatcher.cc:1472-1599; relocalisation, src/Tracking.cc:2295,2309).
+   Keyframe side: kf_kps (angles for the rotation check), kf_mp_valid[i] = vpMPs[i] &&
+   !isBad() && !sAlreadyFound.count(vpMPs[i]), positions / descriptors and
+   mfMinDistance / mfMaxDistance of those map points. cur_preassigned[i2] >= 0 marks
+   CurrentFrame.mvpMapPoints[i2] already set (kept in cur_match). New matches write the
+   keyframe index i into cur_match[i2]. PredictScale is clamped.
+   Returns nmatches. */
+int eao_match_keyframe(eao_matcher* m, const eao_camera* cam, const float* Tcw, float th,
+                       int orb_dist, int check_ori, int n_kf, const eao_keypoint* kf_kps,
+                       const uint8_t* kf_mp_valid, const float* kf_mp_pos,
+                       const uint8_t* kf_mp_desc, const float* kf_mp_min_dist,
+                       const float* kf_mp_max_dist, float log_scale_factor, int n_cur,
+                       const eao_keypoint* cur_kps, const uint8_t* cur_desc,
+                       const int32_t* cur_preassigned, int nlevels, const float* scale_factors,
+                       int32_t* cur_match);
+
 /* SearchForInitialization (src/ORBmatcher.cc:405-520); prev_matched_xy is
    updated in place like vbPrevMatched. */
 int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int check_ori, int n1,
@@ -207,6 +224,13 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
                      const int32_t* boxes, int n_pts, const int32_t* mp_ids, const float* mp_pos,
                      const float* kp_uv, const uint8_t* mp_bad, int32_t* det_out);
 int eao_replay_local_mapping(eao_replay* r);
+/* Frame line segments (Frame::all_lines_eigen rows x1, y1, x2, y2 from the line
+   detector, src/Frame.cc:324-335) for the next n_frames frames replayed by
+   eao_replay_frame / eao_replay_run, one set per frame in order. They feed
+   Tracking::AssociateObjAndLines (src/Tracking.cc:2472-2527) and SampleObjYaw
+   (src/Tracking.cc:2624-2871, flags other than None / iForest). Frames without a
+   staged set have no lines. */
+int eao_replay_lines(eao_replay* r, int n_frames, const int32_t* n_lines, const float* lines);
 /* a recorded stream in one call: frame t is eao_replay_frame on the t-th
    slices of the packed arrays (boxes / points concatenated over frames),
    followed by eao_replay_local_mapping when keyframe[t]. det_out receives 4
@@ -216,6 +240,10 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
                    const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
                    const uint8_t* mp_bad, const uint8_t* keyframe, int32_t* det_out);
 int eao_replay_num_objects(eao_replay* r);
+/* ints[8]: id, class, bad, #frames, #points, last add, #co-association votes, #co-views;
+   floats[20]: center[3], sigma[3], sigma of frame centers[3], cuboid lenth/width/height,
+   R_max, centre spread, projected rect x / w, rotY, #yaw measurements, mfErrorParallel,
+   mfErroeYaw */
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats);
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
 

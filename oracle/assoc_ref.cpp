@@ -13,10 +13,13 @@
  * LocalMapping object maintenance runs when the caller says a keyframe was
  * inserted. Defined behaviour for reference UB: Q4 (int32 wraparound), Q7
  * (out_point = false), Q8 (erase stops after the last outlier), merge of a
- * one-frame object (Q29). Yaw sampling (E14) is out of round-1
- * scope: flags EAO/Full/LineAndiForest behave as iForest here.
+ * one-frame object (Q29). Object lines (Tracking.cc:2472-2527,
+ * AssociateObjAndLines + merge_break_lines) and yaw sampling (E14,
+ * Tracking.cc:2602-2871) run for every flag but None / iForest; the frame's
+ * line segments (Frame::all_lines_eigen) are a replay input.
  */
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -87,6 +90,60 @@ static inline void project(const Cam& c, const float* T, const float* P, float& 
   const float invzc = (float)(1.0 / pc[2]);
   u = c.fx * pc[0] * invzc + c.cx;
   v = c.fy * pc[1] * invzc + c.cy;
+}
+
+
+// ---------------------------------------------------------------- object lines
+// Tracking::AssociateObjAndLines (Tracking.cc:2472-2527) and the cuboid utilities it
+// calls: check_inside_box / align_left_right_edges (detect_3d_cuboid/object_3d_util.cpp:176-194),
+// merge_break_lines (:349-436), fast_RemoveRow (matrix_utils.cpp:201-205).
+static inline double norm2(double x, double y) { return std::sqrt(x * x + y * y); }
+
+static void merge_break_lines(std::vector<double>& L, double dist_th, double angle_deg, double len_th) {
+  int total = (int)L.size() / 4;
+  int counter = 0;
+  bool can = true;
+  const double ath = angle_deg / 180.0 * M_PI;
+  std::vector<double> ang;
+  while (can && counter < 500) {
+    counter++;
+    can = false;
+    ang.assign(total, 0.0);
+    for (int i = 0; i < total; i++) ang[i] = std::atan2(L[4 * i + 3] - L[4 * i + 1], L[4 * i + 2] - L[4 * i]);
+    for (int s1 = 0; s1 < total - 1; s1++) {
+      for (int s2 = s1 + 1; s2 < total; s2++) {
+        const double diff = std::abs(ang[s1] - ang[s2]);
+        if (std::min(diff, M_PI - diff) < ath) {
+          const double d12 = norm2(L[4 * s1 + 2] - L[4 * s2], L[4 * s1 + 3] - L[4 * s2 + 1]);
+          const double d21 = norm2(L[4 * s2 + 2] - L[4 * s1], L[4 * s2 + 3] - L[4 * s1 + 1]);
+          if (d12 < dist_th || d21 < dist_th) {
+            const int a = L[4 * s1] < L[4 * s2] ? s1 : s2;
+            const int b = L[4 * s1 + 2] > L[4 * s2 + 2] ? s1 : s2;
+            const double st[2] = {L[4 * a], L[4 * a + 1]}, en[2] = {L[4 * b + 2], L[4 * b + 3]};
+            const double ma = std::atan2(en[1] - st[1], en[0] - st[0]);
+            const double t = std::abs(ang[s1] - ma);
+            if (std::min(t, M_PI - t) < ath) {
+              L[4 * s1] = st[0];
+              L[4 * s1 + 1] = st[1];
+              L[4 * s1 + 2] = en[0];
+              L[4 * s1 + 3] = en[1];
+              for (int c = 0; c < 4; c++) L[4 * s2 + c] = L[4 * (total - 1) + c];
+              total--;
+              can = true;
+              break;
+            }
+          }
+        }
+      }
+      if (can) break;
+    }
+  }
+  std::vector<double> out;
+  for (int i = 0; i < total; i++) {
+    if (len_th > 0 && !(norm2(L[4 * i + 2] - L[4 * i], L[4 * i + 3] - L[4 * i + 1]) > len_th)) continue;
+    for (int c = 0; c < 4; c++) out.push_back(L[4 * i + c]);
+  }
+  L.swap(out);
 }
 
 // ---------------------------------------------------------------- NP test
@@ -199,6 +256,7 @@ struct Obj2D {
   int mnId = -1, which_time = 0;
   int method = 0;  // replay output: how it was associated
   int input_index = -1;
+  std::vector<double> lines;  // mObjLinesEigen (rows x1, y1, x2, y2), Tracking.cc:2524
   // cv::Mat aliasing (Object.cc:677, Tracking.cc:2563): the detection that
   // creates a map object shares its _Pos buffer with that object's mCenter3D,
   // which ComputeMeanAndStandard later rewrites in place (Object.cc:995).
@@ -206,8 +264,8 @@ struct Obj2D {
 };
 
 struct Cuboid {
-  double corner[8][3];
-  double corner_w[8][3];
+  double corner[8][3] = {};
+  double corner_w[8][3] = {};
   float x_min = 0, x_max = 0, y_min = 0, y_max = 0, z_min = 0, z_max = 0;
   double center[3] = {0, 0, 0};
   float lenth = 0, width = 0, height = 0;
@@ -217,6 +275,7 @@ struct Cuboid {
   double tn[3] = {0, 0, 0};
   float rotY = 0, rotP = 0, rotR = 0;
   float rmax = 0;
+  float err_parallel = 0, err_yaw = 0;  // mfErrorParallel, mfErroeYaw
 };
 
 struct ObjMap {
@@ -234,6 +293,7 @@ struct ObjMap {
   std::map<int, int> reobj, sametime;
   bool bad = false;
   Cuboid cub;
+  std::vector<std::array<float, 5>> angles;  // mvAngleTimesAndScore (Vector5f rows)
 };
 
 static inline const float* fpos(const Obj2D* f) { return f->alias ? f->alias->center : f->pos; }
@@ -313,6 +373,155 @@ class Replay {
   }
 
   bool is(const char* f) const { return flag == f; }
+
+  // frame line sets staged by orc_replay_lines, consumed one per frame
+  std::vector<std::vector<float>> staged_lines;
+  size_t staged_next = 0;
+
+  // Tracking::AssociateObjAndLines, Tracking.cc:2472-2527
+  void associate_lines(const std::vector<Obj2D*>& o2, const std::vector<float>& fl) {
+    std::vector<double> all(fl.begin(), fl.end());  // all_lines_eigen (float Mat -> double)
+    const int n = (int)all.size() / 4;
+    for (int i = 0; i < n; i++)  // align_left_right_edges
+      if (all[4 * i + 2] < all[4 * i]) {
+        std::swap(all[4 * i], all[4 * i + 2]);
+        std::swap(all[4 * i + 1], all[4 * i + 3]);
+      }
+    for (auto* f : o2) {
+      const double l = std::max(0.0, f->bx - 15.0);
+      const double r = (double)std::min(cam.cols, f->bx + f->bw + 15);
+      const double t = std::max(0.0, f->by - 15.0);
+      const double b = (double)std::min(cam.rows, f->by + f->bh + 15);
+      std::vector<double> in;
+      for (int i = 0; i < n; i++) {
+        const double* e = &all[4 * i];
+        if (l <= e[0] && e[0] <= r && t <= e[1] && e[1] <= b && l <= e[2] && e[2] <= r && t <= e[3] &&
+            e[3] <= b)
+          in.insert(in.end(), e, e + 4);
+      }
+      merge_break_lines(in, 20, 5, 30);
+      f->lines.swap(in);
+    }
+  }
+
+  // Tracking::SampleObjYaw (Tracking.cc:2624-2871) with WorldToImg (:2602-2620)
+  void sample_yaw(ObjMap* o) {
+    if (flag == "None" || flag == "iForest") return;
+    const std::vector<double>& L = o->frames.back()->lines;
+    const int nAll = (int)L.size() / 4;
+    int numMax = 0;
+    float fError = 0.0f, fErrorYaw = 0.0f, sampleYaw = 0.0f;
+    Cuboid& c = o->cub;
+    float ctr[3], rel[8][3];
+    for (int a = 0; a < 3; a++) ctr[a] = (float)c.center[a];
+    for (int k = 0; k < 8; k++)
+      for (int a = 0; a < 3; a++) rel[k][a] = (float)c.corner_w[k][a] - ctr[a];
+    for (int i = 0; i < 30; i++) {
+      const float roll = 0.0f, pitch = 0.0f;
+      const float yaw = i < 15 ? (float)((0.0 - i * 3.0) / 180.0 * M_PI) : (float)((0.0 + (i - 15) * 3.0) / 180.0 * M_PI);
+      float error = 0.0f, errorYaw = 0.0f;
+      const float cp = std::cos(pitch), sp = std::sin(pitch), sr = std::sin(roll), cr = std::cos(roll);
+      const float sy = (float)std::sin((double)yaw), cy = (float)std::cos((double)yaw);  // Q26
+      const float R[3][3] = {{cp * cy, (sr * sp * cy) - (cr * sy), (cr * sp * cy) + (sr * sy)},
+                             {cp * sy, (sr * sp * sy) + (cr * cy), (cr * sp * sy) - (sr * cy)},
+                             {-sp, sr * cp, cr * cp}};
+      float px[8], py[8];
+      for (int k = 0; k < 8; k++) {
+        float w[3];
+        for (int r = 0; r < 3; r++) {  // Ryaw * corner + center: cv::Mat gemm (Q12)
+          const float d = R[r][0] * rel[k][0] + R[r][1] * rel[k][1] + R[r][2] * rel[k][2];
+          w[r] = (float)((double)d + (double)ctr[r]);
+        }
+        project(cam, T, w, px[k], py[k]);  // WorldToImg
+      }
+      auto edge = [&](int a, int b, float& ang, float& len) {  // point_b vs point_a, left -> right
+        if (px[b] > px[a])
+          ang = std::atan2(py[b] - py[a], px[b] - px[a]);
+        else
+          ang = std::atan2(py[a] - py[b], px[a] - px[b]);
+        len = std::sqrt((py[b] - py[a]) * (py[b] - py[a]) + (px[b] - px[a]) * (px[b] - px[a]));
+      };
+      float angle1, angle2, angle3, l1, l2, l3;
+      edge(4, 5, angle1, l1);  // point5 -> point6
+      edge(5, 6, angle2, l2);  // point6 -> point7
+      edge(1, 5, angle3, l3);  // point2 -> point6
+      int num = 0;
+      for (int li = 0; li < nAll; li++) {
+        const double x1 = L[4 * li], y1 = L[4 * li + 1], x2 = L[4 * li + 2], y2 = L[4 * li + 3];
+        const float angle = (float)std::atan2(y2 - y1, x2 - x1);
+        const float d1 = (float)std::abs((double)(angle * 180) / M_PI - (double)(angle1 * 180) / M_PI);
+        const float d2 = (float)std::abs((double)(angle * 180) / M_PI - (double)(angle2 * 180) / M_PI);
+        const float d3 = (float)std::abs((double)(angle * 180) / M_PI - (double)(angle3 * 180) / M_PI);
+        const float th = 5.0f;
+        if (o->mnClass == 56) {
+          if ((d2 < th) || (d3 < th)) num++;
+          if (d1 < th) num += 3;
+        } else {
+          const float mn = std::min(std::min(l1, l2), l3);
+          if (mn == l1) {
+            if ((d2 < th) || (d3 < th)) {
+              num++;
+              if (d2 < th) error += d2;
+              if (d3 < th) error += d3;
+            }
+            errorYaw += std::min(d2, d3);
+          }
+          if (mn == l2) {
+            if ((d1 < th) || (d3 < th)) {
+              num++;
+              if (d1 < th) error += d1;
+              if (d3 < th) error += d3;
+            }
+            errorYaw += std::min(d3, d1);
+          }
+          if (mn == l3) {
+            if ((d1 < th) || (d2 < th)) {
+              num++;
+              if (d1 < th) error += d1;
+              if (d2 < th) error += d2;
+            }
+            errorYaw += std::min(d2, d1);
+          }
+        }
+      }
+      if (num == 0) {
+        num = 1;
+        errorYaw = 10.0f;
+      }
+      if (num > numMax) {
+        numMax = num;
+        sampleYaw = yaw;
+        fError = error;
+        fErrorYaw = (float)((double)(errorYaw / (float)num) / 10.0);
+      }
+    }
+    float fScore = (float)((double)((float)numMax / (float)nAll) * (1.0 - 0.1 * (double)fErrorYaw));
+    if (std::isinf(fScore)) fScore = 0.0f;
+    const std::array<float, 5> v = {sampleYaw, 1.0f, fScore, fError, fErrorYaw};
+    bool fresh = true;
+    for (auto& row : o->angles)
+      if (row[0] == v[0]) {
+        row[1] += 1.0f;
+        for (int q = 2; q < 5; q++) row[q] = v[q] * (1 / row[1]) + row[q] * (1 - 1 / row[1]);
+        fresh = false;
+      }
+    if (fresh) o->angles.push_back(v);
+    // std::sort with VIC (index = 1, Tracking.cc:63-68): the same libstdc++ introsort
+    std::sort(o->angles.begin(), o->angles.end(),
+              [](const std::array<float, 5>& l, const std::array<float, 5>& r) { return l[1] > r[1]; });
+    int best = 0;
+    float best_score = 0;
+    for (int i = 0; i < std::min(3, (int)o->angles.size()); i++) {
+      const float f = o->angles[i][2];
+      if (f >= best_score) {
+        best_score = f;
+        best = i;
+      }
+    }
+    c.rotY = o->angles[best][0];
+    c.err_parallel = o->angles[best][3];
+    c.err_yaw = o->angles[best][4];
+  }
 
   // Object_Map::UpdateObjPose, Object.cc:2193-2248
   void update_pose(ObjMap* o) {
@@ -944,6 +1153,16 @@ class Replay {
         }
       }
     }
+    // STEP 3 AssociateObjAndLines (Tracking.cc:1286): the frame's staged line set
+    {
+      static const std::vector<float> none;
+      const std::vector<float>& fl = staged_next < staged_lines.size() ? staged_lines[staged_next] : none;
+      associate_lines(o2, fl);
+      if (staged_next < staged_lines.size() && ++staged_next == staged_lines.size()) {
+        staged_lines.clear();
+        staged_next = 0;
+      }
+    }
     // STEP 4
     for (auto* f : o2) {
       frame_mean(f);
@@ -1103,7 +1322,15 @@ class Replay {
           }
         }
       }
-      // step 10.6 SampleObjYaw: out of round-1 scope (E14); no-op for None/iForest.
+      // step 10.6 SampleObjYaw for regular objects seen this frame (Tracking.cc:1650-1671)
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {
+        ObjMap* o = objs[i];
+        if (o->bad) continue;
+        if ((unsigned long)(long)o->last_add < fid - 5) continue;
+        const int c = o->mnClass;
+        if (c == 73 || c == 64 || c == 65 || c == 66 || c == 56)
+          if ((unsigned long)(long)o->last_add == fid) sample_yaw(o);
+      }
     }
     for (auto* f : o2) {
       int k = f->input_index;
@@ -1178,7 +1405,36 @@ class Replay {
         a->lastlast = b->frames.size() >= 2 ? b->frames[b->frames.size() - 2]->box : b->frames.front()->box;
       }
     }
-    // step 5 (orientation) only has data when yaw sampling ran (E14, out of scope)
+    // step 5. orientation measurements (Object.cc:1842-1901)
+    const int c = a->mnClass;
+    if (c == 73 || c == 64 || c == 65 || c == 66 || c == 56) {
+      for (auto& rr : b->angles) {
+        bool fresh = true;
+        for (auto& rt : a->angles)
+          if (rr[0] == rt[0]) {
+            rt[1] += rr[1];
+            for (int q = 2; q < 5; q++) rt[q] = rt[q] * ((rt[1] - rr[1]) / rt[1]) + rr[q] * (rr[1] / rt[1]);
+            fresh = false;
+            break;
+          }
+        if (fresh) a->angles.push_back(rr);
+      }
+      if (!a->angles.empty()) {
+        int best = 0;
+        float best_score = 0.0f;
+        for (int i = 0; i < std::min(6, (int)a->angles.size()); i++) {
+          const float f = a->angles[i][2];
+          if (f > best_score) {
+            best_score = f;
+            best = i;
+          }
+        }
+        a->cub.rotY = a->angles[best][0];
+        a->cub.err_parallel = a->angles[best][3];
+        a->cub.err_yaw = a->angles[best][4];
+        update_pose(a);
+      }
+    }
   }
 
   void whether_merge(ObjMap* o) {  // Object_Map::WhetherMergeTwoMapObjs, :1607-1655
@@ -1420,6 +1676,13 @@ int orc_replay_frame(orc_replay* r, int frame_id, const float* Tcw, int n_boxes,
   r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv, mp_bad, det_out);
   return (int)r->r.objs.size();
 }
+int orc_replay_lines(orc_replay* r, int n_frames, const int32_t* n_lines, const float* lines) {
+  for (int t = 0; t < n_frames; t++) {
+    r->r.staged_lines.emplace_back(lines, lines + 4 * (size_t)n_lines[t]);
+    lines += 4 * (size_t)n_lines[t];
+  }
+  return 0;
+}
 int orc_replay_local_mapping(orc_replay* r) {
   r->r.local_mapping();
   return 0;
@@ -1448,6 +1711,10 @@ int orc_replay_object(orc_replay* r, int i, int32_t* ints, float* floats) {
   floats[13] = o->cstd_all;
   floats[14] = (float)o->proj.x;
   floats[15] = (float)o->proj.w;
+  floats[16] = o->cub.rotY;
+  floats[17] = (float)o->angles.size();
+  floats[18] = o->cub.err_parallel;
+  floats[19] = o->cub.err_yaw;
   return 0;
 }
 int orc_replay_object_points(orc_replay* r, int i, int32_t* ids, int cap) {

@@ -293,6 +293,91 @@ int orc_search_by_projection_local(const orc_camera* cam, float th, float nnrati
   return nmatches;
 }
 
+// ORBmatcher::SearchByProjection(Frame&, KeyFrame*, const set<MapPoint*>&, th, ORBdist),
+// ORBmatcher.cc:1472-1599 (relocalisation; Tracking.cc:2295,2309).
+// kf_mp_valid[i]: vpMPs[i] && !isBad() && !sAlreadyFound.count(pMP).
+// kf_mp_min_dist / kf_mp_max_dist: mfMinDistance / mfMaxDistance (MapPoint.cc:365-383).
+// cur_preassigned[i2] >= 0 marks CurrentFrame.mvpMapPoints[i2] already set.
+int orc_search_by_projection_keyframe(const orc_camera* cam, const float* Tcw, float th,
+                                      int orb_dist, int check_ori, int n_kf,
+                                      const orc_keypoint* kf_kps, const uint8_t* kf_mp_valid,
+                                      const float* kf_mp_pos, const uint8_t* kf_mp_desc,
+                                      const float* kf_mp_min_dist, const float* kf_mp_max_dist,
+                                      float log_scale_factor, int n_cur,
+                                      const orc_keypoint* cur_kps, const uint8_t* cur_desc,
+                                      const int32_t* cur_preassigned, int nlevels,
+                                      const float* scale_factors, int32_t* cur_match) {
+  Grid* g = new Grid();
+  grid_build(cam, n_cur, cur_kps, *g);
+  for (int i = 0; i < n_cur; i++) cur_match[i] = cur_preassigned ? cur_preassigned[i] : -1;
+  // Ow = -Rcw.t()*tcw (:1478): transposed gemm operand, double accumulation
+  float Ow[3];
+  for (int c = 0; c < 3; c++) {
+    double s = (double)Tcw[c] * Tcw[3];
+    s += (double)Tcw[4 + c] * Tcw[7];
+    s += (double)Tcw[8 + c] * Tcw[11];
+    Ow[c] = (float)(s * -1.0);
+  }
+  int nmatches = 0;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  std::vector<int> cand;
+  for (int i = 0; i < n_kf; i++) {
+    if (!kf_mp_valid[i]) continue;
+    const float* P = kf_mp_pos + 3 * i;
+    float x3Dc[3];
+    transform_point(Tcw, P, x3Dc);
+    const float xc = x3Dc[0], yc = x3Dc[1];
+    const float invzc = (float)(1.0 / x3Dc[2]);  // no depth test here (:1501-1506)
+    const float u = cam->fx * xc * invzc + cam->cx;
+    const float v = cam->fy * yc * invzc + cam->cy;
+    if (u < g->minX || u > g->maxX) continue;
+    if (v < g->minY || v > g->maxY) continue;
+    const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+    double s = 0;
+    for (int k = 0; k < 3; k++) s += (double)PO[k] * PO[k];
+    const float dist3D = (float)std::sqrt(s);  // cv::norm
+    const float maxDistance = 1.2f * kf_mp_max_dist[i];
+    const float minDistance = 0.8f * kf_mp_min_dist[i];
+    if (dist3D < minDistance || dist3D > maxDistance) continue;
+    // PredictScale (MapPoint.cc:385-394); Q13 clamp to the pyramid
+    const float ratio = kf_mp_max_dist[i] / dist3D;
+    int lvl = (int)std::ceil((float)std::log((double)ratio) / log_scale_factor);
+    lvl = std::min(std::max(lvl, 0), nlevels - 1);
+    const float radius = th * scale_factors[lvl];
+    features_in_area(*g, cur_kps, u, v, radius, lvl - 1, lvl + 1, cand);
+    if (cand.empty()) continue;
+    const uint8_t* dMP = kf_mp_desc + 32 * (size_t)i;
+    int bestDist = 256, bestIdx2 = -1;
+    for (int i2 : cand) {
+      if (cur_match[i2] >= 0) continue;
+      const int dist = descriptor_distance(dMP, cur_desc + 32 * (size_t)i2);
+      if (dist < bestDist) {
+        bestDist = dist;
+        bestIdx2 = i2;
+      }
+    }
+    if (bestDist <= orb_dist) {
+      cur_match[bestIdx2] = i;
+      nmatches++;
+      if (check_ori) rotHist[rot_bin(kf_kps[i].angle, cur_kps[bestIdx2].angle)].push_back(bestIdx2);
+    }
+  }
+  if (check_ori) {
+    int ind1 = -1, ind2 = -1, ind3 = -1;
+    three_maxima(rotHist, HISTO_LENGTH, ind1, ind2, ind3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i != ind1 && i != ind2 && i != ind3) {
+        for (int idx : rotHist[i]) {
+          cur_match[idx] = -1;
+          nmatches--;
+        }
+      }
+    }
+  }
+  delete g;
+  return nmatches;
+}
+
 // ORBmatcher::SearchForInitialization, :405-520
 int orc_search_for_initialization(const orc_camera* cam, float nnratio, int check_ori, int n1,
                                   const orc_keypoint* kps1, const uint8_t* desc1, int n2,

@@ -87,6 +87,18 @@ int orc_is_in_frustum(const orc_camera* cam, const float* Tcw, int n_mp, const f
                       float view_cos_limit, float log_scale_factor,
                       uint8_t* in_view, float* proj_xy, int32_t* pred_level, float* view_cos);
 
+/* SearchByProjection(Frame&, KeyFrame*, set<MapPoint*>, th, ORBdist), ORBmatcher.cc:1472-1599
+   (relocalisation). kf_mp_valid[i] = MP present, not bad, not already found. */
+int orc_search_by_projection_keyframe(const orc_camera* cam, const float* Tcw, float th,
+                                      int orb_dist, int check_ori, int n_kf,
+                                      const orc_keypoint* kf_kps, const uint8_t* kf_mp_valid,
+                                      const float* kf_mp_pos, const uint8_t* kf_mp_desc,
+                                      const float* kf_mp_min_dist, const float* kf_mp_max_dist,
+                                      float log_scale_factor, int n_cur,
+                                      const orc_keypoint* cur_kps, const uint8_t* cur_desc,
+                                      const int32_t* cur_preassigned, int nlevels,
+                                      const float* scale_factors, int32_t* cur_match);
+
 /* SearchForInitialization, ORBmatcher.cc:405-520 */
 int orc_search_for_initialization(const orc_camera* cam, float nnratio, int check_ori,
                                   int n1, const orc_keypoint* kps1, const uint8_t* desc1,
@@ -142,7 +154,10 @@ int orc_replay_local_mapping(orc_replay* r);
 int orc_replay_num_objects(orc_replay* r);
 /* per object summary: id, class, bad, nframes, npts, center[3], std[3], cstd[3],
    cuboid extents lenth/width/height, rmax, last_add, rect_project[4] */
-int orc_replay_object(orc_replay* r, int i, int32_t* ints /*8*/, float* floats /*16*/);
+int orc_replay_object(orc_replay* r, int i, int32_t* ints /*8*/, float* floats /*20*/);
+/* frame line segments (Frame::all_lines_eigen rows x1,y1,x2,y2) for the next n_frames
+   orc_replay_frame calls, consumed one set per frame */
+int orc_replay_lines(orc_replay* r, int n_frames, const int32_t* n_lines, const float* lines);
 int orc_replay_object_points(orc_replay* r, int i, int32_t* ids, int cap);
 
 #ifdef __cplusplus

@@ -146,6 +146,21 @@ def match_local(c, th, nnratio, inv, proj, lvl, vc, mp_desc, cur_kps, cur_desc, 
     return n, out
 
 
+def match_keyframe(c, Tcw, th, orb_dist, check_ori, kf_kps, valid, pos, desc, mind, maxd, logsf,
+                   cur_kps, cur_desc, pre, scales):
+    """SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist), ORBmatcher.cc:1472-1599."""
+    out = np.full(len(cur_kps), -1, np.int32)
+    n = lib().orc_search_by_projection_keyframe(
+        ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), ctypes.c_float(th), int(orb_dist),
+        int(check_ori), len(kf_kps), P(kf_kps), P(np.ascontiguousarray(valid, np.uint8)),
+        P(np.ascontiguousarray(pos, np.float32)), P(np.ascontiguousarray(desc, np.uint8)),
+        P(np.ascontiguousarray(mind, np.float32)), P(np.ascontiguousarray(maxd, np.float32)),
+        ctypes.c_float(logsf), len(cur_kps), P(cur_kps), P(np.ascontiguousarray(cur_desc, np.uint8)),
+        P(np.ascontiguousarray(pre, np.int32)) if pre is not None else None, len(scales),
+        P(np.ascontiguousarray(scales, np.float32)), P(out))
+    return n, out
+
+
 def match_init(c, nnratio, check_ori, kps1, desc1, kps2, desc2, prev_xy, window):
     m12 = np.full(len(kps1), -1, np.int32)
     prev = np.ascontiguousarray(prev_xy, np.float32).copy()
@@ -226,10 +241,19 @@ class Replay:
 
     __del__ = close
 
-    def frame(self, fid, T, boxes, ids, pos, uv, bad=None):
+    def lines(self, sets):
+        """Stage frame line segments (list of (L, 4) arrays, one per upcoming frame)."""
+        nl = np.array([len(np.asarray(x).reshape(-1, 4)) for x in sets], np.int32)
+        flat = np.ascontiguousarray(np.concatenate([np.asarray(x, np.float32).reshape(-1, 4) for x in sets])
+                                    if len(sets) else np.zeros((0, 4), np.float32), np.float32)
+        lib().orc_replay_lines(ctypes.c_void_p(self.h), len(sets), P(nl), P(flat))
+
+    def frame(self, fid, T, boxes, ids, pos, uv, bad=None, lines=None):
         boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 5)
         out = np.zeros((len(boxes), 4), np.int32)
         bad = np.zeros(len(ids), np.uint8) if bad is None else np.ascontiguousarray(bad, np.uint8)
+        if lines is not None:
+            self.lines([lines])
         lib().orc_replay_frame(ctypes.c_void_p(self.h), int(fid), P(np.ascontiguousarray(T, np.float32)),
                                len(boxes), P(boxes), len(ids), P(np.ascontiguousarray(ids, np.int32)),
                                P(np.ascontiguousarray(pos, np.float32)), P(np.ascontiguousarray(uv, np.float32)),
@@ -242,7 +266,7 @@ class Replay:
     def objects(self):
         n = lib().orc_replay_num_objects(ctypes.c_void_p(self.h))
         ints = np.zeros((n, 8), np.int32)
-        fl = np.zeros((n, 16), np.float32)
+        fl = np.zeros((n, 20), np.float32)
         pts = []
         for i in range(n):
             lib().orc_replay_object(ctypes.c_void_p(self.h), i, P(ints[i]), P(fl[i]))

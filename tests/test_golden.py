@@ -4,6 +4,7 @@ CPU test: guards the parity target against drift of the restatement."""
 import os
 
 import numpy as np
+import pytest
 
 import pyoracle as orc
 from tools import synth
@@ -43,16 +44,20 @@ def test_np_fixture():
     assert set(stats["verdict"].tolist()) >= {1, 2}
 
 
-def test_replay_fixture():
-    g = load("replay_eao60.npz")
-    fr = synth.assoc_stream(60)
+@pytest.mark.parametrize("name,lines", [("replay_eao60.npz", False), ("replay_eao_lines60.npz", True)])
+def test_replay_fixture(name, lines):
+    g = load(name)
+    fr = synth.assoc_stream(60, lines=lines)
     r = orc.Replay("EAO")
     outs = []
     for t, f in enumerate(fr):
-        outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines")))
         if f["kf"]:
             r.local_mapping()
     assert np.array_equal(np.concatenate(outs), g["det_out"])
     ints, fl, pts = r.objects()
     assert np.array_equal(ints, g["obj_ints"]) and np.array_equal(fl, g["obj_floats"])
     assert np.array_equal(np.concatenate(pts), g["obj_points"])
+    if lines:  # the yaw sampling ran and moved some objects off yaw 0
+        alive = ints[:, 2] == 0
+        assert (fl[:, 17] > 0).any() and (fl[alive, 16] != 0).any()

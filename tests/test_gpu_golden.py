@@ -51,14 +51,15 @@ def test_np_golden():
     assert np.allclose(got["w"], stats["w"], rtol=1e-5)
 
 
-def test_replay_golden():
-    g = load("replay_eao60.npz")
-    fr = synth.assoc_stream(60)
+@pytest.mark.parametrize("name,lines", [("replay_eao60.npz", False), ("replay_eao_lines60.npz", True)])
+def test_replay_golden(name, lines):
+    g = load(name)
+    fr = synth.assoc_stream(60, lines=lines)
     a = ea.Assoc()
     r = ea.Replay(a, "EAO")
     outs = []
     for t, f in enumerate(fr):
-        outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines")))
         if f["kf"]:
             r.local_mapping()
     assert np.array_equal(np.concatenate(outs), g["det_out"])

@@ -1,7 +1,8 @@
 """GPU ORB matching vs the CPU restatement (bit-exact match indices).
 
 Reference: src/ORBmatcher.cc:45-129 (local map), :405-520 (initialization),
-:1328-1470 (motion model), :1647-1663 (Hamming); src/Frame.cc:390-513 (grid,
+:1328-1470 (motion model), :1472-1599 (relocalisation),
+:1647-1663 (Hamming); src/Frame.cc:390-513 (grid,
 frustum).
 """
 import numpy as np
@@ -90,6 +91,53 @@ def test_frustum_and_local(frames):
         ng, mg = m.local(ea.camera(), th, 0.8, inv, proj, lvl, vc, d0, k2, d2, pre, SC)
         no, mo = orc.match_local(orc.cam(), th, 0.8, inv, proj, lvl, vc, d0, k2, d2, pre, SC)
         assert ng == no and np.array_equal(mg, mo), (th, ng, no, int((mg != mo).sum()))
+
+
+def _kf_scene(frames, a, b, seed):
+    """Keyframe a's map points (back-projected keypoints, distance bounds from
+    their octave like MapPoint::UpdateNormalAndDepth, MapPoint.cc:340-370)
+    searched in frame b."""
+    fr, poses = frames
+    k0, d0 = orc.extract(fr[a])
+    k1, d1 = orc.extract(fr[b])
+    rng = np.random.default_rng(seed)
+    pos = synth.backproject(poses[a], k0["x"], k0["y"])
+    Rwc = poses[a][:3, :3].T
+    twc = -Rwc @ poses[a][:3, 3]
+    dist = np.linalg.norm(pos - twc[None, :], axis=1).astype(np.float32)
+    maxd = (dist * SC[k0["octave"]]).astype(np.float32)
+    mind = (maxd / SC[7]).astype(np.float32)
+    valid = (rng.random(len(k0)) < 0.85).astype(np.uint8)
+    pre = np.full(len(k1), -1, np.int32)
+    pre[rng.choice(len(k1), len(k1) // 6, replace=False)] = 7
+    return k0, d0, k1, d1, pos, mind, maxd, valid, pre, poses[b]
+
+
+@pytest.mark.parametrize("th,orbdist,ori", [(10, 100, 1), (3, 64, 1), (10, 100, 0)])
+def test_keyframe_exact(frames, th, orbdist, ori):
+    """Relocalisation projection search (ORBmatcher.cc:1472-1599), the two
+    call shapes of Tracking::Relocalization (Tracking.cc:2295,2309)."""
+    k0, d0, k1, d1, pos, mind, maxd, valid, pre, T = _kf_scene(frames, 0, 2, seed=th)
+    logsf = float(np.log(np.float32(1.2)))
+    ng, mg = ea.Matcher().keyframe(ea.camera(), T, th, orbdist, ori, k0, valid, pos, d0, mind, maxd, logsf,
+                                   k1, d1, pre, SC)
+    no, mo = orc.match_keyframe(orc.cam(), T, th, orbdist, ori, k0, valid, pos, d0, mind, maxd, logsf,
+                                k1, d1, pre, SC)
+    assert ng == no and np.array_equal(mg, mo), (ng, no, int((mg != mo).sum()))
+    assert no > 30
+    assert np.array_equal(mo[pre >= 0], pre[pre >= 0])  # preassigned keypoints are kept
+
+
+def test_keyframe_empty_and_no_preassigned(frames):
+    k0, d0, k1, d1, pos, mind, maxd, valid, pre, T = _kf_scene(frames, 1, 2, seed=4)
+    logsf = float(np.log(np.float32(1.2)))
+    m = ea.Matcher()
+    n, out = m.keyframe(ea.camera(), T, 10, 100, 1, k0[:0], valid[:0], pos[:0], d0[:0], mind[:0], maxd[:0],
+                        logsf, k1, d1, None, SC)
+    assert n == 0 and (out == -1).all()
+    ng, mg = m.keyframe(ea.camera(), T, 10, 100, 1, k0, valid, pos, d0, mind, maxd, logsf, k1, d1, None, SC)
+    no, mo = orc.match_keyframe(orc.cam(), T, 10, 100, 1, k0, valid, pos, d0, mind, maxd, logsf, k1, d1, None, SC)
+    assert ng == no and np.array_equal(mg, mo)
 
 
 def test_initialization(frames):

@@ -18,8 +18,8 @@ def _run(flag, frames, start=1):
     g = ea.Replay(a, flag)
     o = orc.Replay(flag)
     for i, f in enumerate(frames):
-        og = g.frame(i + start, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
-        oo = o.frame(i + start, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+        og = g.frame(i + start, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        oo = o.frame(i + start, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
         assert np.array_equal(og, oo), "frame %d: %s vs %s" % (i, og.tolist(), oo.tolist())
         if f["kf"]:
             g.local_mapping()
@@ -33,9 +33,10 @@ def _run(flag, frames, start=1):
     return oi
 
 
-@pytest.mark.parametrize("flag", ["iForest", "None", "NP", "IoU", "NA", "EAO"])
-def test_replay_flags(flag):
-    frames = synth.assoc_stream(80)
+@pytest.mark.parametrize("flag,lines", [("iForest", False), ("None", False), ("NP", False), ("IoU", False),
+                                        ("NA", False), ("EAO", False), ("EAO", True), ("Full", True)])
+def test_replay_flags(flag, lines):
+    frames = synth.assoc_stream(80, lines=lines)
     ints = _run(flag, frames)
     assert len(ints) > 5
 
@@ -49,7 +50,7 @@ def test_replay_long_bad_points():
 
 
 def test_replay_bench_stream_full():
-    """The benchmark's 405-frame fr3-shaped stream, EAO flag, end to end."""
+    """The benchmark's 405-frame fr3-shaped stream (with line segments), EAO flag, end to end."""
     _run("EAO", synth.assoc_stream_fr3(405))
 
 
@@ -62,7 +63,7 @@ def test_replay_run_stream_matches_per_frame_oracle():
     o = orc.Replay("EAO")
     ref = []
     for i, f in enumerate(frames):
-        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines")))
         if f["kf"]:
             o.local_mapping()
     assert np.array_equal(det, np.concatenate(ref))

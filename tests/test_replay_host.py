@@ -52,8 +52,8 @@ class _HostReplay(ea.Replay):
         finally:
             ea._lib = saved
 
-    def frame(self, *a):
-        return self._with(super().frame, *a)
+    def frame(self, *a, **k):
+        return self._with(lambda *x: super(_HostReplay, self).frame(*x, **k), *a)
 
     def local_mapping(self):
         return self._with(super().local_mapping)
@@ -69,14 +69,15 @@ class _HostReplay(ea.Replay):
     __del__ = close
 
 
-@pytest.mark.parametrize("flag", ["iForest", "None", "NP", "IoU", "NA"])
-def test_host_orchestration_matches_oracle(harness, flag):
-    frames = synth.assoc_stream(60)
+@pytest.mark.parametrize("flag,lines", [("iForest", False), ("None", False), ("NP", False), ("IoU", False),
+                                        ("NA", False), ("EAO", True), ("Full", True), ("NP", True)])
+def test_host_orchestration_matches_oracle(harness, flag, lines):
+    frames = synth.assoc_stream(60, lines=lines)
     g = _HostReplay(harness, flag)
     o = orc.Replay(flag)
     for i, f in enumerate(frames):
-        og = g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
-        oo = o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+        og = g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        oo = o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
         assert np.array_equal(og, oo), (i, og.tolist(), oo.tolist())
         if f["kf"]:
             g.local_mapping()
@@ -95,7 +96,10 @@ def test_host_run_stream_matches_oracle(harness):
     o = orc.Replay("EAO")
     ref = []
     for i, f in enumerate(frames):
-        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines")))
         if f["kf"]:
             o.local_mapping()
     assert np.array_equal(det, np.concatenate(ref))
+    gi, gf, _ = g.objects()
+    oi, of, _ = o.objects()
+    assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)

@@ -64,17 +64,21 @@ def main():
                         **{"f%d" % i: p[0] for i, p in enumerate(pr)}, **{"fv%d" % i: p[1] for i, p in enumerate(pr)},
                         **{"o%d" % i: p[2] for i, p in enumerate(pr)}, **{"ov%d" % i: p[3] for i, p in enumerate(pr)},
                         stats=stats.view(np.uint8))
-    fr = synth.assoc_stream(60)
-    r = orc.Replay("EAO")
-    outs = []
-    for t, f in enumerate(fr):
-        outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
-        if f["kf"]:
-            r.local_mapping()
-    ints, fl, pts = r.objects()
-    np.savez_compressed(os.path.join(OUT, "replay_eao60.npz"), det_out=np.concatenate(outs),
-                        det_count=np.array([len(o) for o in outs], np.int32), obj_ints=ints, obj_floats=fl,
-                        obj_points=np.concatenate(pts), obj_npoints=np.array([len(p) for p in pts], np.int32))
+    for name, lines in (("replay_eao60.npz", False), ("replay_eao_lines60.npz", True)):
+        # EAO flag over 60 frames; the second fixture adds each frame's line
+        # segments (object-line association + yaw sampling, Tracking.cc:2472-2871)
+        fr = synth.assoc_stream(60, lines=lines)
+        r = orc.Replay("EAO")
+        outs = []
+        for t, f in enumerate(fr):
+            outs.append(r.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"],
+                                lines=f.get("lines")))
+            if f["kf"]:
+                r.local_mapping()
+        ints, fl, pts = r.objects()
+        np.savez_compressed(os.path.join(OUT, name), det_out=np.concatenate(outs),
+                            det_count=np.array([len(o) for o in outs], np.int32), obj_ints=ints, obj_floats=fl,
+                            obj_points=np.concatenate(pts), obj_npoints=np.array([len(p) for p in pts], np.int32))
     for n in sorted(os.listdir(OUT)):
         print(n, os.path.getsize(os.path.join(OUT, n)))
 

@@ -171,11 +171,64 @@ def assoc_scene(seed=0xEA1, classes=None, pts_range=(150, 600), n_background=800
     return objs, np.asarray(mp_pos, np.float32), np.asarray(mp_obj, np.int32)
 
 
+# cuboid corner numbering of Object_Map::mCuboid3D (corner_1..8: z-min face
+# counter-clockwise from (x_min, y_min), then the z-max face), Object.cc:1040-1080
+_CORNERS = np.array([[0, 0, 0], [1, 0, 0], [1, 1, 0], [0, 1, 0], [0, 0, 1], [1, 0, 1], [1, 1, 1], [0, 1, 1]], float)
+_EDGES = [(0, 1), (1, 2), (2, 3), (3, 0), (4, 5), (5, 6), (6, 7), (7, 4), (0, 4), (1, 5), (2, 6), (3, 7)]
+
+
+def frame_lines(T, objs, rng, K=TUM3_K, w=640, h=480, n_clutter=12):
+    """Synthetic Frame::all_lines_eigen (SURVEY §8d input 2: "projected cuboid
+    edges +-2 deg noise"): the visible edges of every object's ground-truth box,
+    each rotated about its midpoint by N(0, 1 deg) clipped to +-2 deg, about a
+    third of the long ones broken in two (so merge_break_lines has work), plus
+    random clutter segments; endpoints in random order, float32 (L, 4)."""
+    fx, fy, cx, cy = K
+    segs = []
+    for o in objs:
+        c = o["center"] + (_CORNERS - 0.5) * np.asarray(o["ext"])
+        Pc = c @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+        if (Pc[:, 2] < 0.1).any():
+            continue
+        uv = np.stack([fx * Pc[:, 0] / Pc[:, 2] + cx, fy * Pc[:, 1] / Pc[:, 2] + cy], 1)
+        for a, b in _EDGES:
+            p, q = uv[a], uv[b]
+            if not (0 <= p[0] < w and 0 <= p[1] < h and 0 <= q[0] < w and 0 <= q[1] < h):
+                continue
+            d = q - p
+            ln = float(np.hypot(*d))
+            if ln < 15:
+                continue
+            th = np.deg2rad(float(np.clip(rng.normal(0, 1.0), -2, 2)))
+            m = (p + q) / 2
+            rot = np.array([[np.cos(th), -np.sin(th)], [np.sin(th), np.cos(th)]])
+            p, q = m + rot @ (p - m), m + rot @ (q - m)
+            if ln > 60 and rng.random() < 0.3:
+                t0 = rng.uniform(0.3, 0.7)
+                gap = 4.0 / ln
+                segs.append(np.concatenate([p, p + (q - p) * (t0 - gap)]))
+                segs.append(np.concatenate([p + (q - p) * (t0 + gap), q]))
+            else:
+                segs.append(np.concatenate([p, q]))
+    for _ in range(n_clutter):
+        m = rng.uniform([0, 0], [w, h])
+        ang, ln = rng.uniform(0, np.pi), rng.uniform(10, 80)
+        d = 0.5 * ln * np.array([np.cos(ang), np.sin(ang)])
+        segs.append(np.concatenate([m - d, m + d]))
+    L = np.asarray(segs, np.float64).reshape(-1, 4)
+    flip = rng.random(len(L)) < 0.5
+    L[flip] = L[flip][:, [2, 3, 0, 1]]
+    return L[rng.permutation(len(L))].astype(np.float32)
+
+
 def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None, obs_frac=0.7,
-                 kf_every=5, pts_range=(150, 600), n_background=800):
-    """Per-frame replay inputs for the association path."""
+                 kf_every=5, pts_range=(150, 600), n_background=800, lines=False):
+    """Per-frame replay inputs for the association path.
+    lines=True adds each frame's line segments (frame_lines, own seeded stream
+    0xEA2 so the rest of the stream is unchanged)."""
     fx, fy, cx, cy = K
     rng = np.random.Generator(np.random.PCG64(seed + 1))
+    lrng = np.random.Generator(np.random.PCG64(0xEA2 + seed))
     objs, P, owner = assoc_scene(seed, classes, pts_range, n_background)
     frames = []
     for t in range(n_frames):
@@ -211,13 +264,16 @@ def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None,
         uv = (np.round(uv * 10) / 10).astype(np.float32)
         frames.append(dict(T=T, boxes=boxes, ids=obs.astype(np.int32), pos=P[obs],
                            uv=uv, bad=np.zeros(len(obs), np.uint8), kf=(t % kf_every == kf_every - 1)))
+        if lines:
+            frames[-1]["lines"] = frame_lines(T, objs, lrng, K, w, h)
     return frames
 
 
-def assoc_stream_fr3(n_frames=405, seed=0xEA1):
-    """The benchmark's association workload (BASELINE configs[1], SURVEY §8d input 2)."""
+def assoc_stream_fr3(n_frames=405, seed=0xEA1, lines=True):
+    """The benchmark's association workload (BASELINE configs[1], SURVEY §8d input 2):
+    EAO flag, so the frames carry line segments for the yaw sampling."""
     return assoc_stream(n_frames, seed=seed, classes=FR3_CLASSES, obs_frac=0.5, pts_range=(80, 400),
-                        n_background=400)
+                        n_background=400, lines=lines)
 
 
 # SURVEY.md §8d input 4 (Config C): 64 objects x 2000 map points, 16 classes,
