@@ -218,7 +218,9 @@ def main():
             ev_m0.record(stream)
             match()
             ev_m1.record(stream)
-        torch.cuda.synchronize(dev)
+        # wait for the extraction stream only: a device-wide synchronize would
+        # also serialise against the association thread's launches
+        stream.synchronize()
         if th is not None:
             th.join()
         if record is not None:

@@ -806,7 +806,9 @@ int AssocEngine::init(int device, int mp) {
     return EAO_E_ARG;
   }
   EAO_HIP_CHECK(hipSetDevice(dev));
-  EAO_HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  int lo_pri = 0, hi_pri = 0;  // latency-bound association launches: highest priority
+  EAO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+  EAO_HIP_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, hi_pri));
   EAO_HIP_CHECK(hipMalloc(&d_pts, sizeof(float) * 3 * (size_t)mp * 2));
   EAO_HIP_CHECK(hipMalloc(&d_valid, (size_t)mp * 2));
   EAO_HIP_CHECK(hipMalloc(&d_meta, sizeof(int) * 8 * max_pairs));

@@ -23,6 +23,7 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -35,6 +36,23 @@
 #include "assoc.h"
 #include "common.h"
 #include "shard.h"
+
+
+// Host-side waits of the association chain spin on hipEventQuery: a blocking
+// hipEventSynchronize / hipStreamSynchronize may park the thread and pay a
+// wake-up per wait, and the chain waits a few times per frame.
+static const bool g_spin_wait = [] {
+  const char* v = getenv("EAO_BLOCKING_WAIT");  // A/B switch for measurements
+  return !(v && v[0] == '1');
+}();
+static hipError_t spin_event(hipEvent_t e) {
+  if (!g_spin_wait) return hipEventSynchronize(e);
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    __builtin_ia32_pause();
+  }
+}
 
 namespace eao {
 
@@ -142,6 +160,8 @@ struct Obj {  // Object_Map
   double corner_w[8][3] = {};                  // corner_k_w (pose_without_yaw)
   std::vector<std::array<float, 5>> angles;    // mvAngleTimesAndScore
   float err_par = 0, err_yaw = 0;              // mfErrorParallel, mfErroeYaw
+  bool yaw_due = false;                        // step 10.6 deferred behind the pending forest
+  float yawT[16];                              // ... with the pose of its frame
   int pending = 0;  // 0 none, 1 iForest, 2 iForest then ComputeMeanAndStandard
   int slot = -1;    // in-flight isolation-forest slot, -1 if not launched
 };
@@ -296,6 +316,11 @@ class ReplayEngine {
     u = p->pu;
     v = p->pv;
   }
+  MapPt* mp_lookup(int id) {  // existing map point or null
+    if (id >= 0 && id < (1 << 24)) return (size_t)id < mps_dense.size() ? mps_dense[id].get() : nullptr;
+    auto it = mps.find(id);
+    return it == mps.end() ? nullptr : it->second.get();
+  }
   MapPt* mappoint(int id) {
     if (id >= 0 && id < (1 << 24)) {
       if ((size_t)id >= mps_dense.size()) mps_dense.resize(std::max((size_t)id + 1, mps_dense.size() * 2));
@@ -359,6 +384,7 @@ class ReplayEngine {
     // launch list (the owned objects), their offsets in the packed clouds
     std::vector<int> lc, loff;
     bool launched = false;
+    unsigned long fid = 0;  // frame of the launch (speculative NP stats belong to it)
     // sharded: the all-gathered outcome, an outlier bit mask per object
     // (mask_off into xres) and the speculative NP stats in sp_* order
     bool xdone = true;
@@ -398,6 +424,7 @@ class ReplayEngine {
 
   // forest slots, streams and staging outlive the replay: the next replay on
   // the same engine adopts them (allocation is not per replay)
+  hipEvent_t gpu0_ev = nullptr;  // frame-start launch completion (spin-waited)
   struct Pool {
     std::vector<IfBatch> ifb;
     hipStream_t if_stream[kIfStreams] = {};
@@ -438,6 +465,7 @@ class ReplayEngine {
   ~ReplayEngine() {
     for (hipStream_t st : if_stream)
       if (st) (void)hipStreamSynchronize(st);
+    if (gpu0_ev) (void)hipEventDestroy(gpu0_ev);
     if (A && !A->replay_pool && !ifb.empty()) {
       Pool* p = new Pool();
       p->ifb.swap(ifb);
@@ -582,7 +610,9 @@ class ReplayEngine {
   }
 
   // Tracking::SampleObjYaw (Tracking.cc:2624-2871) with WorldToImg (:2602-2620)
-  void sample_yaw(Obj* o) {
+  void sample_yaw(Obj* o, const float* Tcw) {
+    Pose pv = pz;  // WorldToImg under the pose of the sampled frame
+    std::memcpy(pv.T, Tcw, sizeof(pv.T));
     const std::vector<double>& L = o->frames.back()->line_deg;
     const int nAll = (int)L.size();
     int numMax = 0;
@@ -610,7 +640,7 @@ class ReplayEngine {
           const float d = R[r][0] * rel[k][0] + R[r][1] * rel[k][1] + R[r][2] * rel[k][2];
           w[r] = (float)((double)d + (double)ctr[r]);
         }
-        pz.proj(w, px[k], py[k]);
+        pv.proj(w, px[k], py[k]);
       }
       double adeg[3];
       float len[3];
@@ -806,7 +836,12 @@ class ReplayEngine {
   // order, Q8, then ComputeMeanAndStandard for pending 2)
   int if_init() {
     ifb.resize(kIfBatches);
-    for (int k = 0; k < kIfStreams; k++) EAO_HIP_CHECK(hipStreamCreateWithFlags(&if_stream[k], hipStreamNonBlocking));
+    // the association is the latency-bound chain of the step: its launches get the
+    // highest stream priority so extraction work queued on other streams cannot delay them
+    int lo_pri = 0, hi_pri = 0;
+    EAO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+    for (int k = 0; k < kIfStreams; k++)
+      EAO_HIP_CHECK(hipStreamCreateWithPriority(&if_stream[k], hipStreamNonBlocking, hi_pri));
     for (IfBatch& b : ifb) {
       EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
       EAO_HIP_CHECK(hipMalloc((void**)&b.contrib, sizeof(double) * 50 * (size_t)A->max_points));
@@ -865,6 +900,7 @@ class ReplayEngine {
       }
       if_next = (k + 1) % kIfBatches;
       IfBatch& b = ifb[k];
+      b.fid = cur;
       b.objs.clear();
       b.sp_det.clear();
       b.sp_obj.clear();
@@ -1022,7 +1058,7 @@ class ReplayEngine {
   // completion (no object of the batch has changed since the launch): per
   // owned object an outlier bit mask, then the owned speculative NP stats
   int exchange_batch(IfBatch& b) {
-    if (b.launched) EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+    if (b.launched) EAO_HIP_CHECK(spin_event(b.ev));
     const int nb = (int)b.objs.size();
     const size_t sb = sizeof(eao_np_stats);
     std::vector<size_t> mb(sworld, 0), nsr(sworld, 0);
@@ -1078,7 +1114,7 @@ class ReplayEngine {
       int rc = exchange_batch(b);
       if (rc) return rc;
     } else if (b.launched) {
-      EAO_HIP_CHECK(hipEventSynchronize(b.ev));
+      EAO_HIP_CHECK(spin_event(b.ev));
     }
     int c = 0;
     while (b.objs[c] != o) c++;
@@ -1106,9 +1142,14 @@ class ReplayEngine {
     }
     o->pts.resize(w);
     if (o->pending == 2) mean_std(o);
+    if (o->yaw_due) {  // SampleObjYaw of the launch frame, now that the cuboid is final
+      o->yaw_due = false;
+      sample_yaw(o, o->yawT);
+    }
     const eao_np_stats* sps = sworld > 1 ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
-    for (size_t q = 0; q < b.sp_obj.size(); q++)
-      if (b.sp_obj[q] == c) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
+    if (b.fid == cur)
+      for (size_t q = 0; q < b.sp_obj.size(); q++)
+        if (b.sp_obj[q] == c) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
     o->pending = 0;
     o->slot = -1;
     b.left--;
@@ -1225,7 +1266,9 @@ class ReplayEngine {
     rc = A->np_batch(npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
                      (eao_np_stats*)h_out, A->stream, max_olen);
     if (rc) return rc;
-    EAO_HIP_CHECK(hipStreamSynchronize(A->stream));
+    if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
+    EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
+    EAO_HIP_CHECK(spin_event(gpu0_ev));
     const int* r = (const int*)(h_out + o_r);
     const uint8_t* ok = h_out + o_ok;
     for (int b = 0; b < nb; b++) {
@@ -1284,6 +1327,12 @@ class ReplayEngine {
                       const std::vector<int>& di, const std::vector<int>& oi) {
     if (list.empty() && pairs.empty()) return EAO_OK;
     if (int rc = kick()) return rc;  // pending forests overlap this launch
+    {  // forests left pending by the previous frame: their objects' points are read now
+      Tick tk(&prof[17]);
+      if (int rc = flush_list(list)) return rc;
+      for (auto& pr : pairs)
+        if (int rc = touch(pr.second)) return rc;
+    }
     Tick tk(&prof[7]);
     prof[6] += 1;
     std::vector<int> rects;
@@ -1743,6 +1792,17 @@ class ReplayEngine {
     over.assign(objs.size(), 0);
     double tA = now_us();
     std::vector<MapPt*> tr(npts);
+    bool pend = false;  // forests still pending from the previous frame read positions / flags
+    for (auto& up : objs) pend |= up->pending != 0;
+    for (int i = 0; pend && i < npts; i++) {
+      auto it = mp_lookup(ids[i]);
+      if (!it) continue;
+      const bool nb_ = bad ? bad[i] != 0 : false;
+      if (std::memcmp(it->pos, pos + 3 * i, sizeof(float) * 3) != 0 || it->bad != nb_) {
+        if (int rc = flush(-1)) return rc;
+        pend = false;
+      }
+    }
     for (int i = 0; i < npts; i++) {
       MapPt* p = mappoint(ids[i]);
       for (int a = 0; a < 3; a++) p->pos[a] = pos[3 * i + a];
@@ -1901,8 +1961,11 @@ class ReplayEngine {
       prof[15] += now_us() - tA;
       tA = now_us();
       {
-        Tick tk(&prof[17]);  // end-of-frame forest completion
-        rc = flush(-1);
+        // end of frame: the forests of this frame's updates are launched, not
+        // awaited -- each completes at the first read of its object (next
+        // frame's step 10 at the latest, or earlier if a point it holds changes)
+        Tick tk(&prof[17]);
+        rc = kick();
       }
       if (rc) return rc;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
@@ -1917,6 +1980,7 @@ class ReplayEngine {
             bool ov = false;
             for (int j = (int)objs.size() - 1; j >= 0; j--) {
               if (objs[j]->bad || i == j) continue;
+              if ((rc = touch(o)) || (rc = touch(objs[j].get()))) return rc;  // cuboids read
               if (overlap(o, objs[j].get())) {
                 ov = true;
                 break;
@@ -1943,7 +2007,13 @@ class ReplayEngine {
           Obj* o = objs[i].get();
           if (o->bad) continue;
           if ((unsigned long)(long)o->last_add < fid - 5) continue;
-          if (yaw_class(o->cls) && (unsigned long)(long)o->last_add == fid) sample_yaw(o);
+          if (!(yaw_class(o->cls) && (unsigned long)(long)o->last_add == fid)) continue;
+          if (o->pending) {  // cuboid not final yet: sample when its forest completes
+            o->yaw_due = true;
+            std::memcpy(o->yawT, pz.T, sizeof(o->yawT));
+          } else {
+            sample_yaw(o, pz.T);
+          }
         }
     }
     for (Det* f : o2) {

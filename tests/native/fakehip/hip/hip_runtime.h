@@ -13,7 +13,7 @@
 typedef int hipError_t;
 typedef void* hipStream_t;
 typedef void* hipEvent_t;
-enum { hipSuccess = 0, hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipStreamNonBlocking = 1 };
+enum { hipSuccess = 0, hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipStreamNonBlocking = 1, hipErrorNotReady = 600 };
 struct int2 { int x, y; };
 struct int4 { int x, y, z, w; };
 inline const char* hipGetErrorString(hipError_t) { return "fake"; }
@@ -39,9 +39,12 @@ inline unsigned long long __ballot(bool p) { return p; }
 inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }
 enum { hipEventDisableTiming = 2 };
 inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) { *s = (hipStream_t)1; return 0; }
+inline hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned, int) { *s = (hipStream_t)1; return 0; }
+inline hipError_t hipDeviceGetStreamPriorityRange(int* lo, int* hi) { *lo = 0; *hi = -1; return 0; }
 inline hipError_t hipStreamDestroy(hipStream_t) { return 0; }
 inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = (hipEvent_t)1; return 0; }
 inline hipError_t hipEventDestroy(hipEvent_t) { return 0; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return 0; }
 inline hipError_t hipEventSynchronize(hipEvent_t) { return 0; }
+inline hipError_t hipEventQuery(hipEvent_t) { return 0; }
 inline hipError_t hipMemset(void* p, int v, size_t n) { std::memset(p, v, n); return 0; }

@@ -1,0 +1,31 @@
+"""Isolation-forest latency probe (development aid): wall time per
+eao_iforest_scores_batch call and the in-kernel phase stamps of workgroup
+(0,0) for a range of cloud sizes."""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "eao-slam_amd", "python"))
+import eao_accel as ea  # noqa: E402
+
+a = ea.Assoc()
+rng = np.random.default_rng(0)
+st = np.zeros(24, np.uint64)
+names = ["load", "shufdraw", "writers", "resolve", "gather", "build", "score"]
+for n in (40, 80, 160, 320, 640, 1280, 2560):
+    c = rng.normal([0, 0, 2], [0.1, 0.2, 0.05], (n, 3)).astype(np.float32)
+    for _ in range(3):
+        a.iforest([c])
+    t0 = time.perf_counter()
+    R = 20
+    for _ in range(R):
+        a.iforest([c])
+    dt = (time.perf_counter() - t0) / R * 1e6
+    ea.lib().eao_debug_iforest_stamps(st.ctypes.data_as(ctypes.c_void_p))
+    ph = [int(st[k + 1]) - int(st[k]) for k in range(7)]
+    print("n=%5d call %7.1f us | nodes %4d | " % (n, dt, int(st[10])) +
+          " ".join("%s %d" % (nm, p) for nm, p in zip(names, ph)), flush=True)
