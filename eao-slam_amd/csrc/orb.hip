@@ -18,6 +18,8 @@
 // and -ffp-contract=off so every rounding matches the oracle.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -27,6 +29,7 @@
 #include "orb.h"
 
 namespace eao {
+
 
 __constant__ int c_pattern[1024] = {
 #include "orb_pattern.inc"
@@ -208,20 +211,72 @@ __device__ __forceinline__ int fast_strength(const uint8_t* roi, int RS, int r, 
   return max(0, max(u, -w));
 }
 
-// One workgroup per (row of cells, frame): the band's ROI staged in LDS,
-// the strength of every detection pixel computed once, then one wave per
-// cell applies ORBextractor.cc:789-829 -- FAST at iniTh with in-cell 3x3
-// non-max suppression (neighbours outside the cell's detection window count
-// as 0, Q15), retry at minTh only when the cell found nothing -- and emits
-// the corners row-major.
+// FAST strength of the pixel at p (row stride RS known at compile time, so
+// the 16 ring reads are immediate-offset LDS loads): with A = min over the 16
+// arcs of 9 of the arc's max ring value and B = max over the arcs of the arc's
+// min, S = max(0, v - A, B - v) -- the same integer as fast_strength (the arc
+// min / max of d = v - ring are v - max / v - min), from 3-wide then 9-wide
+// window minima / maxima.
+template <int RS>
+__device__ __forceinline__ int fast_strength_c(const uint8_t* p) {
+  constexpr int off[16] = {3 * RS,  3 * RS + 1,  2 * RS + 2,  RS + 3,  3,  -RS + 3,  -2 * RS + 2,  -3 * RS + 1,
+                           -3 * RS, -3 * RS - 1, -2 * RS - 2, -RS - 3, -3, RS - 3,   2 * RS - 2,  3 * RS - 1};
+  const int v = p[0];
+  int q[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) q[k] = p[off[k]];
+  int mn3[16], mx3[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn3[k] = min(min(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
+    mx3[k] = max(max(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
+  }
+  int A = 255, B = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const int a0 = max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]);
+    const int a1 = max(max(mx3[k + 1], mx3[(k + 4) & 15]), mx3[(k + 7) & 15]);
+    const int b0 = min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]);
+    const int b1 = min(min(mn3[k + 1], mn3[(k + 4) & 15]), mn3[(k + 7) & 15]);
+    A = min(min(A, a0), a1);
+    B = max(max(B, b0), b1);
+  }
+  return max(0, max(v - A, B - v));
+}
+
+// ROI row stride of k_fast_band (bands are <= 512 px wide, + 16-byte alignment slack)
+constexpr int FAST_RS = 544;
+
+// lane l <- lane l-1 (right = false) or l+1 (right = true) across the whole
+// wave (GFX9 DPP wave_shr:1 / wave_shl:1); the missing end lane reads 0
+__device__ __forceinline__ int wave_from_left(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xF, 0xF, true); }
+__device__ __forceinline__ int wave_from_right(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xF, 0xF, true); }
+
+// One workgroup per (row of cells, frame), ORBextractor.cc:789-829 per cell:
+// FAST-9 at iniTh with in-cell 3x3 non-max suppression (neighbours outside the
+// cell's detection window count as 0, Q15), retry at minTh only when the cell
+// found nothing; corners emitted row-major per cell.
+//   1. the band ROI is staged in LDS with 16-byte loads;
+//   2. each wave sweeps 64-column strips down the band (62 output columns, the
+//      two end lanes are halo): a lane computes the FAST strength S of its
+//      column row by row, keeps three rows in registers and gets the left /
+//      right neighbours by DPP wave shifts, so the suppression costs a few
+//      VALU ops instead of nine LDS reads. keep(t) <=> S > t, S >= 2 and S
+//      beats the largest in-window neighbour whenever that one exceeds t;
+//      keep(iniTh) == keep(minTh) && S > iniTh, so one byte per pixel
+//      (S if kept at minTh, else 0) encodes both passes;
+//   3. one wave per cell emits the kept pixels row-major (ballot + popcount),
+//      the iniTh set, or the minTh set when the cell has no iniTh corner.
 __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ frames, int fpitch,
                                                    long long fstride, const uint8_t* __restrict__ pyr,
                                                    long long pstride, const LevelDev* __restrict__ levels,
                                                    const BandDev* __restrict__ bands,
                                                    const CellDev* __restrict__ cells, int iniTh, int minTh,
-                                                   int RS, uint32_t* __restrict__ cand, long long cand_stride,
-                                                   int* __restrict__ cell_cnt, int ncells) {
-  extern __shared__ uint8_t smem[];
+                                                   uint32_t* __restrict__ cand, long long cand_stride,
+                                                   int* __restrict__ cell_cnt, int ncells, int vec_ok) {
+  constexpr int RS = FAST_RS;
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ int16_t bnd[64];  // cell detection-window starts (band coords), then the end
   const BandDev B = bands[blockIdx.x];
   const int f = blockIdx.y, t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const LevelDev& L = levels[B.level];
@@ -235,55 +290,99 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
     pitch = L.pitch;
   }
   const int bw = B.x1 - B.x0, bh = B.y1 - B.y0;
-  uint8_t* roi = smem;
-  uint8_t* S = smem + RS * bh;
-  for (int r = t >> 6; r < bh; r += 4)
-    for (int c = lane; c < bw; c += 64) roi[r * RS + c] = img[(long long)(B.y0 + r) * pitch + B.x0 + c];
-  __syncthreads();
-  // strength of every detection pixel (roi [3, bw-3) x [3, bh-3)), computed once
-  for (int r = 3 + (t >> 6); r < bh - 3; r += 4)
-    for (int c = 3 + lane; c < bw - 3; c += 64) {
-      const int sv = fast_strength(roi, RS, r, c);
-      S[r * RS + c] = (uint8_t)(sv > minTh ? sv : 0);
+  // ROI column c lives at smem[r * RS + sh + c] (16-byte aligned row starts)
+  const int ax0 = vec_ok ? (B.x0 & ~15) : B.x0, sh = B.x0 - ax0;
+  uint8_t* roi = smem + sh;
+  uint8_t* F = smem + RS * bh;
+  if (vec_ok) {
+    const int nvec = (sh + bw + 15) >> 4;
+    for (int idx = t; idx < bh * nvec; idx += 256) {
+      const int r = idx / nvec, v = idx - r * nvec;
+      *(uint4*)(smem + r * RS + 16 * v) = *(const uint4*)(img + (long long)(B.y0 + r) * pitch + ax0 + 16 * v);
     }
+  } else {
+    for (int r = t >> 6; r < bh; r += 4)
+      for (int c = lane; c < bw; c += 64) roi[r * RS + c] = img[(long long)(B.y0 + r) * pitch + B.x0 + c];
+  }
+  for (int k = t; k <= B.ncells; k += 256) {
+    const CellDev c = cells[B.cell_begin + min(k, B.ncells - 1)];
+    bnd[k] = (int16_t)(k < B.ncells ? c.x0 + 3 - B.x0 : c.x1 - 3 - B.x0);
+  }
+  __syncthreads();
+  const int thi = min(max(iniTh, 0), 255), tlo = min(max(minTh, 0), 255);
+  const int y0 = 3, y1 = bh - 3;  // detection rows (every cell of the band)
+  for (int k = wv; 3 + 62 * k < bw - 3; k += 4) {
+    const int x = 2 + 62 * k + lane;  // lane 0 / 63: halo columns
+    const bool inx = x >= 3 && x < bw - 3;
+    const bool outl = inx && lane >= 1 && lane <= 62;
+    int lo = 0, hi = 0;  // the detection window of x's cell
+    if (inx) {
+      int q = 0;
+      while (q + 1 < B.ncells && bnd[q + 1] <= x) q++;
+      lo = bnd[q];
+      hi = bnd[q + 1];
+    }
+    const bool okl = x - 1 >= lo, okr = x + 1 < hi;
+    auto row = [&](int r, int& Sv, int& Lv, int& Rv) {
+      int sv = 0;
+      if (inx && r < y1) {
+        sv = fast_strength_c<RS>(roi + r * RS + x);
+        sv = sv > tlo ? sv : 0;
+      }
+      const int l = wave_from_left(sv), rr = wave_from_right(sv);
+      Sv = sv;
+      Lv = okl ? l : 0;
+      Rv = okr ? rr : 0;
+    };
+    int Sc, Lc, Rc;
+    row(y0, Sc, Lc, Rc);
+    int mp = 0;  // neighbour-row max of row r-1 (row y0-1 is outside every window)
+    for (int r = y0; r < y1; r++) {
+      int Sn, Ln, Rn;
+      row(r + 1, Sn, Ln, Rn);
+      const int mn = max(max(Ln, Sn), Rn);
+      const int M = max(max(mp, mn), max(Lc, Rc));
+      const bool keep = Sc > tlo && Sc >= 2 && (M <= tlo || Sc > M);
+      if (outl) F[r * RS + x] = (uint8_t)(keep ? Sc : 0);
+      mp = max(max(Lc, Sc), Rc);
+      Sc = Sn;
+      Lc = Ln;
+      Rc = Rn;
+    }
+  }
   __syncthreads();
   for (int cc = wv; cc < B.ncells; cc += 4) {
     const int ci = B.cell_begin + cc;
     const CellDev c = cells[ci];
-    // the cell's detection window in band ROI coordinates
-    const int wx0 = c.x0 + 3 - B.x0, wx1 = c.x1 - 3 - B.x0, wy0 = 3, wy1 = c.y1 - c.y0 - 3;
-    const int ww = wx1 - wx0;
+    const int wx0 = bnd[cc], ww = bnd[cc + 1] - wx0;
     uint32_t* out = cand + f * cand_stride + c.slot;
-    int n = 0;
-    for (int pass = 0; pass < 2; pass++) {
-      const int th = min(max(pass == 0 ? iniTh : minTh, 0), 255);
-      n = 0;
-      for (int r = wy0; r < wy1; r++) {
+    int n = 0, m = 0;
+    for (int r = y0; r < y1; r++)
+      for (int c0 = 0; c0 < ww; c0 += 64) {
+        const int x = wx0 + c0 + lane;
+        const int v = c0 + lane < ww ? F[r * RS + x] : 0;
+        const bool hi_ = v > thi;
+        const uint64_t mh = ballot(hi_);
+        if (hi_) {
+          const int pos = n + popc64(mh & lanes_below());
+          // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
+          if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
+        }
+        n += popc64(mh);
+        m += popc64(ballot(v > 0));
+      }
+    if (n == 0 && m > 0) {  // ORBextractor.cc:812 -- retry with minTh only when empty
+      for (int r = y0; r < y1; r++)
         for (int c0 = 0; c0 < ww; c0 += 64) {
           const int x = wx0 + c0 + lane;
-          bool keep = false;
-          int sc = 0;
-          if (c0 + lane < ww) {
-            auto score = [&](int rr, int xx) -> int {
-              if (rr < wy0 || rr >= wy1 || xx < wx0 || xx >= wx1) return 0;
-              const int v = S[rr * RS + xx];
-              return v > th ? v - 1 : 0;
-            };
-            sc = score(r, x);
-            keep = sc > 0 && sc > score(r, x + 1) && sc > score(r, x - 1) && sc > score(r - 1, x - 1) &&
-                   sc > score(r - 1, x) && sc > score(r - 1, x + 1) && sc > score(r + 1, x - 1) &&
-                   sc > score(r + 1, x) && sc > score(r + 1, x + 1);
+          const int v = c0 + lane < ww ? F[r * RS + x] : 0;
+          const uint64_t ml = ballot(v > 0);
+          if (v > 0) {
+            const int pos = n + popc64(ml & lanes_below());
+            if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
           }
-          const uint64_t m = ballot(keep);
-          if (keep) {
-            const int pos = n + popc64(m & lanes_below());
-            // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
-            if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, sc);
-          }
-          n += popc64(m);
+          n += popc64(ml);
         }
-      }
-      if (n > 0) break;  // ORBextractor.cc:812 -- retry with minTh only when empty
     }
     if (lane == 0) cell_cnt[f * ncells + ci] = n;
   }
@@ -1136,12 +1235,18 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[1], s));
   // FAST per band of cells
   {
-    const int RS = (band_w + 3) & ~3;
+    // 16-byte staged rows: level planes are 64-byte pitched; level 0 is the
+    // caller's frame buffer
+    const int vec_ok = ((uintptr_t)d_frames % 16 == 0 && pitch % 16 == 0) ? 1 : 0;
+    if (band_w + 30 > FAST_RS) {
+      set_error("orb: FAST band wider than the LDS row");
+      return EAO_E_CAPACITY;
+    }
     dim3 g((unsigned)bands.size(), nframes);
-    size_t lds = (size_t)RS * band_h * 2;  // roi, strength
+    size_t lds = (size_t)FAST_RS * band_h * 2;  // roi, kept strengths
     hipLaunchKernelGGL(k_fast_band, g, dim3(256), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
-                       d_levels, d_bands, d_cells, p.ini_th_fast, p.min_th_fast, RS, d_cand, cand_stride,
-                       d_cell_cnt, (int)cells.size());
+                       d_levels, d_bands, d_cells, p.ini_th_fast, p.min_th_fast, d_cand, cand_stride,
+                       d_cell_cnt, (int)cells.size(), vec_ok);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[2], s));
   // quadtree distribution
