@@ -400,10 +400,14 @@ struct QNode {
   uint8_t buf, nomore, alive, pad;
 };
 
-constexpr int QCAP = 1024;        // nodes alive at once (N + 4*nIni + margin)
-constexpr int QOS = 5 * QCAP;     // order array (one pass pushes <= 4*QCAP)
+// QCAP: nodes alive at once (N + 4*nIni + margin), chosen per extractor from
+// {256, 512, 1024} so the LDS footprint -- and with it the number of
+// concurrently resident (level, frame) quadtrees -- follows the feature quota
+constexpr int QCAP_MAX = 1024;
 
+template <int QCAP>
 struct QShared {
+  static constexpr int QOS = 5 * QCAP;  // order array (one pass pushes <= 4*QCAP)
   QNode node[QCAP];
   int16_t order[QOS];
   int16_t freel[QCAP];
@@ -417,6 +421,7 @@ __device__ __forceinline__ int child_of(uint32_t k, int mx, int my) {
   return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
 }
 
+template <int QCAP>
 __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ cand,
                                                    long long cand_stride,
                                                    const int* __restrict__ cell_cnt, int ncells,
@@ -425,11 +430,13 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
                                                    uint32_t* __restrict__ qbuf, long long qstride,
                                                    uint32_t* __restrict__ sel, long long sel_stride,
                                                    int* __restrict__ sel_cnt, int nlevels) {
-  __shared__ QShared S;
+  __shared__ QShared<QCAP> S;
+  constexpr int QOS = QShared<QCAP>::QOS;
   const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
   const LevelDev& L = levels[l];
   const uint32_t* C = cand + f * cand_stride;
-  uint32_t* B0 = qbuf + f * qstride + L.cand_off;
+  // ping-pong halves of this (frame, level): [2 cand_off, 2 cand_off + 2 cand_cap) of the frame area
+  uint32_t* B0 = qbuf + f * qstride + 2 * (long long)L.cand_off;
   uint32_t* B1 = B0 + L.cand_cap;
   uint32_t* bufs[2] = {B0, B1};
   // ---- gather candidates in vToDistributeKeys order (cells row-major)
@@ -1068,7 +1075,7 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
     L.cand_cap = cand_total - L.cand_off;
     L.nIni = (int)std::round((float)(L.maxBX - L.minBX) / (L.maxBY - L.minBY));
     L.hX = (float)(L.maxBX - L.minBX) / L.nIni;
-    if (L.nIni < 1 || L.nIni > 16 || L.nfeat + 4 * L.nIni + 16 > QCAP) {
+    if (L.nIni < 1 || L.nIni > 16 || L.nfeat + 4 * L.nIni + 16 > QCAP_MAX) {
       set_error("eao_orb_create: level geometry outside the quadtree kernel limits");
       return EAO_E_ARG;
     }
@@ -1252,9 +1259,11 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   // quadtree distribution
   {
     dim3 g(nl, nframes);
-    hipLaunchKernelGGL(k_distribute, g, dim3(64), 0, s, d_cand, cand_stride, d_cell_cnt,
-                       (int)cells.size(), d_levels, d_cells, d_qbuf, 2 * cand_stride, d_sel,
-                       sel_stride, d_sel_cnt, nl);
+    int need = 0;
+    for (int l = 0; l < nl; l++) need = std::max(need, levels[l].nfeat + 4 * levels[l].nIni + 16);
+    auto kd = need <= 256 ? k_distribute<256> : need <= 512 ? k_distribute<512> : k_distribute<1024>;
+    hipLaunchKernelGGL(kd, g, dim3(64), 0, s, d_cand, cand_stride, d_cell_cnt, (int)cells.size(), d_levels,
+                       d_cells, d_qbuf, 2 * cand_stride, d_sel, sel_stride, d_sel_cnt, nl);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[3], s));
   // blurred levels

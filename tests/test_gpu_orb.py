@@ -84,3 +84,42 @@ def test_extract_1080p():
     ok, od = orc.extract(img, nfeatures=4000)
     _cmp_kps(gk, ok)
     assert np.array_equal(gd, od)
+
+
+def _batch_extract(fr, nfeat, w, h):
+    import torch
+    F = len(fr)
+    dev = torch.device("cuda", 0)
+    orb = ea.Orb(nfeat, 1.2, 8, 20, 7, w, h, max_batch=F)
+    cap = orb.cap
+    d_fr = torch.from_numpy(np.stack(fr)).to(dev)
+    kps = torch.zeros((F, cap, 28), dtype=torch.uint8, device=dev)
+    desc = torch.zeros((F, cap, 32), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    orb.extract_batch_device(d_fr.data_ptr(), F, w, kps.data_ptr(), desc.data_ptr(), cnt.data_ptr(), cap, None)
+    torch.cuda.synchronize()
+    return cnt.cpu().numpy(), kps.cpu().numpy().view(ea.KP_DTYPE).reshape(F, cap), desc.cpu().numpy()
+
+
+def test_batch_full_bench_stream_exact():
+    """The bench's whole 405-frame batch in one launch group: every frame
+    bit-exact. A full batch keeps thousands of (frame, level) workgroups in
+    flight at once, which is what exposes cross-workgroup buffer overlap."""
+    fr, _ = synth.frame_stream(405)
+    n, hk, hd = _batch_extract(fr, 1000, 640, 480)
+    bad = []
+    for t in range(len(fr)):
+        ok, od = orc.extract(fr[t])
+        if not (n[t] == len(ok) and np.array_equal(hk[t, :n[t]], ok) and np.array_equal(hd[t, :n[t]], od)):
+            bad.append(t)
+    assert not bad, "frames differing: %s" % bad[:20]
+
+
+def test_batch_1080p_4000_features_exact():
+    """Config B shape (1920x1080, 4000 features): the largest quadtree
+    capacity instantiation, batched."""
+    fr, _ = synth.frame_stream(12, w=1920, h=1080, seed=0xEA4)
+    n, hk, hd = _batch_extract(fr, 4000, 1920, 1080)
+    for t in range(len(fr)):
+        ok, od = orc.extract(fr[t], 4000)
+        assert n[t] == len(ok) and np.array_equal(hk[t, :n[t]], ok) and np.array_equal(hd[t, :n[t]], od), t
