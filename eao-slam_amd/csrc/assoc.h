@@ -29,6 +29,7 @@ class AssocEngine {
   // isolation forest scratch
   uint32_t* d_mtinit = nullptr;  // [trees][624] mt19937 state of each tree after the first twist
   double* d_contrib = nullptr;   // [max_trees][max_points] path length per (tree, point)
+  double* d_ctab = nullptr;      // [IF_MAXN + 1] CalculateC(n) table (leaf sizes, sample sizes)
   uint32_t cached_seed = 0, cached_trees = 0;
   size_t lds_limit = 0;
   double* d_scores = nullptr;    // [max_points]

@@ -401,6 +401,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
                                                       const uint32_t* __restrict__ mt_init,
                                                       const uint32_t* __restrict__ sample,
                                                       int maxN, int maxS, int npts_total,
+                                                      const double* __restrict__ ctab,
                                                       double* __restrict__ contrib) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const IfLds L(maxN, maxS);
@@ -769,7 +770,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int i = i0 + u * nb;
-      if (i < n) out[i] = (double)depth[u] + iforest_c(nd[u].x >> 2);
+      if (i < n) out[i] = (double)depth[u] + ctab[nd[u].x >> 2];
     }
   }
   if_stamp(7);
@@ -779,6 +780,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
 __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off,
                                                      const int* __restrict__ len,
                                                      const uint32_t* __restrict__ sample,
+                                                     const double* __restrict__ ctab,
                                                      int ntrees, int npts_total,
                                                      const double* __restrict__ contrib,
                                                      double* __restrict__ scores,
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
 #pragma unroll 10
   for (int t = 0; t < ntrees; t++) total += contrib[(long long)t * npts_total + g];
   const double avg = total / (double)ntrees;
-  const double sc = pow(2.0, -avg / iforest_c(sample[c]));
+  const double sc = pow(2.0, -avg / ctab[sample[c]]);
   scores[g] = sc;
   if (scores2) scores2[g] = sc;
 }
@@ -819,6 +821,19 @@ int AssocEngine::init(int device, int mp) {
   EAO_HIP_CHECK(hipMalloc(&d_mtinit, sizeof(uint32_t) * 624 * max_trees));
   EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)mp));
   EAO_HIP_CHECK(hipMalloc(&d_contrib, sizeof(double) * (size_t)mp * max_trees));
+  {  // CalculateC (isolation_forest.h:97-118) of every leaf / sample size, host libm like the reference
+    std::vector<double> c(IF_MAXN + 1, 0.0);
+    for (int k = 2; k <= IF_MAXN; k++) {
+      if (k == 2) {
+        c[k] = 1.0;
+        continue;
+      }
+      const double h = std::log((double)(k - 1)) + 0.5772156649;
+      c[k] = (2.0 * h) - ((2.0 * (double)(k - 1)) / (double)k);
+    }
+    EAO_HIP_CHECK(hipMalloc(&d_ctab, sizeof(double) * c.size()));
+    EAO_HIP_CHECK(hipMemcpy(d_ctab, c.data(), sizeof(double) * c.size(), hipMemcpyHostToDevice));
+  }
   hipDeviceProp_t prop;
   EAO_HIP_CHECK(hipGetDeviceProperties(&prop, dev));
   lds_limit = std::min((size_t)IF_LDS, (size_t)prop.sharedMemPerBlock) - 64;  // static LDS of the kernel
@@ -827,7 +842,7 @@ int AssocEngine::init(int device, int mp) {
 
 AssocEngine::~AssocEngine() {
   if (replay_pool && replay_pool_free) replay_pool_free(replay_pool);
-  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_mtinit, d_scores, d_contrib};
+  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_mtinit, d_scores, d_contrib, d_ctab};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -904,10 +919,10 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     cached_trees = trees;
   }
   hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(1024), L.total, s, pts, off, len,
-                     d_mtinit, d_sample, maxN, maxS, npts_total, contrib);
+                     d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
-                     d_sample, (int)trees, npts_total, (const double*)contrib, scores, scores2);
+                     d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
