@@ -42,11 +42,18 @@ class MatchEngine {
   float* d_T = nullptr;               // [16 * batch]
   float* d_scales = nullptr;          // [32]
   float* d_geo = nullptr;             // [max_kps][4] per-map-point projection (keyframe search)
+  // motion search candidates: MK smallest keys / rotation bins / count per (pair, query)
+  unsigned long long* d_ckeys = nullptr;
+  signed char* d_cbins = nullptr;
+  int* d_ccnt = nullptr;
 
   int init(int device, int max_kps, int max_batch);
   ~MatchEngine();
   int build_grid(const CamDev& cam, const eao_keypoint_dev* kps, const int* counts, int n_single,
                  int cap, int nframes, hipStream_t s);
+  int motion(const CamDev& cd, const float* d_T, float th, int check_ori, const eao_keypoint_dev* d_kps,
+             const uint8_t* d_desc, const int* d_counts, int cap, const uint8_t* d_has, const float* d_pos,
+             const uint8_t* d_mdesc, const float* d_sc, int nframes, int* d_match, int* d_nm, hipStream_t s);
 };
 
 }  // namespace eao

@@ -196,81 +196,203 @@ __device__ __forceinline__ unsigned long long make_key(int dist, int cellk, int 
 __device__ __forceinline__ int key_dist(unsigned long long k) { return (int)(k >> 42); }
 __device__ __forceinline__ int key_idx(unsigned long long k) { return (int)(k & 0x1fffff); }
 
-// SearchByProjection(CurrentFrame, LastFrame, th, bMono=true), ORBmatcher.cc:1328-1470.
-// One wave per pair p: last = slot p, current = slot p+1.
-__global__ __launch_bounds__(64) void k_match_motion(
-    CamDev cam, const float* __restrict__ Tcw, float th, int check_ori,
-    const eao_keypoint_dev* __restrict__ kps, const uint8_t* __restrict__ desc,
-    const int* __restrict__ counts, int cap, const uint8_t* __restrict__ has_mp,
-    const float* __restrict__ mp_pos, const uint8_t* __restrict__ mp_desc,
-    const float* __restrict__ scales, const int* __restrict__ gstart,
-    const int* __restrict__ gitems, int* __restrict__ cur_match, int* __restrict__ nmatches_out) {
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono=true), ORBmatcher.cc:1328-1470,
+// in two phases. The query loop is sequential only through the first-wins
+// assignment (a current keypoint taken by an earlier map point is skipped,
+// Q18), and the winner of a query is the smallest key (distance, window
+// order) among its untaken candidates (Q17). So:
+//   1. k_motion_cand, one thread per (pair, last-frame map point): projection,
+//      window and candidate scan exactly as the reference, keeping the MK
+//      smallest keys with distance <= TH_HIGH (larger ones can never be
+//      assigned) and their rotation bins, plus the candidate count;
+//   2. k_motion_resolve, one wave per pair: walks the queries in order; the
+//      lanes test the query's stored candidates against the taken flags in
+//      LDS at once and the first untaken one wins. Only a query whose MK
+//      stored candidates are all taken while it has more falls back to the
+//      full window scan (rare).
+constexpr int MK = 8;
+
+struct MotionGeom {
+  float u, v, r;
+  int oct;
+  bool ok;
+};
+
+// projection + radius of last-frame map point i for pair (ls -> cs)
+__device__ __forceinline__ MotionGeom motion_geom(const CamDev& cam, const float* T, float th,
+                                                  const eao_keypoint_dev* LK, const uint8_t* HM,
+                                                  const float* MP, const float* scales, int i) {
+  MotionGeom g;
+  g.ok = false;
+  if (!HM[i]) return g;
+  float x3Dc[3];
+  transform_point(T, MP + 3 * i, x3Dc);
+  const float invzc = (float)(1.0 / (double)x3Dc[2]);
+  if (invzc < 0) return g;
+  g.u = fadd(fmul(fmul(cam.fx, x3Dc[0]), invzc), cam.cx);
+  g.v = fadd(fmul(fmul(cam.fy, x3Dc[1]), invzc), cam.cy);
+  if (g.u < cam.minX || g.u > cam.maxX) return g;
+  if (g.v < cam.minY || g.v > cam.maxY) return g;
+  g.oct = LK[i].octave;
+  g.r = fmul(th, scales[g.oct]);
+  g.ok = true;
+  return g;
+}
+
+__global__ __launch_bounds__(256) void k_motion_cand(
+    CamDev cam, const float* __restrict__ Tcw, float th, const eao_keypoint_dev* __restrict__ kps,
+    const uint8_t* __restrict__ desc, const int* __restrict__ counts, int cap,
+    const uint8_t* __restrict__ has_mp, const float* __restrict__ mp_pos, const uint8_t* __restrict__ mp_desc,
+    const float* __restrict__ scales, const int* __restrict__ gstart, const int* __restrict__ gitems,
+    unsigned long long* __restrict__ ckeys, signed char* __restrict__ cbins, int* __restrict__ ccnt) {
+  const int p = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ls = p, cs = p + 1;
+  if (i >= counts[ls]) return;
+  const eao_keypoint_dev* LK = kps + (long long)ls * cap;
+  const eao_keypoint_dev* CK = kps + (long long)cs * cap;
+  const uint8_t* CD = desc + (long long)cs * cap * 32;
+  const int* GS = gstart + (long long)cs * (GRID_CELLS + 1);
+  const int* GI = gitems + (long long)cs * cap;
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
+  const long long qi = (long long)p * cap + i;
+  const MotionGeom g = motion_geom(cam, T, th, LK, has_mp + (long long)ls * cap, mp_pos + (long long)ls * cap * 3,
+                                   scales, i);
+  int n = 0;
+  unsigned long long best[MK];
+#pragma unroll
+  for (int k = 0; k < MK; k++) best[k] = KEY_NONE;
+  if (g.ok) {
+    const Window w = window_cells(cam, g.u, g.v, g.r);
+    if (!w.empty) {
+      const int minL = g.oct - 1, maxL = g.oct + 1;
+      const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+      const uint8_t* d = mp_desc + ((long long)ls * cap + i) * 32;
+      const uint4* pd = (const uint4*)d;
+      const uint4 d0 = pd[0], d1 = pd[1];
+      for (int ck = 0; ck < ncell; ck++) {
+        const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+        for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+          const int i2 = GI[q];
+          const eao_keypoint_dev& kp = CK[i2];
+          if (kp.octave < minL || kp.octave > maxL) continue;
+          if (!(fabsf(fsub(kp.x, g.u)) < g.r && fabsf(fsub(kp.y, g.v)) < g.r)) continue;
+          const uint4* pc = (const uint4*)(CD + 32 * (long long)i2);
+          const uint4 c0 = pc[0], c1 = pc[1];
+          const int dist = __popc(d0.x ^ c0.x) + __popc(d0.y ^ c0.y) + __popc(d0.z ^ c0.z) + __popc(d0.w ^ c0.w) +
+                           __popc(d1.x ^ c1.x) + __popc(d1.y ^ c1.y) + __popc(d1.z ^ c1.z) + __popc(d1.w ^ c1.w);
+          if (dist > TH_HIGH) continue;
+          n++;
+          unsigned long long key = make_key(dist, ck, i2);
+#pragma unroll
+          for (int k = 0; k < MK; k++) {  // sorted insertion, smallest first
+            const unsigned long long lo = key < best[k] ? key : best[k];
+            key = key < best[k] ? best[k] : key;
+            best[k] = lo;
+          }
+        }
+      }
+    }
+  }
+  ccnt[qi] = n;
+  const int nk = min(n, MK);
+  for (int k = 0; k < nk; k++) {
+    ckeys[qi * MK + k] = best[k];
+    cbins[qi * MK + k] = (signed char)rot_bin(LK[i].angle, CK[key_idx(best[k])].angle);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_motion_resolve(
+    CamDev cam, const float* __restrict__ Tcw, float th, int check_ori, const eao_keypoint_dev* __restrict__ kps,
+    const uint8_t* __restrict__ desc, const int* __restrict__ counts, int cap, const uint8_t* __restrict__ has_mp,
+    const float* __restrict__ mp_pos, const uint8_t* __restrict__ mp_desc, const float* __restrict__ scales,
+    const int* __restrict__ gstart, const int* __restrict__ gitems, const unsigned long long* __restrict__ ckeys,
+    const signed char* __restrict__ cbins, const int* __restrict__ ccnt, int* __restrict__ cur_match,
+    int* __restrict__ nmatches_out) {
   __shared__ int match[MAXK];
   __shared__ signed char bins[MAXK];
   __shared__ int hist[HISTO_LENGTH];
+  __shared__ unsigned long long kb[64 * MK];
+  __shared__ signed char bb[64 * MK];
+  __shared__ int nb[64];
   const int p = blockIdx.x, lane = threadIdx.x;
   const int ls = p, cs = p + 1;
   const int n_last = counts[ls], n_cur = counts[cs];
   const eao_keypoint_dev* LK = kps + (long long)ls * cap;
   const eao_keypoint_dev* CK = kps + (long long)cs * cap;
   const uint8_t* CD = desc + (long long)cs * cap * 32;
-  const uint8_t* HM = has_mp + (long long)ls * cap;
-  const float* MP = mp_pos + (long long)ls * cap * 3;
-  const uint8_t* MD = mp_desc + (long long)ls * cap * 32;
   const int* GS = gstart + (long long)cs * (GRID_CELLS + 1);
   const int* GI = gitems + (long long)cs * cap;
-  float T[16];
-  for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
   for (int i = lane; i < n_cur; i += 64) {
     match[i] = -1;
     bins[i] = -1;
   }
-  __syncthreads();
   int nmatches = 0;
-  for (int i = 0; i < n_last; i++) {
-    if (!HM[i]) continue;
-    float x3Dc[3];
-    transform_point(T, MP + 3 * i, x3Dc);
-    const float xc = x3Dc[0], yc = x3Dc[1];
-    const float invzc = (float)(1.0 / (double)x3Dc[2]);
-    if (invzc < 0) continue;
-    const float u = fadd(fmul(fmul(cam.fx, xc), invzc), cam.cx);
-    const float v = fadd(fmul(fmul(cam.fy, yc), invzc), cam.cy);
-    if (u < cam.minX || u > cam.maxX) continue;
-    if (v < cam.minY || v > cam.maxY) continue;
-    const int oct = LK[i].octave;
-    const float r = fmul(th, scales[oct]);
-    const Window w = window_cells(cam, u, v, r);
-    if (w.empty) continue;
-    const int minL = oct - 1, maxL = oct + 1;
-    const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
-    const uint8_t* d = MD + 32 * (long long)i;
-    unsigned long long best = KEY_NONE;
-    for (int ck = lane; ck < ncell; ck += 64) {
-      const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
-      const int cell = ix * GRID_ROWS + iy;
-      for (int q = GS[cell]; q < GS[cell + 1]; q++) {
-        const int i2 = GI[q];
-        const eao_keypoint_dev& kp = CK[i2];
-        if (kp.octave < minL) continue;
-        if (kp.octave > maxL) continue;
-        if (!(fabsf(fsub(kp.x, u)) < r && fabsf(fsub(kp.y, v)) < r)) continue;
-        if (match[i2] >= 0) continue;  // mvpMapPoints[i2] && Observations() > 0
-        const int dist = hamming256(d, CD + 32 * (long long)i2);
-        const unsigned long long key = make_key(dist, ck, i2);
-        best = key < best ? key : best;
+  for (int base = 0; base < n_last; base += 64) {
+    const int nq = min(64, n_last - base);
+    const long long q0 = (long long)p * cap + base;
+    const int myn = lane < nq ? ccnt[q0 + lane] : 0;
+    nb[lane] = myn;
+    __syncthreads();
+    for (int k = lane; k < nq * MK; k += 64) {
+      const int qq = k / MK, c = k - qq * MK;
+      if (c < min(nb[qq], MK)) {
+        kb[k] = ckeys[q0 * MK + k];
+        bb[k] = cbins[q0 * MK + k];
       }
-    }
-    best = wave_min_u64(best);
-    if (best != KEY_NONE && key_dist(best) <= TH_HIGH) {
-      const int i2 = key_idx(best);
-      if (lane == 0) {
-        match[i2] = i;
-        if (check_ori) bins[i2] = (signed char)rot_bin(LK[i].angle, CK[i2].angle);
-      }
-      nmatches++;
     }
     __syncthreads();
+    for (int j = 0; j < nq; j++) {
+      const int n = __builtin_amdgcn_readlane(myn, j);
+      if (n == 0) continue;
+      const int nk = min(n, MK);
+      const unsigned long long key = lane < nk ? kb[j * MK + lane] : KEY_NONE;
+      const bool free_ = lane < nk && match[key_idx(key)] < 0;
+      const uint64_t fm = ballot(free_);
+      int i2 = -1, bin = -1;
+      if (fm) {
+        const int c = __builtin_ctzll(fm);
+        i2 = __builtin_amdgcn_readlane(key_idx(key), c);
+        bin = bb[j * MK + c];
+      } else if (n > MK) {
+        // every stored candidate is taken: the full window scan (as the reference)
+        const int i = base + j;
+        float T[16];
+        for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
+        const MotionGeom g = motion_geom(cam, T, th, LK, has_mp + (long long)ls * cap,
+                                         mp_pos + (long long)ls * cap * 3, scales, i);
+        const Window w = window_cells(cam, g.u, g.v, g.r);
+        const int minL = g.oct - 1, maxL = g.oct + 1;
+        const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+        const uint8_t* d = mp_desc + ((long long)ls * cap + i) * 32;
+        unsigned long long best = KEY_NONE;
+        for (int ck = lane; ck < ncell; ck += 64) {
+          const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+          for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+            const int c2 = GI[q];
+            const eao_keypoint_dev& kp = CK[c2];
+            if (kp.octave < minL || kp.octave > maxL) continue;
+            if (!(fabsf(fsub(kp.x, g.u)) < g.r && fabsf(fsub(kp.y, g.v)) < g.r)) continue;
+            if (match[c2] >= 0) continue;
+            const unsigned long long k2 = make_key(hamming256(d, CD + 32 * (long long)c2), ck, c2);
+            best = k2 < best ? k2 : best;
+          }
+        }
+        best = wave_min_u64(best);
+        if (best != KEY_NONE && key_dist(best) <= TH_HIGH) {
+          i2 = key_idx(best);
+          bin = rot_bin(LK[i].angle, CK[i2].angle);
+        }
+      }
+      if (i2 >= 0) {
+        if (lane == 0) {
+          match[i2] = base + j;
+          bins[i2] = (signed char)bin;
+        }
+        nmatches++;
+      }
+      __syncthreads();
+    }
   }
   if (check_ori) {
     for (int b = lane; b < HISTO_LENGTH; b += 64) hist[b] = 0;
@@ -351,7 +473,7 @@ __global__ __launch_bounds__(256) void k_frustum(CamDev cam, const float* __rest
 // (relocalisation, Tracking.cc:2295,2309). One wave. Phase 1 is lane-parallel: each lane
 // projects its map points (no depth test, as :1501-1506), applies the distance gate and
 // PredictScale (clamped, Q13) and leaves (u, v, radius, level) in geo[]. Phase 2 walks the
-// map points in order with the first-wins assignment (Q17/Q18) like k_match_motion.
+// map points in order with the first-wins assignment (Q17/Q18) like k_motion_resolve.
 __global__ __launch_bounds__(64) void k_match_keyframe(
     CamDev cam, const float* __restrict__ Tg, float th, int orb_dist, int check_ori, int n_kf,
     const eao_keypoint_dev* __restrict__ KK, const uint8_t* __restrict__ valid,
@@ -670,15 +792,38 @@ int MatchEngine::init(int device, int mk, int mb) {
   EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16 * 2));
   EAO_HIP_CHECK(hipMalloc(&d_scales, sizeof(float) * 32));
   EAO_HIP_CHECK(hipMalloc(&d_geo, sizeof(float) * 4 * mk));
+  EAO_HIP_CHECK(hipMalloc(&d_ckeys, sizeof(unsigned long long) * MK * (size_t)mk * max_batch));
+  EAO_HIP_CHECK(hipMalloc(&d_cbins, (size_t)MK * mk * max_batch));
+  EAO_HIP_CHECK(hipMalloc(&d_ccnt, sizeof(int) * (size_t)mk * max_batch));
   return EAO_OK;
 }
 
 MatchEngine::~MatchEngine() {
   void* ptrs[] = {d_gstart, d_gitems, d_kps, d_desc, d_u8, d_f, d_f2, d_f3, d_f4,
-                  d_mdesc, d_i32, d_i32b, d_out, d_T, d_scales, d_geo};
+                  d_mdesc, d_i32, d_i32b, d_out, d_T, d_scales, d_geo, d_ckeys, d_cbins, d_ccnt};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
+}
+
+// the two phases of the motion-model search for pairs (p, p+1), p < nframes-1
+int MatchEngine::motion(const CamDev& cd, const float* d_T, float th, int check_ori, const eao_keypoint_dev* d_kps,
+                        const uint8_t* d_desc, const int* d_counts, int cap, const uint8_t* d_has,
+                        const float* d_pos, const uint8_t* d_mdesc_, const float* d_sc, int nframes, int* d_match,
+                        int* d_nm, hipStream_t s) {
+  const int np = nframes - 1;
+  if (np < 1) return EAO_OK;
+  if ((long long)np * cap > (long long)max_batch * max_kps) {
+    set_error("motion search: scratch too small");
+    return EAO_E_CAPACITY;
+  }
+  hipLaunchKernelGGL(k_motion_cand, dim3((cap + 255) / 256, np), dim3(256), 0, s, cd, d_T, th, d_kps, d_desc,
+                     d_counts, cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt);
+  EAO_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(k_motion_resolve, dim3(np), dim3(64), 0, s, cd, d_T, th, check_ori, d_kps, d_desc, d_counts,
+                     cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt, d_match, d_nm);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
 }
 
 int MatchEngine::build_grid(const CamDev& cam, const eao_keypoint_dev* kps, const int* counts,
@@ -772,9 +917,9 @@ int eao_match_motion(eao_matcher* m, const eao_camera* cam, const float* Tcw, fl
   const CamDev cd = make_cam(*cam);
   int rc = e.build_grid(cd, e.d_kps, e.d_i32, 0, K, 2, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_match_motion, dim3(1), dim3(64), 0, s, cd, e.d_T, th, check_ori, e.d_kps,
-                     e.d_desc, e.d_i32, K, e.d_u8, e.d_f, e.d_mdesc, e.d_scales, e.d_gstart,
-                     e.d_gitems, e.d_out, e.d_out + 2 * K);
+  rc = e.motion(cd, e.d_T, th, check_ori, e.d_kps, e.d_desc, e.d_i32, K, e.d_u8, e.d_f, e.d_mdesc, e.d_scales,
+                2, e.d_out, e.d_out + 2 * K, s);
+  if (rc) return rc;
   EAO_HIP_CHECK(hipGetLastError());
   int nm[2] = {0, 0};
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out + K, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
@@ -800,9 +945,9 @@ int eao_match_motion_batch_device(eao_matcher* m, const eao_camera* cam, int nfr
   const CamDev cd = make_cam(*cam);
   int rc = e.build_grid(cd, (const eao_keypoint_dev*)d_kps, d_counts, 0, cap, nframes, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_match_motion, dim3(nframes - 1), dim3(64), 0, s, cd, d_Tcw, th, check_ori,
-                     (const eao_keypoint_dev*)d_kps, d_desc, d_counts, cap, d_has_mp, d_mp_pos,
-                     d_mp_desc, e.d_scales, e.d_gstart, e.d_gitems, d_cur_match, d_nmatches);
+  rc = e.motion(cd, d_Tcw, th, check_ori, (const eao_keypoint_dev*)d_kps, d_desc, d_counts, cap, d_has_mp, d_mp_pos,
+                d_mp_desc, e.d_scales, nframes, d_cur_match, d_nmatches, s);
+  if (rc) return rc;
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }

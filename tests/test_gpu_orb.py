@@ -12,6 +12,8 @@ from tools import synth
 
 pytestmark = pytest.mark.gpu
 
+SC = orc.orb_params()["scale"]
+
 
 def _cmp_kps(g, o):
     assert len(g) == len(o), (len(g), len(o))
@@ -103,16 +105,49 @@ def _batch_extract(fr, nfeat, w, h):
 
 def test_batch_full_bench_stream_exact():
     """The bench's whole 405-frame batch in one launch group: every frame
-    bit-exact. A full batch keeps thousands of (frame, level) workgroups in
-    flight at once, which is what exposes cross-workgroup buffer overlap."""
-    fr, _ = synth.frame_stream(405)
+    bit-exact, then the 404 motion-model searches of the batch (two-phase
+    kernels) against the oracle pair by pair. A full batch keeps thousands of
+    workgroups in flight at once, which is what exposes cross-workgroup
+    buffer overlap."""
+    import torch
+    fr, poses = synth.frame_stream(405)
     n, hk, hd = _batch_extract(fr, 1000, 640, 480)
     bad = []
+    okps, odesc = [], []
     for t in range(len(fr)):
         ok, od = orc.extract(fr[t])
+        okps.append(ok)
+        odesc.append(od)
         if not (n[t] == len(ok) and np.array_equal(hk[t, :n[t]], ok) and np.array_equal(hd[t, :n[t]], od)):
             bad.append(t)
     assert not bad, "frames differing: %s" % bad[:20]
+    F, cap = len(fr), hk.shape[1]
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(9)
+    has = np.zeros((F, cap), np.uint8)
+    pos = np.zeros((F, cap, 3), np.float32)
+    for t in range(F):
+        has[t, :n[t]] = rng.random(n[t]) < 0.9
+        pos[t, :n[t]] = synth.backproject(poses[t], okps[t]["x"], okps[t]["y"])
+    kps = torch.from_numpy(hk.view(np.uint8).reshape(F, cap, 28)).to(dev)
+    desc = torch.from_numpy(hd).to(dev)
+    cnt = torch.from_numpy(n.astype(np.int32)).to(dev)
+    T = torch.from_numpy(np.stack(poses).astype(np.float32).reshape(F, 16)).to(dev)
+    d_has, d_pos = torch.from_numpy(has).to(dev), torch.from_numpy(pos).to(dev)
+    match = torch.full((F, cap), -1, dtype=torch.int32, device=dev)
+    nm = torch.zeros(F, dtype=torch.int32, device=dev)
+    ea.Matcher(max_kps=cap, max_batch=F).motion_batch_device(
+        ea.camera(), F, cap, T.data_ptr(), 15, 1, kps.data_ptr(), desc.data_ptr(), cnt.data_ptr(), d_has.data_ptr(),
+        d_pos.data_ptr(), desc.data_ptr(), SC, match.data_ptr(), nm.data_ptr(), None)
+    torch.cuda.synchronize()
+    hm, hn = match.cpu().numpy(), nm.cpu().numpy()
+    badm = []
+    for t in range(1, F):
+        no, mo = orc.match_motion(orc.cam(), poses[t], 15, 1, okps[t - 1], has[t - 1, :n[t - 1]],
+                                  pos[t - 1, :n[t - 1]], odesc[t - 1], okps[t], odesc[t], SC)
+        if not (hn[t] == no and np.array_equal(hm[t, :n[t]], mo)):
+            badm.append(t)
+    assert not badm, "pairs differing: %s" % badm[:20]
 
 
 def test_batch_1080p_4000_features_exact():
