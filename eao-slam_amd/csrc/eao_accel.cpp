@@ -158,4 +158,14 @@ int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out) {
   return EAO_OK;
 }
 
+int eao_color_to_gray_batch_device(const uint8_t* d_color, int nframes, int w, int h, int pitch, int channels,
+                                   int rgb, uint8_t* d_gray, int gray_pitch, int device, void* stream) {
+  if (!eao_device_ok(device)) {
+    set_error("no usable gfx950 device (the engine has no CPU fallback)");
+    return EAO_E_NODEVICE;
+  }
+  EAO_HIP_CHECK(hipSetDevice(device));
+  return color_to_gray(d_color, nframes, w, h, pitch, channels, rgb, d_gray, gray_pitch, (hipStream_t)stream);
+}
+
 }  // extern "C"

@@ -98,4 +98,8 @@ class OrbEngine {
   ~OrbEngine();
 };
 
+// cvtColor(CV_{RGB,BGR}[A]2GRAY) of a batch of HBM-resident frames (orb.hip)
+int color_to_gray(const uint8_t* d_src, int nframes, int w, int h, int spitch, int cn, int rgb, uint8_t* d_dst,
+                  int dpitch, hipStream_t s);
+
 }  // namespace eao

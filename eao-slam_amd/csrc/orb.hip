@@ -18,6 +18,8 @@
 // and -ffp-contract=off so every rounding matches the oracle.
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+
 #include <cstdlib>
 
 #include <algorithm>
@@ -386,6 +388,77 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
     }
     if (lane == 0) cell_cnt[f * ncells + ci] = n;
   }
+}
+
+// ---------------------------------------------------------------- frame input
+// cvtColor(..., CV_{RGB,BGR}[A]2GRAY) on 8-bit data (src/Tracking.cc:349-362), the
+// OpenCV 3.2 scalar RGB2Gray<uchar>: gray = (s0*c0 + s1*G2Y + s2*c2 + 2^13) >> 14
+// with (c0, c2) = (R2Y, B2Y) for the RGB codes and (B2Y, R2Y) for the BGR codes
+// (R2Y 4899, G2Y 9617, B2Y 1868). TUM3's Camera.RGB: 1 applies the RGB code to
+// imread's BGR bytes. One thread per 16 output pixels of a frame
+// (rows flattened): 16-byte stores, 16-byte loads when the rows allow it; HBM-bound.
+__global__ __launch_bounds__(256) void k_gray(const uint8_t* __restrict__ src, int w, int h, int spitch,
+                                              long long sstride, int cn, int c0, int c2,
+                                              uint8_t* __restrict__ dst, int dpitch, long long dstride,
+                                              int vec_ok) {
+  constexpr int G2Y = 9617, HALF = 1 << 13;
+  const int f = blockIdx.y, t = threadIdx.x;
+  const uint8_t* S = src + f * sstride;
+  uint8_t* D = dst + f * dstride;
+  if (vec_ok && w % 16 == 0 && spitch == w * cn && dpitch == w) {
+    // dense frame: the block's 256 x 16 pixels are one contiguous run of
+    // 256 * 16 * cn source bytes -- staged through LDS with coalesced 16-byte
+    // loads, converted, stored as 16-byte words
+    __shared__ uint4 stage[256 * 4];
+    const long long px0 = (long long)blockIdx.x * 4096, npx = (long long)w * h;
+    const int nv = cn * 256;  // 16-byte words of the run
+    const uint4* sv = (const uint4*)(S + px0 * cn);
+    const long long words_left = (npx - px0) * cn / 16;
+    for (int k = t; k < nv; k += 256)
+      if (k < words_left) stage[k] = sv[k];
+    __syncthreads();
+    if (px0 + 16 * t >= npx) return;
+    const uint32_t* in = (const uint32_t*)stage + t * 4 * cn;
+    auto byte = [&](int i) -> int { return (int)((in[i >> 2] >> (8 * (i & 3))) & 0xffu); };
+    uint32_t out[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int b = i * cn;
+      const int g = (byte(b) * c0 + byte(b + 1) * G2Y + byte(b + 2) * c2 + HALF) >> 14;
+      out[i >> 2] |= (uint32_t)g << (8 * (i & 3));
+    }
+    *(uint4*)(D + px0 + 16 * t) = make_uint4(out[0], out[1], out[2], out[3]);
+    return;
+  }
+  // general pitches / ragged widths: 16 pixels of one row per thread
+  const int chunks = (w + 15) >> 4;
+  const int idx = blockIdx.x * blockDim.x + t;
+  if (idx >= chunks * h) return;
+  const int y = idx / chunks, x0 = 16 * (idx - y * chunks);
+  const uint8_t* s = S + (long long)y * spitch + (long long)x0 * cn;
+  uint8_t* d = D + (long long)y * dpitch + x0;
+  for (int i = 0; i < 16 && x0 + i < w; i++) {
+    const uint8_t* q = s + i * cn;
+    d[i] = (uint8_t)((q[0] * c0 + q[1] * G2Y + q[2] * c2 + HALF) >> 14);
+  }
+}
+
+int color_to_gray(const uint8_t* d_src, int nframes, int w, int h, int spitch, int cn, int rgb, uint8_t* d_dst,
+                  int dpitch, hipStream_t s) {
+  if (nframes < 1 || w < 1 || h < 1 || (cn != 3 && cn != 4) || spitch < w * cn || dpitch < w) {
+    set_error("eao_color_to_gray_batch_device: bad arguments");
+    return EAO_E_ARG;
+  }
+  constexpr int R2Y = 4899, B2Y = 1868;
+  const int c0 = rgb ? R2Y : B2Y, c2 = rgb ? B2Y : R2Y;
+  const int vec_ok = ((uintptr_t)d_src % 16 == 0 && spitch % 16 == 0 && (uintptr_t)d_dst % 16 == 0 &&
+                      dpitch % 16 == 0) ? 1 : 0;
+  const int chunks = (w + 15) / 16;
+  dim3 g((unsigned)(((long long)chunks * h + 255) / 256), nframes);  // 4096 px per block (dense path)
+  hipLaunchKernelGGL(k_gray, g, dim3(256), 0, s, d_src, w, h, spitch, (long long)spitch * h, cn, c0, c2, d_dst,
+                     dpitch, (long long)dpitch * h, vec_ok);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
 }
 
 // ---------------------------------------------------------------- quadtree

@@ -153,6 +153,15 @@ class Orb:
               "eao_orb_extract_batch_device")
 
 
+def color_to_gray_batch_device(color_ptr, nframes, w, h, pitch, channels, rgb, gray_ptr, gray_pitch, device=0,
+                               stream=None):
+    """eao_color_to_gray_batch_device: cvtColor(CV_RGB2GRAY | CV_BGR2GRAY [A]) of HBM-resident frames."""
+    v = ctypes.c_void_p
+    check(lib().eao_color_to_gray_batch_device(v(color_ptr), nframes, w, h, pitch, channels, 1 if rgb else 0,
+                                               v(gray_ptr), gray_pitch, device, v(stream) if stream else None),
+          "eao_color_to_gray_batch_device")
+
+
 class Matcher:
     """ORBmatcher + Frame grid replacement (reference src/ORBmatcher.cc, src/Frame.cc)."""
 

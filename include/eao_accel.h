@@ -93,6 +93,15 @@ int eao_orb_stage_ms(eao_orb* h, float* ms, int n);
 /* debug taps for parity tests (device work, host results) */
 int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out /* concatenated levels */);
 
+/* --- frame input stage: cvtColor(mImGray, mImGray, CV_RGB2GRAY / CV_BGR2GRAY /
+   CV_RGBA2GRAY / CV_BGRA2GRAY) of Tracking::GrabImageMonocular (src/Tracking.cc:349-362),
+   OpenCV 3.2's fixed-point RGB2Gray<uchar>, for a batch of HBM-resident frames:
+   d_color [n][h][pitch] with `channels` (3 or 4) interleaved u8 per pixel; rgb = mbRGB
+   (Camera.RGB: 1 applies the RGB code to imread's BGR bytes); d_gray
+   [n][h][gray_pitch]. stream = HIP stream (NULL: the default stream). --- */
+int eao_color_to_gray_batch_device(const uint8_t* d_color, int nframes, int w, int h, int pitch, int channels,
+                                   int rgb, uint8_t* d_gray, int gray_pitch, int device, void* stream);
+
 /* --- matching: replaces ORBmatcher (src/ORBmatcher.cc) + Frame grid ---------- */
 typedef struct {
   int32_t img_w, img_h; /* Frame::mnMinX=0..mnMaxX=w, mnMinY=0..mnMaxY=h (k1 == 0) */

@@ -43,6 +43,8 @@ int orc_orb_level_candidates(const uint8_t* level, int w, int h, int iniTh, int 
 /* 7x7 sigma=2 REFLECT_101 blur (8U fixed-point path) */
 int orc_gaussian_blur7(const uint8_t* src, int w, int h, uint8_t* dst);
 float orc_fast_atan2(float y, float x);
+/* cvtColor(CV_{RGB,BGR}[A]2GRAY) (OpenCV 3.2 RGB2Gray<uchar>); rgb: the RGB codes */
+int orc_color_to_gray(const uint8_t* src, int w, int h, int pitch, int cn, int rgb, uint8_t* dst);
 /* full ORBextractor::operator() */
 int orc_orb_extract(const uint8_t* img, int w, int h, int nfeatures, float scale_factor,
                     int nlevels, int iniTh, int minTh,

@@ -589,6 +589,30 @@ using namespace orc;
 
 extern "C" {
 
+// cv::cvtColor(CV_{RGB,BGR}[A]2GRAY), OpenCV 3.2 imgproc/color.cpp RGB2Gray<uchar>:
+// three 256-entry tables (src[0] * coeffs[blueIdx ^ 2], src[1] * G2Y, src[2] *
+// coeffs[blueIdx] + 2^13) summed and shifted by yuv_shift = 14. The RGB codes
+// have blueIdx 2, the BGR codes 0. Called by Tracking::GrabImageMonocular
+// (src/Tracking.cc:349-362).
+int orc_color_to_gray(const uint8_t* src, int w, int h, int pitch, int cn, int rgb, uint8_t* dst) {
+  const int yuv_shift = 14, R2Y = 4899, G2Y = 9617, B2Y = 1868;
+  const int coeffs[3] = {R2Y, G2Y, B2Y};
+  const int blueIdx = rgb ? 2 : 0;
+  int tab[768];
+  int b = 0, g = 0, r = 1 << (yuv_shift - 1);
+  const int db = coeffs[blueIdx ^ 2], dg = coeffs[1], dr = coeffs[blueIdx];
+  for (int i = 0; i < 256; i++, b += db, g += dg, r += dr) {
+    tab[i] = b;
+    tab[i + 256] = g;
+    tab[i + 512] = r;
+  }
+  for (int y = 0; y < h; y++) {
+    const uint8_t* s = src + (size_t)y * pitch;
+    for (int x = 0; x < w; x++, s += cn) dst[(size_t)y * w + x] = (uint8_t)((tab[s[0]] + tab[s[1] + 256] + tab[s[2] + 512]) >> yuv_shift);
+  }
+  return 0;
+}
+
 int orc_orb_params(int nfeatures, float scale_factor, int nlevels, float* scale, float* inv_scale,
                    float* sigma2, float* inv_sigma2, int* feats_per_level, int* umax16) {
   Params p = make_params(nfeatures, scale_factor, nlevels, 20, 7);

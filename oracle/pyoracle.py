@@ -95,6 +95,15 @@ def extract(img, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7):
     return kps[:n.value].copy(), desc[:n.value].copy()
 
 
+def color_to_gray(img, rgb=True):
+    """cvtColor(CV_RGB2GRAY / CV_BGR2GRAY [A]) of an (h, w, 3|4) u8 image."""
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w, cn = img.shape
+    out = np.zeros((h, w), np.uint8)
+    lib().orc_color_to_gray(P(img), w, h, w * cn, cn, 1 if rgb else 0, P(out))
+    return out
+
+
 def blur7(img):
     img = np.ascontiguousarray(img, np.uint8)
     out = np.zeros_like(img)

@@ -158,3 +158,43 @@ def test_batch_1080p_4000_features_exact():
     for t in range(len(fr)):
         ok, od = orc.extract(fr[t], 4000)
         assert n[t] == len(ok) and np.array_equal(hk[t, :n[t]], ok) and np.array_equal(hd[t, :n[t]], od), t
+
+
+@pytest.mark.parametrize("w,h,cn,rgb", [(640, 480, 3, True), (640, 480, 3, False), (533, 37, 4, True), (640, 7, 4, False),
+                                        (61, 9, 3, True)])
+def test_color_to_gray_batch(w, h, cn, rgb):
+    """Frame input stage (src/Tracking.cc:349-362) vs the oracle, vector and
+    ragged-width scalar paths."""
+    import torch
+    rng = np.random.default_rng(w + cn)
+    col = rng.integers(0, 256, (3, h, w, cn), dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    d_col = torch.from_numpy(col).to(dev)
+    d_g = torch.zeros((3, h, w), dtype=torch.uint8, device=dev)
+    ea.color_to_gray_batch_device(d_col.data_ptr(), 3, w, h, w * cn, cn, rgb, d_g.data_ptr(), w)
+    torch.cuda.synchronize()
+    g = d_g.cpu().numpy()
+    for f in range(3):
+        assert np.array_equal(g[f], orc.color_to_gray(col[f], rgb)), f
+
+
+def test_color_frames_through_extraction():
+    """Colour frames -> GPU gray -> batched extraction equals the oracle's
+    cvtColor + ORBextractor on the same frames."""
+    import torch
+    fr, _ = synth.frame_stream(3)
+    rng = np.random.default_rng(4)
+    col = np.stack([np.stack([np.clip(f.astype(np.int16) + rng.integers(-6, 7, f.shape), 0, 255).astype(np.uint8)
+                              for _ in range(3)], -1) for f in fr])
+    dev = torch.device("cuda", 0)
+    d_col = torch.from_numpy(col).to(dev)
+    d_g = torch.zeros((3, 480, 640), dtype=torch.uint8, device=dev)
+    ea.color_to_gray_batch_device(d_col.data_ptr(), 3, 640, 480, 640 * 3, 3, True, d_g.data_ptr(), 640)
+    torch.cuda.synchronize()
+    gray = list(d_g.cpu().numpy())
+    n, hk, hd = _batch_extract(gray, 1000, 640, 480)
+    for t in range(3):
+        og = orc.color_to_gray(col[t], True)
+        assert np.array_equal(gray[t], og)
+        ok, od = orc.extract(og)
+        assert n[t] == len(ok) and np.array_equal(hk[t, :n[t]], ok) and np.array_equal(hd[t, :n[t]], od)

@@ -239,3 +239,19 @@ def test_iforest_matches_libstdcxx_forest(kat, n):
     pts[: n // 20] += rng.uniform(-0.5, 0.5, (n // 20, 3)).astype(np.float32)
     ref = run_kat(kat, "iforest", n, 50, 12345, n // 2, dtype=np.float64, stdin=pts.tobytes())
     assert np.array_equal(orc.iforest(pts), ref)
+
+
+@pytest.mark.parametrize("cn,rgb", [(3, True), (3, False), (4, True), (4, False)])
+def test_color_to_gray_fixed_point(cn, rgb):
+    """cvtColor(CV_{RGB,BGR}[A]2GRAY), OpenCV 3.2 RGB2Gray<uchar>: the oracle's
+    table form equals the closed fixed-point formula, and the TUM3 case
+    (Camera.RGB: 1 on BGR bytes, Q20) weights the first byte by R2Y."""
+    rng = np.random.default_rng(cn * 2 + rgb)
+    img = rng.integers(0, 256, (37, 53, cn), dtype=np.uint8)
+    g = orc.color_to_gray(img, rgb)
+    c0, c2 = (4899, 1868) if rgb else (1868, 4899)
+    ref = ((img[..., 0].astype(np.int64) * c0 + img[..., 1].astype(np.int64) * 9617 +
+            img[..., 2].astype(np.int64) * c2 + 8192) >> 14).astype(np.uint8)
+    assert np.array_equal(g, ref)
+    white = np.full((2, 2, cn), 255, np.uint8)
+    assert (orc.color_to_gray(white, rgb) == 255).all() and (orc.color_to_gray(0 * white, rgb) == 0).all()
