@@ -327,8 +327,13 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
     const bool okl = x - 1 >= lo, okr = x + 1 < hi;
     auto row = [&](int r, int& Sv, int& Lv, int& Rv) {
       int sv = 0;
+#ifdef EAO_FAST_ABL_SWEEP
+      if (inx && r < y1) {
+        sv = roi[r * RS + x] >> 2;
+#else
       if (inx && r < y1) {
         sv = fast_strength_c<RS>(roi + r * RS + x);
+#endif
         sv = sv > tlo ? sv : 0;
       }
       const int l = wave_from_left(sv), rr = wave_from_right(sv);
@@ -353,39 +358,52 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
     }
   }
   __syncthreads();
+#ifdef EAO_FAST_ABL_EMIT
+  return;
+#endif
   for (int cc = wv; cc < B.ncells; cc += 4) {
     const int ci = B.cell_begin + cc;
     const CellDev c = cells[ci];
     const int wx0 = bnd[cc], ww = bnd[cc + 1] - wx0;
     uint32_t* out = cand + f * cand_stride + c.slot;
-    int n = 0, m = 0;
-    for (int r = y0; r < y1; r++)
-      for (int c0 = 0; c0 < ww; c0 += 64) {
-        const int x = wx0 + c0 + lane;
-        const int v = c0 + lane < ww ? F[r * RS + x] : 0;
-        const bool hi_ = v > thi;
-        const uint64_t mh = ballot(hi_);
-        if (hi_) {
-          const int pos = n + popc64(mh & lanes_below());
-          // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
-          if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
-        }
-        n += popc64(mh);
-        m += popc64(ballot(v > 0));
-      }
-    if (n == 0 && m > 0) {  // ORBextractor.cc:812 -- retry with minTh only when empty
-      for (int r = y0; r < y1; r++)
-        for (int c0 = 0; c0 < ww; c0 += 64) {
-          const int x = wx0 + c0 + lane;
-          const int v = c0 + lane < ww ? F[r * RS + x] : 0;
-          const uint64_t ml = ballot(v > 0);
-          if (v > 0) {
-            const int pos = n + popc64(ml & lanes_below());
+    // emit the pixels with F > th row-major; two rows per ballot when the
+    // window is <= 32 wide (lanes 0-31 row r, 32-63 row r+1: ballot order is
+    // still row-major)
+    auto emit = [&](int th) -> int {
+      int n = 0;
+      if (ww <= 32) {
+        const int half = lane >> 5, cx = lane & 31;
+        for (int r0 = y0; r0 < y1; r0 += 2) {
+          const int r = r0 + half;
+          const int x = wx0 + cx;
+          const int v = (cx < ww && r < y1) ? F[r * RS + x] : 0;
+          const bool k = v > th;
+          const uint64_t mk = ballot(k);
+          if (k) {
+            const int pos = n + popc64(mk & lanes_below());
+            // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
             if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
           }
-          n += popc64(ml);
+          n += popc64(mk);
         }
-    }
+      } else {
+        for (int r = y0; r < y1; r++)
+          for (int c0 = 0; c0 < ww; c0 += 64) {
+            const int x = wx0 + c0 + lane;
+            const int v = c0 + lane < ww ? F[r * RS + x] : 0;
+            const bool k = v > th;
+            const uint64_t mk = ballot(k);
+            if (k) {
+              const int pos = n + popc64(mk & lanes_below());
+              if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
+            }
+            n += popc64(mk);
+          }
+      }
+      return n;
+    };
+    int n = emit(thi);
+    if (n == 0) n = emit(0);  // ORBextractor.cc:812 -- retry with minTh only when empty (F > 0 <=> kept at minTh)
     if (lane == 0) cell_cnt[f * ncells + ci] = n;
   }
 }
