@@ -246,6 +246,55 @@ __device__ __forceinline__ int fast_strength_c(const uint8_t* p) {
   return max(0, max(v - A, B - v));
 }
 
+// gfx950 packed 3-input f16 minimum / maximum (two pixels per instruction)
+__device__ __forceinline__ uint32_t pk_min3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_minimum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_pk_maximum3_f16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// fast_strength_c for the two vertically adjacent pixels p (low half) and
+// p + RS (high half) at once. A ring byte b is carried as the f16 1024 + b
+// (bits 0x6400 | b: a normal number, exact), so f16 minimum / maximum order
+// the bytes exactly and the 3- then 9-wide arc windows run on both rows per
+// instruction. The arc bounds A, B come out as 0x6400 | value, so
+// S = max(0, v - A, B - v) is taken on their low bytes as integers.
+// Returns S(row) | S(row + 1) << 16.
+template <int RS>
+__device__ __forceinline__ uint32_t fast_strength_pair(const uint8_t* p) {
+  constexpr int off[16] = {3 * RS,  3 * RS + 1,  2 * RS + 2,  RS + 3,  3,  -RS + 3,  -2 * RS + 2,  -3 * RS + 1,
+                           -3 * RS, -3 * RS - 1, -2 * RS - 2, -RS - 3, -3, RS - 3,   2 * RS - 2,  3 * RS - 1};
+  constexpr uint32_t BIAS = 0x64006400u;
+  uint32_t q[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) q[k] = ((uint32_t)p[off[k]] | ((uint32_t)p[off[k] + RS] << 16)) | BIAS;
+  uint32_t mn3[16], mx3[16];
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    mn3[k] = pk_min3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
+    mx3[k] = pk_max3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
+  }
+  uint32_t A = 0x64ff64ffu, B = BIAS;  // 1024 + 255, 1024 + 0
+#pragma unroll
+  for (int k = 0; k < 16; k += 2) {
+    const uint32_t a0 = pk_max3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
+    const uint32_t a1 = pk_max3(mx3[k + 1], mx3[(k + 4) & 15], mx3[(k + 7) & 15]);
+    const uint32_t b0 = pk_min3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
+    const uint32_t b1 = pk_min3(mn3[k + 1], mn3[(k + 4) & 15], mn3[(k + 7) & 15]);
+    A = pk_min3(A, a0, a1);
+    B = pk_max3(B, b0, b1);
+  }
+  const int v0 = p[0], v1 = p[RS];
+  const int s0 = max(0, max(v0 - (int)(A & 0xff), (int)(B & 0xff) - v0));
+  const int s1 = max(0, max(v1 - (int)((A >> 16) & 0xff), (int)((B >> 16) & 0xff) - v1));
+  return (uint32_t)s0 | ((uint32_t)s1 << 16);
+}
+
 // ROI row stride of k_fast_band (bands are <= 512 px wide, + 16-byte alignment slack)
 constexpr int FAST_RS = 544;
 
@@ -325,28 +374,29 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
       hi = bnd[q + 1];
     }
     const bool okl = x - 1 >= lo, okr = x + 1 < hi;
-    auto row = [&](int r, int& Sv, int& Lv, int& Rv) {
-      int sv = 0;
-#ifdef EAO_FAST_ABL_SWEEP
-      if (inx && r < y1) {
-        sv = roi[r * RS + x] >> 2;
-#else
-      if (inx && r < y1) {
-        sv = fast_strength_c<RS>(roi + r * RS + x);
-#endif
-        sv = sv > tlo ? sv : 0;
-      }
-      const int l = wave_from_left(sv), rr = wave_from_right(sv);
-      Sv = sv;
-      Lv = okl ? l : 0;
-      Rv = okr ? rr : 0;
+    // strengths of rows a and a + 1 of this column (one packed evaluation),
+    // thresholded at minTh (rows >= y1 read as 0), with the in-window left /
+    // right neighbours. Row a + 1 = y1 reads one ROI row past the band, which
+    // is still inside the LDS allocation (the F area) and is masked.
+    auto pair = [&](int a, int (&Sv)[2], int (&Lv)[2], int (&Rv)[2]) {
+      uint32_t sp = 0;
+      if (inx && a < y1) sp = fast_strength_pair<RS>(roi + a * RS + x);
+      int s0 = (int)(sp & 0xffffu), s1 = (int)(sp >> 16);
+      s0 = s0 > tlo ? s0 : 0;
+      s1 = (s1 > tlo && a + 1 < y1) ? s1 : 0;
+      const int l0 = wave_from_left(s0), r0 = wave_from_right(s0);
+      const int l1 = wave_from_left(s1), r1 = wave_from_right(s1);
+      Sv[0] = s0;
+      Sv[1] = s1;
+      Lv[0] = okl ? l0 : 0;
+      Lv[1] = okl ? l1 : 0;
+      Rv[0] = okr ? r0 : 0;
+      Rv[1] = okr ? r1 : 0;
     };
-    int Sc, Lc, Rc;
-    row(y0, Sc, Lc, Rc);
+    int Sc = 0, Lc = 0, Rc = 0;
     int mp = 0;  // neighbour-row max of row r-1 (row y0-1 is outside every window)
-    for (int r = y0; r < y1; r++) {
-      int Sn, Ln, Rn;
-      row(r + 1, Sn, Ln, Rn);
+    // finalise row r (held in Sc/Lc/Rc) once row r + 1 is known
+    auto fin = [&](int r, int Sn, int Ln, int Rn) {
       const int mn = max(max(Ln, Sn), Rn);
       const int M = max(max(mp, mn), max(Lc, Rc));
       const bool keep = Sc > tlo && Sc >= 2 && (M <= tlo || Sc > M);
@@ -355,6 +405,19 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
       Sc = Sn;
       Lc = Ln;
       Rc = Rn;
+    };
+    if (y0 < y1) {
+      int S2[2], L2[2], R2[2];
+      pair(y0, S2, L2, R2);
+      Sc = S2[0];
+      Lc = L2[0];
+      Rc = R2[0];
+      fin(y0, S2[1], L2[1], R2[1]);
+      for (int a = y0 + 2; a <= y1; a += 2) {
+        pair(a, S2, L2, R2);
+        fin(a - 1, S2[0], L2[0], R2[0]);
+        if (a < y1) fin(a, S2[1], L2[1], R2[1]);
+      }
     }
   }
   __syncthreads();
