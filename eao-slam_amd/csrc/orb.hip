@@ -693,29 +693,45 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
     const int mx = q.x0 + hx, my = q.y0 + hy;
     const uint32_t* src = bufs[q.buf] + q.beg;
     uint32_t* dst = bufs[q.buf ^ 1] + q.beg;
-    int cnt4[4] = {0, 0, 0, 0};
-    for (int c0 = 0; c0 < q.cnt; c0 += 64) {
-      const int idx = c0 + lane;
-      const int ch = idx < q.cnt ? child_of(src[idx], mx, my) : 4;
+    // keys are read in groups of RK * 64 with all RK loads in flight
+    // together; a node of <= RK * 64 keys keeps them in registers for the
+    // scatter pass, larger nodes read each group again
+    constexpr int RK = 8;
+    uint32_t kr[RK];
+    int chr[RK];
+    auto load = [&](int base) {
 #pragma unroll
-      for (int c = 0; c < 4; c++) cnt4[c] += popc64(ballot(ch == c));
+      for (int j = 0; j < RK; j++) {
+        const int idx = base + 64 * j + lane;
+        kr[j] = idx < q.cnt ? src[idx] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < RK; j++) chr[j] = base + 64 * j + lane < q.cnt ? child_of(kr[j], mx, my) : 4;
+    };
+    int cnt4[4] = {0, 0, 0, 0};
+    for (int base = 0; base < q.cnt; base += 64 * RK) {
+      load(base);
+#pragma unroll
+      for (int j = 0; j < RK; j++)
+        if (base + 64 * j < q.cnt) {
+#pragma unroll
+          for (int c = 0; c < 4; c++) cnt4[c] += popc64(ballot(chr[j] == c));
+        }
     }
     int off4[4] = {0, cnt4[0], cnt4[0] + cnt4[1], cnt4[0] + cnt4[1] + cnt4[2]};
     int run4[4] = {0, 0, 0, 0};
-    for (int c0 = 0; c0 < q.cnt; c0 += 64) {
-      const int idx = c0 + lane;
-      uint32_t k = 0;
-      int ch = 4;
-      if (idx < q.cnt) {
-        k = src[idx];
-        ch = child_of(k, mx, my);
-      }
+    for (int base = 0; base < q.cnt; base += 64 * RK) {
+      if (q.cnt > 64 * RK) load(base);
 #pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint64_t m = ballot(ch == c);
-        if (ch == c) dst[off4[c] + run4[c] + popc64(m & lanes_below())] = k;
-        run4[c] += popc64(m);
-      }
+      for (int j = 0; j < RK; j++)
+        if (base + 64 * j < q.cnt) {
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const uint64_t m = ballot(chr[j] == c);
+            if (chr[j] == c) dst[off4[c] + run4[c] + popc64(m & lanes_below())] = kr[j];
+            run4[c] += popc64(m);
+          }
+        }
     }
     const int16_t rx0[4] = {q.x0, (int16_t)mx, q.x0, (int16_t)mx};
     const int16_t ry0[4] = {q.y0, q.y0, (int16_t)my, (int16_t)my};
@@ -787,12 +803,19 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
     nToExpand = 0;
     nvcur = 0;
     const int end = QOS;
-    for (int i = head; i < end; i++) {
-      const int s = S.order[i];
-      if (s < 0) continue;
-      if (S.node[s].nomore) continue;
-      divide(s);
-      if (overflow) break;
+    // walk the list in order, 64 positions at a time: the nodes to divide
+    // are found by ballot (divide only writes positions < head and its own,
+    // so the flags read for later positions of the chunk stay valid)
+    for (int c0 = head; c0 < end && !overflow; c0 += 64) {
+      const int i = c0 + lane;
+      const int s = i < end ? (int)S.order[i] : -1;
+      uint64_t m = ballot(s >= 0 && !S.node[s >= 0 ? s : 0].nomore);
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        divide(__builtin_amdgcn_readlane(s, b));
+        if (overflow) break;
+      }
     }
     compact();
     if (alive >= N || alive == prevSize) {
@@ -847,26 +870,30 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
       }
     }
   }
-  // ---- retain the best keypoint per node, in list order
+  // ---- retain the best keypoint per node (largest score, first in the
+  // node's key order on ties), in list order: one node per lane, 64 nodes
+  // at a time, outputs placed by ballot prefix (final nodes hold few keys)
   int outn = 0;
-  for (int i = head; i < QOS; i++) {
-    const int s = S.order[i];
-    if (s < 0) continue;
-    const QNode q = S.node[s];
-    const uint32_t* src = bufs[q.buf] + q.beg;
-    int best_s = -1, best_i = 0x7fffffff;
-    for (int idx = lane; idx < q.cnt; idx += 64) {
-      const int sc = kp_s(src[idx]);
-      if (sc > best_s) {
-        best_s = sc;
-        best_i = idx;
+  for (int c0 = head; c0 < QOS; c0 += 64) {
+    const int i = c0 + lane;
+    const int s = i < QOS ? S.order[i] : -1;
+    uint32_t bk = 0;
+    if (s >= 0) {
+      const int cnt = S.node[s].cnt;
+      const uint32_t* src = bufs[S.node[s].buf] + S.node[s].beg;
+      int best_s = -1;
+      for (int idx = 0; idx < cnt; idx++) {
+        const uint32_t k = src[idx];
+        if (kp_s(k) > best_s) {
+          best_s = kp_s(k);
+          bk = k;
+        }
       }
     }
-    const int mx = wave_max_int(best_s);
-    const int cand_i = best_s == mx ? best_i : 0x7fffffff;
-    const int bi = wave_min_int(cand_i);
-    if (lane == 0 && outn < L.sel_cap) S_out[outn] = src[bi];
-    outn++;
+    const uint64_t m = ballot(s >= 0);
+    const int p = outn + popc64(m & lanes_below());
+    if (s >= 0 && p < L.sel_cap) S_out[p] = bk;
+    outn += popc64(m);
   }
   if (lane == 0) sel_cnt[f * nlevels + l] = overflow ? -1 : min(outn, L.sel_cap);
 }
