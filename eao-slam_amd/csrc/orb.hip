@@ -923,21 +923,23 @@ __device__ float fast_atan2(float y, float x) {
 }
 
 // ---------------------------------------------------------------- blur
+constexpr int BLUR_TH = 32;  // output rows per blur tile
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level, the clone
 // ORBextractor::operator() blurs before computeDescriptors (:1085-1086): 8U
 // fixed point, separable (exact in integers): horizontal sums of 8-bit
 // pixels x 8-bit taps stay below 2^16, then (sum_v + 2^15) >> 16, saturated.
-// One workgroup per 64 x 16 output tile.
+// One workgroup per 64 x BLUR_TH output tile (BLUR_TH + 6 staged rows).
 __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, int fpitch,
                                               long long fstride, const uint8_t* __restrict__ pyr,
                                               long long pstride, const LevelDev* __restrict__ levels,
                                               const BlurTile* __restrict__ tiles,
                                               const int* __restrict__ gk, uint8_t* __restrict__ blur,
                                               long long bstride) {
-  // in: 22 rows x 72 cols (x0-4 .. x0+67), word aligned; hs: horizontal sums
-  // (< 2^16) packed two per word, 22 rows x 64 cols
-  __shared__ uint32_t in[22][18];
-  __shared__ uint32_t hs[22][32];
+  // in: BLUR_TH+6 rows x 72 cols (x0-4 .. x0+67), word aligned; hs: horizontal
+  // sums (< 2^16) packed two per word, BLUR_TH+6 rows x 64 cols
+  constexpr int NR = BLUR_TH + 6;
+  __shared__ uint32_t in[NR][18];
+  __shared__ uint32_t hs[NR][32];
   const BlurTile T = tiles[blockIdx.x];
   const int f = blockIdx.y, t = threadIdx.x;
   const LevelDev& L = levels[T.level];
@@ -950,15 +952,15 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
     img = pyr + f * pstride + L.plane_off;
     pitch = L.pitch;
   }
-  const bool interior = T.x0 >= 4 && T.x0 + 68 <= L.w && T.y0 >= 3 && T.y0 + 19 <= L.h && (pitch & 3) == 0;
+  const bool interior = T.x0 >= 4 && T.x0 + 68 <= L.w && T.y0 >= 3 && T.y0 + BLUR_TH + 3 <= L.h && (pitch & 3) == 0;
   if (interior) {
-    for (int i = t; i < 22 * 18; i += 256) {
+    for (int i = t; i < NR * 18; i += 256) {
       const int r = i / 18, c = i - r * 18;
       in[r][c] = *(const uint32_t*)(img + (long long)(T.y0 - 3 + r) * pitch + T.x0 - 4 + 4 * c);
     }
   } else {
     uint8_t* inb = (uint8_t*)&in[0][0];
-    for (int i = t; i < 22 * 72; i += 256) {
+    for (int i = t; i < NR * 72; i += 256) {
       const int r = i / 72, c = i - r * 72;
       int yy = T.y0 - 3 + r, xx = T.x0 - 4 + c;
       // REFLECT_101 on the isolated level (gfedcb|abcdefgh|gfedcba)
@@ -975,7 +977,7 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
   for (int i = 0; i < 7; i++) k[i] = gk[i];
   // horizontal: item (row, group of 4 columns): columns 4g..4g+3 use input
   // bytes 4g+1 .. 4g+10 (input column 0 is x0-4)
-  for (int i = t; i < 22 * 16; i += 256) {
+  for (int i = t; i < NR * 16; i += 256) {
     const int r = i >> 4, g = i & 15;
     const uint32_t w0 = in[r][g], w1 = in[r][g + 1], w2 = in[r][g + 2];
     int px[12];
@@ -997,27 +999,29 @@ __global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames
     hs[r][2 * g + 1] = h[2] | (h[3] << 16);
   }
   __syncthreads();
-  // vertical: thread -> (row, 4 columns)
-  const int r = t >> 4, g = t & 15;
-  const int x = T.x0 + 4 * g, y = T.y0 + r;
-  if (y >= L.h || x >= L.w) return;
-  uint32_t acc[4] = {0, 0, 0, 0};
+  // vertical: item -> (row, 4 columns)
+  for (int it = t; it < BLUR_TH * 16; it += 256) {
+    const int r = it >> 4, g = it & 15;
+    const int x = T.x0 + 4 * g, y = T.y0 + r;
+    if (y >= L.h || x >= L.w) continue;
+    uint32_t acc[4] = {0, 0, 0, 0};
 #pragma unroll
-  for (int j = 0; j < 7; j++) {
-    const uint32_t a0 = hs[r + j][2 * g], a1 = hs[r + j][2 * g + 1];
-    acc[0] += (uint32_t)k[j] * (a0 & 0xffffu);
-    acc[1] += (uint32_t)k[j] * (a0 >> 16);
-    acc[2] += (uint32_t)k[j] * (a1 & 0xffffu);
-    acc[3] += (uint32_t)k[j] * (a1 >> 16);
-  }
-  uint32_t ow = 0;
+    for (int j = 0; j < 7; j++) {
+      const uint32_t a0 = hs[r + j][2 * g], a1 = hs[r + j][2 * g + 1];
+      acc[0] += (uint32_t)k[j] * (a0 & 0xffffu);
+      acc[1] += (uint32_t)k[j] * (a0 >> 16);
+      acc[2] += (uint32_t)k[j] * (a1 & 0xffffu);
+      acc[3] += (uint32_t)k[j] * (a1 >> 16);
+    }
+    uint32_t ow = 0;
 #pragma unroll
-  for (int o = 0; o < 4; o++) ow |= min((acc[o] + (1u << 15)) >> 16, 255u) << (8 * o);
-  uint8_t* out = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
-  if (x + 4 <= L.w) {
-    *(uint32_t*)out = ow;  // pitch and x are multiples of 4
-  } else {
-    for (int o = 0; o < 4 && x + o < L.w; o++) out[o] = (uint8_t)(ow >> (8 * o));
+    for (int o = 0; o < 4; o++) ow |= min((acc[o] + (1u << 15)) >> 16, 255u) << (8 * o);
+    uint8_t* out = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
+    if (x + 4 <= L.w) {
+      *(uint32_t*)out = ow;  // pitch and x are multiples of 4
+    } else {
+      for (int o = 0; o < 4 && x + o < L.w; o++) out[o] = (uint8_t)(ow >> (8 * o));
+    }
   }
 }
 
@@ -1334,7 +1338,7 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
     for (int l = 0; l < nl; l++) {
       LevelDev& L = levels[l];
       L.blur_off = l == 0 ? 0 : l0 + L.plane_off;
-      for (int y = 0; y < L.h; y += 16)
+      for (int y = 0; y < L.h; y += BLUR_TH)
         for (int x = 0; x < L.w; x += 64) btiles.push_back(BlurTile{(int16_t)l, 0, (int16_t)x, (int16_t)y});
     }
     blur_bytes = (l0 + poff + 255) & ~255LL;
