@@ -923,7 +923,7 @@ __device__ float fast_atan2(float y, float x) {
 }
 
 // ---------------------------------------------------------------- blur
-constexpr int BLUR_TH = 32;  // output rows per blur tile
+constexpr int BLUR_TH = 64;  // output rows per blur tile
 // GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level, the clone
 // ORBextractor::operator() blurs before computeDescriptors (:1085-1086): 8U
 // fixed point, separable (exact in integers): horizontal sums of 8-bit
