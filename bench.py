@@ -102,6 +102,26 @@ class Stream:
         self.n = nframes
 
 
+
+def pmc_traffic(kernel, frames):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
+    (FETCH_SIZE and WRITE_SIZE in separate runs of tools/pmc_extract.py over the same
+    405-frame stream; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note).
+    A counter run cannot sit inside the timed region, so this is the profiled figure
+    for the same launch shape; None when the summaries are absent or for another size."""
+    if frames != 405:
+        return None
+    tot = 0.0
+    for f in ("r01_pmc_fetch_final.txt", "r01_pmc_write_final.txt"):
+        p = os.path.join(ROOT, "profiles", f)
+        if not os.path.exists(p):
+            return None
+        hit = [l.split() for l in open(p) if l.split()[:1] == ["eao::" + kernel.split()[0]]]
+        if not hit:
+            return None
+        tot += float(hit[0][-1])
+    return tot
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -278,7 +298,7 @@ def main():
     names = stage_names()
     dom = int(np.argmax(stage))
     dom_name = names[dom]
-    kernels = {"pyramid": "k_resize (x7)", "fast": "k_fast", "distribute": "k_distribute", "blur": "k_blur",
+    kernels = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute", "blur": "k_blur",
                "describe": "k_describe"}
 
     result = None
@@ -307,7 +327,8 @@ def main():
                                    "%d ORB features, 8 levels, assoc flag EAO: iForest + object lines + yaw sampling)" % (F, NFEAT),
                        "frames_per_step": F, "features": NFEAT, "levels": NLEV, "parallelism": "frames%d" % world},
             "roofline": {"bound": "hbm", "kernel": kernels[dom_name], "achieved": ach, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": None,
+                         "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
+                         "traffic": pmc_traffic(kernels[dom_name], F),
                          "algorithmic_bytes_per_launch": dom_bytes * F,
                          "avg_launch_ms": float(stage[dom])},
             "stages_ms_per_step": {n: float(v) for n, v in zip(names, stage)},
