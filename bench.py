@@ -1,39 +1,52 @@
 """bench.py -- frames/s of the EAO-SLAM hot path (ORB extract + motion-model
-match + EAO ensemble association) on a synthetic TUM-fr3-shaped 640x480 stream.
+match + EAO ensemble association) on TUM-fr3-shaped 640x480 streams.
 
-Workload (BASELINE.json configs[1], SURVEY.md §8d input 2): "mono_tum EAO
-fr3_long_office 640x480, 1xMI355X".  One *step* is one pass of the hot path
-over the whole 405-frame stream, everything resident in HBM before timing:
+Configs (BASELINE.json):
+  --config eao   (default) configs[1] "mono_tum EAO fr3_long_office 640x480, 1xMI355X":
+                 the demo list's 405 frames (rgb_seq_pose.txt), association flag EAO.
+  --config full  configs[2] "mono_tum Full fr3_long_office": all 2582 frames of
+                 rgb_full_demo.txt, flag Full (iForest + line alignment + EAO).
+  --config c     configs[3] "Synthetic 640x480 stream, 64 objects x 2k map-points, assoc
+                 sharded via RCCL": the object-sharded association.
 
-  1. ORBextractor::operator() for all 405 frames (eao_orb_extract_batch_device,
-     src/ORBextractor.cc:1060-1135)          -- 10 kernel launches,
-  2. SearchByProjection(CurrentFrame, LastFrame, 15, mono) for the 404
-     consecutive pairs (eao_match_motion_batch_device, src/ORBmatcher.cc:1328)
-                                              -- 2 launches,
-  3. the object-association replay of Tracking.cc:1199-1530 + LocalMapping
-     object maintenance over the 405 frames' YOLO boxes (eao_replay_run: frame
-     by frame, NP test / isolation forest / projected rects on the GPU,
-     decisions on the host).
-     It runs on its own host thread + HIP stream, overlapped with 1-2 the way
-     the reference's Tracking thread overlaps the next frame's extraction.
+One *step* (eao / full) is one pass of the hot path over the whole stream, every input
+resident before timing:
+  1. ORBextractor::operator() of every frame (eao_orb_extract_batch_device,
+     src/ORBextractor.cc:1043-1105) -- HBM-resident frames, one batch;
+  2. SearchByProjection(CurrentFrame, LastFrame, 15, mono) of every consecutive pair
+     (eao_match_motion_batch_device, src/ORBmatcher.cc:1328-1470);
+  3. the object-association replay of Tracking.cc:1241-1696 + LocalMapping's object
+     maintenance (eao_replay_run: frame by frame, NP test / isolation forest / projected
+     rects on the GPU, decisions on the host) over the stream's detections.
+     It runs on its own host thread + HIP streams, overlapped with 1-2, the way the
+     reference's Tracking thread overlaps the next frame's extraction.
 
-The EAO flag is the full ensemble: IoU / NP / projected IoU / t-test
-association, isolation forests, and the object-line association + yaw sampling
-(Tracking.cc:2472-2527, 2624-2871) over each frame's synthetic line segments
-(projected ground-truth cuboid edges, +-2 deg noise, broken edges, clutter).
+Inputs: the association runs on the reference's own fr3_long_office detections
+(data/yolo_txts, scores parsed as 0 -- SURVEY Q1) and GT poses (data/groundtruth.txt), as
+committed in tests/golden/fr3_inputs.npz; the 3-D object clouds, tracked map points and
+line segments are synthesised around them (tools/synth.assoc_stream_fr3_real). The TUM
+images are not available: the extraction frames are procedurally rendered 640x480 views
+(tools/synth.frame_stream; the Full config cycles 405 of them forth and back).
 
-Multi-GPU: frames are independent units, so each rank processes
-its own 405-frame stream shard with no data-path collective ("scaling":
-"weak"); value = all ranks' frames / max-over-ranks time.
+Multi-GPU: `--gpus N` without a torchrun environment starts N rank processes itself
+(before anything touches the GPU). eao / full: every rank replays its own copy of the
+stream -- independent camera streams, no data-path collective ("scaling": "weak"), value
+= all ranks' frames / max-over-ranks time. c: every rank replays the same stream, object
+o's GPU work runs on rank o.id % N and the result records are all-gathered over RCCL
+("scaling": "strong").
 
-cpu_baseline: the CPU restatement under oracle/ (kind "port", 1 core) timed on
-rank 0 only on a bounded sample -- extraction + matching on the first
---cpu-frames frames and the association replay over the full stream -- and
-the sample's outputs are checked against the GPU's (parity block).
+cpu_baseline: the CPU restatement under oracle/ (kind "port") rebuilt here with
+-O3 -march=native, timed on rank 0 on a bounded sample: (a) the reference's shape, one
+thread for extraction + matching + association; (b) all cores: extraction and matching
+frame-parallel over std::threads, the association (one decision chain) on one thread
+beside them. `value` is (b); (a) is reported under "single_thread". The sample's outputs
+are checked against the GPU's (parity block).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -45,17 +58,37 @@ for _p in (ROOT, os.path.join(ROOT, "eao-slam_amd", "python")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-import torch  # noqa: E402  (device memory, streams, torch.distributed: plumbing)
-import torch.distributed as dist  # noqa: E402
-
-import eao_accel as ea  # noqa: E402
-import eao_dist  # noqa: E402
-from tools import synth  # noqa: E402
-
 W, H = 640, 480
 NFEAT, NLEV, SCALE = 1000, 8, 1.2
 MOTION_TH = 15            # Tracking::TrackWithMotionModel, monocular (th=15)
 PEAK_HBM_GBS = 8000.0     # MI355X_MICROARCH.md: HBM3E peak
+METRIC = "frames/sec (extract+match+EAO-assoc) on 640x480; CPU-ref parity on assoc IDs"
+CONFIGS = {
+    "eao": dict(flag="EAO", start=None, n=None, cpu_assoc=405,
+                workload="mono_tum EAO fr3_long_office 640x480 (BASELINE configs[1]: rgb_seq_pose.txt, 405 frames)"),
+    "full": dict(flag="Full", start=0, n=2582, cpu_assoc=600,
+                 workload="mono_tum Full fr3_long_office 640x480 (BASELINE configs[2]: rgb_full_demo.txt, "
+                          "2582 frames)"),
+}
+RENDERED = 405  # procedurally rendered extraction frames per rank (longer streams cycle them)
+
+
+def launch_ranks(nranks, argv, script=None):
+    """--gpus N outside torchrun: start N fresh rank processes of `script` (this file by
+    default; nothing in this process has touched the GPU) with the torchrun environment,
+    rendezvous on 127.0.0.1, and return the worst exit status; rank 0 prints the JSON line."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
 
 
 def level_sizes():
@@ -73,73 +106,77 @@ def algorithmic_bytes(n_kps):
     lv = [w * h for w, h in level_sizes()]
     l0, upper = lv[0], sum(lv[1:])
     return {
-        # resize: read level l-1, write level l (l = 1..7)
-        "pyramid": sum(lv[:-1]) + upper,
-        # FAST: every level plane read once
-        "fast": l0 + upper,
-        # blur: every level read once and its blurred copy written once
-        "blur": 2 * (l0 + upper),
-        # orient (raw level) + describe (blurred level), outputs 28 B kp + 32 B desc
-        "describe": 2 * (l0 + upper) + n_kps * 60,
-        # SURVEY §8d per-frame figure for the whole extraction
-        "extract": l0 + 2 * upper + n_kps * 60,
+        "pyramid": sum(lv[:-1]) + upper,        # resize: read level l-1, write level l (l = 1..7)
+        "fast": l0 + upper,                     # FAST: every level plane read once
+        "blur": 2 * (l0 + upper),               # blur: every level read once, blurred copy written once
+        "describe": 2 * (l0 + upper) + n_kps * 60,  # orient (raw) + describe (blurred), 28 B kp + 32 B desc
+        "extract": l0 + 2 * upper + n_kps * 60,     # SURVEY §8d per-frame figure for the whole extraction
     }
 
 
-def stage_names():
-    return ["pyramid", "fast", "distribute", "blur", "describe"]
+STAGES = ["pyramid", "fast", "distribute", "blur", "describe"]
+KERNELS = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute", "blur": "k_blur",
+           "describe": "k_describe"}
 
 
-class Stream:
-    """All inputs of one rank's step, resident in HBM."""
-
-    def __init__(self, nframes, seed, dev):
-        frames, poses = synth.frame_stream(nframes, seed=seed)
-        self.poses = np.stack(poses).astype(np.float32)
-        self.host_frames = frames
-        self.d_frames = torch.from_numpy(np.stack(frames)).to(dev)
-        self.assoc = synth.assoc_stream_fr3(nframes, seed=0xEA1 + (seed - 0xEA0))
-        self.n = nframes
-
+def pingpong(n, m):
+    """Frame index of step t when m rendered frames are cycled forth and back."""
+    p = np.arange(n) % (2 * m - 2) if m > 1 else np.zeros(n, np.int64)
+    return np.where(p < m, p, 2 * m - 2 - p)
 
 
 def pmc_traffic(kernel, frames):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 --pmc passes
-    (FETCH_SIZE and WRITE_SIZE in separate runs of tools/pmc_extract.py over the same
-    405-frame stream; FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note).
-    A counter run cannot sit inside the timed region, so this is the profiled figure
-    for the same launch shape; None when the summaries are absent or for another size."""
+    """HBM bytes per launch of `kernel` from committed rocprofv3 --pmc passes (FETCH_SIZE and
+    WRITE_SIZE in separate runs of tools/pmc_extract.py over the same 405-frame launch,
+    FETCH_SIZE doubled per MI355X_MICROARCH.md's gfx950 note). A counter run cannot sit inside
+    the timed region, so this is the profiled figure of the same launch shape, NOT a
+    measurement of this run; None for another shape or when the summaries are absent."""
     if frames != 405:
-        return None
-    tot = 0.0
-    for f in ("r01_pmc_fetch_final.txt", "r01_pmc_write_final.txt"):
+        return None, None
+    pairs = [("r02_pmc_fetch.txt", "r02_pmc_write.txt"), ("r01_pmc_fetch_final.txt", "r01_pmc_write_final.txt")]
+    names = next((pr for pr in pairs if all(os.path.exists(os.path.join(ROOT, "profiles", f)) for f in pr)), None)
+    if names is None:
+        return None, None
+    tot, src = 0.0, []
+    for f in names:
         p = os.path.join(ROOT, "profiles", f)
-        if not os.path.exists(p):
-            return None
         hit = [l.split() for l in open(p) if l.split()[:1] == ["eao::" + kernel.split()[0]]]
         if not hit:
-            return None
+            return None, None
         tot += float(hit[0][-1])
-    return tot
+        src.append("profiles/" + f)
+    return tot, "rocprofv3 --pmc (profiled, committed: %s), same launch shape; not measured in this run" % ", ".join(src)
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--frames", type=int, default=405)
-    ap.add_argument("--cpu-frames", type=int, default=60, help="extract+match CPU sample size")
+    ap.add_argument("--config", choices=["eao", "full", "c"], default="eao")
+    ap.add_argument("--frames", type=int, default=0, help="override the stream length")
+    ap.add_argument("--cpu-frames", type=int, default=60, help="extract+match single-thread CPU sample")
+    ap.add_argument("--cpu-mt-frames", type=int, default=256, help="extract+match all-cores CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
     args = ap.parse_args()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        return launch_ranks(args.gpus, sys.argv[1:])
+
+    import torch  # device memory, streams, torch.distributed: plumbing
+    import torch.distributed as dist
+    import eao_accel as ea
+    import eao_dist
 
     rank, world, local = eao_dist.env_rank()
-    # one process per GPU; ranks beyond the visible devices (a rehearsal of
-    # several ranks on one card) share devices round-robin
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     ndev = torch.cuda.device_count()
     if ndev < 1:
         raise RuntimeError("no GPU visible: the engine has no CPU fallback")
-    gpu = local % ndev
+    gpu = local % ndev  # ranks beyond the visible devices (a rehearsal on one card) share them
+    if args.config == "c":
+        return run_config_c(args, rank, world, gpu)
     if world > 1:
         backend = os.environ.get("EAO_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
         if backend == "nccl":
@@ -148,52 +185,58 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
-    local = gpu
-    if not ea.device_ok(local):
+    if not ea.device_ok(gpu):
         raise RuntimeError("no gfx950 device: the engine has no CPU fallback")
+    from tools import synth
+    cfg = CONFIGS[args.config]
 
-    F = args.frames
-    data = Stream(F, 0xEA0 + rank, dev)
+    # ---- inputs: the association stream (real fr3 detections + GT poses) and the frames
+    assoc_frames = synth.assoc_stream_fr3_real(cfg["start"], cfg["n"])
+    if args.frames:
+        assoc_frames = assoc_frames[:args.frames]
+    F = len(assoc_frames)
+    rendered, rposes = synth.frame_stream(min(F, RENDERED), seed=0xEA0 + rank)
+    idx = pingpong(F, len(rendered))
+    poses = rposes[idx].astype(np.float32)
+    # the extraction / matching stream runs on a dedicated HIP stream (a NULL handle would
+    # select the engine's own stream, which torch events do not see); buffers are made on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+    assert sptr != 0
+    d_frames = torch.from_numpy(rendered).to(dev)[torch.from_numpy(idx).to(dev)].contiguous()
 
-    orb = ea.Orb(NFEAT, SCALE, NLEV, 20, 7, W, H, max_batch=F, device=local)
+    orb = ea.Orb(NFEAT, SCALE, NLEV, 20, 7, W, H, max_batch=F, device=gpu)
     cap = orb.cap
     sc = orb.scale_tables()[0]
     cam = ea.camera()
-    matcher = ea.Matcher(max_kps=cap, max_batch=F, device=local)
-    assoc = ea.Assoc(device=local)
+    matcher = ea.Matcher(max_kps=cap, max_batch=F, device=gpu)
+    assoc = ea.Assoc(device=gpu)
 
     u8, i32, f32 = torch.uint8, torch.int32, torch.float32
     d_kps = torch.zeros((F, cap, 28), dtype=u8, device=dev)
     d_desc = torch.zeros((F, cap, 32), dtype=u8, device=dev)
     d_cnt = torch.zeros(F, dtype=i32, device=dev)
-    d_T = torch.from_numpy(data.poses.reshape(F, 16)).to(dev)
+    d_T = torch.from_numpy(poses.reshape(F, 16)).to(dev)
     d_has = torch.zeros((F, cap), dtype=u8, device=dev)
     d_mpos = torch.zeros((F, cap, 3), dtype=f32, device=dev)
     d_mdesc = torch.zeros((F, cap, 32), dtype=u8, device=dev)
     d_match = torch.full((F, cap), -1, dtype=i32, device=dev)
     d_nm = torch.zeros(F, dtype=i32, device=dev)
-    # a dedicated stream: the engine launches on it (a NULL handle would
-    # select the engine's own stream, which torch events do not see)
-    stream = torch.cuda.Stream(dev)
-    torch.cuda.set_stream(stream)
-    sptr = stream.cuda_stream
-    assert sptr != 0
+    stream.synchronize()
 
     def extract():
-        orb.extract_batch_device(d_frames_ptr, F, W, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(),
+        orb.extract_batch_device(d_frames.data_ptr(), F, W, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(),
                                  cap, sptr)
-
-    d_frames_ptr = data.d_frames.data_ptr()
 
     def match():
         matcher.motion_batch_device(cam, F, cap, d_T.data_ptr(), MOTION_TH, 1, d_kps.data_ptr(),
                                     d_desc.data_ptr(), d_cnt.data_ptr(), d_has.data_ptr(), d_mpos.data_ptr(),
                                     d_mdesc.data_ptr(), sc, d_match.data_ptr(), d_nm.data_ptr(), sptr)
 
-    # -- the map the motion model tracks against: every keypoint of frame t-1
-    # holds a map point on the scene plane (backprojected with the GT pose,
-    # descriptor = its observation's).  Built once, untimed: it is the map
-    # state (an input of SearchByProjection), not an output of the step.
+    # -- the map the motion model tracks against: every keypoint of frame t-1 holds a map
+    # point on the scene plane (backprojected with the pose, descriptor = its observation's).
+    # Built once, untimed: it is map state (an input of SearchByProjection), not an output.
     extract()
     torch.cuda.synchronize()
     cnt = d_cnt.cpu().numpy()
@@ -202,28 +245,25 @@ def main():
     has = np.zeros((F, cap), np.uint8)
     for t in range(F):
         n = int(cnt[t])
-        mpos[t, :n] = synth.backproject(data.poses[t], kps[t, :n]["x"], kps[t, :n]["y"])
+        mpos[t, :n] = synth.backproject(poses[t], kps[t, :n]["x"], kps[t, :n]["y"])
         has[t, :n] = 1
     d_mpos.copy_(torch.from_numpy(mpos))
     d_has.copy_(torch.from_numpy(has))
     d_mdesc.copy_(d_desc)
 
-    # the recorded detections / map-point observations of the stream, packed
-    # once (host-resident input of the association, like the frames in HBM)
-    packed = ea.Replay.pack(data.assoc)
-
+    # the recorded detections / map-point observations of the stream, packed once
+    # (host-resident input of the association, like the frames in HBM)
+    packed = ea.Replay.pack(assoc_frames)
     last = {"replay": None}
 
     def associate(out):
-        # the previous pass's replay is torn down first, so its forest slots,
-        # streams and pinned staging pass to this one instead of being
-        # allocated afresh (eao_replay_destroy hands them to the engine)
+        # the previous pass's replay is torn down first, so its forest slots, streams and
+        # pinned staging pass to this one (eao_replay_destroy hands them to the engine)
         if last["replay"] is not None:
             last["replay"].close()
-        rp = ea.Replay(assoc, "EAO")
+        rp = ea.Replay(assoc, cfg["flag"])
         last["replay"] = rp
-        det = rp.run(packed)  # eao_replay_run: frame-by-frame association + local mapping
-        out["det"] = det
+        out["det"] = rp.run(packed)  # eao_replay_run: frame-by-frame association + local mapping
         out["replay"] = rp  # object state read back after the timed region
 
     orb.set_timing(True)
@@ -247,9 +287,9 @@ def main():
             ev_m0.record(stream)
             match()
             ev_m1.record(stream)
-        # wait for the extraction stream only (a device-wide synchronize would
-        # also serialise against the association thread's launches), politely:
-        # the association thread is the critical path and needs its core
+        # wait for the extraction stream only (a device-wide synchronize would also serialise
+        # against the association thread's launches), politely: the association thread is
+        # the critical path and needs its core
         ev_done.record(stream)
         while not ev_done.query():
             time.sleep(2e-4)
@@ -274,19 +314,20 @@ def main():
     elapsed = eao_dist.max_over_ranks(time.perf_counter() - t0, dev)
 
     # frame input stage (measured beside the step, not in it):
-    # cvtColor(CV_RGB2GRAY) of the same stream as 3-channel frames resident in HBM
-    d_color = data.d_frames.unsqueeze(-1).repeat(1, 1, 1, 3)
-    d_gray = torch.empty_like(data.d_frames)
+    # cvtColor(CV_RGB2GRAY) of the stream as 3-channel frames resident in HBM
+    Fg = min(F, 405)
+    d_color = d_frames[:Fg].unsqueeze(-1).repeat(1, 1, 1, 3)
+    d_gray = torch.empty_like(d_frames[:Fg])
     ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ea.color_to_gray_batch_device(d_color.data_ptr(), F, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, local, sptr)
+    ea.color_to_gray_batch_device(d_color.data_ptr(), Fg, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, gpu, sptr)
     reps = 10
     ev_g0.record(stream)
     for _ in range(reps):
-        ea.color_to_gray_batch_device(d_color.data_ptr(), F, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, local, sptr)
+        ea.color_to_gray_batch_device(d_color.data_ptr(), Fg, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, gpu, sptr)
     ev_g1.record(stream)
     torch.cuda.synchronize(dev)
     gray_ms = ev_g0.elapsed_time(ev_g1) / reps
-    gray_bytes = F * W * H * 4  # read 3 B + write 1 B per pixel
+    gray_bytes = Fg * W * H * 4  # read 3 B + write 1 B per pixel
     del d_color, d_gray
 
     total_frames = F * args.steps * world
@@ -295,22 +336,20 @@ def main():
     match_ms = float(np.mean(rec["match_ms"]))
     n_kps = float(d_cnt.float().mean().item())
     ab = algorithmic_bytes(n_kps)
-    names = stage_names()
     dom = int(np.argmax(stage))
-    dom_name = names[dom]
-    kernels = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute", "blur": "k_blur",
-               "describe": "k_describe"}
+    dom_name = STAGES[dom]
 
     result = None
     if rank == 0:
         dom_bytes = ab.get(dom_name)
-        if dom_bytes is None:  # distribute: candidates + selections, data dependent -> use extract figure
+        if dom_bytes is None:  # distribute: candidates + selections, data dependent -> use the extract figure
             dom_bytes = ab["extract"]
         ach = dom_bytes * F / (stage[dom] * 1e-3) / 1e9
         ext_ms = float(stage.sum())
-        ext_gbs = ab["extract"] * F / (ext_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(KERNELS[dom_name], F)
+        nb = np.array([len(f["boxes"]) for f in assoc_frames])
         result = {
-            "metric": "frames/sec (extract+match+EAO-assoc) on 640x480; CPU-ref parity on assoc IDs",
+            "metric": METRIC,
             "value": total_frames / elapsed,
             "unit": "frames/s",
             "n_gpus": world,
@@ -321,95 +360,237 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (procedural textured plane along a smooth camera path; seeded object clouds "
-                    "observed as ~8 YOLO-shaped boxes and ~800 tracked map points per frame; SURVEY.md §8d input 2)",
-            "config": {"workload": "mono_tum EAO fr3_long_office 640x480 (synthetic, %d frames/rank/step, "
-                                   "%d ORB features, 8 levels, assoc flag EAO: iForest + object lines + yaw sampling)" % (F, NFEAT),
-                       "frames_per_step": F, "features": NFEAT, "levels": NLEV, "parallelism": "frames%d" % world},
-            "roofline": {"bound": "hbm", "kernel": kernels[dom_name], "achieved": ach, "peak": PEAK_HBM_GBS,
-                         "unit": "GB/s", "frac": ach / PEAK_HBM_GBS,
-                         "traffic": pmc_traffic(kernels[dom_name], F),
-                         "algorithmic_bytes_per_launch": dom_bytes * F,
-                         "avg_launch_ms": float(stage[dom])},
-            "stages_ms_per_step": {n: float(v) for n, v in zip(names, stage)},
+            "data": "reference fr3_long_office inputs: the real YOLO boxes of data/yolo_txts (%d boxes, scores "
+                    "parsed as 0 per Tracking.cc:435-466) and GT poses of data/groundtruth.txt for %d frames; "
+                    "synthetic 3-D object clouds / tracked map points (%.0f per frame) / line segments around "
+                    "them; procedurally rendered 640x480 extraction frames (TUM images absent)"
+                    % (int(nb.sum()), F, np.mean([len(f["ids"]) for f in assoc_frames])),
+            "config": {"workload": cfg["workload"] + ", %d frames/rank/step, %d ORB features, 8 levels, assoc flag "
+                                                     "%s" % (F, NFEAT, cfg["flag"]),
+                       "frames_per_step": F, "features": NFEAT, "levels": NLEV, "assoc_flag": cfg["flag"],
+                       "parallelism": "streams%d" % world},
+            "roofline": {"bound": "hbm", "kernel": KERNELS[dom_name], "achieved": ach, "peak": PEAK_HBM_GBS,
+                         "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": dom_bytes * F, "avg_launch_ms": float(stage[dom])},
+            "stages_ms_per_step": {n: float(v) for n, v in zip(STAGES, stage)},
             "extract_ms_per_step": ext_ms,
             "extract_fps": F / (ext_ms * 1e-3),
-            "extract_gbs": ext_gbs,
+            "extract_gbs": ab["extract"] * F / (ext_ms * 1e-3) / 1e9,
             "match_ms_per_step": match_ms,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
-                                  "ms_per_405_frames": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
+                                  "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
                                   "note": "measured beside the step (the bench workload is mono frames)"},
             "mean_keypoints": n_kps,
             "mean_matches": float(d_nm[1:].float().mean().item()),
+            "assoc_detections": int(nb.sum()),
         }
+        prof = np.zeros(24)
+        ea.lib().eao_replay_profile(out["replay"].h, ea.P(prof))
+        result["assoc_profile_us_per_frame"] = {
+            "frame": prof[0] / F, "local_mapping": prof[1] / F, "forest_wait": prof[3] / F,
+            "frame_start": prof[14] / F, "assoc_loop": prof[15] / F, "forest_launches_per_frame": prof[2] / F}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"], result["parity"] = cpu_baseline(args, data, kps, cnt, mpos, has, sc, d_desc,
-                                                                d_match, d_nm, out)
+        result["cpu_baseline"], result["parity"] = cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt,
+                                                                mpos, has, sc, d_desc, d_match, d_nm, out)
+        result["gpu_over_cpu"] = {"all_cores": result["value"] / result["cpu_baseline"]["value"],
+                                  "single_thread": result["value"] / result["cpu_baseline"]["single_thread"]["value"]}
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
+    return 0
 
 
-def cpu_baseline(args, data, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu_out):
-    """Time the oracle (CPU restatement, 1 thread) on a bounded sample and
-    check the GPU outputs of the same sample against it."""
-    nb = np.cumsum([0] + [len(f["boxes"]) for f in data.assoc])
-    gpu_ids = [gpu_out["det"][nb[t]:nb[t + 1]] for t in range(data.n)]
-    gpu_objects = gpu_out["replay"].objects()
+def cpu_model():
+    try:
+        for l in open("/proc/cpuinfo"):
+            if l.startswith("model name"):
+                return l.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu_out):
+    """Time the oracle (CPU restatement, -O3 -march=native built here) on a bounded sample
+    and check the GPU outputs of the same sample against it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as orc  # checker / CPU baseline only
+    orc.use_native()
+    F = len(assoc_frames)
+    nb = np.cumsum([0] + [len(f["boxes"]) for f in assoc_frames])
+    det = gpu_out["det"]
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))  # this job's CPU share (16 on the GPU box)
 
-    k = min(args.cpu_frames, data.n)
+    # (a) the reference's shape: one thread
+    k = min(args.cpu_frames, F)
+    frames_k = d_frames[:k].cpu().numpy()
     desc = d_desc.cpu().numpy()
     match = d_match.cpu().numpy()
     nm = d_nm.cpu().numpy()
     t0 = time.perf_counter()
     okps, odesc = [], []
     for t in range(k):
-        a, b = orc.extract(data.host_frames[t], NFEAT, SCALE, NLEV)
+        a, b = orc.extract(frames_k[t], NFEAT, SCALE, NLEV)
         okps.append(a)
         odesc.append(b)
     t_ext = (time.perf_counter() - t0) / k
     bad_kp = [t for t in range(k) if not (int(cnt[t]) == len(okps[t]) and np.array_equal(kps[t, :int(cnt[t])], okps[t])
                                           and np.array_equal(desc[t, :int(cnt[t])], odesc[t]))]
-    ok_kp = not bad_kp
     c = orc.cam()
     t0 = time.perf_counter()
     omatch = []
     for t in range(1, k):
         n0 = len(okps[t - 1])
-        omatch.append(orc.match_motion(c, data.poses[t], MOTION_TH, 1, okps[t - 1], has[t - 1, :n0],
+        omatch.append(orc.match_motion(c, poses[t], MOTION_TH, 1, okps[t - 1], has[t - 1, :n0],
                                        mpos[t - 1, :n0], odesc[t - 1], okps[t], odesc[t], sc))
     t_match = (time.perf_counter() - t0) / max(1, k - 1)
     bad_match = [t for t in range(1, k) if not (omatch[t - 1][0] == int(nm[t])
                                                 and np.array_equal(match[t, :int(cnt[t])], omatch[t - 1][1]))]
-    ok_match = not bad_match
+    ka = min(cfg["cpu_assoc"], F)
     t0 = time.perf_counter()
-    rp = orc.Replay("EAO")
+    rp = orc.Replay(cfg["flag"])
     ok_assoc = True
-    for t, f in enumerate(data.assoc):
+    for t in range(ka):
+        f = assoc_frames[t]
         ids = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
-        ok_assoc &= np.array_equal(ids, gpu_ids[t])
+        ok_assoc &= bool(np.array_equal(ids, det[nb[t]:nb[t + 1]]))
         if f["kf"]:
             rp.local_mapping()
-    t_assoc = (time.perf_counter() - t0) / data.n
-    oi, of, _ = rp.objects()
-    gi, gf, _ = gpu_objects
-    ok_obj = np.array_equal(oi, gi) and np.allclose(of, gf, rtol=1e-5, atol=1e-5, equal_nan=True)
-    per_frame = t_ext + t_match + t_assoc
-    base = {"value": 1.0 / per_frame, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": "oracle/ CPU restatement (g++ -O2, 1 thread): extract %d frames, motion-match %d pairs, "
-                      "association replay over all %d frames; per-frame ms extract %.2f match %.2f assoc %.2f"
-                      % (k, k - 1, data.n, 1e3 * t_ext, 1e3 * t_match, 1e3 * t_assoc)}
-    parity = {"frames_checked_extract": k, "keypoints_descriptors_bitexact": bool(ok_kp),
-              "match_ids_bitexact": bool(ok_match), "mismatch_frames": (bad_kp[:5], bad_match[:5]), "assoc_ids_identical": bool(ok_assoc),
-              "object_stats_1e-5": bool(ok_obj)}
+    t_assoc = (time.perf_counter() - t0) / ka
+    ok_obj = None
+    if ka == F:
+        oi, of, _ = rp.objects()
+        gi, gf, _ = gpu_out["replay"].objects()
+        ok_obj = bool(np.array_equal(oi, gi) and np.allclose(of, gf, rtol=1e-5, atol=1e-5, equal_nan=True))
+
+    # (b) all cores: extraction + matching frame-parallel, association on one thread beside
+    km = min(args.cpu_mt_frames, F)
+    frames_m = d_frames[:km].cpu().numpy()
+    sec, mk, md, mn, mm, mnm = orc.extract_match_mt(frames_m, poses[:km].reshape(km, 16), has[:km], mpos[:km], sc,
+                                                    threads)
+    bad_mt = [t for t in range(km) if not (int(mn[t]) == int(cnt[t]) and np.array_equal(mk[t, :mn[t]], kps[t, :mn[t]])
+                                           and (t == 0 or np.array_equal(mm[t, :mn[t]], match[t, :mn[t]])))]
+    t_em_mt = sec / km
+    single = 1.0 / (t_ext + t_match + t_assoc)
+    allc = 1.0 / max(t_em_mt, t_assoc)  # pipelined: the association thread is the bound
+    base = {"value": allc, "unit": "frames/s", "cores": threads, "kind": "port",
+            "cpu": cpu_model(), "nproc": os.cpu_count(),
+            "sample": "oracle/ CPU restatement (g++ -O3 -march=native -ffp-contract=off, built on this host): "
+                      "extract+match %d frames frame-parallel on %d std::threads (%.2f ms/frame), association replay "
+                      "(%s flag, one thread) over the first %d of %d frames (%.2f ms/frame); frames/s = 1/max of the "
+                      "two (pipelined)" % (km, threads, 1e3 * t_em_mt, cfg["flag"], ka, F, 1e3 * t_assoc),
+            "single_thread": {"value": single, "cores": 1,
+                              "sample": "one thread: extract %d frames (%.2f ms/frame), motion-match %d pairs "
+                                        "(%.2f ms/pair), association %d frames (%.2f ms/frame)"
+                                        % (k, 1e3 * t_ext, k - 1, 1e3 * t_match, ka, 1e3 * t_assoc)}}
+    parity = {"frames_checked_extract": k, "keypoints_descriptors_bitexact": not bad_kp,
+              "match_ids_bitexact": not bad_match, "mismatch_frames": (bad_kp[:5], bad_match[:5]),
+              "frames_checked_all_cores_leg": km, "all_cores_leg_identical": not bad_mt,
+              "all_cores_leg_mismatch_frames": bad_mt[:5],
+              "frames_checked_assoc": ka, "assoc_ids_identical": bool(ok_assoc), "object_stats_1e-5": ok_obj}
     return base, parity
 
 
+def run_config_c(args, rank, world, gpu):
+    """BASELINE configs[3] / SURVEY §8d input 4 + §8e: the object-sharded association of a
+    synthetic stream, 64 objects x 2000 map points (16 classes), 8 detections per frame
+    observing m in [50, 300] points each. Every rank replays the same stream; object o's GPU
+    work (NP pairs, projected rect, isolation forest) runs on rank o.id % world and the result
+    records are all-gathered over RCCL (eao_replay_shard_rccl), or over a gloo callback with
+    EAO_SHARD_EXCHANGE=gloo (a rehearsal of several ranks on one device)."""
+    import torch.distributed as dist
+    import eao_accel as ea
+    import eao_dist
+    from tools import synth
+    nfr = args.frames or 1000
+    exch = os.environ.get("EAO_SHARD_EXCHANGE", "rccl")
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only (id broadcast, barrier, timing)
+    if not ea.device_ok(gpu):
+        raise RuntimeError("no gfx950 device: the engine has no CPU fallback")
+    frames = synth.assoc_stream_config_c(nfr)
+    packed = ea.Replay.pack(frames)
+    assoc = ea.Assoc(device=gpu)
+
+    def make():
+        rp = ea.Replay(assoc, "EAO")
+        if world > 1:
+            if exch == "gloo":
+                rp.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
+            else:
+                uid = eao_dist.broadcast_bytes(ea.rccl_unique_id() if rank == 0 else None)
+                rp.shard(rank, world, unique_id=uid)
+        return rp
+
+    for _ in range(args.warmup):
+        make().run(packed)
+    elapsed, det, rp = 0.0, None, None
+    eao_dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if rp is not None:
+            rp.close()
+        rp = make()
+        det = rp.run(packed)
+    eao_dist.barrier()
+    elapsed = eao_dist.max_over_ranks(time.perf_counter() - t0)
+    st = rp.shard_stats() if world > 1 else {"exchanges": 0, "bytes_per_rank": 0.0, "exchange_us": 0.0}
+    prof = np.zeros(24, np.float64)
+    ea.lib().eao_replay_profile(rp.h, ea.P(prof))
+    result = None
+    if rank == 0:
+        nb = [len(f["boxes"]) for f in frames]
+        result = {
+            "metric": "frames/sec (EAO association, Config C: 64 objects x 2k points, sharded by object)",
+            "value": nfr * args.steps / elapsed, "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (SURVEY.md §8d input 4: 64 Gaussian object clouds x 2000 points + 5%% outliers, "
+                    "16 classes, %.1f boxes and %.0f map points per frame)"
+                    % (np.mean(nb), np.mean([len(f["ids"]) for f in frames])),
+            "config": {"workload": "Config C association (BASELINE configs[3]), %d frames" % nfr,
+                       "parallelism": "objects%d" % world, "exchange": exch if world > 1 else None},
+            "exchange": {"count": st["exchanges"], "bytes_per_rank_per_exchange":
+                         st["bytes_per_rank"] / max(1, st["exchanges"]),
+                         "us_per_exchange": st["exchange_us"] / max(1, st["exchanges"]),
+                         "exchanges_per_frame": st["exchanges"] / nfr},
+            "replay_profile_us_per_frame": {"iforest_wait": prof[3] / nfr, "np": prof[5] / nfr,
+                                            "frame_start": prof[7] / nfr},
+        }
+        if not args.no_cpu_baseline and args.cpu_frames > 0:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import pyoracle as orc  # checker / CPU baseline only
+            orc.use_native()
+            k = min(max(args.cpu_frames, 200), nfr)
+            o = orc.Replay("EAO")
+            off = np.cumsum([0] + nb)
+            ok = True
+            t0 = time.perf_counter()
+            for t in range(k):
+                f = frames[t]
+                ids = o.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+                ok &= bool(np.array_equal(ids, det[off[t]:off[t + 1]]))
+                if f["kf"]:
+                    o.local_mapping()
+            dt = time.perf_counter() - t0
+            result["cpu_baseline"] = {"value": k / dt, "unit": "frames/s", "cores": 1, "kind": "port",
+                                      "cpu": cpu_model(),
+                                      "sample": "oracle/ CPU restatement (-O3 -march=native, 1 thread: the "
+                                                "association is one decision chain), first %d frames" % k}
+            result["parity"] = {"frames_checked": k, "assoc_ids_identical": ok}
+    rp.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result, default=float), flush=True)
+    return 0
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

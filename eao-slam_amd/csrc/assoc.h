@@ -51,6 +51,8 @@ class AssocEngine {
                     hipStream_t s, int max_len, int max_sample, int npts_total,
                     double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
                     double* scores2 = nullptr);  // optional second copy of the scores
+  // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples
+  bool iforest_fits(int max_len, int max_sample) const;
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
 };

@@ -906,7 +906,7 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     return EAO_E_CAPACITY;
   }
   const IfLds L(maxN, maxS);
-  if (maxN > IF_MAXN || L.total > lds_limit) {
+  if (!iforest_fits(maxN, maxS)) {
     set_error("iforest: cloud exceeds the LDS-resident tree capacity");
     return EAO_E_CAPACITY;
   }
@@ -925,6 +925,10 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
+}
+
+bool AssocEngine::iforest_fits(int max_len, int max_sample) const {
+  return max_len <= IF_MAXN && IfLds(max_len, max_sample).total <= lds_limit;
 }
 
 int AssocEngine::rects(const CamDev& cam, const float* Tg, int nclouds, const float* pts,

@@ -4,13 +4,14 @@
 // Pipeline per batch of frames (all HBM-resident, one stream):
 //   k_resize      x7  level l from level l-1 (cv::resize INTER_LINEAR 8U,
 //                     fixed point, ORBextractor.cc:1120)
-//   k_fast        x1  one wave per (grid cell, frame): ROI staged in LDS,
-//                     FAST-9/16 + cornerScore + in-cell 3x3 NMS, iniTh with
+//   k_fast_band   x1  one 4-wave workgroup per (band of cells <= 512 px, frame):
+//                     band ROI staged in LDS, packed-f16 FAST strength swept
+//                     down 62-column strips, in-cell 3x3 NMS by DPP, iniTh with
 //                     minTh retry for empty cells (ORBextractor.cc:789-829)
 //   k_distribute  x1  one wave per (level, frame): DistributeOctTree with
 //                     the reference's list order (ORBextractor.cc:539-763)
 //   k_blur        x1  7x7 sigma-2 Gaussian of every level (separable, fixed
-//                     point, REFLECT_101), 64x16 tiles (:1085-1086)
+//                     point, REFLECT_101), 64x64 output tiles (:1085-1086)
 //   k_describe    x1  one wave per selected keypoint: IC_Angle on the level,
 //                     the 512 rBRIEF taps gathered from the blurred level,
 //                     256-bit descriptor, final scaling (:77-147, :1076-1104)
@@ -68,183 +69,11 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src,
 }
 
 // ---------------------------------------------------------------- FAST
-__constant__ int c_off16[16][2] = {{0, 3},  {1, 3},   {2, 2},   {3, 1},   {3, 0},  {3, -1},
-                                   {2, -2}, {1, -3},  {0, -3},  {-1, -3}, {-2, -2}, {-3, -1},
-                                   {-3, 0}, {-3, 1},  {-2, 2},  {-1, 3}};
-
-// FAST-9/16 test + OpenCV cornerScore<16>; returns 0 when not a corner.
-__device__ __forceinline__ int fast_pixel(const uint8_t* roi, int RS, int r, int c, int th) {
-  const int v = roi[r * RS + c];
-  int d[25];
-  uint32_t dk = 0, br = 0;
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int p = roi[(r + c_off16[k][1]) * RS + c + c_off16[k][0]];
-    d[k] = v - p;
-    dk |= (uint32_t)(p < v - th) << k;
-    br |= (uint32_t)(p > v + th) << k;
-  }
-  uint32_t md = dk | (dk << 16), mb = br | (br << 16);
-  uint32_t rd = md, rb = mb;
-#pragma unroll
-  for (int s = 1; s <= 8; s++) {
-    rd &= md >> s;
-    rb &= mb >> s;
-  }
-  if (((rd | rb) & 0xffffu) == 0) return 0;
-#pragma unroll
-  for (int k = 16; k < 25; k++) d[k] = d[k - 16];
-  int a0 = th;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int a = min(d[k + 1], d[k + 2]);
-    a = min(a, d[k + 3]);
-    a = min(a, d[k + 4]);
-    a = min(a, d[k + 5]);
-    a = min(a, d[k + 6]);
-    a = min(a, d[k + 7]);
-    a = min(a, d[k + 8]);
-    a0 = max(a0, min(a, d[k]));
-    a0 = max(a0, min(a, d[k + 9]));
-  }
-  int b0 = -a0;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int b = max(d[k + 1], d[k + 2]);
-    b = max(b, d[k + 3]);
-    b = max(b, d[k + 4]);
-    b = max(b, d[k + 5]);
-    b = max(b, d[k + 6]);
-    b = max(b, d[k + 7]);
-    b = max(b, d[k + 8]);
-    b0 = min(b0, max(b, d[k]));
-    b0 = min(b0, max(b, d[k + 9]));
-  }
-  return -b0 - 1;
-}
-
-__global__ __launch_bounds__(64) void k_fast(const uint8_t* __restrict__ frames, int fpitch,
-                                             long long fstride, const uint8_t* __restrict__ pyr,
-                                             long long pstride, const LevelDev* __restrict__ levels,
-                                             const CellDev* __restrict__ cells, int iniTh, int minTh,
-                                             int RS, int RH, uint32_t* __restrict__ cand,
-                                             long long cand_stride, int* __restrict__ cell_cnt,
-                                             int ncells) {
-  extern __shared__ uint8_t smem[];
-  uint8_t* roi = smem;
-  uint8_t* sc = smem + RS * RH;
-  const int ci = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
-  const CellDev c = cells[ci];
-  const LevelDev& L = levels[c.level];
-  const uint8_t* img;
-  int pitch;
-  if (c.level == 0) {
-    img = frames + f * fstride;
-    pitch = fpitch;
-  } else {
-    img = pyr + f * pstride + L.plane_off;
-    pitch = L.pitch;
-  }
-  const int rw = c.x1 - c.x0, rh = c.y1 - c.y0;
-  for (int idx = lane; idx < rw * rh; idx += 64) {
-    const int r = idx / rw, cc = idx - r * rw;
-    roi[r * RS + cc] = img[(long long)(c.y0 + r) * pitch + c.x0 + cc];
-  }
-  uint32_t* out = cand + f * cand_stride + c.slot;
-  int n = 0;
-  for (int pass = 0; pass < 2; pass++) {
-    int th = pass == 0 ? iniTh : minTh;
-    th = min(max(th, 0), 255);
-    for (int idx = lane; idx < rw * rh; idx += 64) sc[(idx / rw) * RS + idx % rw] = 0;
-    __syncthreads();
-    for (int r = 3; r < rh - 3; r++)
-      for (int cc = 3 + lane; cc < rw - 3; cc += 64) sc[r * RS + cc] = (uint8_t)fast_pixel(roi, RS, r, cc, th);
-    __syncthreads();
-    n = 0;
-    for (int r = 3; r < rh - 3; r++) {
-      for (int c0 = 3; c0 < rw - 3; c0 += 64) {
-        const int cc = c0 + lane;
-        bool keep = false;
-        int s = 0;
-        if (cc < rw - 3) {
-          s = sc[r * RS + cc];
-          const uint8_t* p = sc + r * RS + cc;
-          keep = s > p[1] && s > p[-1] && s > p[-RS - 1] && s > p[-RS] && s > p[-RS + 1] &&
-                 s > p[RS - 1] && s > p[RS] && s > p[RS + 1];
-        }
-        const uint64_t m = ballot(keep);
-        if (keep) {
-          const int pos = n + popc64(m & lanes_below());
-          if (pos < c.cap) out[pos] = pack_kp(cc + c.j * L.wCell, r + c.i * L.hCell, s);
-        }
-        n += popc64(m);
-      }
-    }
-    if (n > 0) break;  // ORBextractor.cc:812 -- retry with minTh only when empty
-    __syncthreads();
-  }
-  if (lane == 0) cell_cnt[f * ncells + ci] = n;
-}
-
-// FAST corner strength of a pixel: S = max over the 16 arcs of 9 of
-// max(min d, min -d), d = centre - ring. The pixel is a FAST-9 corner at
-// threshold th iff S > th, and OpenCV's cornerScore<16> at that threshold is
-// then S - 1 (its a0 starts at th < S), so one strength map serves both the
-// iniTh pass and the minTh retry.
-__device__ __forceinline__ int fast_strength(const uint8_t* roi, int RS, int r, int c) {
-  const int v = roi[r * RS + c];
-  int d[25];
-#pragma unroll
-  for (int k = 0; k < 16; k++) d[k] = v - (int)roi[(r + c_off16[k][1]) * RS + c + c_off16[k][0]];
-#pragma unroll
-  for (int k = 16; k < 25; k++) d[k] = d[k - 16];
-  int u = -256, w = 256;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    int a = min(d[k + 1], d[k + 2]), b = max(d[k + 1], d[k + 2]);
-#pragma unroll
-    for (int q = 3; q <= 8; q++) {
-      a = min(a, d[k + q]);
-      b = max(b, d[k + q]);
-    }
-    u = max(u, max(min(a, d[k]), min(a, d[k + 9])));
-    w = min(w, min(max(b, d[k]), max(b, d[k + 9])));
-  }
-  return max(0, max(u, -w));
-}
-
-// FAST strength of the pixel at p (row stride RS known at compile time, so
-// the 16 ring reads are immediate-offset LDS loads): with A = min over the 16
-// arcs of 9 of the arc's max ring value and B = max over the arcs of the arc's
-// min, S = max(0, v - A, B - v) -- the same integer as fast_strength (the arc
-// min / max of d = v - ring are v - max / v - min), from 3-wide then 9-wide
-// window minima / maxima.
-template <int RS>
-__device__ __forceinline__ int fast_strength_c(const uint8_t* p) {
-  constexpr int off[16] = {3 * RS,  3 * RS + 1,  2 * RS + 2,  RS + 3,  3,  -RS + 3,  -2 * RS + 2,  -3 * RS + 1,
-                           -3 * RS, -3 * RS - 1, -2 * RS - 2, -RS - 3, -3, RS - 3,   2 * RS - 2,  3 * RS - 1};
-  const int v = p[0];
-  int q[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) q[k] = p[off[k]];
-  int mn3[16], mx3[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn3[k] = min(min(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
-    mx3[k] = max(max(q[k], q[(k + 1) & 15]), q[(k + 2) & 15]);
-  }
-  int A = 255, B = 0;
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const int a0 = max(max(mx3[k], mx3[(k + 3) & 15]), mx3[(k + 6) & 15]);
-    const int a1 = max(max(mx3[k + 1], mx3[(k + 4) & 15]), mx3[(k + 7) & 15]);
-    const int b0 = min(min(mn3[k], mn3[(k + 3) & 15]), mn3[(k + 6) & 15]);
-    const int b1 = min(min(mn3[k + 1], mn3[(k + 4) & 15]), mn3[(k + 7) & 15]);
-    A = min(min(A, a0), a1);
-    B = max(max(B, b0), b1);
-  }
-  return max(0, max(v - A, B - v));
-}
+// FAST corner strength of a pixel (cv::FAST-9/16 + cornerScore<16>, ORBextractor.cc:809-815):
+// with A = min over the 16 arcs of 9 ring pixels of the arc's max and B = max over the arcs
+// of the arc's min, S = max(0, v - A, B - v). The pixel is a FAST-9 corner at threshold th
+// iff S > th, and cornerScore<16> at that threshold is then S - 1 (its a0 starts at th < S),
+// so one strength map serves both the iniTh pass and the minTh retry.
 
 // gfx950 packed 3-input f16 minimum / maximum (two pixels per instruction)
 __device__ __forceinline__ uint32_t pk_min3(uint32_t a, uint32_t b, uint32_t c) {
@@ -258,7 +87,7 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
   return d;
 }
 
-// fast_strength_c for the two vertically adjacent pixels p (low half) and
+// The FAST strength (above) for the two vertically adjacent pixels p (low half) and
 // p + RS (high half) at once. A ring byte b is carried as the f16 1024 + b
 // (bits 0x6400 | b: a normal number, exact), so f16 minimum / maximum order
 // the bytes exactly and the 3- then 9-wide arc windows run on both rows per

@@ -913,6 +913,15 @@ class ReplayEngine {
         tot += n;
       }
       const int nb = (int)b.objs.size();
+      {  // capacity over the whole batch, not only the owned objects: every rank of a
+         // sharded replay must reach the same verdict (no rank left waiting in an exchange)
+        int maxN_all = 0;
+        for (Obj* o : b.objs) maxN_all = std::max(maxN_all, (int)o->pts.size());
+        if (!A->iforest_fits(maxN_all, maxN_all / 2)) {
+          set_error("replay: object exceeds the isolation-forest capacity");
+          return EAO_E_CAPACITY;
+        }
+      }
       Tick tpk(&prof[23]);
       // speculative NP: every later detection of this frame that will run the
       // NP test against these objects (same class, >= 20 points, Object.cc:255-339)
@@ -1284,6 +1293,11 @@ class ReplayEngine {
   int rects_np(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
                std::vector<int>& rects, std::vector<eao_np_stats>& stats) {
     if (sworld == 1) return rects_np_launch(list, pairs, rects, stats);
+    for (auto& pr : pairs)  // capacity checked on every rank before the owner split (same verdict)
+      if (pr.second->pts.size() > (size_t)NP_MAXN) {
+        set_error("replay: object exceeds the NP kernel capacity");
+        return EAO_E_CAPACITY;
+      }
     std::vector<Obj*> L;
     std::vector<std::pair<Det*, Obj*>> P;
     std::vector<int> nl(sworld, 0), npr(sworld, 0);

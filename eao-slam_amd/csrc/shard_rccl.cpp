@@ -57,10 +57,15 @@ struct RcclExchanger : Exchanger {
   int grow(size_t bytes) {
     if (bytes <= cap) return EAO_OK;
     const size_t c = std::max(bytes, 2 * cap);
+    // every pointer is released and cleared before reallocating, so a failed
+    // allocation below never leaves the destructor a stale pointer to free again
+    if (stream) EAO_HIP_CHECK(hipStreamSynchronize(stream));
     if (h_send) (void)hipHostFree(h_send);
     if (h_recv) (void)hipHostFree(h_recv);
     if (d_send) (void)hipFree(d_send);
     if (d_recv) (void)hipFree(d_recv);
+    h_send = h_recv = d_send = d_recv = nullptr;
+    cap = 0;
     EAO_HIP_CHECK(hipHostMalloc((void**)&h_send, c, 0));
     EAO_HIP_CHECK(hipHostMalloc((void**)&h_recv, c * world, 0));
     EAO_HIP_CHECK(hipMalloc((void**)&d_send, c));
@@ -94,6 +99,36 @@ Exchanger* make_rccl_exchanger(int dev, int rank, int world, const void* unique_
 }
 
 }  // namespace eao
+
+// one-rank RCCL exchange self-test: a world-1 communicator from a fresh unique id,
+// one all-gather of a byte pattern through the replay's exchanger (pinned staging,
+// H2D, ncclAllGather, D2H, stream sync), result compared with the pattern
+extern "C" int eao_rccl_selftest(int device, int bytes) {
+  if (bytes <= 0) return EAO_E_ARG;
+  if (!eao_device_ok(device)) {
+    eao::set_error("no usable gfx950 device");
+    return EAO_E_NODEVICE;
+  }
+  uint8_t uid[128];
+  if (int rc = eao_rccl_unique_id(uid)) return rc;
+  int rc = 0;
+  eao::Exchanger* x = eao::make_rccl_exchanger(device, 0, 1, uid, &rc);
+  if (!x) return rc;
+  // the requested size, then one past the initial 4 KB staging (grow() reallocates)
+  for (size_t n : {(size_t)bytes, (size_t)bytes + 4097}) {
+    std::string send(n, '\0'), recv(n, '\1');
+    for (size_t i = 0; i < n; i++) send[i] = (char)(i * 131 + 7);
+    rc = x->allgather(send.data(), &recv[0], n);
+    if (!rc && recv != send) {
+      eao::set_error("eao_rccl_selftest: gathered bytes differ");
+      rc = EAO_E_HIP;
+    }
+    if (rc) break;
+  }
+  delete x;
+  if (rc) return rc;
+  return EAO_OK;
+}
 
 extern "C" int eao_rccl_unique_id(uint8_t* out) {
   if (!out) return EAO_E_ARG;

@@ -70,6 +70,11 @@ def rccl_unique_id():
     return out.tobytes()
 
 
+def rccl_selftest(device=0, nbytes=1000):
+    """eao_rccl_selftest: one-rank RCCL all-gathers through the replay's exchanger."""
+    check(lib().eao_rccl_selftest(int(device), int(nbytes)), "eao_rccl_selftest")
+
+
 def device_ok(dev=0):
     return bool(lib().eao_device_ok(dev))
 

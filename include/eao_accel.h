@@ -267,6 +267,9 @@ int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
    eao_replay_shard_callback: the all-gather is the caller's (e.g. gloo). */
 typedef int (*eao_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes_per_rank);
 int eao_rccl_unique_id(uint8_t* out128);
+/* One-rank self-test of the RCCL exchanger of eao_replay_shard_rccl: a world-1 communicator,
+   all-gathers of `bytes` and bytes + 4097 (staging regrowth), results compared. 0 = ok. */
+int eao_rccl_selftest(int device, int bytes);
 int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* unique_id128);
 int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx);
 /* [0] exchanges, [1] bytes per rank, [2] us spent in the exchange */

@@ -71,6 +71,13 @@ int orc_search_by_projection_motion(const orc_camera* cam, const float* Tcw, flo
                                     int n_cur, const orc_keypoint* cur_kps, const uint8_t* cur_desc,
                                     int nlevels, const float* scale_factors,
                                     int32_t* cur_match);
+/* bench.py's all-cores CPU baseline leg (baseline_mt.cpp): frame-parallel extraction of
+   n frames, then the motion search of every pair (t-1, t), over `threads` std::threads */
+double orc_extract_match_mt(const uint8_t* frames, int n, int w, int h, int nfeatures, float scale_factor,
+                            int nlevels, int iniTh, int minTh, const orc_camera* cam, const float* Tcw,
+                            const uint8_t* has, const float* mpos, float th, int check_ori, const float* scales,
+                            int cap, int threads, orc_keypoint* kps, uint8_t* desc, int* nkp, int32_t* match,
+                            int* nmatch);
 
 /* SearchByProjection(Frame&, vector<MapPoint*>, th), ORBmatcher.cc:45-129, for map
    points already passed through isInFrustum (track_* inputs, Frame.cc:390-446). */

@@ -30,6 +30,17 @@ def build():
     subprocess.check_call(["make", "-s", "-C", HERE])
 
 
+def use_native():
+    """Switch to the -O3 -march=native build of the same sources (bench.py's timed CPU
+    baseline), compiling it on this machine first; must precede the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("pyoracle: library already loaded")
+    subprocess.check_call(["make", "-s", "-j4", "-C", HERE, "native"])
+    LIB_PATH = os.path.join(HERE, "_build_native", "liboracle.so")
+    return LIB_PATH
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -40,6 +51,7 @@ def lib():
         for f in ("orc_bbox_iou", "orc_bbox_former", "orc_bbox_latter"):
             getattr(_lib, f).restype = ctypes.c_float
         _lib.orc_replay_create.restype = ctypes.c_void_p
+        _lib.orc_extract_match_mt.restype = ctypes.c_double
         _lib.orc_replay_destroy.argtypes = [ctypes.c_void_p]
         for f in ("orc_replay_frame", "orc_replay_local_mapping", "orc_replay_num_objects",
                   "orc_replay_object", "orc_replay_object_points"):
@@ -93,6 +105,28 @@ def extract(img, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7):
                                cap, ctypes.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def extract_match_mt(frames, Tcw, has, mpos, scales, threads, th=15, check_ori=1, nfeatures=1000, scale=1.2,
+                     nlevels=8, ini=20, mn=7, c=None):
+    """Frame-parallel extraction of frames (n, h, w) then motion matching of every pair
+    (t-1, t) over `threads` std::threads (baseline_mt.cpp); returns (seconds, kps, desc,
+    nkp, match, nmatch). has/mpos: map state of each frame's keypoints, cap slots."""
+    frames = np.ascontiguousarray(frames, np.uint8)
+    n, h, w = frames.shape
+    cap = nfeatures + 64 * nlevels + 64
+    kps = np.zeros((n, cap), KP_DTYPE)
+    desc = np.zeros((n, cap, 32), np.uint8)
+    nkp = np.zeros(n, np.int32)
+    match = np.full((n, cap), -1, np.int32)
+    nmatch = np.zeros(n, np.int32)
+    c = cam(w, h) if c is None else c
+    sec = lib().orc_extract_match_mt(P(frames), n, w, h, nfeatures, ctypes.c_float(scale), nlevels, ini, mn,
+                                     ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)),
+                                     P(np.ascontiguousarray(has, np.uint8)), P(np.ascontiguousarray(mpos, np.float32)),
+                                     ctypes.c_float(th), int(check_ori), P(np.ascontiguousarray(scales, np.float32)),
+                                     cap, int(threads), P(kps), P(desc), P(nkp), P(match), P(nmatch))
+    return sec, kps, desc, nkp, match, nmatch
 
 
 def color_to_gray(img, rgb=True):

@@ -54,6 +54,7 @@ int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const flo
   for (int k = 0; k < nclouds; k++) ok[k] = orc_project_rect(&c, T, len[k], pts + 3 * off[k], rect + 4 * k) == 0;
   return 0;
 }
+bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }
 AssocEngine::~AssocEngine() {}
 }  // namespace eao
 

@@ -58,3 +58,31 @@ def test_gloo_world2_shards_and_reductions():
         assert p.exitcode == 0
     assert [(r[2], r[3]) for r in res] == [(0, 203), (203, 405)]
     assert all(r[4] == 2.5 and r[5] == 405 for r in res)
+
+
+_RANK_SCRIPT = r'''
+import os, sys, torch, torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+assert (r, w) == (int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])) and os.environ["LOCAL_RANK"] == str(r)
+t = torch.tensor([float(r + 1)])
+dist.all_reduce(t)
+dist.barrier()
+dist.destroy_process_group()
+if r == 0:
+    print("ranks-ok %d %.0f %s" % (w, t.item(), " ".join(sys.argv[1:])), flush=True)
+'''
+
+
+def test_bench_launcher_world2(tmp_path, capfd):
+    """bench.py --gpus 2 outside torchrun starts two fresh rank processes (launch_ranks) that
+    rendezvous on 127.0.0.1 with the torchrun environment; rank 0 reports."""
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(_RANK_SCRIPT)
+    env_before = {k: os.environ.get(k) for k in ("RANK", "WORLD_SIZE")}
+    rc = bench.launch_ranks(2, ["--gpus", "2", "--steps", "1"], script=str(script))
+    assert rc == 0
+    out = capfd.readouterr().out
+    assert "ranks-ok 2 3 --gpus 2 --steps 1" in out
+    assert {k: os.environ.get(k) for k in env_before} == env_before  # the parent's environment is untouched

@@ -120,3 +120,11 @@ def test_config_c_sharded_world2_matches_oracle(mode):
         _check(outs, objs, ref)
         assert st["exchanges"] > 0
     assert res[0][3]["exchanges"] == res[1][3]["exchanges"]
+
+
+def test_rccl_exchanger_world1():
+    """The RCCL exchanger of eao_replay_shard_rccl on a world-1 communicator: pinned staging,
+    H2D, ncclAllGather, D2H and the stream sync run, the staging regrows past 4 KB, and the
+    gathered bytes equal the sent ones (shard_rccl.cpp)."""
+    ea.rccl_selftest(0, 1000)
+    ea.rccl_selftest(0, 64)

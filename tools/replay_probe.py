@@ -1,4 +1,6 @@
-"""Wall-clock breakdown of the association replay on the engine."""
+"""Wall-clock breakdown of the association replay on the engine (development aid).
+
+python tools/replay_probe.py [dense] [full]   -- prints eao_replay_profile's counters per pass."""
 import os
 import sys
 import time
@@ -11,18 +13,30 @@ sys.path.insert(0, os.path.join(ROOT, "eao-slam_amd", "python"))
 import eao_accel as ea  # noqa: E402
 from tools import synth  # noqa: E402
 
-frames = synth.assoc_stream_fr3(405) if "dense" not in sys.argv else synth.assoc_stream(405)
+# eao_replay_profile slots (replay.cpp prof[]): times in us, counts marked #
+NAMES = {0: "frame", 1: "local_mapping", 2: "#forest_launch", 3: "forest_complete", 4: "#np_launch",
+         5: "np_relaunch", 6: "#frame_start", 7: "frame_start_rt", 8: "#frames", 9: "#spec_np",
+         12: "steps1-3", 13: "steps4-9", 14: "frame_start_total", 15: "assoc_loop", 16: "same_cls_flush",
+         17: "pending_flush", 18: "kick", 19: "launch", 20: "#retire", 21: "retire", 22: "kick_scan",
+         23: "pack"}
+
+if "full" in sys.argv:
+    frames = synth.assoc_stream_fr3(2582)
+elif "dense" in sys.argv:
+    frames = synth.assoc_stream(405)
+else:
+    frames = synth.assoc_stream_fr3(405)
+packed = ea.Replay.pack(frames)
 a = ea.Assoc()
-for rep in range(2):
+for rep in range(3):
     rp = ea.Replay(a, "EAO")
     t0 = time.perf_counter()
-    for t, f in enumerate(frames):
-        rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
-        if f["kf"]:
-            rp.local_mapping()
+    rp.run(packed)
     dt = time.perf_counter() - t0
     pr = np.zeros(24)
     ea.lib().eao_replay_profile(rp.h, ea.P(pr))
-    print("wall %.1f ms (%.0f us/frame): frame %.0f lm %.0f | iforest %d %.0f | np %d %.0f | rects %d %.0f (us)"
-          % (dt * 1e3, dt * 1e6 / len(frames), pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7]))
+    nf = len(frames)
+    print("pass %d: wall %.1f ms (%.0f us/frame)" % (rep, dt * 1e3, dt * 1e6 / nf))
+    print("   " + "  ".join("%s=%.0f%s" % (NAMES[k], pr[k] / (1 if NAMES[k][0] == "#" else nf),
+                                          "" if NAMES[k][0] == "#" else "us/f") for k in sorted(NAMES)))
     rp.close()

@@ -15,6 +15,8 @@ generated procedurally from fixed seeds:
 All arithmetic is numpy with explicit seeds (PCG64), so results are identical
 here and on the GPU box.
 """
+import os
+
 import numpy as np
 
 TUM3_K = (535.4, 539.2, 320.1, 247.6)  # Examples/Monocular/TUM3.yaml:8-11
@@ -221,6 +223,46 @@ def frame_lines(T, objs, rng, K=TUM3_K, w=640, h=480, n_clutter=12):
     return L[rng.permutation(len(L))].astype(np.float32)
 
 
+def frame_lines_vec(T, objs, rng, K=TUM3_K, w=640, h=480, n_clutter=12):
+    """frame_lines' segment model, vectorised over objects and edges (its own draw
+    order; used by the fr3 streams, whose maps hold ~100 objects)."""
+    fx, fy, cx, cy = K
+    if not objs:
+        return np.zeros((0, 4), np.float32)
+    ctr = np.stack([o["center"] for o in objs])
+    ext = np.stack([np.asarray(o["ext"], np.float64) for o in objs])
+    c = ctr[:, None, :] + (_CORNERS[None] - 0.5) * ext[:, None, :]  # (O, 8, 3)
+    Pc = c @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+    front = (Pc[..., 2] >= 0.1).all(1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        uv = np.stack([fx * Pc[..., 0] / Pc[..., 2] + cx, fy * Pc[..., 1] / Pc[..., 2] + cy], -1)
+    ea, eb = np.array([e[0] for e in _EDGES]), np.array([e[1] for e in _EDGES])
+    p, q = uv[:, ea].reshape(-1, 2), uv[:, eb].reshape(-1, 2)  # (O*12, 2)
+    inside = lambda a: (a[:, 0] >= 0) & (a[:, 0] < w) & (a[:, 1] >= 0) & (a[:, 1] < h)
+    ln = np.hypot(*(q - p).T)
+    keep = np.repeat(front, len(_EDGES)) & inside(p) & inside(q) & (ln >= 15)
+    p, q, ln = p[keep], q[keep], ln[keep]
+    th = np.deg2rad(np.clip(rng.normal(0, 1.0, len(p)), -2, 2))
+    m = (p + q) / 2
+    cs, sn = np.cos(th)[:, None], np.sin(th)[:, None]
+    rot = lambda a: m + np.concatenate([cs * (a - m)[:, :1] - sn * (a - m)[:, 1:], sn * (a - m)[:, :1] + cs * (a - m)[:, 1:]], 1)
+    p, q = rot(p), rot(q)
+    brk = (ln > 60) & (rng.random(len(p)) < 0.3)
+    t0 = rng.uniform(0.3, 0.7, len(p))
+    gap = 4.0 / np.maximum(ln, 1e-9)
+    segs = [np.concatenate([p[~brk], q[~brk]], 1),
+            np.concatenate([p[brk], p[brk] + (q[brk] - p[brk]) * (t0[brk] - gap[brk])[:, None]], 1),
+            np.concatenate([p[brk] + (q[brk] - p[brk]) * (t0[brk] + gap[brk])[:, None], q[brk]], 1)]
+    mc = rng.uniform([0, 0], [w, h], (n_clutter, 2))
+    ang, cl = rng.uniform(0, np.pi, n_clutter), rng.uniform(10, 80, n_clutter)
+    dd = 0.5 * cl[:, None] * np.stack([np.cos(ang), np.sin(ang)], 1)
+    segs.append(np.concatenate([mc - dd, mc + dd], 1))
+    L = np.concatenate(segs).astype(np.float64)
+    flip = rng.random(len(L)) < 0.5
+    L[flip] = L[flip][:, [2, 3, 0, 1]]
+    return L[rng.permutation(len(L))].astype(np.float32)
+
+
 def assoc_stream(n_frames=405, seed=0xEA1, K=TUM3_K, w=640, h=480, classes=None, obs_frac=0.7,
                  kf_every=5, pts_range=(150, 600), n_background=800, lines=False):
     """Per-frame replay inputs for the association path.
@@ -274,6 +316,145 @@ def assoc_stream_fr3(n_frames=405, seed=0xEA1, lines=True):
     EAO flag, so the frames carry line segments for the yaw sampling."""
     return assoc_stream(n_frames, seed=seed, classes=FR3_CLASSES, obs_frac=0.5, pts_range=(80, 400),
                         n_background=400, lines=lines)
+
+
+# ----------------------------------------------------------------------------
+# The reference's own fr3_long_office inputs (BASELINE configs[1] and [2], SURVEY §8d
+# inputs 2-3): the real per-frame YOLO boxes of data/yolo_txts (scores parsed as 0, Q1)
+# and the camera poses of data/groundtruth.txt, as committed in tests/golden/fr3_inputs.npz
+# by tools/make_fr3_inputs.py.  The TUM images and the map the reference would build are
+# not available, so the 3-D side is synthesised around the real detections: every box's
+# centre ray is pushed to the depth its class size implies, same-class estimates are
+# clustered into objects, and each object gets a seeded Gaussian point cloud (+5 %
+# outliers, seed 0xEA1) of its class extent; background points fill the room.  The
+# tracked map points of a frame are the visible points (GT pose), sub-sampled.
+FR3_FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                           "fr3_inputs.npz")
+# COCO (darknet 0-based) class extents in metres (x, y, z = up) for the classes in yolo_txts
+FR3_EXTENT = dict(CLASS_EXTENT)
+FR3_EXTENT.update({15: (0.4, 0.2, 0.3), 44: (0.04, 0.15, 0.03), 45: (0.15, 0.15, 0.07), 60: (1.2, 0.8, 0.75),
+                   63: (0.35, 0.25, 0.02), 65: (0.05, 0.18, 0.03), 67: (0.07, 0.02, 0.14), 69: (0.5, 0.5, 0.4),
+                   75: (0.15, 0.15, 0.3), 76: (0.08, 0.18, 0.02)})
+
+
+def fr3_inputs():
+    d = np.load(FR3_FIXTURE)
+    return {k: d[k] for k in d.files}
+
+
+def tum_Tcw(p):
+    """TUM pose row (tx ty tz qx qy qz qw, camera-to-world) -> Tcw (4x4 float32)."""
+    x, y, z, w = p[3:7]
+    R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                  [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                  [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+    T = np.eye(4)
+    T[:3, :3] = R.T
+    T[:3, 3] = -R.T @ np.asarray(p[:3], np.float64)
+    return T.astype(np.float32)
+
+
+def fr3_world(start, n_frames, seed=0xEA1, K=TUM3_K, pts_range=(80, 400), n_background=1500, min_dets=10):
+    """Objects (class, centre, extent, point cloud) clustered from the real boxes of frames
+    [start, start + n_frames) and the background points; returns (objs, P, Tcw list)."""
+    fx, fy, cx, cy = K
+    d = fr3_inputs()
+    boxes, off = d["boxes"].astype(np.float64), d["box_off"]
+    Ts = [tum_Tcw(d["pose"][t]) for t in range(start, start + n_frames)]
+    # per-detection 3-D centre estimates (vectorised), in frame order
+    est, ecls = [], []
+    for i, t in enumerate(range(start, start + n_frames)):
+        b = boxes[off[t]:off[t + 1]]
+        b = b[(b[:, 3] > 0) & (b[:, 4] > 0)]
+        if not len(b):
+            continue
+        ext = np.asarray([FR3_EXTENT.get(int(c), (0.2, 0.2, 0.2)) for c in b[:, 0]])
+        dep = np.clip(np.sqrt((fx * ext[:, :2].max(1) / b[:, 3]) * (fy * ext[:, 2] / b[:, 4])), 0.4, 5.0)
+        ray = np.stack([(b[:, 1] + b[:, 3] / 2 - cx) / fx, (b[:, 2] + b[:, 4] / 2 - cy) / fy, np.ones(len(b))], 1)
+        Rcw, tcw = Ts[i][:3, :3].astype(np.float64), Ts[i][:3, 3].astype(np.float64)
+        est.append((ray * dep[:, None]) @ Rcw - (Rcw.T @ tcw)[None, :])
+        ecls.append(b[:, 0].astype(np.int64))
+    est, ecls = np.concatenate(est), np.concatenate(ecls)
+    # greedy sequential clustering per class (running means), then merge close clusters
+    centers = []
+    for c in np.unique(ecls):
+        X = est[ecls == c]
+        r = max(0.4, float(max(FR3_EXTENT.get(int(c), (0.2, 0.2, 0.2)))))
+        S = np.zeros((0, 3))
+        N = np.zeros(0)
+        for x in X:
+            if len(N):
+                dist = np.linalg.norm(S / N[:, None] - x, axis=1)
+                j = int(np.argmin(dist))
+                if dist[j] < r:
+                    S[j] += x
+                    N[j] += 1
+                    continue
+            S = np.vstack([S, x])
+            N = np.append(N, 1.0)
+        merged = True
+        while merged and len(N) > 1:
+            merged = False
+            M = S / N[:, None]
+            D = np.linalg.norm(M[:, None] - M[None], axis=2) + np.eye(len(N)) * 1e9
+            a, b = np.unravel_index(int(np.argmin(D)), D.shape)
+            if D[a, b] < r:
+                S[a] += S[b]
+                N[a] += N[b]
+                S, N = np.delete(S, b, 0), np.delete(N, b)
+                merged = True
+        for s, k in zip(S, N):
+            if k >= min_dets:
+                centers.append((int(c), s / k))
+    rng = np.random.Generator(np.random.PCG64(seed))
+    objs, pos = [], []
+    for c, center in centers:
+        ext = np.asarray(FR3_EXTENT.get(c, (0.2, 0.2, 0.2)))
+        n = int(rng.integers(*pts_range))
+        p = np.clip(rng.normal(0, 1, (n, 3)) * (ext / 4), -ext / 2, ext / 2) + center
+        n_out = max(1, n // 20)
+        p[:n_out] = center + rng.uniform(-1, 1, (n_out, 3)) * (ext / 2 + 0.25)
+        objs.append(dict(cls=c, center=center, ext=ext, first=len(pos), n=n))
+        pos.extend(p.tolist())
+    cs = np.asarray([o["center"] for o in objs])
+    lo, hi = cs.min(0) - 1.0, cs.max(0) + 1.0
+    pos.extend(rng.uniform(lo, hi, (n_background, 3)).tolist())
+    return objs, np.asarray(pos, np.float32), Ts
+
+
+def assoc_stream_fr3_real(start=None, n_frames=None, seed=0xEA1, K=TUM3_K, w=640, h=480, lines=True,
+                          obs_frac=0.5, max_obs=1000, kf_every=5):
+    """Replay inputs on the reference's fr3_long_office detections and GT poses.
+    Defaults: the demo list (rgb_seq_pose.txt, 405 frames, BASELINE configs[1]);
+    start=0, n_frames=2582 is the Full list (rgb_full_demo.txt, configs[2])."""
+    fx, fy, cx, cy = K
+    d = fr3_inputs()
+    if start is None:
+        start = int(d["demo_first"])
+        n_frames = len(d["demo_timestamps"]) if n_frames is None else n_frames
+    if n_frames is None:
+        n_frames = len(d["timestamps"]) - start
+    boxes, off = d["boxes"].astype(np.int32), d["box_off"]
+    objs, P, Ts = fr3_world(start, n_frames, seed, K)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    lrng = np.random.Generator(np.random.PCG64(0xEA2 + seed))
+    frames = []
+    for i, t in enumerate(range(start, start + n_frames)):
+        T = Ts[i]
+        Pc = P @ T[:3, :3].T.astype(np.float64) + T[:3, 3]
+        z = Pc[:, 2]
+        with np.errstate(divide="ignore", invalid="ignore"):
+            u = fx * Pc[:, 0] / z + cx
+            v = fy * Pc[:, 1] / z + cy
+        vis = (z > 0.1) & (u >= 0) & (u < w) & (v >= 0) & (v < h)
+        obs = np.nonzero(vis & (rng.random(len(P)) < obs_frac))[0]
+        obs = obs[rng.permutation(len(obs))][:max_obs]
+        uv = (np.round(np.stack([u[obs], v[obs]], 1) * 10) / 10).astype(np.float32)
+        frames.append(dict(T=T, boxes=boxes[off[t]:off[t + 1]].reshape(-1, 5).copy(), ids=obs.astype(np.int32),
+                           pos=P[obs], uv=uv, bad=np.zeros(len(obs), np.uint8), kf=(i % kf_every == kf_every - 1)))
+        if lines:
+            frames[-1]["lines"] = frame_lines_vec(T, objs, lrng, K, w, h)
+    return frames
 
 
 # SURVEY.md §8d input 4 (Config C): 64 objects x 2000 map points, 16 classes,
