@@ -136,6 +136,7 @@ struct Det {  // Object_2D
   float sum[3] = {0, 0, 0}, pos[3] = {0, 0, 0};
   bool bad = false;
   int mnId = -1, method = 0, index = -1;
+  unsigned long fid = 0;  // the frame it was detected in
   Obj* alias = nullptr;  // _Pos shares mCenter3D's buffer (Object.cc:677, Tracking.cc:2563)
   // mObjLinesEigen (Tracking.cc:2524): the line angles SampleObjYaw reads, in degrees
   // as (double)(atan2f-rounded angle * 180) / pi -- only kept for yaw-sampled classes
@@ -164,6 +165,19 @@ struct Obj {  // Object_Map
   float yawT[16];                              // ... with the pose of its frame
   int pending = 0;  // 0 none, 1 iForest, 2 iForest then ComputeMeanAndStandard
   int slot = -1;    // in-flight isolation-forest slot, -1 if not launched
+  // Effects of later detections of the same frame that depend on this object's pending
+  // forest (it was updated earlier in the frame, so it can no longer be associated this
+  // frame -- every such effect is a vote or a projected-rect recompute): applied in order
+  // when the forest completes, with the pose of their frame (ReplayEngine::associate).
+  enum { DFR_PROJ = 0, DFR_PROJ_IF_NP = 1, DFR_VOTE_IF_NP = 2 };
+  struct Dfr {
+    int kind;
+    Det* det;     // the detection whose NP verdict against this object decides (kinds 1, 2)
+    Obj* target;  // the object that receives the vote (kind 2)
+  };
+  std::vector<Dfr> dfr;
+  float dfrT[16];
+  bool proj_dfr = false;  // a projected-rect recompute is among them
 };
 const float* Det::P() const { return alias ? alias->center : pos; }
 
@@ -1156,6 +1170,31 @@ class ReplayEngine {
       sample_yaw(o, o->yawT);
     }
     const eao_np_stats* sps = sworld > 1 ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
+    if (!o->dfr.empty()) {  // effects of later same-frame detections, in their order
+      for (const Obj::Dfr& d : o->dfr) {
+        if (d.kind != Obj::DFR_PROJ) {
+          // NP verdict of (d.det, o) on the post-forest cloud: one of the speculative
+          // pairs evaluated behind this forest (kick() includes every later detection)
+          int v = -2;
+          if (b.fid == d.det->fid)
+            for (size_t q = 0; q < b.sp_obj.size(); q++)
+              if (b.sp_obj[q] == c && b.sp_det[q] == d.det->index) {
+                v = sps[q].verdict;
+                break;
+              }
+          if (v < 0) {
+            set_error(v == -2 ? "replay: deferred NP verdict missing" : "replay: NP pair outside kernel capacity");
+            pend_err = v == -2 ? EAO_E_STATE : EAO_E_CAPACITY;
+            continue;
+          }
+          if (v == 2) continue;  // fails: the object was not in vNP
+        }
+        if (d.kind == Obj::DFR_VOTE_IF_NP) reobj(d.target, o->id);
+        else proj_with(o, o->dfrT);
+      }
+      o->dfr.clear();
+      o->proj_dfr = false;
+    }
     if (b.fid == cur)
       for (size_t q = 0; q < b.sp_obj.size(); q++)
         if (b.sp_obj[q] == c) np_cache[{b.sp_det[q], o->id}] = NpEntry{sps[q], b.sp_ver[q]};
@@ -1200,6 +1239,38 @@ class ReplayEngine {
     if (ymx > pz.rows) ymx = (float)pz.rows;
     o->proj = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
   }
+
+  // ComputeProjectRectFrame under a stored pose (a deferred recompute, complete_forest)
+  void proj_with(Obj* o, const float* T) {
+    if (o->pts.empty()) return;
+    Pose pv = pz;
+    std::memcpy(pv.T, T, sizeof(pv.T));
+    float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+    for (MapPt* p : o->pts) {
+      float u, v;
+      pv.proj(p->pos, u, v);
+      xmn = std::min(xmn, u);
+      xmx = std::max(xmx, u);
+      ymn = std::min(ymn, v);
+      ymx = std::max(ymx, v);
+    }
+    if (xmn < 0) xmn = 0;
+    if (ymn < 0) ymn = 0;
+    if (xmx > pz.cols) xmx = (float)pz.cols;
+    if (ymx > pz.rows) ymx = (float)pz.rows;
+    o->proj = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
+  }
+  void defer(Obj* o, int kind, Det* f, Obj* target) {
+    if (o->dfr.empty()) std::memcpy(o->dfrT, pz.T, sizeof(o->dfrT));
+    o->dfr.push_back(Obj::Dfr{kind, f, target});
+    if (kind != Obj::DFR_VOTE_IF_NP) o->proj_dfr = true;
+  }
+  // an object updated earlier in this frame whose forest has not completed: a later
+  // detection's decisions cannot associate it (DataAssociateUpdate returns false), so
+  // its forest-dependent effects on them are deferred instead of waited for
+  bool held(const Obj* o) const { return o->pending && o->last_add == (int)cur; }
+  // o->proj is about to be read: apply a deferred recompute first
+  int proj_read(Obj* o) { return o->proj_dfr ? touch(o) : EAO_OK; }
 
   // projected rects (step 10.1, Object_Map::ComputeProjectRectFrame) of `list`
   // and NoParaDataAssociation statistics of the (det, obj) `pairs`: one packed
@@ -1410,6 +1481,13 @@ class ReplayEngine {
   // Object_Map::DataAssociateUpdate, Object.cc:1313-1554
   bool update(Obj* o, Det* f, int Flag) {
     if (f->cls != o->cls) return false;
+    if (held(o)) {
+      // already updated in this frame: the reference returns false at the mnLastAddID
+      // check below; of the work before it only the projected rect of flags 2/3 (from the
+      // post-forest points) is an effect, and it is deferred to the forest's completion
+      if (Flag == 2 || Flag == 3) defer(o, Obj::DFR_PROJ, f, nullptr);
+      return false;
+    }
     if (touch(o)) return false;
     if (Flag != 1 && Flag != 4) {
       project_rect_host(o);
@@ -1506,8 +1584,14 @@ class ReplayEngine {
     cur_np_done = false;
     int rc;
     {
-      Tick tk(&prof[16]);  // waits for same-class forests
-      rc = flush(f->cls);
+      Tick tk(&prof[16]);
+      // same-class objects with a pending forest were updated earlier in this frame (the
+      // frame start completed the older ones): they are held, not waited for (held());
+      // launch their forests now, with this and every later detection's NP pairs behind them
+      for (auto& up : objs)
+        if (up->cls == f->cls && up->pending && !held(up.get()))
+          if ((rc = touch(up.get()))) return rc;
+      rc = kick();
     }
     if (rc) return rc;
     const IRect RC = f->box;
@@ -1560,6 +1644,7 @@ class ReplayEngine {
           Obj* o = objs[i].get();
           if (f->cls != o->cls || o->bad) continue;
           if (byIou && i == iouId) continue;  // its verdict is never used (Object.cc:283-284)
+          if (held(o)) continue;  // verdict at its forest's completion
           if (!np_fresh(f->index, i)) need.push_back(i);
         }
       }
@@ -1584,11 +1669,18 @@ class ReplayEngine {
         if (rc) return rc;
       }
       cur_np_done = true;
+      // vNP in the reference's order; a held object (verdict pending) enters as -1 - i:
+      // it would fail DataAssociateUpdate, so it only decides votes and a rect recompute
+      std::vector<int> ord;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {
         Obj* o = objs[i].get();
         if (f->cls != o->cls || o->bad) continue;
         if (m_small) break;  // verdict 0
         if (byIou && i == iouId) continue;
+        if (held(o)) {
+          ord.push_back(-1 - i);
+          continue;
+        }
         const int v = np_cache[{f->index, i}].st.verdict;
         if (v < 0) {
           set_error("replay: NP pair outside kernel capacity");
@@ -1596,22 +1688,33 @@ class ReplayEngine {
         }
         if (v == 2) continue;
         vNP.push_back(i);
+        ord.push_back(i);
       }
-      if (!vNP.empty()) {
-        if (byIou) {
-          for (int k : vNP)
+      if (byIou) {
+        for (int k : ord) {
+          if (k >= 0) {
             if (k != iouId) reobj(objs[iouId].get(), objs[k]->id);
-        } else {
-          for (size_t i = 0; i < vNP.size(); i++) {
-            if (update(objs[vNP[i]].get(), f, 2)) {
+          } else {
+            defer(objs[-1 - k].get(), Obj::DFR_VOTE_IF_NP, f, objs[iouId].get());
+          }
+        }
+      } else {
+        Obj* won = nullptr;
+        for (int k : ord) {
+          if (!won) {
+            if (k < 0) {
+              // in vNP iff it passes: its failed update would recompute its projected rect
+              defer(objs[-1 - k].get(), Obj::DFR_PROJ_IF_NP, f, nullptr);
+            } else if (update(objs[k].get(), f, 2)) {
               byNp = true;
-              npId = vNP[i];
+              npId = k;
               f->method = 2;
-              if (vNP.size() > i + 1) {
-                for (size_t j = i + 1; j < vNP.size(); j++) reobj(objs[vNP[i]].get(), objs[vNP[j]]->id);
-                break;
-              }
+              won = objs[k].get();
             }
+          } else if (k >= 0) {
+            reobj(won, objs[k]->id);
+          } else {
+            defer(objs[-1 - k].get(), Obj::DFR_VOTE_IF_NP, f, won);
           }
         }
       }
@@ -1626,6 +1729,7 @@ class ReplayEngine {
         Obj* o = objs[i].get();
         if (f->cls != o->cls || o->bad) continue;
         if (f->pts.size() >= 10 && (int)o->frames.size() > 8) continue;
+        if ((rc = proj_read(o))) return rc;
         const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
         if (a >= 0.25 && a > fmax) {
           fmax = a;
@@ -1661,6 +1765,7 @@ class ReplayEngine {
         if (f->cls != o->cls || o->bad) continue;
         const int df = (int)o->frames.size();
         if (df <= 8) continue;
+        if ((rc = proj_read(o))) return rc;
         const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
         const float dx = std::fabs(o->center[0] - f->pos[0]), dy = std::fabs(o->center[1] - f->pos[1]),
                     dz = std::fabs(o->center[2] - f->pos[2]);
@@ -1799,6 +1904,7 @@ class ReplayEngine {
       f->bh = boxes[5 * k + 4];
       f->box = IRect(f->bx, f->by, f->bw, f->bh);
       f->index = k;
+      f->fid = fid;
       maxcls = std::max(maxcls, f->cls);
       o2.push_back(f.get());
       dets.push_back(std::move(f));
@@ -1994,7 +2100,9 @@ class ReplayEngine {
             bool ov = false;
             for (int j = (int)objs.size() - 1; j >= 0; j--) {
               if (objs[j]->bad || i == j) continue;
-              if ((rc = touch(o)) || (rc = touch(objs[j].get()))) return rc;  // cuboids read
+              // cuboids read: final unless a new object's ComputeMeanAndStandard follows its forest
+              if ((o->pending == 2 && (rc = touch(o))) || (objs[j]->pending == 2 && (rc = touch(objs[j].get()))))
+                return rc;
               if (overlap(o, objs[j].get())) {
                 ov = true;
                 break;

@@ -114,7 +114,8 @@ def extract_match_mt(frames, Tcw, has, mpos, scales, threads, th=15, check_ori=1
     nkp, match, nmatch). has/mpos: map state of each frame's keypoints, cap slots."""
     frames = np.ascontiguousarray(frames, np.uint8)
     n, h, w = frames.shape
-    cap = nfeatures + 64 * nlevels + 64
+    cap = has.shape[1]  # keypoint slots per frame: the caller's map-state row stride
+    assert has.shape == (n, cap) and mpos.shape == (n, cap, 3)
     kps = np.zeros((n, cap), KP_DTYPE)
     desc = np.zeros((n, cap, 32), np.uint8)
     nkp = np.zeros(n, np.int32)

@@ -103,3 +103,24 @@ def test_host_run_stream_matches_oracle(harness):
     gi, gf, _ = g.objects()
     oi, of, _ = o.objects()
     assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+
+
+@pytest.mark.parametrize("flag", ["EAO", "Full"])
+def test_host_fr3_real_stream_matches_oracle(harness, flag):
+    """The reference's fr3 detections (tools/synth.assoc_stream_fr3_real): many same-class
+    boxes per frame, so later detections meet objects whose forests are still pending
+    (the held / deferred path of replay.cpp's associate) on every frame."""
+    frames = synth.assoc_stream_fr3_real()[:150]
+    g = _HostReplay(harness, flag)
+    det = g._with(ea.Replay.run, g, ea.Replay.pack(frames))
+    o = orc.Replay(flag)
+    ref = []
+    for i, f in enumerate(frames):
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines")))
+        if f["kf"]:
+            o.local_mapping()
+    assert np.array_equal(det, np.concatenate(ref))
+    gi, gf, gp = g.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert all(np.array_equal(x, y) for x, y in zip(gp, op))

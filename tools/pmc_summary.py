@@ -1,6 +1,7 @@
 """Per-kernel PMC summary of a rocprofv3 --pmc database (rocpd sqlite):
-mean counter value per dispatch; FETCH_SIZE doubled (gfx950 correction,
-MI355X_MICROARCH.md HBM section) and reported in bytes."""
+mean counter value per dispatch; FETCH_SIZE / WRITE_SIZE in bytes with FETCH_SIZE
+doubled (gfx950 correction, MI355X_MICROARCH.md HBM section); SQ_* counters raw
+(SQ_INSTS_* per wave instruction; SQ_*_CYCLES in quad-cycles)."""
 import sqlite3
 import sys
 
@@ -17,12 +18,15 @@ def main(db, out=None):
         v = r[idx["value"]]
         d = agg.setdefault(name, {}).setdefault(cn, [])
         d.append(v)
-    lines = ["%-32s %-12s %10s %16s %16s" % ("kernel", "counter", "dispatches", "mean/dispatch", "corrected_B")]
+    lines = ["%-32s %-20s %10s %16s %16s" % ("kernel", "counter", "dispatches", "mean/dispatch", "corrected")]
     for k, cs in sorted(agg.items()):
         for cn, vs in sorted(cs.items()):
             m = sum(vs) / len(vs)
-            corr = m * 1024 * (2 if cn == "FETCH_SIZE" else 1)  # FETCH/WRITE_SIZE are in KiB
-            lines.append("%-32s %-12s %10d %16.1f %16.0f" % (k[:32], cn, len(vs), m, corr))
+            if cn in ("FETCH_SIZE", "WRITE_SIZE"):  # KiB -> bytes; FETCH_SIZE doubled (gfx950)
+                corr = m * 1024 * (2 if cn == "FETCH_SIZE" else 1)
+            else:
+                corr = m
+            lines.append("%-32s %-20s %10d %16.1f %16.0f" % (k[:32], cn, len(vs), m, corr))
     txt = "\n".join(lines) + "\n"
     if out:
         open(out, "w").write(txt)

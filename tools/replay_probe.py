@@ -1,6 +1,6 @@
 """Wall-clock breakdown of the association replay on the engine (development aid).
 
-python tools/replay_probe.py [dense] [full]   -- prints eao_replay_profile's counters per pass."""
+python tools/replay_probe.py [synth] [full]   -- prints eao_replay_profile's counters per pass."""
 import os
 import sys
 import time
@@ -20,16 +20,16 @@ NAMES = {0: "frame", 1: "local_mapping", 2: "#forest_launch", 3: "forest_complet
          17: "pending_flush", 18: "kick", 19: "launch", 20: "#retire", 21: "retire", 22: "kick_scan",
          23: "pack"}
 
-if "full" in sys.argv:
-    frames = synth.assoc_stream_fr3(2582)
-elif "dense" in sys.argv:
-    frames = synth.assoc_stream(405)
-else:
-    frames = synth.assoc_stream_fr3(405)
+if "full" in sys.argv:  # BASELINE configs[2]: the Full list, real detections
+    frames, flag = synth.assoc_stream_fr3_real(0, 2582), "Full"
+elif "synth" in sys.argv:  # round-1 synthetic stream
+    frames, flag = synth.assoc_stream_fr3(405), "EAO"
+else:  # BASELINE configs[1]: the demo list, real detections
+    frames, flag = synth.assoc_stream_fr3_real(), "EAO"
 packed = ea.Replay.pack(frames)
 a = ea.Assoc()
 for rep in range(3):
-    rp = ea.Replay(a, "EAO")
+    rp = ea.Replay(a, flag)
     t0 = time.perf_counter()
     rp.run(packed)
     dt = time.perf_counter() - t0
