@@ -33,6 +33,9 @@ class AssocEngine {
   uint32_t cached_seed = 0, cached_trees = 0;
   size_t lds_limit = 0;
   double* d_scores = nullptr;    // [max_points]
+  // the erase decision of IsolationForestDeleteOutliers, score > th (th = 0.6f, or 0.65f
+  // for class 62), taken exactly as glibc's pow would: x = -E[h]/c(psi) >= pow_x0[k]
+  double pow_x0[2] = {0, 0};
   int max_pairs = 256, max_clouds = 64, max_trees = 64;
   // resources a finished association replay hands to the next one on this
   // engine (forest batch slots, streams, pinned staging; opaque, replay.cpp)
@@ -45,7 +48,9 @@ class AssocEngine {
   int np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                const int* d_flen, const float* d_op, const uint8_t* d_ov, const int* d_ooff,
                const int* d_olen, eao_np_stats* d_out, hipStream_t s, int max_olen,
-               const double* d_oscore = nullptr, const float* d_oth = nullptr);
+               // per pair: the device scores of the object's pending forest (null: none) and its
+               // erase threshold -- the erasure is applied on the fly
+               const double* const* d_os_ptr = nullptr, const float* d_oth = nullptr);
   int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
                     hipStream_t s, int max_len, int max_sample, int npts_total,
@@ -54,7 +59,8 @@ class AssocEngine {
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples
   bool iforest_fits(int max_len, int max_sample) const;
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
-            const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s);
+            const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s,
+            const double* const* d_os_ptr = nullptr, const float* d_oth = nullptr);
 };
 
 AssocEngine* assoc_engine(eao_assoc* a);

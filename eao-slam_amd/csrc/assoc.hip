@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ ov,
                                                   const int* __restrict__ ooff,
                                                   const int* __restrict__ olen, int Pmax,
-                                                  const double* __restrict__ oscore,
+                                                  const double* const* __restrict__ os_ptr,
                                                   const float* __restrict__ oth,
                                                   eao_np_stats* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float dsm[];
@@ -176,9 +176,11 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   const int ntot = olen[p];
   // optional isolation-forest erasure applied on the fly (points with score >
   // th leave the object, Object.cc:1284-1300): the pair is then evaluated on
-  // the object exactly as it stands after IsolationForestDeleteOutliers
-  const double* OS = oscore ? oscore + ooff[p] : nullptr;
-  const float th = oscore ? oth[p] : 0.f;
+  // the object exactly as it stands after IsolationForestDeleteOutliers. The
+  // scores are the forest's device output, read once the forest has completed
+  // (stream order / an event wait before this launch); null: no pending forest
+  const double* OS = os_ptr ? os_ptr[p] : nullptr;
+  const float th = OS ? oth[p] : 0.f;
   auto kept = [&](int i) { return !OS || !(OS[i] > (double)th); };
   int cnt3[3] = {0, 0, 0};
   for (int i = t; i < mt; i += 256) cnt3[0] += FV[i] ? 1 : 0;
@@ -278,15 +280,26 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
                                                const float* __restrict__ pts,
                                                const int* __restrict__ off,
                                                const int* __restrict__ len, int* __restrict__ rect,
-                                               uint8_t* __restrict__ ok) {
+                                               uint8_t* __restrict__ ok,
+                                               const double* const* __restrict__ os_ptr,
+                                               const float* __restrict__ oth) {
   __shared__ float red[4][4];
+  __shared__ int s_kept;
   const int c = blockIdx.x, t = threadIdx.x;
-  const int n = len[c];
+  int n = len[c];
   const float* P = pts + 3 * (long long)off[c];
+  // a pending isolation forest's erasure applied on the fly (as in k_np_pairs)
+  const double* OS = os_ptr ? os_ptr[c] : nullptr;
+  const double th = OS ? (double)oth[c] : 0.0;
+  if (t == 0) s_kept = 0;
   float T[16];
   for (int k = 0; k < 16; k++) T[k] = Tg[k];
   float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
+  int kept = 0;
+  __syncthreads();
   for (int i = t; i < n; i += 256) {
+    if (OS && OS[i] > th) continue;
+    kept++;
     float u, v;
     project_pt(cam, T, P + 3 * i, u, v);
     xmn = fminf(xmn, u);
@@ -300,6 +313,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
     ymn = fminf(ymn, __shfl_xor(ymn, o, 64));
     ymx = fmaxf(ymx, __shfl_xor(ymx, o, 64));
   }
+  if (OS && kept) atomicAdd(&s_kept, kept);
   const int w = t >> 6;
   if ((t & 63) == 0) {
     red[w][0] = xmn;
@@ -315,6 +329,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
       ymn = fminf(ymn, red[k][2]);
       ymx = fmaxf(ymx, red[k][3]);
     }
+    if (OS) n = s_kept;
     if (n <= 0) {
       ok[c] = 0;
       return;
@@ -776,7 +791,8 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   if_stamp(7);
 }
 
-// score = 2^(-E[h(x)] / c(psi)), E[h] summed over the trees in order
+// score = 2^(-E[h(x)] / c(psi)), E[h] summed over the trees in order (GetAnomalyScores,
+// isolation_forest.h:499-530)
 __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off,
                                                      const int* __restrict__ len,
                                                      const uint32_t* __restrict__ sample,
@@ -784,7 +800,7 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
                                                      int ntrees, int npts_total,
                                                      const double* __restrict__ contrib,
                                                      double* __restrict__ scores,
-                                                     double* __restrict__ scores2) {
+                                                     double* __restrict__ scores2, double x0a, double x0b) {
   const int c = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len[c]) return;
@@ -792,14 +808,54 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
   double total = 0;
 #pragma unroll 10
   for (int t = 0; t < ntrees; t++) total += contrib[(long long)t * npts_total + g];
-  const double avg = total / (double)ntrees;
-  const double sc = pow(2.0, -avg / ctab[sample[c]]);
+  const double x = -(total / (double)ntrees) / ctab[sample[c]];
+  double sc = pow(2.0, x);
+  // IsolationForestDeleteOutliers erases score > 0.6f (0.65f for class 62), Object.cc:
+  // 1284-1300, with glibc's pow: make `sc > th` agree with its exact decision x >= x0
+  // for both thresholds (only scores within an ulp or two of a threshold move)
+  const double tha = (double)0.6f, thb = (double)0.65f;
+  if (x >= x0a) {
+    if (!(sc > tha)) sc = __longlong_as_double(__double_as_longlong(tha) + 1);
+  } else if (sc > tha) {
+    sc = tha;
+  }
+  if (x >= x0b) {
+    if (!(sc > thb)) sc = __longlong_as_double(__double_as_longlong(thb) + 1);
+  } else if (sc > thb) {
+    sc = thb;
+  }
   scores[g] = sc;
   if (scores2) scores2[g] = sc;
 }
 
 
 // ================================================================ host
+// The smallest double x with pow(2, x) > th under this host's libm (glibc, as the
+// reference's IsolationForestDeleteOutliers computes the score): the erase decision
+// score > th is then x >= x0 exactly, on the host and on the device (k_iforest_tree).
+// Checked monotone over +-256 ulps around it.
+static double pow_threshold(double th) {
+  double lo = std::log2(th) - 1e-9, hi = std::log2(th) + 1e-9;
+  while (!(std::pow(2.0, lo) <= th)) lo -= 1e-9;
+  while (!(std::pow(2.0, hi) > th)) hi += 1e-9;
+  while (std::nextafter(lo, hi) < hi) {
+    double mid = lo + (hi - lo) / 2;
+    if (mid <= lo || mid >= hi) mid = std::nextafter(lo, hi);
+    if (std::pow(2.0, mid) > th) hi = mid;
+    else lo = mid;
+  }
+  double a = hi, b = hi;
+  for (int k = 0; k < 256; k++) {
+    a = std::nextafter(a, -INFINITY);
+    if (std::pow(2.0, a) > th || !(std::pow(2.0, b) > th)) {
+      set_error("pow_threshold: libm pow not monotone near the iForest threshold");
+      break;
+    }
+    b = std::nextafter(b, INFINITY);
+  }
+  return hi;
+}
+
 int AssocEngine::init(int device, int mp) {
   dev = device;
   max_points = mp;
@@ -821,6 +877,8 @@ int AssocEngine::init(int device, int mp) {
   EAO_HIP_CHECK(hipMalloc(&d_mtinit, sizeof(uint32_t) * 624 * max_trees));
   EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)mp));
   EAO_HIP_CHECK(hipMalloc(&d_contrib, sizeof(double) * (size_t)mp * max_trees));
+  pow_x0[0] = pow_threshold((double)0.6f);
+  pow_x0[1] = pow_threshold((double)0.65f);
   {  // CalculateC (isolation_forest.h:97-118) of every leaf / sample size, host libm like the reference
     std::vector<double> c(IF_MAXN + 1, 0.0);
     for (int k = 2; k <= IF_MAXN; k++) {
@@ -851,12 +909,12 @@ AssocEngine::~AssocEngine() {
 int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                           const int* d_flen, const float* d_op, const uint8_t* d_ov,
                           const int* d_ooff, const int* d_olen, eao_np_stats* d_out,
-                          hipStream_t s, int max_olen, const double* d_oscore, const float* d_oth) {
+                          hipStream_t s, int max_olen, const double* const* d_os_ptr, const float* d_oth) {
   if (npairs <= 0) return EAO_OK;
   int P = 8;
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
   hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), sizeof(float) * 3 * P, s, d_fp, d_fv, d_foff,
-                     d_flen, d_op, d_ov, d_ooff, d_olen, P, d_oscore, d_oth, d_out);
+                     d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -922,7 +980,8 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
                      d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
-                     d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2);
+                     d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,
+                     pow_x0[0], pow_x0[1]);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -932,9 +991,10 @@ bool AssocEngine::iforest_fits(int max_len, int max_sample) const {
 }
 
 int AssocEngine::rects(const CamDev& cam, const float* Tg, int nclouds, const float* pts,
-                       const int* off, const int* len, int* rect, uint8_t* ok, hipStream_t s) {
+                       const int* off, const int* len, int* rect, uint8_t* ok, hipStream_t s,
+                       const double* const* os_ptr, const float* oth) {
   if (nclouds <= 0) return EAO_OK;
-  hipLaunchKernelGGL(k_rects, dim3(nclouds), dim3(256), 0, s, cam, Tg, pts, off, len, rect, ok);
+  hipLaunchKernelGGL(k_rects, dim3(nclouds), dim3(256), 0, s, cam, Tg, pts, off, len, rect, ok, os_ptr, oth);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -1068,6 +1128,12 @@ int eao_project_rects(eao_assoc* a, const eao_camera* cam, const float* Tcw, int
   EAO_HIP_CHECK(hipMemcpyAsync(rect, e.d_rect, sizeof(int) * 4 * nclouds, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipMemcpyAsync(ok, e.d_ok, nclouds, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  return EAO_OK;
+}
+
+int eao_iforest_erase_threshold(float th, double* x0) {
+  if (!x0 || !(th > 0.0f && th < 1.0f)) return EAO_E_ARG;
+  *x0 = pow_threshold((double)th);
   return EAO_OK;
 }
 

@@ -317,8 +317,13 @@ class ReplayEngine {
   CamDev camdev;
   bool biForest = true;  // Object.cc:31 (sticky)
   std::vector<std::unique_ptr<Obj>> objs;
-  // map points by id: dense table for ids in [0, 2^24), a map beyond
-  std::vector<std::unique_ptr<MapPt>> mps_dense;
+  // map points by id: ids in [0, 2^24) live in an arena of fixed blocks indexed by id
+  // (stable addresses, and the points of an object -- ids of one neighbourhood -- sit
+  // next to each other, so the host loops over clouds stream instead of chasing
+  // pointers); other ids in a map
+  static constexpr int kMpBlock = 1024;
+  std::vector<std::unique_ptr<MapPt[]>> mp_blocks;
+  std::vector<std::unique_ptr<uint8_t[]>> mp_live;
   std::map<int, std::unique_ptr<MapPt>> mps;
   PosSet posset;
   unsigned epoch = 1;  // bumped whenever the pose changes
@@ -331,19 +336,30 @@ class ReplayEngine {
     v = p->pv;
   }
   MapPt* mp_lookup(int id) {  // existing map point or null
-    if (id >= 0 && id < (1 << 24)) return (size_t)id < mps_dense.size() ? mps_dense[id].get() : nullptr;
+    if (id >= 0 && id < (1 << 24)) {
+      const size_t b = (size_t)id / kMpBlock, k = (size_t)id % kMpBlock;
+      return b < mp_blocks.size() && mp_live[b] && mp_live[b][k] ? &mp_blocks[b][k] : nullptr;
+    }
     auto it = mps.find(id);
     return it == mps.end() ? nullptr : it->second.get();
   }
   MapPt* mappoint(int id) {
     if (id >= 0 && id < (1 << 24)) {
-      if ((size_t)id >= mps_dense.size()) mps_dense.resize(std::max((size_t)id + 1, mps_dense.size() * 2));
-      std::unique_ptr<MapPt>& u = mps_dense[id];
-      if (!u) {
-        u.reset(new MapPt());
-        u->id = id;
+      const size_t b = (size_t)id / kMpBlock, k = (size_t)id % kMpBlock;
+      if (b >= mp_blocks.size()) {
+        mp_blocks.resize(b + 1);
+        mp_live.resize(b + 1);
       }
-      return u.get();
+      if (!mp_blocks[b]) {
+        mp_blocks[b].reset(new MapPt[kMpBlock]);
+        mp_live[b].reset(new uint8_t[kMpBlock]());
+      }
+      MapPt* p = &mp_blocks[b][k];
+      if (!mp_live[b][k]) {
+        mp_live[b][k] = 1;
+        p->id = id;
+      }
+      return p;
     }
     std::unique_ptr<MapPt>& u = mps[id];
     if (!u) {
@@ -991,13 +1007,15 @@ class ReplayEngine {
       b.launched = nl > 0;
       if (!b.launched) continue;
       // in: forest meta [3 nl] | object points [3 np] | object valid [np] | NP meta [4 ns] | th [ns] |
-      //     frame points [3 nfp] | frame valid [nfp]
-      // out (host): scores [np] doubles | NP stats [ns]; device: scores [np] for the NP kernel
+      //     score pointers [ns] | frame points [3 nfp] | frame valid [nfp]
+      // out (host): scores [np] doubles | NP stats [ns]; device: scores [np] for the NP kernels
+      // (the speculative pairs here, the next frame start's rects / pairs, frame_start_gpu)
       const size_t o_pts = al16(sizeof(int) * 3 * nl);
       const size_t o_oval = o_pts + sizeof(float) * 3 * (size_t)np;
       const size_t o_spm = al16(o_oval + np);
       const size_t o_th = o_spm + sizeof(int) * 4 * ns;
-      const size_t o_fp = al16(o_th + sizeof(float) * ns);
+      const size_t o_osp = al16(o_th + sizeof(float) * ns);
+      const size_t o_fp = al16(o_osp + sizeof(double*) * ns);
       const size_t o_fval = o_fp + sizeof(float) * 3 * (size_t)nfp;
       const size_t in_bytes = ns ? o_fval + nfp : o_pts + sizeof(float) * 3 * (size_t)np;
       b.sp_out = al16(sizeof(double) * np);
@@ -1033,6 +1051,7 @@ class ReplayEngine {
       if (ns) {
         int* spm = (int*)(b.h_in + o_spm);
         float* th = (float*)(b.h_in + o_th);
+        const double** osp = (const double**)(b.h_in + o_osp);
         float* fpt = (float*)(b.h_in + o_fp);
         uint8_t* fval = b.h_in + o_fval;
         for (size_t z = 0; z < sdets.size(); z++) {
@@ -1050,6 +1069,7 @@ class ReplayEngine {
           spm[2 * ns + j] = b.loff[c];
           spm[3 * ns + j] = (int)o->pts.size();
           th[j] = o->cls == 62 ? 0.65f : 0.6f;
+          osp[j] = (const double*)b.d_out + b.loff[c];  // device scores of this forest
         }
       }
       hipStream_t st = if_stream[k % kIfStreams];
@@ -1062,14 +1082,14 @@ class ReplayEngine {
       // NP pairs, to device memory too
       int rc = A->iforest_batch(nl, (const float*)(b.d_in + o_pts), dm, dm + nl, 50, 12345,
                                 (const uint32_t*)(dm + 2 * nl), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
-                                ns ? (double*)b.d_out : nullptr);
+                                (double*)b.d_out);
       if (rc) return rc;
       if (ns) {
         const int* spm = (const int*)(b.d_in + o_spm);
         const float* dfp = (const float*)(b.d_in + o_fp);
         rc = A->np_batch(ns, dfp, b.d_in + o_fval, spm, spm + ns, (const float*)(b.d_in + o_pts), b.d_in + o_oval,
                          spm + 2 * ns, spm + 3 * ns, (eao_np_stats*)(b.h_out + b.sp_out), st, max_olen,
-                         (const double*)b.d_out, (const float*)(b.d_in + o_th));
+                         (const double* const*)(b.d_in + o_osp), (const float*)(b.d_in + o_th));
         if (rc) return rc;
         prof[9] += ns;
       }
@@ -1296,11 +1316,33 @@ class ReplayEngine {
       add(pr.first, pr.first->pts);
       add(pr.second, pr.second->pts);
     }
-    // in: rect meta [2 nb] | pair meta [4 npairs] | Tcw [16] | points [3 total] | valid [total]
+    // objects whose isolation forest is still running: their clouds are uploaded as they
+    // stand and the kernels, queued behind the forest (event wait), drop the points the
+    // forest erases on the fly -- the host completes the forest after this launch
+    std::vector<const double*> os_l(nb, nullptr), os_p(npairs, nullptr);
+    std::vector<float> th_l(nb, 0.f), th_p(npairs, 0.f);
+    std::vector<int> wait_slots;
+    bool chained = false;
+    auto inflight = [&](Obj* o, const double*& ptr, float& th) {
+      if (sworld != 1 || !o->pending || o->slot < 0) return;
+      IfBatch& b = ifb[o->slot];
+      if (!b.launched) return;
+      int c = 0;
+      while (b.objs[c] != o) c++;
+      ptr = (const double*)b.d_out + b.loff[c];
+      th = o->cls == 62 ? 0.65f : 0.6f;
+      chained = true;
+      if (std::find(wait_slots.begin(), wait_slots.end(), o->slot) == wait_slots.end()) wait_slots.push_back(o->slot);
+    };
+    for (int b = 0; b < nb; b++) inflight(list[b], os_l[b], th_l[b]);
+    for (int k = 0; k < npairs; k++) inflight(pairs[k].second, os_p[k], th_p[k]);
+    // in: rect meta [2 nb] | pair meta [4 npairs] | Tcw [16] | points [3 total] | valid [total] |
+    //     (chained) score pointers [nb + npairs] | thresholds [nb + npairs]
     // out: stats [npairs] | rects [4 nb] | ok [nb]
     const size_t o_pm = sizeof(int) * 2 * (size_t)nb, o_T = al16(o_pm + sizeof(int) * 4 * (size_t)npairs);
     const size_t o_pts = o_T + sizeof(float) * 16, o_val = o_pts + sizeof(float) * 3 * total;
-    const size_t in_bytes = o_val + total;
+    const size_t o_osp = al16(o_val + total), o_oth = o_osp + sizeof(double*) * (size_t)(nb + npairs);
+    const size_t in_bytes = chained ? o_oth + sizeof(float) * (size_t)(nb + npairs) : o_val + total;
     const size_t o_r = sizeof(eao_np_stats) * (size_t)npairs, o_ok = o_r + sizeof(int) * 4 * (size_t)nb;
     int rc = stage(in_bytes, o_ok + nb);
     if (rc) return rc;
@@ -1328,23 +1370,38 @@ class ReplayEngine {
       pmeta[npairs + k] = (int)pr.first->pts.size();
       pmeta[2 * npairs + k] = offs[pr.second];
       pmeta[3 * npairs + k] = (int)pr.second->pts.size();
-      if (pmeta[3 * npairs + k] > NP_MAXN) {
+      if (pmeta[3 * npairs + k] > NP_MAXN && !os_p[k]) {  // chained: the kernel checks after the erasure
         set_error("replay: object exceeds the NP kernel capacity");
         return EAO_E_CAPACITY;
       }
       max_olen = std::max(max_olen, pmeta[3 * npairs + k]);
     }
+    if (chained) {
+      const double** osp = (const double**)(h_in + o_osp);
+      float* oth = (float*)(h_in + o_oth);
+      for (int b = 0; b < nb; b++) {
+        osp[b] = os_l[b];
+        oth[b] = th_l[b];
+      }
+      for (int k = 0; k < npairs; k++) {
+        osp[nb + k] = os_p[k];
+        oth[nb + k] = th_p[k];
+      }
+    }
     EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
+    for (int k : wait_slots) EAO_HIP_CHECK(hipStreamWaitEvent(A->stream, ifb[k].ev, 0));
     const int* drm = (const int*)d_in;
     const int* dpm = (const int*)(d_in + o_pm);
     const float* dpts = (const float*)(d_in + o_pts);
     const uint8_t* dval = d_in + o_val;
+    const double* const* dosp = chained ? (const double* const*)(d_in + o_osp) : nullptr;
+    const float* doth = chained ? (const float*)(d_in + o_oth) : nullptr;
     // results go straight into pinned host memory
     rc = A->rects(camdev, (const float*)(d_in + o_T), nb, dpts, drm, drm + nb, (int*)(h_out + o_r), h_out + o_ok,
-                  A->stream);
+                  A->stream, dosp, doth);
     if (rc) return rc;
     rc = A->np_batch(npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
-                     (eao_np_stats*)h_out, A->stream, max_olen);
+                     (eao_np_stats*)h_out, A->stream, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
@@ -1412,18 +1469,30 @@ class ReplayEngine {
                       const std::vector<int>& di, const std::vector<int>& oi) {
     if (list.empty() && pairs.empty()) return EAO_OK;
     if (int rc = kick()) return rc;  // pending forests overlap this launch
-    {  // forests left pending by the previous frame: their objects' points are read now
+    auto complete_pending = [&]() -> int {
+      // forests left pending by the previous frame: their objects' points are read now
       Tick tk(&prof[17]);
       if (int rc = flush_list(list)) return rc;
       for (auto& pr : pairs)
         if (int rc = touch(pr.second)) return rc;
-    }
-    Tick tk(&prof[7]);
-    prof[6] += 1;
+      return EAO_OK;
+    };
+    // one rank: the launch is queued behind those forests on the GPU (erasure applied on
+    // the fly, rects_np_launch) and the host completes them afterwards, so the host never
+    // waits twice; sharded, the forests complete first (their outcome is all-gathered)
+    if (sworld > 1)
+      if (int rc = complete_pending()) return rc;
     std::vector<int> rects;
     std::vector<eao_np_stats> st;
-    int rc = rects_np(list, pairs, rects, st);
-    if (rc) return rc;
+    {
+      Tick tk(&prof[7]);
+      prof[6] += 1;
+      if (int rc = rects_np(list, pairs, rects, st)) return rc;
+    }
+    // completion before the results are applied: a deferred projected-rect recompute of
+    // the previous frame must not overwrite this frame's step 10.1 rect
+    if (sworld == 1)
+      if (int rc = complete_pending()) return rc;
     for (size_t b = 0; b < list.size(); b++)
       if (rects[5 * b + 4]) list[b]->proj = IRect(rects[5 * b], rects[5 * b + 1], rects[5 * b + 2], rects[5 * b + 3]);
     for (size_t k = 0; k < pairs.size(); k++) np_cache[{di[k], oi[k]}] = NpEntry{st[k], over[oi[k]]};
@@ -2249,6 +2318,8 @@ class ReplayEngine {
   }
 
   int iforest_now(Obj* o) {  // synchronous forest (LocalMapping merge path)
+    Tick tk(&prof[11]);
+    prof[10] += 1;
     o->pending = std::max(o->pending, 1);
     return complete_forest(o);
   }

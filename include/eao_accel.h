@@ -213,6 +213,12 @@ int eao_np_test_batch(eao_assoc* a, int npairs, const float* frame_pts, const ui
 int eao_iforest_scores_batch(eao_assoc* a, int nclouds, const float* pts, const int32_t* off,
                              const int32_t* len, uint32_t trees, uint32_t seed,
                              const uint32_t* sample_size, double* scores);
+/* The isolation-forest erase decision score > th (IsolationForestDeleteOutliers, th = 0.6f or
+   0.65f for class 62, src/Object.cc:1284-1300) as the engine takes it: with
+   x = -E[h] / c(psi), score = pow(2, x) exceeds th exactly when x >= *x0, x0 being the
+   smallest double for which the host libm's pow(2, x) > th (so a device pow that differs
+   by an ulp cannot flip an erasure). Host-only; no device needed. */
+int eao_iforest_erase_threshold(float th, double* x0);
 
 /* Object_Map::ComputeProjectRectFrame (src/Object.cc:1558-1603) for a batch of
    clouds under one pose; rect[c*4] = x,y,w,h (cv::Rect). Empty cloud -> rect

@@ -21,12 +21,13 @@ CamDev make_cam(const eao_camera& c) {
 }
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
-                          eao_np_stats* out, hipStream_t, int, const double* oscore, const float* oth) {
+                          eao_np_stats* out, hipStream_t, int, const double* const* os_ptr, const float* oth) {
   for (int p = 0; p < npairs; p++) {
     std::vector<float> pts;
     std::vector<uint8_t> val;
+    const double* os = os_ptr ? os_ptr[p] : nullptr;
     for (int i = 0; i < olen[p]; i++) {  // the forest's erasure, as the kernel applies it
-      if (oscore && oscore[ooff[p] + i] > (double)oth[p]) continue;
+      if (os && os[i] > (double)oth[p]) continue;
       pts.insert(pts.end(), op + 3 * (ooff[p] + i), op + 3 * (ooff[p] + i) + 3);
       val.push_back(ov[ooff[p] + i]);
     }
@@ -49,9 +50,16 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
   return 0;
 }
 int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const float* pts, const int* off,
-                       const int* len, int* rect, uint8_t* ok, hipStream_t) {
+                       const int* len, int* rect, uint8_t* ok, hipStream_t, const double* const* os_ptr,
+                       const float* oth) {
   orc_camera c{(int)cam.maxX, (int)cam.maxY, cam.fx, cam.fy, cam.cx, cam.cy};
-  for (int k = 0; k < nclouds; k++) ok[k] = orc_project_rect(&c, T, len[k], pts + 3 * off[k], rect + 4 * k) == 0;
+  for (int k = 0; k < nclouds; k++) {
+    std::vector<float> kept;
+    const double* os = os_ptr ? os_ptr[k] : nullptr;
+    for (int i = 0; i < len[k]; i++)  // a pending forest's erasure, as the kernel applies it
+      if (!(os && os[i] > (double)oth[k])) kept.insert(kept.end(), pts + 3 * (off[k] + i), pts + 3 * (off[k] + i) + 3);
+    ok[k] = orc_project_rect(&c, T, (int)kept.size() / 3, kept.data(), rect + 4 * k) == 0;
+  }
   return 0;
 }
 bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }

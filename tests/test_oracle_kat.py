@@ -255,3 +255,24 @@ def test_color_to_gray_fixed_point(cn, rgb):
     assert np.array_equal(g, ref)
     white = np.full((2, 2, cn), 255, np.uint8)
     assert (orc.color_to_gray(white, rgb) == 255).all() and (orc.color_to_gray(0 * white, rgb) == 0).all()
+
+
+def test_iforest_erase_threshold_matches_libm_pow():
+    """eao_iforest_erase_threshold: the engine erases a point when x = -E[h]/c(psi) >= x0,
+    x0 the smallest double with pow(2, x) > th under glibc (what the reference's
+    2^(-E[h]/c) > 0.6 / 0.65 comparison evaluates, Object.cc:1284-1300)."""
+    import ctypes
+    import math
+    import eao_accel as ea
+    L = ea.lib()
+    for th in (0.6, 0.65):
+        x0 = ctypes.c_double()
+        assert L.eao_iforest_erase_threshold(ctypes.c_float(th), ctypes.byref(x0)) == 0
+        thd = float(np.float32(th))
+        x = x0.value
+        assert math.pow(2.0, x) > thd
+        below = x
+        for _ in range(64):
+            below = math.nextafter(below, -math.inf)
+            assert math.pow(2.0, below) <= thd
+        assert abs(x - math.log2(thd)) < 1e-12

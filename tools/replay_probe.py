@@ -15,7 +15,7 @@ from tools import synth  # noqa: E402
 
 # eao_replay_profile slots (replay.cpp prof[]): times in us, counts marked #
 NAMES = {0: "frame", 1: "local_mapping", 2: "#forest_launch", 3: "forest_complete", 4: "#np_launch",
-         5: "np_relaunch", 6: "#frame_start", 7: "frame_start_rt", 8: "#frames", 9: "#spec_np",
+         5: "np_relaunch", 6: "#frame_start", 7: "frame_start_rt", 8: "#frames", 9: "#spec_np", 10: "#lm_forests", 11: "lm_forest",
          12: "steps1-3", 13: "steps4-9", 14: "frame_start_total", 15: "assoc_loop", 16: "same_cls_flush",
          17: "pending_flush", 18: "kick", 19: "launch", 20: "#retire", 21: "retire", 22: "kick_scan",
          23: "pack"}
