@@ -1,9 +1,9 @@
 // assoc.hip -- EAO object-association kernels on gfx950 (reference src/Object.cc,
 // include/isolation_forest.h).
 //
-//   k_np_pairs     one workgroup per (detection, object) pair: the Wilcoxon
-//                  rank-sum of NoParaDataAssociation (Object.cc:714-930) as
-//                  sort + rank counting (counts identical to the O(m*n) loop)
+//   k_np_pairs     one 1024-thread workgroup per (detection, object) pair: the
+//                  Wilcoxon rank-sum of NoParaDataAssociation (Object.cc:714-930)
+//                  as sort + rank counting (counts identical to the O(m*n) loop)
 //   k_rects        one workgroup per cloud: ComputeProjectRectFrame (:1558-1603)
 //   k_iforest_tree one workgroup per (tree, cloud): IsolationTree::Build with
 //                  the libstdc++-11 mt19937 / Lemire / shuffle / canonical-float
@@ -25,6 +25,21 @@
 
 namespace eao {
 
+// in-kernel phase stamps (workgroup 0 of k_np_pairs: slots 0-7 under EAO_NP_PROF;
+// workgroup (0,0) of k_iforest_tree: slots 0-7, 10), read through
+// eao_debug_iforest_stamps: development instrumentation, a few SALU ops
+__device__ unsigned long long g_if_stamp[24];
+#ifdef EAO_NP_PROF
+#define NP_STAMP(k)                                                                   \
+  if (blockIdx.x == 0 && threadIdx.x == 0) {                                          \
+    unsigned long long _t;                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");        \
+    g_if_stamp[k] = _t;                                                               \
+  }
+#else
+#define NP_STAMP(k)
+#endif
+
 // ---------------------------------------------------------------- NP test
 __device__ __forceinline__ void cswap(float& a, float& b, bool up) {
   if ((a > b) == up) {
@@ -34,36 +49,78 @@ __device__ __forceinline__ void cswap(float& a, float& b, bool up) {
   }
 }
 
-// ascending bitonic sort of three LDS arrays at once, P = 2^e >= 8 (INF
-// padded). Runs of 8 consecutive elements are merged in registers (strides
-// 4, 2, 1); longer strides go through LDS with 4 pairs per thread in flight.
-__device__ void block_sort3(float* S0, float* S1, float* S2, int P) {
-  float* S[3] = {S0, S1, S2};
-  const int nt = blockDim.x, tid = threadIdx.x;
-  const int groups = P >> 3, half = P >> 1;
-  // k = 2, 4, 8 entirely in registers
-  for (int g = tid; g < groups; g += nt) {
-    const int base = g << 3;
+// One bitonic compare-exchange step of a 256-element run held by one wave in
+// registers (element r * 64 + lane in v[r]), partner i ^ J: lanes for J < 64 (DPP /
+// swizzle / permlane, xor_lane), registers for J = 64, 128. The pair (lo, hi) swaps
+// when (S[lo] > S[hi]) == ascending, ascending = ((i & K) == 0) with i the element's
+// index in the whole array (base + r * 64 + lane): block_sort3's exact network.
+template <int J>
+__device__ __forceinline__ void reg_step3(float (&v)[3][4], int base, int K) {
+  const int lane = threadIdx.x & 63;
+  float o[3][4];  // the values before this step (in-lane partners read them)
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) o[a][r] = v[a][r];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int i = base + r * 64 + lane;
+    const bool up = (i & K) == 0;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      float v[8];
-      const float4 lo = *(const float4*)(S[a] + base), hi = *(const float4*)(S[a] + base + 4);
-      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-#pragma unroll
-      for (int k = 2; k <= 8; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-          for (int i = 0; i < 8; i++)
-            if ((i & j) == 0) cswap(v[i], v[i | j], ((base + i) & k) == 0);
-      *(float4*)(S[a] + base) = make_float4(v[0], v[1], v[2], v[3]);
-      *(float4*)(S[a] + base + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      float pv;
+      bool lo;
+      if constexpr (J < 64) {
+        pv = __int_as_float(xor_lane<J>(__float_as_int(o[a][r])));
+        lo = (lane & J) == 0;
+      } else {
+        pv = o[a][r ^ (J / 64)];
+        lo = (r & (J / 64)) == 0;
+      }
+      const float x = lo ? o[a][r] : pv, y = lo ? pv : o[a][r];  // values at lo / hi
+      const bool sw = (x > y) == up;
+      v[a][r] = sw ? pv : o[a][r];
     }
   }
+}
+// j = jmax .. 1 of stage K on a register-held run
+__device__ __forceinline__ void reg_merge3(float (&v)[3][4], int base, int K, int jmax) {
+  if (jmax >= 128) reg_step3<128>(v, base, K);
+  if (jmax >= 64) reg_step3<64>(v, base, K);
+  if (jmax >= 32) reg_step3<32>(v, base, K);
+  if (jmax >= 16) reg_step3<16>(v, base, K);
+  if (jmax >= 8) reg_step3<8>(v, base, K);
+  if (jmax >= 4) reg_step3<4>(v, base, K);
+  if (jmax >= 2) reg_step3<2>(v, base, K);
+  reg_step3<1>(v, base, K);
+}
+
+// Ascending bitonic sort of three LDS arrays at once, P = 2^e >= 256 (INF padded),
+// 256 threads: every 256-element run is sorted by one wave in registers (stages
+// K <= 256, no barrier); for K >= 512 the strides >= 256 go through LDS (one barrier
+// each) and the strides < 256 run in registers again -- 4 + 2 e barriers instead of
+// e (e + 1) / 2.
+__device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
+  float* S[3] = {S0, S1, S2};
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
+  const int runs = P >> 8;
+  for (int q = w; q < runs; q += nw) {
+    const int base = q << 8;
+    float v[3][4];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) v[a][r] = S[a][base + r * 64 + lane];
+    for (int K = 2; K <= 256; K <<= 1) reg_merge3(v, base, K, K >> 1);
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) S[a][base + r * 64 + lane] = v[a][r];
+  }
   __syncthreads();
-  for (int k = 16; k <= P; k <<= 1) {
-    for (int j = k >> 1; j >= 8; j >>= 1) {
+  const int half = P >> 1, nt = blockDim.x;
+  for (int K = 512; K <= P; K <<= 1) {
+    for (int j = K >> 1; j >= 256; j >>= 1) {
       for (int p0 = tid; p0 < half; p0 += 4 * nt) {
         float x[4][3], y[4][3];
         int ii[4];
@@ -80,7 +137,7 @@ __device__ void block_sort3(float* S0, float* S1, float* S2, int P) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           if (p0 + u * nt >= half) continue;
-          const bool up = (ii[u] & k) == 0;
+          const bool up = (ii[u] & K) == 0;
 #pragma unroll
           for (int a = 0; a < 3; a++)
             if ((x[u][a] > y[u][a]) == up) {
@@ -91,46 +148,21 @@ __device__ void block_sort3(float* S0, float* S1, float* S2, int P) {
       }
       __syncthreads();
     }
-    for (int g = tid; g < groups; g += nt) {
-      const int base = g << 3;
-      const bool up = (base & k) == 0;
+    for (int q = w; q < runs; q += nw) {
+      const int base = q << 8;
+      float v[3][4];
 #pragma unroll
-      for (int a = 0; a < 3; a++) {
-        float v[8];
-        const float4 lo = *(const float4*)(S[a] + base), hi = *(const float4*)(S[a] + base + 4);
-        v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
-        v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      for (int a = 0; a < 3; a++)
 #pragma unroll
-        for (int j = 4; j > 0; j >>= 1)
+        for (int r = 0; r < 4; r++) v[a][r] = S[a][base + r * 64 + lane];
+      reg_merge3(v, base, K, 128);
 #pragma unroll
-          for (int i = 0; i < 8; i++)
-            if ((i & j) == 0) cswap(v[i], v[i | j], up);
-        *(float4*)(S[a] + base) = make_float4(v[0], v[1], v[2], v[3]);
-        *(float4*)(S[a] + base + 4) = make_float4(v[4], v[5], v[6], v[7]);
-      }
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) S[a][base + r * 64 + lane] = v[a][r];
     }
     __syncthreads();
   }
-}
-
-
-// lower_bound / upper_bound of x in the ascending virtual array S[0], S[step],
-// ..., S[(n-1)*step] (the NP subsample is never materialised)
-__device__ __forceinline__ void bounds(const float* S, int n, int step, float x, int& lo, int& hi) {
-  int a = 0, b = n;
-  while (a < b) {
-    const int mid = (a + b) >> 1;
-    if (S[mid * step] < x) a = mid + 1;
-    else b = mid;
-  }
-  lo = a;
-  b = n;
-  while (a < b) {
-    const int mid = (a + b) >> 1;
-    if (S[mid * step] <= x) a = mid + 1;
-    else b = mid;
-  }
-  hi = a;
 }
 
 // block-wide sums of K ints (result valid in every thread); red: >= K*16 ints
@@ -152,8 +184,11 @@ __device__ __forceinline__ void block_sum_n(int (&v)[K], int* red) {
   __syncthreads();
 }
 
-// dynamic LDS: the 3 sorted axes, P floats each
-__global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
+// dynamic LDS: the 3 sorted axes, P floats each. NPT = 1024 threads: the pair's
+// latency chain (global reads, the sort's barrier phases, the searches) is what
+// costs, so a pair gets a whole CU's worth of waves
+constexpr int NPT = 1024;
+__global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
                                                   const int* __restrict__ flen,
@@ -182,22 +217,24 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   const double* OS = os_ptr ? os_ptr[p] : nullptr;
   const float th = OS ? oth[p] : 0.f;
   auto kept = [&](int i) { return !OS || !(OS[i] > (double)th); };
+  NP_STAMP(0);
   int cnt3[3] = {0, 0, 0};
-  for (int i = t; i < mt; i += 256) cnt3[0] += FV[i] ? 1 : 0;
-  for (int i = t; i < ntot; i += 256)
+  for (int i = t; i < mt; i += NPT) cnt3[0] += FV[i] ? 1 : 0;
+  for (int i = t; i < ntot; i += NPT)
     if (kept(i)) {
       cnt3[1] += OV[i] ? 1 : 0;
       cnt3[2] += 1;
     }
   if (t == 0) wpos[0] = 0;
   block_sum_n<3>(cnt3, red);
+  NP_STAMP(1);
   const int m = cnt3[0], nvalid = cnt3[1], nt = cnt3[2];
   eao_np_stats r;
   r.m = m;
   r.n = nvalid;
   for (int a = 0; a < 3; a++) r.w[a] = r.cnt_gt[a] = r.cnt_lt[a] = r.cnt_eq[a] = 0.f;
   r.r1 = r.r2 = 0.f;
-  int P = 8;
+  int P = 256;  // block_sort3_fast: whole 256-element runs
   while (P < nvalid) P <<= 1;
   if (m < 20 || nvalid < 20 || nvalid > NP_MAXN || P > Pmax) {
     if (t == 0) {
@@ -210,31 +247,64 @@ __global__ __launch_bounds__(256) void k_np_pairs(const float* __restrict__ fp,
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
-  // compact the valid object points (order irrelevant: sorted next)
-  for (int i = t; i < ntot; i += 256)
-    if (OV[i] && kept(i)) {
-      const int d = atomicAdd(&wpos[0], 1);
+  // compact the valid object points (order irrelevant: sorted next): a wave places
+  // its kept lanes by ballot rank after one LDS atomic for its base
+  const int lane = t & 63;
+  for (int i0 = 0; i0 < ntot; i0 += NPT) {
+    const int i = i0 + t;
+    const bool keep = i < ntot && OV[i] && kept(i);
+    const uint64_t mk = ballot(keep);
+    int base = 0;
+    if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const int d = base + popc64(mk & lanes_below());
       S[0][d] = O[3 * i];
       S[1][d] = O[3 * i + 1];
       S[2][d] = O[3 * i + 2];
     }
-  for (int i = nvalid + t; i < P; i += 256) S[0][i] = S[1][i] = S[2][i] = INFINITY;
+  }
+  for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
   __syncthreads();
-  block_sort3(S[0], S[1], S[2], P);
+  NP_STAMP(2);
+  block_sort3_fast(S[0], S[1], S[2], P);
+  NP_STAMP(3);
   // rank counts against x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-830)
   int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = t; i < mt; i += 256) {
+  for (int i = t; i < mt; i += NPT) {
     if (!FV[i]) continue;
+    // the six binary searches (lower / upper bound per axis) advance together, so
+    // their LDS reads overlap instead of forming one 6 log n chain
+    const float x[3] = {F[3 * i], F[3 * i + 1], F[3 * i + 2]};
+    int lo[3] = {0, 0, 0}, lb[3] = {nsamp, nsamp, nsamp}, hi[3] = {0, 0, 0}, hb[3] = {nsamp, nsamp, nsamp};
+    for (bool more = true; more;) {
+      more = false;
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        if (lo[a] < lb[a]) {
+          const int mid = (lo[a] + lb[a]) >> 1;
+          if (S[a][mid * step] < x[a]) lo[a] = mid + 1;
+          else lb[a] = mid;
+          more |= lo[a] < lb[a];
+        }
+        if (hi[a] < hb[a]) {
+          const int mid = (hi[a] + hb[a]) >> 1;
+          if (S[a][mid * step] <= x[a]) hi[a] = mid + 1;
+          else hb[a] = mid;
+          more |= hi[a] < hb[a];
+        }
+      }
+    }
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      int lo, hi;
-      bounds(S[a], nsamp, step, F[3 * i + a], lo, hi);
-      c9[3 * a] += lo;
-      c9[3 * a + 2] += hi - lo;
-      c9[3 * a + 1] += nsamp - hi;
+      c9[3 * a] += lo[a];
+      c9[3 * a + 2] += hi[a] - lo[a];
+      c9[3 * a + 1] += nsamp - hi[a];
     }
   }
+  NP_STAMP(4);
   block_sum_n<9>(c9, red);
+  NP_STAMP(5);
   for (int a = 0; a < 3; a++) {
     r.cnt_gt[a] = (float)c9[3 * a];
     r.cnt_lt[a] = (float)c9[3 * a + 1];
@@ -348,9 +418,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 
 // ---------------------------------------------------------------- iForest
 
-// in-kernel phase stamps of k_iforest_tree (workgroup (0,0)), read through
-// eao_debug_iforest_stamps: development instrumentation, a few SALU ops
-__device__ unsigned long long g_if_stamp[24];
+
 // EAO_IF_PROF builds only (tools/micro): cycles of the register-path node
 // sub-steps of workgroup (0,0) accumulated in g_if_stamp[12..17]
 #ifdef EAO_IF_PROF
@@ -911,9 +979,9 @@ int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, co
                           const int* d_ooff, const int* d_olen, eao_np_stats* d_out,
                           hipStream_t s, int max_olen, const double* const* d_os_ptr, const float* d_oth) {
   if (npairs <= 0) return EAO_OK;
-  int P = 8;
+  int P = 256;  // k_np_pairs sorts whole 256-element runs
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(256), sizeof(float) * 3 * P, s, d_fp, d_fv, d_foff,
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), sizeof(float) * 3 * P, s, d_fp, d_fv, d_foff,
                      d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;

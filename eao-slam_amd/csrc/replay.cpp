@@ -388,7 +388,7 @@ class ReplayEngine {
   int kept_pos = -1;              // the detection being associated
   bool cur_np_done = false;       // ... and whether its NP step has read the cache
   // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
-  double prof[24] = {0};
+  double prof[32] = {0};
   static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
@@ -1549,6 +1549,7 @@ class ReplayEngine {
 
   // Object_Map::DataAssociateUpdate, Object.cc:1313-1554
   bool update(Obj* o, Det* f, int Flag) {
+    Tick tku(&prof[28]);
     if (f->cls != o->cls) return false;
     if (held(o)) {
       // already updated in this frame: the reference returns false at the mnLastAddID
@@ -2157,6 +2158,7 @@ class ReplayEngine {
         rc = kick();
       }
       if (rc) return rc;
+      Tick tke(&prof[30]);
       for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
         if (flag == "NA") continue;
         Obj* o = objs[i].get();
@@ -2418,14 +2420,22 @@ class ReplayEngine {
 
   int local_mapping() {
     Tick tk(&prof[1]);
-    int rc = flush(-1);
+    int rc;
+    {
+      Tick t0(&prof[24]);
+      rc = flush(-1);
+    }
     if (rc) return rc;
-    for (auto& up : objs) {
-      Obj* o = up.get();
-      if (o->pts.size() < 10 || o->bad) continue;
-      mean_std(o);
+    {
+      Tick t1(&prof[25]);
+      for (auto& up : objs) {
+        Obj* o = up.get();
+        if (o->pts.size() < 10 || o->bad) continue;
+        mean_std(o);
+      }
     }
     if (flag == "NA" || flag == "IoU" || flag == "NP") return EAO_OK;
+    Tick t2(&prof[26]);
     for (auto& up : objs) {
       Obj* o = up.get();
       if (o->bad) continue;
@@ -2541,6 +2551,12 @@ int eao_replay_profile(eao_replay* r, double* out12) {
   if (!r || !out12) return EAO_E_ARG;
   std::memcpy(out12, r->r.prof, sizeof(double) * 24);
   return EAO_OK;
+}
+
+int eao_replay_profile_n(eao_replay* r, double* out, int n) {
+  if (!r || !out || n < 0) return EAO_E_ARG;
+  std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 32));
+  return std::min(n, 32);
 }
 
 }  // extern "C"

@@ -10,6 +10,7 @@ import pytest
 
 import eao_accel as ea
 import pyoracle as orc
+from tools import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -73,3 +74,51 @@ def test_project_rects(frames):
     for c, g in zip(clouds, got):
         assert np.array_equal(g, orc.project_rect(orc.cam(), poses[1], c))
     assert ok.all()
+
+
+def test_np_pairs_int32_wrap_q4():
+    """NoParaDataAssociation's bounds use int products (Object.cc:905-911): m*n*(m+n+1)
+    overflows int32 from m = 564 with n = 3m. Engine and oracle define the
+    wrap as two's complement: a negative product gives NaN bounds (verdict 2), a product
+    past 2^32 wraps positive (finite, shifted bounds). Counts and bounds must agree."""
+    rng = np.random.default_rng(0x64)
+    fs, os_, exp = [], [], []
+    for m, n in ((564, 1692), (600, 1800), (800, 2400), (700, 900)):
+        f = _cloud(rng, m, [1, 2, 3], 0.1)
+        o = _cloud(rng, n, [1, 2, 3], 0.1)
+        fs.append((f, np.ones(m, np.uint8)))
+        os_.append((o, np.ones(n, np.uint8)))
+        exp.append(orc.np_test(f, fs[-1][1], o, os_[-1][1]))
+    got = ea.Assoc().np_batch(fs, os_)
+    for g, o in zip(got, exp):
+        assert g["verdict"] == o["verdict"] and g["m"] == o["m"] and g["n"] == o["n"]
+        assert np.array_equal(g["cnt_gt"], o["cnt_gt"]) and np.array_equal(g["cnt_lt"], o["cnt_lt"])
+        assert np.array_equal(g["cnt_eq"], o["cnt_eq"])
+        assert np.allclose([g["r1"], g["r2"]], [o["r1"], o["r2"]], rtol=1e-6, equal_nan=True)
+    assert np.isnan(exp[0]["r1"]) and exp[0]["verdict"] == 2  # 564*1692*2257 wraps negative
+
+
+def test_biforest_state_per_replay_q6():
+    """Object.cc's biForest is a process global that flag "None" clears for good (SURVEY
+    Q6); a mono_tum process runs one flag, and a replay models one such process: a "None"
+    replay launches no isolation forest, and a later "EAO" replay in the same process
+    starts with biForest set, as a fresh mono_tum EAO run does."""
+    frames = synth.assoc_stream(40)
+    a = ea.Assoc()
+    none = ea.Replay(a, "None")
+    none.run(ea.Replay.pack(frames))
+    prof = np.zeros(24)
+    ea.lib().eao_replay_profile(none.h, ea.P(prof))
+    assert prof[2] == 0  # no forest launched
+    none.close()
+    eao = ea.Replay(a, "EAO")
+    det = eao.run(ea.Replay.pack(frames))
+    ea.lib().eao_replay_profile(eao.h, ea.P(prof))
+    assert prof[2] > 0
+    o = orc.Replay("EAO")
+    ref = []
+    for i, f in enumerate(frames):
+        ref.append(o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            o.local_mapping()
+    assert np.array_equal(det, np.concatenate(ref))

@@ -276,3 +276,19 @@ def test_iforest_erase_threshold_matches_libm_pow():
             below = math.nextafter(below, -math.inf)
             assert math.pow(2.0, below) <= thd
         assert abs(x - math.log2(thd)) < 1e-12
+
+
+def test_np_bounds_int32_wrap_q4():
+    """The oracle's NoParaDataAssociation bounds against an independent restatement of
+    Object.cc:905-911 with int32 two's-complement products."""
+    def wrap(x):
+        return (x + 2 ** 31) % 2 ** 32 - 2 ** 31
+    rng = np.random.default_rng(5)
+    for m, n in ((564, 1692), (600, 1800), (800, 2400), (100, 300)):
+        f = rng.normal(0, 0.1, (m, 3)).astype(np.float32)
+        o = rng.normal(0, 0.1, (n, 3)).astype(np.float32)
+        r = orc.np_test(f, np.ones(m, np.uint8), o, np.ones(n, np.uint8))
+        q = int(np.fix(wrap(m * n * (m + n + 1)) / 12))  # C integer division truncates
+        base = 0.5 * m * (m + n + 1)
+        sp = 1.282 * np.sqrt(np.float64(q)) if q >= 0 else np.nan
+        assert np.allclose([r["r1"], r["r2"]], [np.float32(base - sp), np.float32(base + sp)], rtol=1e-7, equal_nan=True)
