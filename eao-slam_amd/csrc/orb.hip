@@ -173,7 +173,9 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
   // ROI column c lives at smem[r * RS + sh + c] (16-byte aligned row starts)
   const int ax0 = vec_ok ? (B.x0 & ~15) : B.x0, sh = B.x0 - ax0;
   uint8_t* roi = smem + sh;
-  uint8_t* F = smem + RS * bh;
+  // kept strengths of the detection rows / columns [3, bh - 3) x [3, bw - 3) only,
+  // addressed F[r * RS + x] (so the block needs RS * (2 bh - 6) bytes of LDS)
+  uint8_t* F = smem + RS * bh - (3 * RS + 3);
   if (vec_ok) {
     const int nvec = (sh + bw + 15) >> 4;
     for (int idx = t; idx < bh * nvec; idx += 256) {
@@ -242,10 +244,18 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
       Lc = L2[0];
       Rc = R2[0];
       fin(y0, S2[1], L2[1], R2[1]);
-      for (int a = y0 + 2; a <= y1; a += 2) {
+      // two row pairs per trip: their strength evaluations are independent, so the
+      // LDS reads and VALU chains of one hide the latencies of the other
+      for (int a = y0 + 2; a <= y1; a += 4) {
+        int S4[2], L4[2], R4[2];
         pair(a, S2, L2, R2);
+        pair(a + 2, S4, L4, R4);
         fin(a - 1, S2[0], L2[0], R2[0]);
         if (a < y1) fin(a, S2[1], L2[1], R2[1]);
+        if (a + 2 <= y1) {
+          fin(a + 1, S4[0], L4[0], R4[0]);
+          if (a + 2 < y1) fin(a + 2, S4[1], L4[1], R4[1]);
+        }
       }
     }
   }
@@ -253,49 +263,46 @@ __global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ f
 #ifdef EAO_FAST_ABL_EMIT
   return;
 #endif
+  // ---- emission, one wave per cell, one lane per detection row: the lane counts
+  // its row's kept pixels (F > iniTh, F > 0), the cell takes the iniTh set or -- when
+  // that is empty -- the minTh set (ORBextractor.cc:812), an exclusive wave scan of the
+  // row counts places every row, and each lane writes its row's corners in column
+  // order: the cell's candidates come out row-major as cv::FAST emits them
+  const int nr = y1 - y0;  // <= 64 (host checks)
   for (int cc = wv; cc < B.ncells; cc += 4) {
     const int ci = B.cell_begin + cc;
     const CellDev c = cells[ci];
     const int wx0 = bnd[cc], ww = bnd[cc + 1] - wx0;
     uint32_t* out = cand + f * cand_stride + c.slot;
-    // emit the pixels with F > th row-major; two rows per ballot when the
-    // window is <= 32 wide (lanes 0-31 row r, 32-63 row r+1: ballot order is
-    // still row-major)
-    auto emit = [&](int th) -> int {
-      int n = 0;
-      if (ww <= 32) {
-        const int half = lane >> 5, cx = lane & 31;
-        for (int r0 = y0; r0 < y1; r0 += 2) {
-          const int r = r0 + half;
-          const int x = wx0 + cx;
-          const int v = (cx < ww && r < y1) ? F[r * RS + x] : 0;
-          const bool k = v > th;
-          const uint64_t mk = ballot(k);
-          if (k) {
-            const int pos = n + popc64(mk & lanes_below());
-            // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
-            if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
-          }
-          n += popc64(mk);
-        }
-      } else {
-        for (int r = y0; r < y1; r++)
-          for (int c0 = 0; c0 < ww; c0 += 64) {
-            const int x = wx0 + c0 + lane;
-            const int v = c0 + lane < ww ? F[r * RS + x] : 0;
-            const bool k = v > th;
-            const uint64_t mk = ballot(k);
-            if (k) {
-              const int pos = n + popc64(mk & lanes_below());
-              if (pos < c.cap) out[pos] = pack_kp(x - wx0 + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
-            }
-            n += popc64(mk);
-          }
+    const int r = y0 + lane;
+    const uint8_t* row = F + r * RS + wx0;
+    int ci_ = 0, cm = 0;
+    if (lane < nr)
+      for (int x = 0; x < ww; x++) {
+        const int v = row[x];
+        ci_ += v > thi ? 1 : 0;
+        cm += v > 0 ? 1 : 0;
       }
-      return n;
-    };
-    int n = emit(thi);
-    if (n == 0) n = emit(0);  // ORBextractor.cc:812 -- retry with minTh only when empty (F > 0 <=> kept at minTh)
+    const bool use_ini = wave_sum(ci_) > 0;
+    const int th = use_ini ? thi : 0;
+    const int cnt = use_ini ? ci_ : cm;
+    int pre = cnt;  // inclusive scan over the lanes (rows)
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(pre, o, 64);
+      if (lane >= o) pre += u;
+    }
+    const int n = __shfl(pre, 63, 64);
+    int k = pre - cnt;
+    if (lane < nr && cnt > 0)
+      for (int x = 0; x < ww; x++) {
+        const int v = row[x];
+        if (v > th) {
+          // FAST coordinates are relative to the cell ROI (ORBextractor.cc:821-826)
+          if (k < c.cap) out[k] = pack_kp(x + 3 + c.j * L.wCell, r + c.i * L.hCell, v - 1);
+          k++;
+        }
+      }
     if (lane == 0) cell_cnt[f * ncells + ci] = n;
   }
 }
@@ -1264,7 +1271,11 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
       return EAO_E_CAPACITY;
     }
     dim3 g((unsigned)bands.size(), nframes);
-    size_t lds = (size_t)FAST_RS * band_h * 2;  // roi, kept strengths
+    if (band_h - 6 > 64 || band_h < 7) {  // k_fast_band emits one detection row per lane
+      set_error("orb: FAST cell rows exceed one wave");
+      return EAO_E_CAPACITY;
+    }
+    size_t lds = (size_t)FAST_RS * (2 * band_h - 6);  // roi, kept strengths of the detection rows
     hipLaunchKernelGGL(k_fast_band, g, dim3(256), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
                        d_levels, d_bands, d_cells, p.ini_th_fast, p.min_th_fast, d_cand, cand_stride,
                        d_cell_cnt, (int)cells.size(), vec_ok);
