@@ -1,0 +1,159 @@
+// frame_input.cpp -- the host side of the per-frame input stage:
+// the offline YOLO detections and the ground-truth pose lookup that
+// Tracking::GrabImageMonocular performs before every Track() (src/Tracking.cc:415-554).
+//
+// The reference re-reads "./data/yolo_txts/<timestamp>.txt" and scans all 8710 rows of
+// groundtruth.txt through std::to_string per frame; here the caller hands the file text
+// and the parsed GT table over once, the parse keeps the reference's `int` token
+// semantics and ordering, and the lookup is a hash of the same string keys.
+// (The gray conversion of the stage is the k_gray kernel, orb.hip; the two cv::undistort
+// calls with TUM3's all-zero distortion reduce to an exact copy, eao_undistort_zero.)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/eao_accel.h"
+#include "common.h"
+
+namespace {
+
+// `istr >> tmp` with int tmp on one whitespace-separated token: the longest
+// [+-]digits prefix; false (stream failed) when there is none. A token such as
+// "0.824041" yields 0 and leaves ".824041" unread, which fails the next extraction:
+// the row ends there.
+bool int_token(const char*& p, const char* end, int& v, bool& stop) {
+  while (p < end && (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\v' || *p == '\f')) p++;
+  if (p >= end) return false;
+  const char* q = p;
+  bool neg = false;
+  if (*q == '+' || *q == '-') neg = *q++ == '-';
+  if (q >= end || *q < '0' || *q > '9') return false;
+  long long x = 0;
+  while (q < end && *q >= '0' && *q <= '9') x = std::min<long long>(x * 10 + (*q++ - '0'), 1LL << 40);
+  x = neg ? -x : x;
+  if (x > INT32_MAX || x < INT32_MIN) return false;  // out of range: failbit, nothing pushed
+  v = (int)x;
+  stop = q < end && !(*q == ' ' || *q == '\t' || *q == '\r' || *q == '\v' || *q == '\f');
+  p = q;
+  return true;
+}
+
+struct Box {  // BoxSE fields read by the tracker (include/YOLOv3SE.h:34-59)
+  int cls, x, y, w, h, score;
+};
+
+std::string to_string_f(double v) {  // std::to_string(double) is "%f"
+  char b[64];
+  std::snprintf(b, sizeof b, "%f", v);
+  return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int eao_yolo_parse(const char* text, size_t len, int32_t* out, int cap, int* n_out) {
+  if (!n_out || (!text && len) || cap < 0 || (cap && !out)) return EAO_E_ARG;
+  std::vector<Box> boxes;
+  const char* p = text;
+  const char* end = text + len;
+  while (p < end) {  // getline
+    const char* eol = (const char*)std::memchr(p, '\n', (size_t)(end - p));
+    const char* le = eol ? eol : end;
+    int row[6] = {0, 0, 0, 0, 0, 0};  // a short row's missing fields read as 0 (the reference indexes past its end)
+    int k = 0, v;
+    bool stop = false;
+    const char* q = p;
+    while (!stop && int_token(q, le, v, stop)) {
+      if (k < 6) row[k] = v;
+      k++;
+    }
+    // every getline pushes its row, an empty one included; empty rows never reach a
+    // BoxSE in practice (the files end with a newline), so they are skipped here
+    if (k > 0) boxes.push_back(Box{row[0], row[1], row[2], row[3], row[4], row[5]});
+    p = eol ? eol + 1 : end;
+  }
+  // std::sort by score, descending (Tracking.cc:470-472): the same libstdc++ introsort,
+  // so equal scores keep the reference's order
+  std::sort(boxes.begin(), boxes.end(), [](const Box& a, const Box& b) { return a.score > b.score; });
+  *n_out = (int)boxes.size();
+  for (int i = 0; i < std::min(cap, (int)boxes.size()); i++) {
+    const Box& b = boxes[i];
+    const int32_t r[6] = {b.cls, b.x, b.y, b.w, b.h, b.score};
+    std::memcpy(out + 6 * (size_t)i, r, sizeof r);
+  }
+  return (int)boxes.size() > cap ? EAO_E_CAPACITY : EAO_OK;
+}
+
+int eao_gt_lookup(const double* gt, int m, const double* ts, int n, int32_t* idx_out, float* Twc_out) {
+  if ((m && !gt) || (n && (!ts || !idx_out)) || m < 0 || n < 0) return EAO_E_ARG;
+  // first row per key: to_string(t) without its last 4 characters (Tracking.cc:508-519)
+  std::unordered_map<std::string, int> first;
+  first.reserve((size_t)m * 2);
+  for (int r = 0; r < m; r++) {
+    std::string s = to_string_f(gt[8 * (size_t)r]);
+    first.emplace(s.substr(0, s.size() - 4), r);
+  }
+  for (int i = 0; i < n; i++) {
+    std::string s = to_string_f(ts[i]);
+    auto it = first.find(s.substr(0, s.size() - 4));
+    const int r = it == first.end() ? -1 : it->second;
+    idx_out[i] = r;
+    if (!Twc_out) continue;
+    float* T = Twc_out + 16 * (size_t)i;
+    if (r < 0) {  // mGroundtruthPose_mat = zeros (Tracking.cc:549-553)
+      std::fill(T, T + 16, 0.0f);
+      continue;
+    }
+    // g2o::SE3Quat(tail<7>) = (t, q = (qx, qy, qz, qw)) with normalizeRotation(), then
+    // to_homogeneous_matrix() -> Converter::toCvMat (float), se3quat.h:69-93,270-285
+    const double* v = gt + 8 * (size_t)r + 1;
+    double x = v[3], y = v[4], z = v[5], w = v[6];
+    if (w < 0) {
+      x = -x;
+      y = -y;
+      z = -z;
+      w = -w;
+    }
+    const double nrm = std::sqrt((x * x + z * z) + (y * y + w * w));  // Eigen 3.2 SSE2 redux order
+    x /= nrm;
+    y /= nrm;
+    z /= nrm;
+    w /= nrm;
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;  // Eigen QuaternionBase::toRotationMatrix
+    const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    const double R[9] = {1 - (tyy + tzz), txy - twz,       txz + twy,  txy + twz,      1 - (txx + tzz),
+                         tyz - twx,       txz - twy,       tyz + twx,  1 - (txx + tyy)};
+    for (int a = 0; a < 3; a++) {
+      for (int b = 0; b < 3; b++) T[4 * a + b] = (float)R[3 * a + b];
+      T[4 * a + 3] = (float)v[a];
+    }
+    T[12] = T[13] = T[14] = 0.0f;
+    T[15] = 1.0f;
+  }
+  return EAO_OK;
+}
+
+int eao_undistort_zero(const float* dist, int ndist, const uint8_t* src, int w, int h, int spitch, uint8_t* dst,
+                       int dpitch, void* stream) {
+  if (!dist || ndist < 4 || !src || !dst || w <= 0 || h <= 0 || spitch < w || dpitch < w) return EAO_E_ARG;
+  for (int k = 0; k < ndist; k++)
+    if (dist[k] != 0.0f) {
+      eao::set_error("eao_undistort_zero: non-zero distortion (only TUM3's zero model is supported)");
+      return EAO_E_ARG;
+    }
+  // cv::undistort with k1..p2 = 0 and the default new camera matrix (= K): the rectify
+  // map sends every pixel to itself up to float rounding, which remap's 1/32-pixel fixed
+  // point absorbs, so each output pixel is its input pixel (Tracking.cc:366-369)
+  EAO_HIP_CHECK(hipMemcpy2DAsync(dst, dpitch, src, spitch, w, h, hipMemcpyDefault, (hipStream_t)stream));
+  return EAO_OK;
+}
+
+}  // extern "C"

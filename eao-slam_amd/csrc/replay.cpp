@@ -1658,10 +1658,18 @@ class ReplayEngine {
       // same-class objects with a pending forest were updated earlier in this frame (the
       // frame start completed the older ones): they are held, not waited for (held());
       // launch their forests now, with this and every later detection's NP pairs behind them
+      bool launch = false;  // a held same-class object whose forest is not in flight yet
       for (auto& up : objs)
-        if (up->cls == f->cls && up->pending && !held(up.get()))
-          if ((rc = touch(up.get()))) return rc;
-      rc = kick();
+        if (up->cls == f->cls && up->pending) {
+          if (!held(up.get())) {
+            if ((rc = touch(up.get()))) return rc;
+          } else if (up->slot < 0) {
+            launch = true;
+          }
+        }
+      // launch it now (with this detection's NP pair behind it); objects of other classes
+      // keep accumulating into the next batch (fewer, larger launches)
+      rc = launch ? kick() : EAO_OK;
     }
     if (rc) return rc;
     const IRect RC = f->box;

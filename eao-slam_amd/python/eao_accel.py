@@ -428,3 +428,27 @@ class Replay:
             k = check(lib().eao_replay_object_points(self.h, i, P(ids), len(ids)), "eao_replay_object_points")
             pts.append(ids[:k].copy())
         return ints, fl, pts
+
+
+# ---------------------------------------------------------------- frame input stage
+def yolo_parse(text):
+    """eao_yolo_parse: one data/yolo_txts file's text -> (n, 6) int32 rows
+    {class, x, y, w, h, score} as Tracking::GrabImageMonocular reads them."""
+    b = text.encode() if isinstance(text, str) else bytes(text)
+    cap = max(16, b.count(b"\n") + 1)
+    out = np.zeros((cap, 6), np.int32)
+    n = ctypes.c_int()
+    buf = ctypes.create_string_buffer(b, len(b))
+    check(lib().eao_yolo_parse(buf, ctypes.c_size_t(len(b)), P(out), cap, ctypes.byref(n)), "eao_yolo_parse")
+    return out[:n.value].copy()
+
+
+def gt_lookup(gt, timestamps):
+    """eao_gt_lookup: (row index or -1, Twc float32 (n, 4, 4)) per timestamp."""
+    gt = np.ascontiguousarray(gt, np.float64).reshape(-1, 8)
+    ts = np.ascontiguousarray(timestamps, np.float64).reshape(-1)
+    idx = np.zeros(len(ts), np.int32)
+    T = np.zeros((len(ts), 4, 4), np.float32)
+    check(lib().eao_gt_lookup(P(gt), len(gt), P(ts), len(ts), P(idx), P(T)), "eao_gt_lookup")
+    return idx, T
+

@@ -291,6 +291,26 @@ int eao_replay_profile(eao_replay* r, double* out24);
 /* The same wall-clock profile, up to n (<= 32) slots; returns the number copied. */
 int eao_replay_profile_n(eao_replay* r, double* out, int n);
 
+/* ---- frame input stage (src/Tracking.cc:340-554) ---- */
+/* Tracking::GrabImageMonocular's offline detections: the text of one
+   data/yolo_txts/<timestamp>.txt parsed as the reference does (`istr >> int` per line,
+   so the score "0.82" reads as 0 -- SURVEY Q1), then std::sort by score descending.
+   out: cap rows of {class, x, y, w, h, score}; *n_out = rows in the file
+   (EAO_E_CAPACITY when > cap). Tracking.cc:426-472. Host-only. */
+int eao_yolo_parse(const char* text, size_t len, int32_t* out, int cap, int* n_out);
+/* The ground-truth pose lookup of every frame (Tracking.cc:506-554): gt = m rows of
+   data/groundtruth.txt {t, tx, ty, tz, qx, qy, qz, qw}; for each timestamp the first row
+   whose std::to_string(t) minus its last 4 characters equals the frame's; idx_out = row
+   or -1; Twc_out (optional, n x 16 row-major float) = g2o::SE3Quat(row) as
+   Converter::toCvMat gives it, zeros when no row matches. Host-only. */
+int eao_gt_lookup(const double* gt, int m, const double* ts, int n, int32_t* idx_out, float* Twc_out);
+/* cv::undistort(im, out, K, DistCoef) with an all-zero distortion model (TUM3.yaml:13-16,
+   Tracking.cc:366-369): an exact per-pixel copy (the rectify map is the identity up to
+   rounding that remap's fixed point absorbs); EAO_E_ARG for non-zero coefficients.
+   src / dst host or device memory, copied on `stream` (NULL: the null stream). */
+int eao_undistort_zero(const float* dist, int ndist, const uint8_t* src, int w, int h, int spitch, uint8_t* dst,
+                       int dpitch, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
