@@ -334,6 +334,8 @@ def main():
     ms_per_step = 1000.0 * elapsed / args.steps
     stage = np.mean(np.stack(rec["stage_ms"]), 0)
     match_ms = float(np.mean(rec["match_ms"]))
+    searches = search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc,
+                           d_cnt, d_has, d_mpos, match_ms)
     n_kps = float(d_cnt.float().mean().item())
     ab = algorithmic_bytes(n_kps)
     dom = int(np.argmax(stage))
@@ -378,6 +380,7 @@ def main():
             "extract_fps": F / (ext_ms * 1e-3),
             "extract_gbs": ab["extract"] * F / (ext_ms * 1e-3) / 1e9,
             "match_ms_per_step": match_ms,
+            "searches": searches,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
                                   "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
@@ -403,6 +406,94 @@ def main():
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
     return 0
+
+
+def search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc, d_cnt,
+                d_has, d_mpos, motion_ms, reps=5):
+    """The single-frame searches beside the step, batched over the stream's F-1 frame
+    pairs (search t: frame t's map points / keypoints against frame t+1), HBM-resident,
+    each timed with HIP events on the bench stream (ms per batch of F-1 searches):
+      local    -- SearchByProjection(Frame&, vector<MapPoint*>, th=1) (TrackLocalMap,
+                  ORBmatcher.cc:45-129), map points projected by the next pose;
+      keyframe -- SearchByProjection(Frame&, KeyFrame*, sFound, 10, 100) (relocalisation,
+                  ORBmatcher.cc:1472-1599), frame t as the candidate keyframe;
+      init     -- SearchForInitialization(F1, F2, ..., 100) (ORBmatcher.cc:405-520).
+    Parity of these kernels is the -m gpu tests' job (tests/test_gpu_match.py)."""
+    dev = d_kps.device
+    S = F - 1
+    kp_sz = d_kps.shape[2]
+    fx, fy, cx, cy = cam.fx, cam.fy, cam.cx, cam.cy
+    inv = np.zeros((S, cap), np.uint8)
+    proj = np.zeros((S, cap, 2), np.float32)
+    lvl = np.zeros((S, cap), np.int32)
+    mind = np.zeros((S, cap), np.float32)
+    maxd = np.zeros((S, cap), np.float32)
+    sc_np = np.asarray(sc, np.float32)
+    for t in range(S):
+        n = int(cnt[t])
+        P = mpos[t, :n].astype(np.float64)
+        T = poses[t + 1].astype(np.float64)
+        Pc = P @ T[:3, :3].T + T[:3, 3]
+        z = np.where(Pc[:, 2] > 0, Pc[:, 2], 1.0)
+        u, v = fx * Pc[:, 0] / z + cx, fy * Pc[:, 1] / z + cy
+        inv[t, :n] = (Pc[:, 2] > 0) & (u >= 0) & (u <= cam.img_w) & (v >= 0) & (v <= cam.img_h)
+        proj[t, :n, 0], proj[t, :n, 1] = u, v
+        lvl[t, :n] = kps[t, :n]["octave"]
+        Tt = poses[t].astype(np.float64)
+        Ow = -Tt[:3, :3].T @ Tt[:3, 3]
+        dist = np.linalg.norm(P - Ow[None, :], axis=1)
+        maxd[t, :n] = dist * sc_np[kps[t, :n]["octave"]]
+        mind[t, :n] = maxd[t, :n] / sc_np[-1]
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_inv, d_proj, d_lvl = up(inv), up(proj), up(lvl)
+    d_vc = torch.ones((S, cap), dtype=torch.float32, device=dev)
+    d_mind, d_maxd = up(mind), up(maxd)
+    d_T1 = up(poses[1:].reshape(S, 16).astype(np.float32))
+    prev0 = torch.zeros((S, cap, 2), dtype=torch.float32, device=dev)
+    for t in range(S):
+        n = int(cnt[t])
+        prev0[t, :n, 0] = torch.from_numpy(kps[t, :n]["x"].astype(np.float32))
+        prev0[t, :n, 1] = torch.from_numpy(kps[t, :n]["y"].astype(np.float32))
+    d_prev = prev0.clone()
+    out = torch.full((S, cap), -1, dtype=torch.int32, device=dev)
+    nm = torch.zeros(S, dtype=torch.int32, device=dev)
+    q_kps, c_kps = d_kps.data_ptr(), d_kps.data_ptr() + cap * kp_sz
+    q_desc, c_desc = d_desc.data_ptr(), d_desc.data_ptr() + cap * 32
+    q_n, c_n = d_cnt.data_ptr(), d_cnt.data_ptr() + 4
+    sp = stream.cuda_stream
+    logsf = float(np.log(np.float32(SCALE)))
+
+    def local():
+        matcher.local_batch_device(cam, S, 1.0, 0.8, cap, q_n, d_inv.data_ptr(), d_proj.data_ptr(),
+                                   d_lvl.data_ptr(), d_vc.data_ptr(), q_desc, cap, c_n, c_kps, c_desc, None, sc,
+                                   out.data_ptr(), nm.data_ptr(), sp)
+
+    def keyframe():
+        matcher.keyframe_batch_device(cam, S, d_T1.data_ptr(), 10, 100, 1, cap, q_n, q_kps, d_has.data_ptr(),
+                                      d_mpos.data_ptr(), q_desc, d_mind.data_ptr(), d_maxd.data_ptr(), logsf, cap,
+                                      c_n, c_kps, c_desc, None, sc, out.data_ptr(), nm.data_ptr(), sp)
+
+    def init():
+        matcher.init_batch_device(cam, S, 0.9, 1, cap, q_n, q_kps, q_desc, cap, c_n, c_kps, c_desc,
+                                  d_prev.data_ptr(), 100, out.data_ptr(), nm.data_ptr(), sp)
+
+    res = {"searches_per_batch": S, "motion_ms": motion_ms, "motion_us_per_search": motion_ms * 1e3 / S}
+    for name, fn in (("local", local), ("keyframe", keyframe), ("init", init)):
+        fn()  # warm
+        ms = []
+        for _ in range(reps):
+            if name == "init":
+                d_prev.copy_(prev0)  # updated in place (vbPrevMatched), restored outside the timed region
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            ms.append(e0.elapsed_time(e1))
+        res[name + "_ms"] = float(np.mean(ms))
+        res[name + "_us_per_search"] = float(np.mean(ms)) * 1e3 / S
+        res[name + "_mean_matches"] = float(nm.float().mean().item())
+    return res
 
 
 def cpu_model():

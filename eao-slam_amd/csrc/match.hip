@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_grid(const eao_keypoint_dev* __restrict
   __shared__ int cnt[GRID_CELLS];
   __shared__ int part[256];
   const int f = blockIdx.x, t = threadIdx.x;
-  const int n = counts ? counts[f] : n_single;
+  const int n = counts ? min(counts[f], cap) : n_single;
   const eao_keypoint_dev* K = kps + (long long)f * cap;
   int* S = gstart + (long long)f * (GRID_CELLS + 1);
   int* I = gitems + (long long)f * cap;
@@ -469,6 +469,249 @@ __global__ __launch_bounds__(256) void k_frustum(CamDev cam, const float* __rest
   vcos[i] = viewCos;
 }
 
+// ---- candidate phases of the single-frame searches (local map, relocalisation,
+// initialisation): one thread per query scans its window exactly as the sequential
+// search does and keeps the MK smallest keys (distance, window order, index) among the
+// candidates that no later assignment can add back, plus the candidate count. The
+// sequential phase then decides a query from its stored keys when they settle it
+// (enough of them still pass the assignment-dependent test, or the query has no more
+// candidates) and falls back to the full window scan otherwise -- the same answer.
+// a batch of independent searches: search f reads its queries at f * qs and its
+// frame at f * cs (grid slot f), with per-search counts; a single call passes
+// null counts (the scalar ones apply) and zero strides
+struct BatchDims {
+  const int* nq;
+  const int* nc;
+  int qs, cs;
+};
+template <typename T>
+__device__ __forceinline__ T* at_slot(T* p, int f, long long stride) {
+  return p ? p + f * stride : p;
+}
+
+__device__ __forceinline__ void keep_smallest(unsigned long long (&best)[MK], unsigned long long key) {
+#pragma unroll
+  for (int k = 0; k < MK; k++) {  // sorted insertion, smallest first
+    const unsigned long long lo = key < best[k] ? key : best[k];
+    key = key < best[k] ? best[k] : key;
+    best[k] = lo;
+  }
+}
+__device__ __forceinline__ void store_keys(unsigned long long* __restrict__ ckeys, int* __restrict__ ccnt, int q,
+                                           int n, const unsigned long long (&best)[MK]) {
+  ccnt[q] = n;
+  for (int k = 0; k < min(n, MK); k++) ckeys[(long long)q * MK + k] = best[k];
+}
+
+// SearchByProjection(Frame&, vector<MapPoint*>, th) candidates, ORBmatcher.cc:45-114
+__global__ __launch_bounds__(256) void k_local_cand(
+    CamDev cam, float th, int n_mp, const uint8_t* __restrict__ inview, const float* __restrict__ proj,
+    const int* __restrict__ level, const float* __restrict__ vcos, const uint8_t* __restrict__ mdesc,
+    const eao_keypoint_dev* __restrict__ CK, const uint8_t* __restrict__ CD, const int* __restrict__ pre, int nlevels,
+    const float* __restrict__ scales, const int* __restrict__ GS, const int* __restrict__ GI,
+    unsigned long long* __restrict__ ckeys, int* __restrict__ ccnt, BatchDims bd) {
+  const int f = blockIdx.y, iMP = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bd.nq) n_mp = min(bd.nq[f], bd.qs);
+  if (iMP >= n_mp) return;
+  inview = at_slot(inview, f, bd.qs);
+  proj = at_slot(proj, f, 2LL * bd.qs);
+  level = at_slot(level, f, bd.qs);
+  vcos = at_slot(vcos, f, bd.qs);
+  mdesc = at_slot(mdesc, f, 32LL * bd.qs);
+  CK = at_slot(CK, f, bd.cs);
+  CD = at_slot(CD, f, 32LL * bd.cs);
+  pre = at_slot(pre, f, bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  unsigned long long best[MK];
+#pragma unroll
+  for (int k = 0; k < MK; k++) best[k] = KEY_NONE;
+  int n = 0;
+  if (inview[iMP]) {
+    const int L = min(max(level[iMP], 0), nlevels - 1);  // Q13 clamp
+    float r = vcos[iMP] > 0.998f ? 2.5f : 4.0f;
+    if (th != 1.0f) r = fmul(r, th);
+    const float rr = fmul(r, scales[L]);
+    const float x = proj[2 * iMP], y = proj[2 * iMP + 1];
+    const Window w = window_cells(cam, x, y, rr);
+    if (!w.empty) {
+      const int minL = L - 1, maxL = L;
+      const bool checkL = (minL > 0) || (maxL >= 0);
+      const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+      const uint8_t* d = mdesc + 32 * (long long)iMP;
+      for (int ck = 0; ck < ncell; ck++) {
+        const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+        for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+          const int idx = GI[q];
+          const eao_keypoint_dev& kp = CK[idx];
+          if (checkL) {
+            if (kp.octave < minL) continue;
+            if (maxL >= 0 && kp.octave > maxL) continue;
+          }
+          if (!(fabsf(fsub(kp.x, x)) < rr && fabsf(fsub(kp.y, y)) < rr)) continue;
+          if (pre && pre[idx] >= 0) continue;  // taken before the search starts
+          n++;
+          keep_smallest(best, make_key(hamming256(d, CD + 32 * (long long)idx), ck, idx));
+        }
+      }
+    }
+  }
+  store_keys(ckeys, ccnt, iMP, n, best);
+}
+
+// SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) candidates,
+// ORBmatcher.cc:1472-1560: the query geometry (projection without a depth test,
+// distance gate, PredictScale clamped -- Q13) into geo[], then the window scan
+__global__ __launch_bounds__(256) void k_keyframe_cand(
+    CamDev cam, const float* __restrict__ Tg, float th, int n_kf, const uint8_t* __restrict__ valid,
+    const float* __restrict__ pos, const uint8_t* __restrict__ mdesc, const float* __restrict__ mind,
+    const float* __restrict__ maxd, float logsf, const eao_keypoint_dev* __restrict__ CK,
+    const uint8_t* __restrict__ CD, const int* __restrict__ pre, int nlevels, const float* __restrict__ scales,
+    const int* __restrict__ GS, const int* __restrict__ GI, float4* __restrict__ geo,
+    unsigned long long* __restrict__ ckeys, int* __restrict__ ccnt, BatchDims bd) {
+  const int f = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bd.nq) n_kf = min(bd.nq[f], bd.qs);
+  if (i >= n_kf) return;
+  Tg = at_slot(Tg, f, bd.qs ? 16 : 0);
+  valid = at_slot(valid, f, bd.qs);
+  pos = at_slot(pos, f, 3LL * bd.qs);
+  mdesc = at_slot(mdesc, f, 32LL * bd.qs);
+  mind = at_slot(mind, f, bd.qs);
+  maxd = at_slot(maxd, f, bd.qs);
+  CK = at_slot(CK, f, bd.cs);
+  CD = at_slot(CD, f, 32LL * bd.cs);
+  pre = at_slot(pre, f, bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  geo = at_slot(geo, f, bd.qs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tg[k];
+  float Ow[3];  // -Rcw^T tcw: transposed gemm operand, double accumulation (see k_frustum)
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    double s = (double)T[c] * (double)T[3];
+    s = __dadd_rn(s, (double)T[4 + c] * (double)T[7]);
+    s = __dadd_rn(s, (double)T[8 + c] * (double)T[11]);
+    Ow[c] = (float)(s * -1.0);
+  }
+  float4 g = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
+  if (valid[i]) {
+    const float* P = pos + 3 * i;
+    float Pc[3];
+    transform_point(T, P, Pc);
+    const float invzc = (float)(1.0 / (double)Pc[2]);
+    const float u = fadd(fmul(fmul(cam.fx, Pc[0]), invzc), cam.cx);
+    const float v = fadd(fmul(fmul(cam.fy, Pc[1]), invzc), cam.cy);
+    const float PO[3] = {fsub(P[0], Ow[0]), fsub(P[1], Ow[1]), fsub(P[2], Ow[2])};
+    double s = 0;
+    for (int k = 0; k < 3; k++) s = __dadd_rn(s, __dmul_rn((double)PO[k], (double)PO[k]));
+    const float dist3D = (float)sqrt(s);
+    const float maxDistance = fmul(1.2f, maxd[i]);
+    const float minDistance = fmul(0.8f, mind[i]);
+    if (!(u < cam.minX || u > cam.maxX || v < cam.minY || v > cam.maxY || dist3D < minDistance ||
+          dist3D > maxDistance)) {
+      const float ratio = fdiv(maxd[i], dist3D);
+      int lvl = (int)ceilf(fdiv((float)log((double)ratio), logsf));
+      lvl = min(max(lvl, 0), nlevels - 1);
+      g = make_float4(u, v, fmul(th, scales[lvl]), __int_as_float(lvl));
+    }
+  }
+  geo[i] = g;
+  unsigned long long best[MK];
+#pragma unroll
+  for (int k = 0; k < MK; k++) best[k] = KEY_NONE;
+  int n = 0;
+  const int lvl = __float_as_int(g.w);
+  if (lvl >= 0) {
+    const float u = g.x, v = g.y, r = g.z;
+    const Window w = window_cells(cam, u, v, r);
+    if (!w.empty) {
+      const int minL = lvl - 1, maxL = lvl + 1;
+      const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+      const uint8_t* d = mdesc + 32 * (long long)i;
+      for (int ck = 0; ck < ncell; ck++) {
+        const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+        for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+          const int i2 = GI[q];
+          const eao_keypoint_dev& kp = CK[i2];
+          if (minL > 0 && kp.octave < minL) continue;  // bCheckLevels: minL > 0 || maxL >= 0
+          if (kp.octave > maxL) continue;
+          if (!(fabsf(fsub(kp.x, u)) < r && fabsf(fsub(kp.y, v)) < r)) continue;
+          if (pre && pre[i2] >= 0) continue;
+          n++;
+          keep_smallest(best, make_key(hamming256(d, CD + 32 * (long long)i2), ck, i2));
+        }
+      }
+    }
+  }
+  store_keys(ckeys, ccnt, i, n, best);
+}
+
+// SearchForInitialization candidates, ORBmatcher.cc:405-450: level-0 keypoints of frame 1
+// in a square window around their previous matches (the vMatchedDistance test is the
+// assignment-dependent part, applied in k_match_init)
+__global__ __launch_bounds__(256) void k_init_cand(
+    CamDev cam, int n1, const eao_keypoint_dev* __restrict__ K1, const uint8_t* __restrict__ D1,
+    const eao_keypoint_dev* __restrict__ K2, const uint8_t* __restrict__ D2, const float* __restrict__ prev, int window,
+    const int* __restrict__ GS, const int* __restrict__ GI, unsigned long long* __restrict__ ckeys,
+    int* __restrict__ ccnt, BatchDims bd) {
+  const int f = blockIdx.y, i1 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bd.nq) n1 = min(bd.nq[f], bd.qs);
+  if (i1 >= n1) return;
+  K1 = at_slot(K1, f, bd.qs);
+  D1 = at_slot(D1, f, 32LL * bd.qs);
+  prev = at_slot(prev, f, 2LL * bd.qs);
+  K2 = at_slot(K2, f, bd.cs);
+  D2 = at_slot(D2, f, 32LL * bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  unsigned long long best[MK];
+#pragma unroll
+  for (int k = 0; k < MK; k++) best[k] = KEY_NONE;
+  int n = 0;
+  if (K1[i1].octave <= 0) {
+    const float r = (float)window;
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1];
+    const Window w = window_cells(cam, x, y, r);
+    if (!w.empty) {
+      const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+      const uint8_t* d1 = D1 + 32 * (long long)i1;
+      for (int ck = 0; ck < ncell; ck++) {
+        const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+        for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+          const int i2 = GI[q];
+          const eao_keypoint_dev& kp = K2[i2];
+          if (kp.octave < 0 || kp.octave > 0) continue;
+          if (!(fabsf(fsub(kp.x, x)) < r && fabsf(fsub(kp.y, y)) < r)) continue;
+          n++;
+          keep_smallest(best, make_key(hamming256(d1, D2 + 32 * (long long)i2), ck, i2));
+        }
+      }
+    }
+  }
+  store_keys(ckeys, ccnt, i1, n, best);
+}
+
+// stored keys of queries [base, base + nq) into LDS (kb: MK per query, nb: counts)
+__device__ __forceinline__ void stage_keys(const unsigned long long* __restrict__ ckeys, const int* __restrict__ ccnt,
+                                           int base, int nq, unsigned long long* kb, int* nb) {
+  const int lane = threadIdx.x;
+  __syncthreads();
+  nb[lane] = lane < nq ? ccnt[base + lane] : 0;
+  __syncthreads();
+  for (int k = lane; k < nq * MK; k += 64) {
+    const int qq = k / MK, c = k - qq * MK;
+    if (c < min(nb[qq], MK)) kb[k] = ckeys[(long long)base * MK + k];
+  }
+  __syncthreads();
+}
+
 // SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist), ORBmatcher.cc:1472-1599
 // (relocalisation, Tracking.cc:2295,2309). One wave. Phase 1 is lane-parallel: each lane
 // projects its map points (no depth test, as :1501-1506), applies the distance gate and
@@ -481,64 +724,59 @@ __global__ __launch_bounds__(64) void k_match_keyframe(
     const float* __restrict__ mind, const float* __restrict__ maxd, float logsf, int n_cur,
     const eao_keypoint_dev* __restrict__ CK, const uint8_t* __restrict__ CD,
     const int* __restrict__ pre, int nlevels, const float* __restrict__ scales,
-    const int* __restrict__ GS, const int* __restrict__ GI, float4* __restrict__ geo,
-    int* __restrict__ out, int* __restrict__ nmatch_out) {
+    const int* __restrict__ GS, const int* __restrict__ GI, const float4* __restrict__ geo,
+    const unsigned long long* __restrict__ ckeys, const int* __restrict__ ccnt,
+    int* __restrict__ out, int* __restrict__ nmatch_out, BatchDims bd) {
   __shared__ int match[MAXK];
   __shared__ signed char bins[MAXK];
   __shared__ int hist[HISTO_LENGTH];
-  const int lane = threadIdx.x;
-  float T[16];
-  for (int k = 0; k < 16; k++) T[k] = Tg[k];
-  float Ow[3];  // -Rcw^T tcw: transposed gemm operand, double accumulation (see k_frustum)
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    double s = (double)T[c] * (double)T[3];
-    s = __dadd_rn(s, (double)T[4 + c] * (double)T[7]);
-    s = __dadd_rn(s, (double)T[8 + c] * (double)T[11]);
-    Ow[c] = (float)(s * -1.0);
+  __shared__ unsigned long long kb[64 * MK];
+  __shared__ int nb[64];
+  const int lane = threadIdx.x, f = blockIdx.x;
+  if (bd.nq) {
+    n_kf = min(bd.nq[f], bd.qs);
+    n_cur = min(bd.nc[f], bd.cs);
   }
+  KK = at_slot(KK, f, bd.qs);
+  mdesc = at_slot(mdesc, f, 32LL * bd.qs);
+  geo = at_slot(geo, f, bd.qs);
+  CK = at_slot(CK, f, bd.cs);
+  CD = at_slot(CD, f, 32LL * bd.cs);
+  pre = at_slot(pre, f, bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  out = at_slot(out, f, bd.cs);
+  nmatch_out += f;
   for (int i = lane; i < n_cur; i += 64) {
     match[i] = pre ? pre[i] : -1;
     bins[i] = -1;
   }
-  for (int i = lane; i < n_kf; i += 64) {
-    float4 g = make_float4(0.f, 0.f, 0.f, __int_as_float(-1));
-    if (valid[i]) {
-      const float* P = pos + 3 * i;
-      float Pc[3];
-      transform_point(T, P, Pc);
-      const float invzc = (float)(1.0 / (double)Pc[2]);
-      const float u = fadd(fmul(fmul(cam.fx, Pc[0]), invzc), cam.cx);
-      const float v = fadd(fmul(fmul(cam.fy, Pc[1]), invzc), cam.cy);
-      const float PO[3] = {fsub(P[0], Ow[0]), fsub(P[1], Ow[1]), fsub(P[2], Ow[2])};
-      double s = 0;
-      for (int k = 0; k < 3; k++) s = __dadd_rn(s, __dmul_rn((double)PO[k], (double)PO[k]));
-      const float dist3D = (float)sqrt(s);
-      const float maxDistance = fmul(1.2f, maxd[i]);
-      const float minDistance = fmul(0.8f, mind[i]);
-      if (!(u < cam.minX || u > cam.maxX || v < cam.minY || v > cam.maxY ||
-            dist3D < minDistance || dist3D > maxDistance)) {
-        const float ratio = fdiv(maxd[i], dist3D);
-        int lvl = (int)ceilf(fdiv((float)log((double)ratio), logsf));
-        lvl = min(max(lvl, 0), nlevels - 1);
-        g = make_float4(u, v, fmul(th, scales[lvl]), __int_as_float(lvl));
-      }
-    }
-    geo[i] = g;
-  }
-  __syncthreads();
   int nmatches = 0;
   for (int i = 0; i < n_kf; i++) {
+    if ((i & 63) == 0) stage_keys(ckeys, ccnt, i, min(64, n_kf - i), kb, nb);
+    const int n = nb[i & 63];
+    if (n == 0) continue;  // not projected into the frame, or no candidate
+    // the smallest stored key whose keypoint is still free is the search's answer;
+    // only when every stored one is taken and the query has more candidates does the
+    // window have to be scanned again
+    const int nk = min(n, MK);
+    const unsigned long long sk = lane < nk ? kb[(i & 63) * MK + lane] : KEY_NONE;
+    const uint64_t fm = ballot(lane < nk && match[key_idx(sk)] < 0);
+    unsigned long long best = KEY_NONE;
+    if (fm) {
+      const int l = __builtin_ctzll(fm);
+      best = (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, l) |
+             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), l) << 32);
+    } else if (n > MK) {
     const float4 g = geo[i];
     const int lvl = __float_as_int(g.w);
-    if (lvl < 0) continue;
     const float u = g.x, v = g.y, r = g.z;
     const Window w = window_cells(cam, u, v, r);
-    if (w.empty) continue;
     const int minL = lvl - 1, maxL = lvl + 1;
     const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
     const uint8_t* d = mdesc + 32 * (long long)i;
-    unsigned long long best = KEY_NONE;
     for (int ck = lane; ck < ncell; ck += 64) {
       const int ix = w.x0 + ck / ncy, iy = w.y0 + ck % ncy;
       const int cell = ix * GRID_ROWS + iy;
@@ -555,6 +793,7 @@ __global__ __launch_bounds__(64) void k_match_keyframe(
       }
     }
     best = wave_min_u64(best);
+    }
     if (best != KEY_NONE && key_dist(best) <= orb_dist) {
       const int i2 = key_idx(best);
       if (lane == 0) {
@@ -596,22 +835,58 @@ __global__ __launch_bounds__(64) void k_match_local(
     const uint8_t* __restrict__ mdesc, int n_cur, const eao_keypoint_dev* __restrict__ CK,
     const uint8_t* __restrict__ CD, const int* __restrict__ pre, int nlevels,
     const float* __restrict__ scales, const int* __restrict__ GS, const int* __restrict__ GI,
-    int* __restrict__ out, int* __restrict__ nmatch_out) {
+    const unsigned long long* __restrict__ ckeys, const int* __restrict__ ccnt, int* __restrict__ out,
+    int* __restrict__ nmatch_out, BatchDims bd) {
   __shared__ int match[MAXK];
-  const int lane = threadIdx.x;
+  __shared__ unsigned long long kb[64 * MK];
+  __shared__ int nb[64];
+  const int lane = threadIdx.x, f = blockIdx.x;
+  if (bd.nq) {
+    n_mp = min(bd.nq[f], bd.qs);
+    n_cur = min(bd.nc[f], bd.cs);
+  }
+  proj = at_slot(proj, f, 2LL * bd.qs);
+  level = at_slot(level, f, bd.qs);
+  vcos = at_slot(vcos, f, bd.qs);
+  mdesc = at_slot(mdesc, f, 32LL * bd.qs);
+  CK = at_slot(CK, f, bd.cs);
+  CD = at_slot(CD, f, 32LL * bd.cs);
+  pre = at_slot(pre, f, bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  out = at_slot(out, f, bd.cs);
+  nmatch_out += f;
   for (int i = lane; i < n_cur; i += 64) match[i] = pre ? pre[i] : -1;
   __syncthreads();
   const bool bFactor = th != 1.0f;
   int nmatches = 0;
   for (int iMP = 0; iMP < n_mp; iMP++) {
-    if (!inview[iMP]) continue;
+    if ((iMP & 63) == 0) stage_keys(ckeys, ccnt, iMP, min(64, n_mp - iMP), kb, nb);
+    const int n = nb[iMP & 63];
+    if (n == 0) continue;  // not in view, or no candidate
+    // best and second best among the free candidates: the two smallest free stored
+    // keys when two of them are free or the query has no more candidates
+    const int nk = min(n, MK);
+    const unsigned long long sk = lane < nk ? kb[(iMP & 63) * MK + lane] : KEY_NONE;
+    const uint64_t fm = ballot(lane < nk && match[key_idx(sk)] < 0);
+    unsigned long long m1 = KEY_NONE, m2 = KEY_NONE;
+    auto lane_key = [&](int l) {
+      return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, l) |
+             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), l) << 32);
+    };
+    if (__builtin_popcountll(fm) >= 2 || n <= MK) {
+      if (fm) m1 = lane_key(__builtin_ctzll(fm));
+      const uint64_t f2 = fm & (fm - 1);
+      if (f2) m2 = lane_key(__builtin_ctzll(f2));
+    } else {
     const int L = min(max(level[iMP], 0), nlevels - 1);  // Q13 clamp
     float r = vcos[iMP] > 0.998f ? 2.5f : 4.0f;
     if (bFactor) r = fmul(r, th);
     const float rr = fmul(r, scales[L]);
     const float x = proj[2 * iMP], y = proj[2 * iMP + 1];
     const Window w = window_cells(cam, x, y, rr);
-    if (w.empty) continue;
     const int minL = L - 1, maxL = L;
     const bool checkL = (minL > 0) || (maxL >= 0);
     const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
@@ -639,8 +914,9 @@ __global__ __launch_bounds__(64) void k_match_local(
         }
       }
     }
-    const unsigned long long m1 = wave_min_u64(b1);
-    const unsigned long long m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    m1 = wave_min_u64(b1);
+    m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    }
     if (m1 == KEY_NONE) continue;
     const int bestDist = key_dist(m1);
     if (bestDist <= TH_HIGH) {
@@ -664,13 +940,30 @@ __global__ __launch_bounds__(64) void k_match_init(
     CamDev cam, float nnratio, int check_ori, int n1, const eao_keypoint_dev* __restrict__ K1,
     const uint8_t* __restrict__ D1, int n2, const eao_keypoint_dev* __restrict__ K2,
     const uint8_t* __restrict__ D2, float* __restrict__ prev, int window,
-    const int* __restrict__ GS, const int* __restrict__ GI, int* __restrict__ m12,
-    int* __restrict__ nmatch_out) {
+    const int* __restrict__ GS, const int* __restrict__ GI, const unsigned long long* __restrict__ ckeys,
+    const int* __restrict__ ccnt, int* __restrict__ m12, int* __restrict__ nmatch_out, BatchDims bd) {
+  __shared__ unsigned long long kb[64 * MK];
+  __shared__ int nb[64];
   __shared__ int mdist[MAXK];
   __shared__ int m21[MAXK];
   __shared__ signed char bins1[MAXK];
   __shared__ int hist[HISTO_LENGTH];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x, f = blockIdx.x;
+  if (bd.nq) {
+    n1 = min(bd.nq[f], bd.qs);
+    n2 = min(bd.nc[f], bd.cs);
+  }
+  K1 = at_slot(K1, f, bd.qs);
+  D1 = at_slot(D1, f, 32LL * bd.qs);
+  prev = at_slot(prev, f, 2LL * bd.qs);
+  K2 = at_slot(K2, f, bd.cs);
+  D2 = at_slot(D2, f, 32LL * bd.cs);
+  GS = at_slot(GS, f, GRID_CELLS + 1);
+  GI = at_slot(GI, f, bd.cs);
+  ckeys = at_slot(ckeys, f, (long long)MK * bd.qs);
+  ccnt = at_slot(ccnt, f, bd.qs);
+  m12 = at_slot(m12, f, bd.qs);
+  nmatch_out += f;
   for (int i = lane; i < n2; i += 64) {
     mdist[i] = INT_MAX;
     m21[i] = -1;
@@ -683,10 +976,26 @@ __global__ __launch_bounds__(64) void k_match_init(
   int nmatches = 0;
   const float r = (float)window;
   for (int i1 = 0; i1 < n1; i1++) {
-    if (K1[i1].octave > 0) continue;
+    if ((i1 & 63) == 0) stage_keys(ckeys, ccnt, i1, min(64, n1 - i1), kb, nb);
+    const int n = nb[i1 & 63];
+    if (n == 0) continue;  // a level > 0 keypoint, or no candidate
+    // the vMatchedDistance test (a keypoint of frame 2 is open to strictly closer
+    // matches only) decides among the stored keys when two pass or no more exist
+    const int nk = min(n, MK);
+    const unsigned long long sk = lane < nk ? kb[(i1 & 63) * MK + lane] : KEY_NONE;
+    const uint64_t fm = ballot(lane < nk && !(mdist[key_idx(sk)] <= key_dist(sk)));
+    unsigned long long m1 = KEY_NONE, m2 = KEY_NONE;
+    auto lane_key = [&](int l) {
+      return (unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sk, l) |
+             ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sk >> 32), l) << 32);
+    };
+    if (__builtin_popcountll(fm) >= 2 || n <= MK) {
+      if (fm) m1 = lane_key(__builtin_ctzll(fm));
+      const uint64_t f2 = fm & (fm - 1);
+      if (f2) m2 = lane_key(__builtin_ctzll(f2));
+    } else {
     const float x = prev[2 * i1], y = prev[2 * i1 + 1];
     const Window w = window_cells(cam, x, y, r);
-    if (w.empty) continue;
     const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
     const uint8_t* d1 = D1 + 32 * (long long)i1;
     unsigned long long b1 = KEY_NONE, b2 = KEY_NONE;
@@ -709,8 +1018,9 @@ __global__ __launch_bounds__(64) void k_match_init(
         }
       }
     }
-    const unsigned long long m1 = wave_min_u64(b1);
-    const unsigned long long m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    m1 = wave_min_u64(b1);
+    m2 = wave_min_u64(b1 == m1 ? b2 : b1);
+    }
     if (m1 == KEY_NONE) continue;
     const int bestDist = key_dist(m1);
     const int bestDist2 = m2 == KEY_NONE ? INT_MAX : key_dist(m2);
@@ -791,7 +1101,7 @@ int MatchEngine::init(int device, int mk, int mb) {
   EAO_HIP_CHECK(hipMalloc(&d_out, sizeof(int) * (mk * 2 + 16)));
   EAO_HIP_CHECK(hipMalloc(&d_T, sizeof(float) * 16 * 2));
   EAO_HIP_CHECK(hipMalloc(&d_scales, sizeof(float) * 32));
-  EAO_HIP_CHECK(hipMalloc(&d_geo, sizeof(float) * 4 * mk));
+  EAO_HIP_CHECK(hipMalloc(&d_geo, sizeof(float) * 4 * (size_t)mk * max_batch));
   EAO_HIP_CHECK(hipMalloc(&d_ckeys, sizeof(unsigned long long) * MK * (size_t)mk * max_batch));
   EAO_HIP_CHECK(hipMalloc(&d_cbins, (size_t)MK * mk * max_batch));
   EAO_HIP_CHECK(hipMalloc(&d_ccnt, sizeof(int) * (size_t)mk * max_batch));
@@ -952,6 +1262,106 @@ int eao_match_motion_batch_device(eao_matcher* m, const eao_camera* cam, int nfr
   return EAO_OK;
 }
 
+// ---- batched, HBM-resident single-frame searches: search f reads query slot f and
+// frame slot f; one candidate launch over all searches, one resolving wave per search
+static int batch_args(eao_matcher* m, const eao_camera* cam, int nsearch, int qcap, int cap, int nlevels,
+                      const void* q_counts, const void* c_counts, const char* what) {
+  if (!m || !cam || nsearch < 1 || qcap < 1 || cap < 1 || nlevels < 1 || nlevels > 32 || !q_counts || !c_counts)
+    return EAO_E_ARG;
+  if (nsearch > m->e.max_batch || qcap > m->e.max_kps || cap > m->e.max_kps) {
+    set_error(std::string(what) + ": more searches than max_batch or slots larger than max_kps");
+    return EAO_E_CAPACITY;
+  }
+  return EAO_OK;
+}
+
+int eao_match_local_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, float th, float nnratio,
+                                 int mp_cap, const int32_t* d_n_mp, const uint8_t* d_in_view, const float* d_proj_xy,
+                                 const int32_t* d_pred_level, const float* d_view_cos, const uint8_t* d_mp_desc,
+                                 int cap, const int32_t* d_n_cur, const eao_keypoint* d_cur_kps,
+                                 const uint8_t* d_cur_desc, const int32_t* d_cur_preassigned, int nlevels,
+                                 const float* scale_factors, int32_t* d_cur_match, int32_t* d_nmatches,
+                                 void* stream) {
+  int rc = batch_args(m, cam, nsearch, mp_cap, cap, nlevels, d_n_mp, d_n_cur, "eao_match_local_batch_device");
+  if (rc) return rc;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  const auto* CK = (const eao_keypoint_dev*)d_cur_kps;
+  rc = e.build_grid(cd, CK, d_n_cur, 0, cap, nsearch, s);
+  if (rc) return rc;
+  const BatchDims bd{d_n_mp, d_n_cur, mp_cap, cap};
+  hipLaunchKernelGGL(k_local_cand, dim3((mp_cap + 255) / 256, nsearch), dim3(256), 0, s, cd, th, 0, d_in_view,
+                     d_proj_xy, d_pred_level, d_view_cos, d_mp_desc, CK, d_cur_desc, d_cur_preassigned, nlevels,
+                     e.d_scales, e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, bd);
+  hipLaunchKernelGGL(k_match_local, dim3(nsearch), dim3(64), 0, s, cd, th, nnratio, 0, d_in_view, d_proj_xy,
+                     d_pred_level, d_view_cos, d_mp_desc, 0, CK, d_cur_desc, d_cur_preassigned, nlevels, e.d_scales,
+                     e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, d_cur_match, d_nmatches, bd);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+int eao_match_keyframe_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, const float* d_Tcw,
+                                    float th, int orb_dist, int check_ori, int kf_cap, const int32_t* d_n_kf,
+                                    const eao_keypoint* d_kf_kps, const uint8_t* d_kf_mp_valid,
+                                    const float* d_kf_mp_pos, const uint8_t* d_kf_mp_desc,
+                                    const float* d_kf_mp_min_dist, const float* d_kf_mp_max_dist,
+                                    float log_scale_factor, int cap, const int32_t* d_n_cur,
+                                    const eao_keypoint* d_cur_kps, const uint8_t* d_cur_desc,
+                                    const int32_t* d_cur_preassigned, int nlevels, const float* scale_factors,
+                                    int32_t* d_cur_match, int32_t* d_nmatches, void* stream) {
+  int rc = batch_args(m, cam, nsearch, kf_cap, cap, nlevels, d_n_kf, d_n_cur, "eao_match_keyframe_batch_device");
+  if (rc) return rc;
+  if (!d_Tcw) return EAO_E_ARG;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  const CamDev cd = make_cam(*cam);
+  const auto* CK = (const eao_keypoint_dev*)d_cur_kps;
+  const auto* KK = (const eao_keypoint_dev*)d_kf_kps;
+  rc = e.build_grid(cd, CK, d_n_cur, 0, cap, nsearch, s);
+  if (rc) return rc;
+  const BatchDims bd{d_n_kf, d_n_cur, kf_cap, cap};
+  hipLaunchKernelGGL(k_keyframe_cand, dim3((kf_cap + 255) / 256, nsearch), dim3(256), 0, s, cd, d_Tcw, th, 0,
+                     d_kf_mp_valid, d_kf_mp_pos, d_kf_mp_desc, d_kf_mp_min_dist, d_kf_mp_max_dist, log_scale_factor,
+                     CK, d_cur_desc, d_cur_preassigned, nlevels, e.d_scales, e.d_gstart, e.d_gitems,
+                     reinterpret_cast<float4*>(e.d_geo), e.d_ckeys, e.d_ccnt, bd);
+  hipLaunchKernelGGL(k_match_keyframe, dim3(nsearch), dim3(64), 0, s, cd, d_Tcw, th, orb_dist, check_ori, 0, KK,
+                     d_kf_mp_valid, d_kf_mp_pos, d_kf_mp_desc, d_kf_mp_min_dist, d_kf_mp_max_dist, log_scale_factor, 0,
+                     CK, d_cur_desc, d_cur_preassigned, nlevels, e.d_scales, e.d_gstart, e.d_gitems,
+                     reinterpret_cast<const float4*>(e.d_geo), e.d_ckeys, e.d_ccnt, d_cur_match, d_nmatches, bd);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+int eao_match_init_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, float nnratio, int check_ori,
+                                int cap1, const int32_t* d_n1, const eao_keypoint* d_kps1, const uint8_t* d_desc1,
+                                int cap2, const int32_t* d_n2, const eao_keypoint* d_kps2, const uint8_t* d_desc2,
+                                float* d_prev_matched_xy, int window, int32_t* d_matches12, int32_t* d_nmatches,
+                                void* stream) {
+  int rc = batch_args(m, cam, nsearch, cap1, cap2, 1, d_n1, d_n2, "eao_match_init_batch_device");
+  if (rc) return rc;
+  MatchEngine& e = m->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  const CamDev cd = make_cam(*cam);
+  const auto* K1 = (const eao_keypoint_dev*)d_kps1;
+  const auto* K2 = (const eao_keypoint_dev*)d_kps2;
+  rc = e.build_grid(cd, K2, d_n2, 0, cap2, nsearch, s);
+  if (rc) return rc;
+  const BatchDims bd{d_n1, d_n2, cap1, cap2};
+  hipLaunchKernelGGL(k_init_cand, dim3((cap1 + 255) / 256, nsearch), dim3(256), 0, s, cd, 0, K1, d_desc1, K2,
+                     d_desc2, d_prev_matched_xy, window, e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, bd);
+  hipLaunchKernelGGL(k_match_init, dim3(nsearch), dim3(64), 0, s, cd, nnratio, check_ori, 0, K1, d_desc1, 0, K2,
+                     d_desc2, d_prev_matched_xy, window, e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, d_matches12,
+                     d_nmatches, bd);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
 int eao_is_in_frustum(eao_matcher* m, const eao_camera* cam, const float* Tcw, int n_mp,
                       const float* mp_pos, const float* mp_normal, const float* mp_min_dist,
                       const float* mp_max_dist, float view_cos_limit, float log_scale_factor,
@@ -1007,10 +1417,14 @@ int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnrat
   const CamDev cd = make_cam(*cam);
   int rc = e.build_grid(cd, e.d_kps, nullptr, n_cur, K, 1, s);
   if (rc) return rc;
+  if (n_mp > 0)
+    hipLaunchKernelGGL(k_local_cand, dim3((n_mp + 255) / 256), dim3(256), 0, s, cd, th, n_mp, e.d_u8, e.d_f,
+                       e.d_i32, e.d_f2, e.d_mdesc, e.d_kps, e.d_desc, cur_preassigned ? e.d_i32b : nullptr, nlevels,
+                       e.d_scales, e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, BatchDims{});
   hipLaunchKernelGGL(k_match_local, dim3(1), dim3(64), 0, s, cd, th, nnratio, n_mp, e.d_u8, e.d_f, e.d_i32,
                      e.d_f2, e.d_mdesc, n_cur, e.d_kps, e.d_desc,
                      cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart,
-                     e.d_gitems, e.d_out, e.d_out + 2 * K);
+                     e.d_gitems, e.d_ckeys, e.d_ccnt, e.d_out, e.d_out + 2 * K, BatchDims{});
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
@@ -1052,11 +1466,17 @@ int eao_match_keyframe(eao_matcher* m, const eao_camera* cam, const float* Tcw, 
   const CamDev cd = make_cam(*cam);
   int rc = e.build_grid(cd, e.d_kps, nullptr, n_cur, K, 1, s);
   if (rc) return rc;
+  if (n_kf > 0)
+    hipLaunchKernelGGL(k_keyframe_cand, dim3((n_kf + 255) / 256), dim3(256), 0, s, cd, e.d_T, th, n_kf, e.d_u8,
+                       e.d_f, e.d_mdesc, e.d_f3, e.d_f3 + K, log_scale_factor, e.d_kps, e.d_desc,
+                       cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart, e.d_gitems,
+                       reinterpret_cast<float4*>(e.d_geo), e.d_ckeys, e.d_ccnt, BatchDims{});
   hipLaunchKernelGGL(k_match_keyframe, dim3(1), dim3(64), 0, s, cd, e.d_T, th, orb_dist, check_ori,
                      n_kf, e.d_kps + K, e.d_u8, e.d_f, e.d_mdesc, e.d_f3, e.d_f3 + K,
                      log_scale_factor, n_cur, e.d_kps, e.d_desc,
                      cur_preassigned ? e.d_i32b : nullptr, nlevels, e.d_scales, e.d_gstart,
-                     e.d_gitems, reinterpret_cast<float4*>(e.d_geo), e.d_out, e.d_out + 2 * K);
+                     e.d_gitems, reinterpret_cast<const float4*>(e.d_geo), e.d_ckeys, e.d_ccnt, e.d_out,
+                     e.d_out + 2 * K, BatchDims{});
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
@@ -1083,9 +1503,13 @@ int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int che
   const CamDev cd = make_cam(*cam);
   int rc = e.build_grid(cd, e.d_kps, nullptr, n2, K, 1, s);
   if (rc) return rc;
+  if (n1 > 0)
+    hipLaunchKernelGGL(k_init_cand, dim3((n1 + 255) / 256), dim3(256), 0, s, cd, n1, e.d_kps + K,
+                       e.d_desc + (size_t)K * 32, e.d_kps, e.d_desc, e.d_f, window, e.d_gstart, e.d_gitems,
+                       e.d_ckeys, e.d_ccnt, BatchDims{});
   hipLaunchKernelGGL(k_match_init, dim3(1), dim3(64), 0, s, cd, nnratio, check_ori, n1,
                      e.d_kps + K, e.d_desc + (size_t)K * 32, n2, e.d_kps, e.d_desc, e.d_f, window,
-                     e.d_gstart, e.d_gitems, e.d_out, e.d_out + 2 * K);
+                     e.d_gstart, e.d_gitems, e.d_ckeys, e.d_ccnt, e.d_out, e.d_out + 2 * K, BatchDims{});
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(matches12, e.d_out, sizeof(int) * n1, hipMemcpyDeviceToHost, s));

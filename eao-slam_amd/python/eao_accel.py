@@ -262,6 +262,37 @@ class Matcher:
               "eao_match_motion_batch_device")
 
 
+    # batched HBM-resident single-frame searches: the arguments are device pointers
+    # (ints), slot strides q_cap / cap; see include/eao_accel.h
+    def local_batch_device(self, cam, nsearch, th, nnratio, mp_cap, n_mp, inv, proj, lvl, vc, mp_desc, cap, n_cur,
+                           cur_kps, cur_desc, pre, scales, match, nmatch, stream=None):
+        sc = np.ascontiguousarray(scales, np.float32)
+        v = ctypes.c_void_p
+        check(lib().eao_match_local_batch_device(
+            self.h, ctypes.byref(cam), nsearch, ctypes.c_float(th), ctypes.c_float(nnratio), mp_cap, v(n_mp), v(inv),
+            v(proj), v(lvl), v(vc), v(mp_desc), cap, v(n_cur), v(cur_kps), v(cur_desc), v(pre) if pre else None,
+            len(sc), P(sc), v(match), v(nmatch), v(stream) if stream else None), "eao_match_local_batch_device")
+
+    def keyframe_batch_device(self, cam, nsearch, T, th, orb_dist, check_ori, kf_cap, n_kf, kf_kps, valid, pos, desc,
+                              mind, maxd, logsf, cap, n_cur, cur_kps, cur_desc, pre, scales, match, nmatch,
+                              stream=None):
+        sc = np.ascontiguousarray(scales, np.float32)
+        v = ctypes.c_void_p
+        check(lib().eao_match_keyframe_batch_device(
+            self.h, ctypes.byref(cam), nsearch, v(T), ctypes.c_float(th), int(orb_dist), int(check_ori), kf_cap,
+            v(n_kf), v(kf_kps), v(valid), v(pos), v(desc), v(mind), v(maxd), ctypes.c_float(logsf), cap, v(n_cur),
+            v(cur_kps), v(cur_desc), v(pre) if pre else None, len(sc), P(sc), v(match), v(nmatch),
+            v(stream) if stream else None), "eao_match_keyframe_batch_device")
+
+    def init_batch_device(self, cam, nsearch, nnratio, check_ori, cap1, n1, kps1, desc1, cap2, n2, kps2, desc2, prev,
+                          window, m12, nmatch, stream=None):
+        v = ctypes.c_void_p
+        check(lib().eao_match_init_batch_device(
+            self.h, ctypes.byref(cam), nsearch, ctypes.c_float(nnratio), int(check_ori), cap1, v(n1), v(kps1),
+            v(desc1), cap2, v(n2), v(kps2), v(desc2), v(prev), int(window), v(m12), v(nmatch),
+            v(stream) if stream else None), "eao_match_init_batch_device")
+
+
 class Assoc:
     """Object_2D / Object_Map math replacement (reference src/Object.cc, isolation_forest.h)."""
 

@@ -184,6 +184,37 @@ int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int che
                    const eao_keypoint* kps2, const uint8_t* desc2, float* prev_matched_xy,
                    int window, int32_t* matches12);
 
+/* batched, HBM-resident forms of the three single-frame searches above (same
+   arguments per search; no reference counterpart batches them -- the tracker calls
+   one per frame, Tracking.cc:1985 (local map), :2295,2309 (relocalisation),
+   :1042 (initialisation) -- this is the form a multi-stream / multi-camera caller
+   queues). Search f reads query slot f ([nsearch][q_cap] arrays with counts
+   d_n_*[f]) and frame slot f ([nsearch][cap] keypoints / descriptors / preassigned
+   with counts d_n_cur[f]); outputs are [nsearch][cap] (init: [nsearch][cap1]) plus
+   d_nmatches[f]. Keyframe poses d_Tcw are [nsearch][16]. Asynchronous on `stream`
+   (NULL: the matcher's own stream). */
+int eao_match_local_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, float th, float nnratio,
+                                 int mp_cap, const int32_t* d_n_mp, const uint8_t* d_in_view, const float* d_proj_xy,
+                                 const int32_t* d_pred_level, const float* d_view_cos, const uint8_t* d_mp_desc,
+                                 int cap, const int32_t* d_n_cur, const eao_keypoint* d_cur_kps,
+                                 const uint8_t* d_cur_desc, const int32_t* d_cur_preassigned, int nlevels,
+                                 const float* scale_factors, int32_t* d_cur_match, int32_t* d_nmatches,
+                                 void* stream);
+int eao_match_keyframe_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, const float* d_Tcw,
+                                    float th, int orb_dist, int check_ori, int kf_cap, const int32_t* d_n_kf,
+                                    const eao_keypoint* d_kf_kps, const uint8_t* d_kf_mp_valid,
+                                    const float* d_kf_mp_pos, const uint8_t* d_kf_mp_desc,
+                                    const float* d_kf_mp_min_dist, const float* d_kf_mp_max_dist,
+                                    float log_scale_factor, int cap, const int32_t* d_n_cur,
+                                    const eao_keypoint* d_cur_kps, const uint8_t* d_cur_desc,
+                                    const int32_t* d_cur_preassigned, int nlevels, const float* scale_factors,
+                                    int32_t* d_cur_match, int32_t* d_nmatches, void* stream);
+int eao_match_init_batch_device(eao_matcher* m, const eao_camera* cam, int nsearch, float nnratio, int check_ori,
+                                int cap1, const int32_t* d_n1, const eao_keypoint* d_kps1, const uint8_t* d_desc1,
+                                int cap2, const int32_t* d_n2, const eao_keypoint* d_kps2, const uint8_t* d_desc2,
+                                float* d_prev_matched_xy, int window, int32_t* d_matches12, int32_t* d_nmatches,
+                                void* stream);
+
 /* --- EAO association: replaces Object_2D / Object_Map math (src/Object.cc) -- */
 typedef struct {
   int32_t verdict; /* 0: m<20, 1: pass, 2: fail -- NoParaDataAssociation return */
