@@ -108,14 +108,14 @@ def algorithmic_bytes(n_kps):
     return {
         "pyramid": sum(lv[:-1]) + upper,        # resize: read level l-1, write level l (l = 1..7)
         "fast": l0 + upper,                     # FAST: every level plane read once
-        "blur": 2 * (l0 + upper),               # blur: every level read once, blurred copy written once
-        "describe": 2 * (l0 + upper) + n_kps * 60,  # orient (raw) + describe (blurred), 28 B kp + 32 B desc
+        # orient + blur + describe from the raw levels (each read once), 28 B kp + 32 B desc written
+        "describe": l0 + upper + n_kps * 60,
         "extract": l0 + 2 * upper + n_kps * 60,     # SURVEY §8d per-frame figure for the whole extraction
     }
 
 
-STAGES = ["pyramid", "fast", "distribute", "blur", "describe"]
-KERNELS = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute", "blur": "k_blur",
+STAGES = ["pyramid", "fast", "distribute", "describe"]  # the level blur is fused into k_describe
+KERNELS = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
            "describe": "k_describe"}
 
 

@@ -32,18 +32,12 @@ struct LevelDev {
   float scale, size;          // mvScaleFactor[l], PATCH_SIZE*scale truncated
   int tab_x, tab_y, xmax;     // resize tables
   int pad1;
-  long long blur_off;         // byte offset of the blurred level plane in a frame's blur area
 };
 
 struct BandDev {              // one row of FAST cells of a level
   int16_t level, ncells;
   int16_t x0, y0, x1, y1;     // union of the cells' ROIs
   int cell_begin;
-};
-
-struct BlurTile {             // 64 x 16 output tile of one level
-  int16_t level, pad;
-  int16_t x0, y0;
 };
 
 struct CellDev {
@@ -64,13 +58,12 @@ class OrbEngine {
   std::vector<int> resize_xofs, resize_yrows;
   std::vector<short> resize_ia, resize_ib;
   std::vector<int2> slot_map;
-  long long pyr_bytes = 0, blur_bytes = 0, cand_stride = 0, sel_stride = 0;
-  std::vector<BlurTile> btiles;
+  long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;
   std::vector<BandDev> bands;
   int band_w = 0, band_h = 0;  // largest band ROI
   int cap = 0, roi_stride = 0, roi_rows = 0;
-  // optional per-stage timing: events around resize / fast / distribute / blur / describe
-  static constexpr int kStages = 5;
+  // optional per-stage timing: events around resize / fast / distribute / describe (blur fused)
+  static constexpr int kStages = 4;
   bool timing = false;
   hipEvent_t ev[kStages + 1] = {};
 
@@ -81,8 +74,6 @@ class OrbEngine {
   short *d_ia = nullptr, *d_ib = nullptr;
   int2* d_slot_map = nullptr;
   uint8_t* d_pyr = nullptr;
-  uint8_t* d_blur = nullptr;  // per frame: the 7x7 sigma-2 blur of every level (ORBextractor.cc:1085-1086)
-  BlurTile* d_btiles = nullptr;
   BandDev* d_bands = nullptr;
   uint32_t *d_cand = nullptr, *d_qbuf = nullptr, *d_sel = nullptr;
   int *d_cell_cnt = nullptr, *d_sel_cnt = nullptr;

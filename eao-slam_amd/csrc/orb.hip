@@ -10,11 +10,11 @@
 //                     minTh retry for empty cells (ORBextractor.cc:789-829)
 //   k_distribute  x1  one wave per (level, frame): DistributeOctTree with
 //                     the reference's list order (ORBextractor.cc:539-763)
-//   k_blur        x1  7x7 sigma-2 Gaussian of every level (separable, fixed
-//                     point, REFLECT_101), 64x64 output tiles (:1085-1086)
-//   k_describe    x1  one wave per selected keypoint: IC_Angle on the level,
-//                     the 512 rBRIEF taps gathered from the blurred level,
-//                     256-bit descriptor, final scaling (:77-147, :1076-1104)
+//   k_describe    x1  one wave per selected keypoint: the raw 43x43 patch in LDS,
+//                     IC_Angle on it, the 7x7 sigma-2 blur (REFLECT_101) fused --
+//                     horizontal sums of the patch, vertical sums at the 512
+//                     rBRIEF taps only -- 256-bit descriptor, final scaling
+//                     (:77-147, :1076-1104; blur :1085-1086)
 // Bit-exactness: integer paths are exact; float paths use __f*_rn intrinsics
 // and -ffp-contract=off so every rounding matches the oracle.
 #include <hip/hip_runtime.h>
@@ -758,122 +758,30 @@ __device__ float fast_atan2(float y, float x) {
   return a;
 }
 
-// ---------------------------------------------------------------- blur
-constexpr int BLUR_TH = 64;  // output rows per blur tile
-// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of every level, the clone
-// ORBextractor::operator() blurs before computeDescriptors (:1085-1086): 8U
-// fixed point, separable (exact in integers): horizontal sums of 8-bit
-// pixels x 8-bit taps stay below 2^16, then (sum_v + 2^15) >> 16, saturated.
-// One workgroup per 64 x BLUR_TH output tile (BLUR_TH + 6 staged rows).
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ frames, int fpitch,
-                                              long long fstride, const uint8_t* __restrict__ pyr,
-                                              long long pstride, const LevelDev* __restrict__ levels,
-                                              const BlurTile* __restrict__ tiles,
-                                              const int* __restrict__ gk, uint8_t* __restrict__ blur,
-                                              long long bstride) {
-  // in: BLUR_TH+6 rows x 72 cols (x0-4 .. x0+67), word aligned; hs: horizontal
-  // sums (< 2^16) packed two per word, BLUR_TH+6 rows x 64 cols
-  constexpr int NR = BLUR_TH + 6;
-  __shared__ uint32_t in[NR][18];
-  __shared__ uint32_t hs[NR][32];
-  const BlurTile T = tiles[blockIdx.x];
-  const int f = blockIdx.y, t = threadIdx.x;
-  const LevelDev& L = levels[T.level];
-  const uint8_t* img;
-  int pitch;
-  if (T.level == 0) {
-    img = frames + f * fstride;
-    pitch = fpitch;
-  } else {
-    img = pyr + f * pstride + L.plane_off;
-    pitch = L.pitch;
-  }
-  const bool interior = T.x0 >= 4 && T.x0 + 68 <= L.w && T.y0 >= 3 && T.y0 + BLUR_TH + 3 <= L.h && (pitch & 3) == 0;
-  if (interior) {
-    for (int i = t; i < NR * 18; i += 256) {
-      const int r = i / 18, c = i - r * 18;
-      in[r][c] = *(const uint32_t*)(img + (long long)(T.y0 - 3 + r) * pitch + T.x0 - 4 + 4 * c);
-    }
-  } else {
-    uint8_t* inb = (uint8_t*)&in[0][0];
-    for (int i = t; i < NR * 72; i += 256) {
-      const int r = i / 72, c = i - r * 72;
-      int yy = T.y0 - 3 + r, xx = T.x0 - 4 + c;
-      // REFLECT_101 on the isolated level (gfedcb|abcdefgh|gfedcba)
-      if (L.h == 1) yy = 0;
-      while (yy < 0 || yy >= L.h) yy = yy < 0 ? -yy : 2 * L.h - 2 - yy;
-      if (L.w == 1) xx = 0;
-      while (xx < 0 || xx >= L.w) xx = xx < 0 ? -xx : 2 * L.w - 2 - xx;
-      inb[r * 72 + c] = img[(long long)yy * pitch + xx];
-    }
-  }
-  __syncthreads();
-  int k[7];
-#pragma unroll
-  for (int i = 0; i < 7; i++) k[i] = gk[i];
-  // horizontal: item (row, group of 4 columns): columns 4g..4g+3 use input
-  // bytes 4g+1 .. 4g+10 (input column 0 is x0-4)
-  for (int i = t; i < NR * 16; i += 256) {
-    const int r = i >> 4, g = i & 15;
-    const uint32_t w0 = in[r][g], w1 = in[r][g + 1], w2 = in[r][g + 2];
-    int px[12];
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      px[q] = (w0 >> (8 * q)) & 255;
-      px[4 + q] = (w1 >> (8 * q)) & 255;
-      px[8 + q] = (w2 >> (8 * q)) & 255;
-    }
-    uint32_t h[4];
-#pragma unroll
-    for (int o = 0; o < 4; o++) {
-      uint32_t v = 0;
-#pragma unroll
-      for (int j = 0; j < 7; j++) v += (uint32_t)(k[j] * px[o + 1 + j]);
-      h[o] = v;
-    }
-    hs[r][2 * g] = h[0] | (h[1] << 16);
-    hs[r][2 * g + 1] = h[2] | (h[3] << 16);
-  }
-  __syncthreads();
-  // vertical: item -> (row, 4 columns)
-  for (int it = t; it < BLUR_TH * 16; it += 256) {
-    const int r = it >> 4, g = it & 15;
-    const int x = T.x0 + 4 * g, y = T.y0 + r;
-    if (y >= L.h || x >= L.w) continue;
-    uint32_t acc[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 7; j++) {
-      const uint32_t a0 = hs[r + j][2 * g], a1 = hs[r + j][2 * g + 1];
-      acc[0] += (uint32_t)k[j] * (a0 & 0xffffu);
-      acc[1] += (uint32_t)k[j] * (a0 >> 16);
-      acc[2] += (uint32_t)k[j] * (a1 & 0xffffu);
-      acc[3] += (uint32_t)k[j] * (a1 >> 16);
-    }
-    uint32_t ow = 0;
-#pragma unroll
-    for (int o = 0; o < 4; o++) ow |= min((acc[o] + (1u << 15)) >> 16, 255u) << (8 * o);
-    uint8_t* out = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
-    if (x + 4 <= L.w) {
-      *(uint32_t*)out = ow;  // pitch and x are multiples of 4
-    } else {
-      for (int o = 0; o < 4 && x + o < L.w; o++) out[o] = (uint8_t)(ow >> (8 * o));
-    }
-  }
-}
-
 // ---------------------------------------------------------------- describe
-// One wave per selected keypoint: IC_Angle on the raw level, then the 256
-// rBRIEF tests (4 per lane) gathered from the blurred level. Keypoints lie
-// >= 19 px inside the level (minBorder 16 + FAST 3) and the rotated pattern
-// reaches <= 18 px, so no border handling is needed here.
+// GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of the level, fused: the reference
+// blurs a clone of every level (ORBextractor.cc:1085-1086) and computeDescriptors reads
+// 512 pattern taps of it around each keypoint. Here one wave per keypoint stages the
+// raw 43 x 43 patch (pattern reach 18 + blur 3) in LDS, takes IC_Angle from it, forms
+// the horizontal 7-tap sums of the 43 x 37 rows it needs and finishes the vertical sum
+// only at the 512 rotated taps -- no blurred plane in HBM. Blur arithmetic is the 8U
+// fixed point of cv::GaussianBlur, exact in integers: horizontal sums of 8-bit pixels
+// x 8-bit taps stay below 2^16, then (sum_v + 2^15) >> 16, saturated.
+constexpr int PR = 21;          // staged patch radius
+constexpr int PW = 2 * PR + 1;  // staged rows
+constexpr int PD = 13;          // staged dwords per row (12 + one pad for the last column group)
+constexpr int HC = 40;          // horizontal sums per row: dx = -18 .. 21 (37 used)
+
+// one workgroup = 4 waves = 4 keypoints; control flow stays uniform over the barriers
 __global__ __launch_bounds__(256) void k_describe(
     const uint8_t* __restrict__ frames, int fpitch, long long fstride,
-    const uint8_t* __restrict__ pyr, long long pstride, const uint8_t* __restrict__ blur,
-    long long bstride, const LevelDev* __restrict__ levels,
+    const uint8_t* __restrict__ pyr, long long pstride, const LevelDev* __restrict__ levels,
     const uint32_t* __restrict__ sel, long long sel_stride, const int* __restrict__ sel_cnt,
     const int2* __restrict__ slot_map, int nslots, int nlevels, const int* __restrict__ umax,
-    eao_keypoint_dev* __restrict__ out_kps, uint8_t* __restrict__ out_desc, int* __restrict__ out_cnt,
-    int cap) {
+    const int* __restrict__ gk, eao_keypoint_dev* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
+    int* __restrict__ out_cnt, int cap) {
+  __shared__ uint32_t raw[4][PW][PD];
+  __shared__ uint16_t hs[4][PW][HC];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int slot = blockIdx.x * 4 + w;
   const int f = blockIdx.y;
@@ -883,45 +791,103 @@ __global__ __launch_bounds__(256) void k_describe(
     for (int i = 0; i < nlevels; i++) tot += max(cnts[i], 0);
     out_cnt[f] = tot;
   }
-  if (slot >= nslots) return;
-  const int2 sm = slot_map[slot];  // (level, index within level)
-  const int l = sm.x, k = sm.y;
-  if (k >= cnts[l]) return;
-  int off = 0;
-  for (int i = 0; i < l; i++) off += max(cnts[i], 0);
-  const LevelDev& L = levels[l];
-  const uint32_t pk = sel[f * sel_stride + L.sel_off + k];
-  const int x = kp_x(pk) + L.minBX, y = kp_y(pk) + L.minBY;
-  const uint8_t* img;
-  int pitch;
-  if (l == 0) {
-    img = frames + f * fstride;
-    pitch = fpitch;
-  } else {
-    img = pyr + f * pstride + L.plane_off;
-    pitch = L.pitch;
+  int2 sm = make_int2(0, 0);
+  bool active = slot < nslots;
+  if (active) {
+    sm = slot_map[slot];  // (level, index within level)
+    active = sm.y < cnts[sm.x];
   }
-  // ---- IC_Angle (ORBextractor.cc:77-104): integer moments, wave reduction
+  const int l = sm.x, k = sm.y;
+  const LevelDev& L = levels[l];
+  int x = 0, y = 0, off = 0;
+  uint32_t pk = 0;
+  uint8_t* rb = (uint8_t*)&raw[w][0][0];
+  if (active) {
+    pk = sel[f * sel_stride + L.sel_off + k];
+    x = kp_x(pk) + L.minBX;
+    y = kp_y(pk) + L.minBY;
+    const uint8_t* img;
+    int pitch;
+    if (l == 0) {
+      img = frames + f * fstride;
+      pitch = fpitch;
+    } else {
+      img = pyr + f * pstride + L.plane_off;
+      pitch = L.pitch;
+    }
+    const int xa = (x - PR) & ~3;
+    if (x - PR >= 0 && x + PR < L.w && y - PR >= 0 && y + PR < L.h && (pitch & 3) == 0 && xa + 48 <= pitch) {
+      // interior: 12 aligned dwords per row from x - PR rounded down; `off` bytes of lead
+      off = x - PR - xa;
+      const uint32_t* src = (const uint32_t*)(img + (long long)(y - PR) * pitch + xa);
+      for (int i = lane; i < PW * 12; i += 64) {
+        const int r = i / 12, c = i - r * 12;
+        raw[w][r][c] = src[r * (pitch >> 2) + c];
+      }
+    } else {
+      // near the level edge: bytes with REFLECT_101 on the isolated level (gfedcb|abcdefgh|gfedcba)
+      for (int i = lane; i < PW * PW; i += 64) {
+        const int r = i / PW, c = i - r * PW;
+        int yy = y - PR + r, xx = x - PR + c;
+        if (L.h == 1) yy = 0;
+        while (yy < 0 || yy >= L.h) yy = yy < 0 ? -yy : 2 * L.h - 2 - yy;
+        if (L.w == 1) xx = 0;
+        while (xx < 0 || xx >= L.w) xx = xx < 0 ? -xx : 2 * L.w - 2 - xx;
+        rb[r * 4 * PD + c] = img[(long long)yy * pitch + xx];
+      }
+    }
+    if (lane < PW) raw[w][lane][12] = 0;
+  }
+  __syncthreads();
+  // ---- IC_Angle (ORBextractor.cc:77-104) on the raw patch: integer moments, wave reduction
   int m10 = 0, m01 = 0;
-  const uint8_t* center = img + (long long)y * pitch + x;
-  if (lane < 31) m10 += (lane - 15) * center[lane - 15];
-  for (int v = 1 + (lane >> 5); v <= 15; v += 2) {
-    const int d = umax[v];
-    const int u = (lane & 31) - d;
-    if (u <= d) {
-      const int vp = center[u + v * pitch], vm = center[u - v * pitch];
-      m10 += u * (vp + vm);
-      m01 += v * (vp - vm);
+  const uint8_t* center = rb + PR * 4 * PD + off + PR;
+  if (active) {
+    if (lane < 31) m10 += (lane - 15) * center[lane - 15];
+    for (int v = 1 + (lane >> 5); v <= 15; v += 2) {
+      const int d = umax[v];
+      const int u = (lane & 31) - d;
+      if (u <= d) {
+        const int vp = center[u + v * 4 * PD], vm = center[u - v * 4 * PD];
+        m10 += u * (vp + vm);
+        m01 += v * (vp - vm);
+      }
+    }
+    // ---- horizontal 7-tap sums: item (row, group of 4 output columns); output column c
+    // (dx = c - 18) sums staged bytes off + c .. off + c + 6 -- v_dot4 on realigned words
+    const uint32_t K0 = (uint32_t)gk[0] | ((uint32_t)gk[1] << 8) | ((uint32_t)gk[2] << 16) | ((uint32_t)gk[3] << 24);
+    const uint32_t K1 = (uint32_t)gk[4] | ((uint32_t)gk[5] << 8) | ((uint32_t)gk[6] << 16);
+    for (int i = lane; i < PW * (HC / 4); i += 64) {
+      const int r = i / (HC / 4), g = i - r * (HC / 4);
+      const uint32_t* rw = &raw[w][r][g];
+      const uint32_t W0 = rw[0], W1 = rw[1], W2 = rw[2], W3 = rw[3];
+      const uint32_t A0 = __builtin_amdgcn_alignbyte(W1, W0, off);
+      const uint32_t A1 = __builtin_amdgcn_alignbyte(W2, W1, off);
+      const uint32_t A2 = __builtin_amdgcn_alignbyte(W3, W2, off);
+      uint32_t h[4];
+      h[0] = __builtin_amdgcn_udot4(A0, K0, __builtin_amdgcn_udot4(A1, K1, 0u, false), false);
+#pragma unroll
+      for (int o = 1; o < 4; o++) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(A1, A0, o), hi = __builtin_amdgcn_alignbyte(A2, A1, o);
+        h[o] = __builtin_amdgcn_udot4(lo, K0, __builtin_amdgcn_udot4(hi, K1, 0u, false), false);
+      }
+      uint32_t* hw = (uint32_t*)&hs[w][r][4 * g];
+      hw[0] = h[0] | (h[1] << 16);
+      hw[1] = h[2] | (h[3] << 16);
     }
   }
   m10 = wave_sum(m10);
   m01 = wave_sum(m01);
+  __syncthreads();
+  if (!active) return;  // no barrier follows
   const float angle = fast_atan2((float)m01, (float)m10);
-  // ---- rBRIEF (ORBextractor.cc:108-147) on the blurred level
+  // ---- rBRIEF (ORBextractor.cc:108-147): the vertical 7-tap sum at each rotated tap
   const float factorPI = (float)(M_PI / 180.f);
   const float ang = fmul(angle, factorPI);
   const float a = (float)cos((double)ang), b = (float)sin((double)ang);
-  const uint8_t* bc = blur + f * bstride + L.blur_off + (long long)y * L.pitch + x;
+  int kv[7];
+#pragma unroll
+  for (int j = 0; j < 7; j++) kv[j] = gk[j];
   const int byte = lane >> 1, half = lane & 1;
   int px[8];
 #pragma unroll
@@ -930,13 +896,19 @@ __global__ __launch_bounds__(256) void k_describe(
     const float fx = (float)c_pattern[2 * pi], fy = (float)c_pattern[2 * pi + 1];
     const int dy = dev_round(fadd(fmul(fx, b), fmul(fy, a)));
     const int dx = dev_round(fsub(fmul(fx, a), fmul(fy, b)));
-    px[e] = bc[dy * L.pitch + dx];
+    const uint16_t* col = &hs[w][PR + dy - 3][dx + 18];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int j = 0; j < 7; j++) acc += (uint32_t)kv[j] * col[j * HC];
+    px[e] = (int)min((acc + (1u << 15)) >> 16, 255u);
   }
   int nib = 0;
 #pragma unroll
   for (int t = 0; t < 4; t++) nib |= (px[2 * t] < px[2 * t + 1]) << t;
   const int other = __shfl_xor(nib, 1, 64);
-  const long long oi = (long long)f * cap + off + k;
+  int off_l = 0;
+  for (int i = 0; i < l; i++) off_l += max(cnts[i], 0);
+  const long long oi = (long long)f * cap + off_l + k;
   if (half == 0) out_desc[oi * 32 + byte] = (uint8_t)(nib | (other << 4));
   if (lane == 0) {
     eao_keypoint_dev kp;
@@ -1167,18 +1139,6 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
       c = e;
     }
   }
-  {
-    // blur area: level 0 plane then levels 1.. in the pyramid layout
-    const long long l0 = (long long)levels[0].pitch * levels[0].h;
-    btiles.clear();
-    for (int l = 0; l < nl; l++) {
-      LevelDev& L = levels[l];
-      L.blur_off = l == 0 ? 0 : l0 + L.plane_off;
-      for (int y = 0; y < L.h; y += BLUR_TH)
-        for (int x = 0; x < L.w; x += 64) btiles.push_back(BlurTile{(int16_t)l, 0, (int16_t)x, (int16_t)y});
-    }
-    blur_bytes = (l0 + poff + 255) & ~255LL;
-  }
   cand_stride = ((long long)cand_total + 63) & ~63LL;
   sel_stride = ((long long)sel_total + 63) & ~63LL;
   cap = sel_total;
@@ -1210,9 +1170,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
   if ((rc = up((void**)&d_umax, umax.data(), umax.size() * sizeof(int)))) return rc;
   if ((rc = up((void**)&d_gk, gk.data(), gk.size() * sizeof(int)))) return rc;
   if ((rc = up((void**)&d_slot_map, slot_map.data(), slot_map.size() * sizeof(int2)))) return rc;
-  if ((rc = up((void**)&d_btiles, btiles.data(), btiles.size() * sizeof(BlurTile)))) return rc;
   if ((rc = up((void**)&d_bands, bands.data(), bands.size() * sizeof(BandDev)))) return rc;
-  EAO_HIP_CHECK(hipMalloc(&d_blur, blur_bytes * B));
   EAO_HIP_CHECK(hipMalloc(&d_pyr, std::max<long long>(pyr_bytes, 256) * B));
   EAO_HIP_CHECK(hipMalloc(&d_cand, cand_stride * sizeof(uint32_t) * B));
   EAO_HIP_CHECK(hipMalloc(&d_qbuf, 2 * cand_stride * sizeof(uint32_t) * B));
@@ -1229,7 +1187,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
 
 OrbEngine::~OrbEngine() {
   void* ptrs[] = {d_levels, d_cells, d_xofs, d_ia, d_yrows, d_ib, d_umax, d_gk, d_slot_map,
-                  d_btiles, d_bands, d_blur, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
+                  d_bands, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
                   d_out_desc, d_out_cnt};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
@@ -1291,22 +1249,15 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
                        d_cells, d_qbuf, 2 * cand_stride, d_sel, sel_stride, d_sel_cnt, nl);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[3], s));
-  // blurred levels
-  {
-    dim3 g((unsigned)btiles.size(), nframes);
-    hipLaunchKernelGGL(k_blur, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels,
-                       d_btiles, d_gk, d_blur, blur_bytes);
-  }
-  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
-  // orientation + descriptors
+  // orientation + blur at the pattern taps + descriptors
   {
     const int nslots = (int)slot_map.size();
     dim3 g((nslots + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_blur,
-                       blur_bytes, d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax,
-                       d_kps, d_desc, d_counts, out_cap);
+    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels,
+                       d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax, d_gk, d_kps, d_desc,
+                       d_counts, out_cap);
   }
-  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[5], s));
+  if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }

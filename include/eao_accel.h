@@ -85,9 +85,10 @@ int eao_orb_extract_batch_device(eao_orb* h, const uint8_t* d_frames, int nframe
                                  eao_keypoint* d_kps, uint8_t* d_desc, int32_t* d_counts, int cap,
                                  void* stream);
 /* per-stage timing of the batched path (HIP events on the launch stream):
-   enable once, then after a run eao_orb_stage_ms writes min(n, 5) values in
-   ms -- pyramid (7 resizes), FAST cells, quadtree distribution, level blur,
-   orient+describe -- and returns the number of stages (5). */
+   enable once, then after a run eao_orb_stage_ms writes min(n, 4) values in
+   ms -- pyramid (7 resizes), FAST cells, quadtree distribution, orient + blur +
+   describe (the level blur is fused into the descriptor kernel) -- and returns the
+   number of stages (4). */
 int eao_orb_set_timing(eao_orb* h, int on);
 int eao_orb_stage_ms(eao_orb* h, float* ms, int n);
 /* debug taps for parity tests (device work, host results) */

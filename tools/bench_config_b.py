@@ -61,8 +61,8 @@ def algorithmic_bytes(n_kps):
     """Per-frame algorithmic bytes of each stage (bench.py's accounting at 1080p)."""
     lv = [w * h for w, h in level_sizes()]
     l0, upper = lv[0], sum(lv[1:])
-    return {"pyramid": sum(lv[:-1]) + upper, "fast": l0 + upper, "blur": 2 * (l0 + upper),
-            "describe": 2 * (l0 + upper) + n_kps * 60, "extract": l0 + 2 * upper + n_kps * 60}
+    return {"pyramid": sum(lv[:-1]) + upper, "fast": l0 + upper,
+            "describe": l0 + upper + n_kps * 60, "extract": l0 + 2 * upper + n_kps * 60}
 
 
 def main():
@@ -174,7 +174,7 @@ def main():
 
     result = None
     if rank == 0:
-        names = ["pyramid", "fast", "distribute", "blur", "describe"]
+        names = ["pyramid", "fast", "distribute", "describe"]  # blur fused into k_describe
         stage = np.mean(np.stack(stages), 0)
         n_kps = float(d_cnt.float().mean().item())
         ab = algorithmic_bytes(n_kps)
@@ -182,7 +182,7 @@ def main():
         dom_bytes = ab.get(names[dom], ab["extract"])
         ach = dom_bytes * F / (stage[dom] * 1e-3) / 1e9
         ext_ms = float(stage.sum())
-        kern = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute", "blur": "k_blur",
+        kern = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
                 "describe": "k_describe"}
         result = {
             "metric": "frames/sec (ORB extract+match) on 1920x1080, 4000 features, 8 levels",

@@ -32,4 +32,4 @@ for it in range(12):
         st.append(orb.stage_ms())
 m = np.mean(np.stack(st), 0)
 print("frames %d %dx%d: " % (F, W, H) + " ".join("%s %.3f" % (k, v) for k, v in
-      zip(["pyramid", "fast", "distribute", "blur", "describe"], m)) + " | total %.3f ms" % m.sum(), flush=True)
+      zip(["pyramid", "fast", "distribute", "describe"], m)) + " | total %.3f ms" % m.sum(), flush=True)
