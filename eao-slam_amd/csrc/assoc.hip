@@ -53,71 +53,63 @@ __device__ __forceinline__ void cswap(float& a, float& b, bool up) {
 // registers (element r * 64 + lane in v[r]), partner i ^ J: lanes for J < 64 (DPP /
 // swizzle / permlane, xor_lane), registers for J = 64, 128. The pair (lo, hi) swaps
 // when (S[lo] > S[hi]) == ascending, ascending = ((i & K) == 0) with i the element's
-// index in the whole array (base + r * 64 + lane): block_sort3's exact network.
+// index in the whole array (base + r * 64 + lane): the exact bitonic network.
 template <int J>
-__device__ __forceinline__ void reg_step3(float (&v)[3][4], int base, int K) {
+__device__ __forceinline__ void reg_step(float (&v)[4], int base, int K) {
   const int lane = threadIdx.x & 63;
-  float o[3][4];  // the values before this step (in-lane partners read them)
+  float o[4];  // the values before this step (in-lane partners read them)
 #pragma unroll
-  for (int a = 0; a < 3; a++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) o[a][r] = v[a][r];
+  for (int r = 0; r < 4; r++) o[r] = v[r];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const int i = base + r * 64 + lane;
     const bool up = (i & K) == 0;
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      float pv;
-      bool lo;
-      if constexpr (J < 64) {
-        pv = __int_as_float(xor_lane<J>(__float_as_int(o[a][r])));
-        lo = (lane & J) == 0;
-      } else {
-        pv = o[a][r ^ (J / 64)];
-        lo = (r & (J / 64)) == 0;
-      }
-      const float x = lo ? o[a][r] : pv, y = lo ? pv : o[a][r];  // values at lo / hi
-      const bool sw = (x > y) == up;
-      v[a][r] = sw ? pv : o[a][r];
+    float pv;
+    bool lo;
+    if constexpr (J < 64) {
+      pv = __int_as_float(xor_lane<J>(__float_as_int(o[r])));
+      lo = (lane & J) == 0;
+    } else {
+      pv = o[r ^ (J / 64)];
+      lo = (r & (J / 64)) == 0;
     }
+    const float x = lo ? o[r] : pv, y = lo ? pv : o[r];  // values at lo / hi
+    const bool sw = (x > y) == up;
+    v[r] = sw ? pv : o[r];
   }
 }
 // j = jmax .. 1 of stage K on a register-held run
-__device__ __forceinline__ void reg_merge3(float (&v)[3][4], int base, int K, int jmax) {
-  if (jmax >= 128) reg_step3<128>(v, base, K);
-  if (jmax >= 64) reg_step3<64>(v, base, K);
-  if (jmax >= 32) reg_step3<32>(v, base, K);
-  if (jmax >= 16) reg_step3<16>(v, base, K);
-  if (jmax >= 8) reg_step3<8>(v, base, K);
-  if (jmax >= 4) reg_step3<4>(v, base, K);
-  if (jmax >= 2) reg_step3<2>(v, base, K);
-  reg_step3<1>(v, base, K);
+__device__ __forceinline__ void reg_merge(float (&v)[4], int base, int K, int jmax) {
+  if (jmax >= 128) reg_step<128>(v, base, K);
+  if (jmax >= 64) reg_step<64>(v, base, K);
+  if (jmax >= 32) reg_step<32>(v, base, K);
+  if (jmax >= 16) reg_step<16>(v, base, K);
+  if (jmax >= 8) reg_step<8>(v, base, K);
+  if (jmax >= 4) reg_step<4>(v, base, K);
+  if (jmax >= 2) reg_step<2>(v, base, K);
+  reg_step<1>(v, base, K);
 }
 
-// Ascending bitonic sort of three LDS arrays at once, P = 2^e >= 256 (INF padded),
-// 256 threads: every 256-element run is sorted by one wave in registers (stages
-// K <= 256, no barrier); for K >= 512 the strides >= 256 go through LDS (one barrier
-// each) and the strides < 256 run in registers again -- 4 + 2 e barriers instead of
-// e (e + 1) / 2.
+// Ascending bitonic sort of three LDS arrays, P = 2^e >= 256 (INF padded): every
+// (256-element run, array) is one wave's job, sorted in registers (stages K <= 256,
+// no barrier) -- three waves already for P = 256; for K >= 512 the strides >= 256 go
+// through LDS (one barrier each) and the strides < 256 run in registers again --
+// 4 + 2 e barriers instead of e (e + 1) / 2.
 __device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
-  float* S[3] = {S0, S1, S2};
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, nw = blockDim.x >> 6;
-  const int runs = P >> 8;
-  for (int q = w; q < runs; q += nw) {
-    const int base = q << 8;
-    float v[3][4];
+  const int jobs = 3 * (P >> 8);
+  for (int q = w; q < jobs; q += nw) {
+    float* A = q % 3 == 0 ? S0 : (q % 3 == 1 ? S1 : S2);
+    const int base = (q / 3) << 8;
+    float v[4];
 #pragma unroll
-    for (int a = 0; a < 3; a++)
+    for (int r = 0; r < 4; r++) v[r] = A[base + r * 64 + lane];
+    for (int K = 2; K <= 256; K <<= 1) reg_merge(v, base, K, K >> 1);
 #pragma unroll
-      for (int r = 0; r < 4; r++) v[a][r] = S[a][base + r * 64 + lane];
-    for (int K = 2; K <= 256; K <<= 1) reg_merge3(v, base, K, K >> 1);
-#pragma unroll
-    for (int a = 0; a < 3; a++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) S[a][base + r * 64 + lane] = v[a][r];
+    for (int r = 0; r < 4; r++) A[base + r * 64 + lane] = v[r];
   }
   __syncthreads();
+  float* S[3] = {S0, S1, S2};
   const int half = P >> 1, nt = blockDim.x;
   for (int K = 512; K <= P; K <<= 1) {
     for (int j = K >> 1; j >= 256; j >>= 1) {
@@ -148,40 +140,18 @@ __device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
       }
       __syncthreads();
     }
-    for (int q = w; q < runs; q += nw) {
-      const int base = q << 8;
-      float v[3][4];
+    for (int q = w; q < jobs; q += nw) {
+      float* A = q % 3 == 0 ? S0 : (q % 3 == 1 ? S1 : S2);
+      const int base = (q / 3) << 8;
+      float v[4];
 #pragma unroll
-      for (int a = 0; a < 3; a++)
+      for (int r = 0; r < 4; r++) v[r] = A[base + r * 64 + lane];
+      reg_merge(v, base, K, 128);
 #pragma unroll
-        for (int r = 0; r < 4; r++) v[a][r] = S[a][base + r * 64 + lane];
-      reg_merge3(v, base, K, 128);
-#pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) S[a][base + r * 64 + lane] = v[a][r];
+      for (int r = 0; r < 4; r++) A[base + r * 64 + lane] = v[r];
     }
     __syncthreads();
   }
-}
-
-// block-wide sums of K ints (result valid in every thread); red: >= K*16 ints
-template <int K>
-__device__ __forceinline__ void block_sum_n(int (&v)[K], int* red) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int k = 0; k < K; k++) v[k] = wave_sum(v[k]);
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < K; k++) red[k * 16 + w] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    int t = 0;
-    for (int i = 0; i < nw; i++) t += red[k * 16 + i];
-    v[k] = t;
-  }
-  __syncthreads();
 }
 
 // dynamic LDS: the 3 sorted axes, P floats each. NPT = 1024 threads: the pair's
@@ -218,17 +188,61 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   const float th = OS ? oth[p] : 0.f;
   auto kept = [&](int i) { return !OS || !(OS[i] > (double)th); };
   NP_STAMP(0);
-  int cnt3[3] = {0, 0, 0};
-  for (int i = t; i < mt; i += NPT) cnt3[0] += FV[i] ? 1 : 0;
-  for (int i = t; i < ntot; i += NPT)
-    if (kept(i)) {
-      cnt3[1] += OV[i] ? 1 : 0;
-      cnt3[2] += 1;
+  const int lane = t & 63;
+  // this thread's frame point, prefetched (the usual m <= NPT case); its latency
+  // overlaps the object pass below
+  float f0[3] = {0.f, 0.f, 0.f};
+  bool fv0 = false;
+  if (t < mt) {
+    fv0 = FV[t] != 0;
+    f0[0] = F[3 * t];
+    f0[1] = F[3 * t + 1];
+    f0[2] = F[3 * t + 2];
+  }
+  if (t < 9) red[t] = 0;
+  if (t < 4) wpos[t] = 0;
+  __syncthreads();
+  float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
+  // one pass over the object: the valid kept points compacted into the sort arrays
+  // (order irrelevant: sorted next; a wave places its lanes by ballot rank after one
+  // LDS atomic for its base) and the counts m, nvalid, nt
+  int mc = fv0 ? 1 : 0, ntk = 0;
+  for (int i = t + NPT; i < mt; i += NPT) mc += FV[i] ? 1 : 0;
+  for (int i0 = 0; i0 < ntot; i0 += NPT) {
+    const int i = i0 + t;
+    const bool in = i < ntot;
+    float x = 0.f, y = 0.f, z = 0.f;
+    bool kp = false, keep = false;
+    if (in) {
+      x = O[3 * i];
+      y = O[3 * i + 1];
+      z = O[3 * i + 2];
+      kp = kept(i);
+      keep = kp && OV[i];
     }
-  if (t == 0) wpos[0] = 0;
-  block_sum_n<3>(cnt3, red);
+    ntk += kp ? 1 : 0;
+    const uint64_t mk = ballot(keep);
+    int base = 0;
+    if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+    base = __shfl(base, 0, 64);
+    if (keep) {
+      const int d = base + popc64(mk & lanes_below());
+      if (d < Pmax) {
+        S[0][d] = x;
+        S[1][d] = y;
+        S[2][d] = z;
+      }
+    }
+  }
+  mc = wave_sum(mc);
+  ntk = wave_sum(ntk);
+  if (lane == 0) {
+    if (mc) atomicAdd(&wpos[1], mc);
+    if (ntk) atomicAdd(&wpos[2], ntk);
+  }
+  __syncthreads();
   NP_STAMP(1);
-  const int m = cnt3[0], nvalid = cnt3[1], nt = cnt3[2];
+  const int m = wpos[1], nvalid = wpos[0], nt = wpos[2];
   eao_np_stats r;
   r.m = m;
   r.n = nvalid;
@@ -243,27 +257,9 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
     }
     return;
   }
-  float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
-  // compact the valid object points (order irrelevant: sorted next): a wave places
-  // its kept lanes by ballot rank after one LDS atomic for its base
-  const int lane = t & 63;
-  for (int i0 = 0; i0 < ntot; i0 += NPT) {
-    const int i = i0 + t;
-    const bool keep = i < ntot && OV[i] && kept(i);
-    const uint64_t mk = ballot(keep);
-    int base = 0;
-    if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
-    base = __shfl(base, 0, 64);
-    if (keep) {
-      const int d = base + popc64(mk & lanes_below());
-      S[0][d] = O[3 * i];
-      S[1][d] = O[3 * i + 1];
-      S[2][d] = O[3 * i + 2];
-    }
-  }
   for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
   __syncthreads();
   NP_STAMP(2);
@@ -272,38 +268,51 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   // rank counts against x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-830)
   int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = t; i < mt; i += NPT) {
-    if (!FV[i]) continue;
-    // the six binary searches (lower / upper bound per axis) advance together, so
-    // their LDS reads overlap instead of forming one 6 log n chain
-    const float x[3] = {F[3 * i], F[3 * i + 1], F[3 * i + 2]};
-    int lo[3] = {0, 0, 0}, lb[3] = {nsamp, nsamp, nsamp}, hi[3] = {0, 0, 0}, hb[3] = {nsamp, nsamp, nsamp};
-    for (bool more = true; more;) {
-      more = false;
+    float x[3];
+    if (i == t) {
+      if (!fv0) continue;
+      x[0] = f0[0];
+      x[1] = f0[1];
+      x[2] = f0[2];
+    } else {
+      if (!FV[i]) continue;
+      x[0] = F[3 * i];
+      x[1] = F[3 * i + 1];
+      x[2] = F[3 * i + 2];
+    }
+    // the six bound searches (lower / upper per axis over A[k] = S[a][k * step], k <
+    // nsamp) run branch-free for the same ceil(log2 nsamp) rounds in every lane, so each
+    // round's six LDS reads issue together
+    int bl[3] = {0, 0, 0}, bu[3] = {0, 0, 0};
+    for (int n = nsamp; n > 1;) {
+      const int half = n >> 1;
 #pragma unroll
       for (int a = 0; a < 3; a++) {
-        if (lo[a] < lb[a]) {
-          const int mid = (lo[a] + lb[a]) >> 1;
-          if (S[a][mid * step] < x[a]) lo[a] = mid + 1;
-          else lb[a] = mid;
-          more |= lo[a] < lb[a];
-        }
-        if (hi[a] < hb[a]) {
-          const int mid = (hi[a] + hb[a]) >> 1;
-          if (S[a][mid * step] <= x[a]) hi[a] = mid + 1;
-          else hb[a] = mid;
-          more |= hi[a] < hb[a];
-        }
+        const float vl = S[a][(bl[a] + half) * step], vu = S[a][(bu[a] + half) * step];
+        bl[a] = vl < x[a] ? bl[a] + half : bl[a];
+        bu[a] = vu <= x[a] ? bu[a] + half : bu[a];
       }
+      n -= half;
     }
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-      c9[3 * a] += lo[a];
-      c9[3 * a + 2] += hi[a] - lo[a];
-      c9[3 * a + 1] += nsamp - hi[a];
+      const int lo = bl[a] + (S[a][bl[a] * step] < x[a] ? 1 : 0);   // #samples < x
+      const int hi = bu[a] + (S[a][bu[a] * step] <= x[a] ? 1 : 0);  // #samples <= x
+      c9[3 * a] += lo;
+      c9[3 * a + 2] += hi - lo;
+      c9[3 * a + 1] += nsamp - hi;
     }
   }
   NP_STAMP(4);
-  block_sum_n<9>(c9, red);
+  // block sums: wave sums, then one LDS atomic per wave and counter
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    c9[k] = wave_sum(c9[k]);
+    if (lane == 0 && c9[k]) atomicAdd(&red[k], c9[k]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 9; k++) c9[k] = red[k];
   NP_STAMP(5);
   for (int a = 0; a < 3; a++) {
     r.cnt_gt[a] = (float)c9[3 * a];
@@ -494,7 +503,6 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   uint2* nodes = (uint2*)(smem + L.nodes);
   uint16_t* right = (uint16_t*)(smem + L.right);
   uint8_t* ndep = (uint8_t*)(smem + L.ndep);  // node depth, preorder (right links derive from it)
-  __shared__ int s_nn;
   __shared__ int s_nodes_bad;
 
   const int tr = blockIdx.x, c = blockIdx.y;
@@ -625,13 +633,17 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     const int* K0 = (const int*)B0;
     const int maxDepth = (int)ceil(log2((double)psi));
     int sf = 0, sl = psi - 1, sd = 0;  // lane 0 = root
+    int spar = -1;                     // parent id of a pending right child, else -1
     int sp = 1, nn = 0, bad = 0;
     while (sp > 0 && !bad) {
       sp--;
       const int first = __builtin_amdgcn_readlane(sf, sp);
       const int last = __builtin_amdgcn_readlane(sl, sp);
       const int depth = __builtin_amdgcn_readlane(sd, sp);
+      const int par = __builtin_amdgcn_readlane(spar, sp);
       const int me = nn++;
+      // right links for the score walk, written as each right child gets its id
+      if (par >= 0 && lane == 0) right[par] = (uint16_t)me;
       const int cnt = last - first + 1;
       if (lane == 0) ndep[me] = (uint8_t)depth;
       if (cnt < 2 || depth >= maxDepth) {
@@ -645,7 +657,14 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const int kx = has ? src[first + lane] : INT_MAX;
         const int ky = has ? src[psi + first + lane] : INT_MAX;
         const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
-        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, ndep);
+        IFP_T(rs0);
+        const int nn0 = nn;
+        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, ndep, right);
+        IFP_T(rs1);
+        IFP_ACC(21, rs0, rs1);
+        IFP_ACC(22, 0ull, 1ull);
+        IFP_ACC(23, 0ull, (unsigned long long)(nn - nn0));
+        (void)nn0;
         continue;
       }
       if (cnt <= 64) {
@@ -657,7 +676,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const int z = has ? src[2 * psi + first + lane] : 0;
         uint64_t mask = ballot(has);
         int d = depth, node = me, ssp = 0;
-        int slo = 0, shi = 0, sdd = 0;
+        int slo = 0, shi = 0, sdd = 0, spp = 0;
         while (true) {
           IFP_T(t0);
           IFP_ACC(20, 0ull, 1ull);
@@ -695,6 +714,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
                   slo = (int)(uint32_t)rmk;
                   shi = (int)(uint32_t)(rmk >> 32);
                   sdd = d + 1;
+                  spp = node;
                 }
                 ssp++;
                 mask = lm;  // left child next (node + 1)
@@ -717,6 +737,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
           mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(slo, ssp) |
                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(shi, ssp) << 32);
           d = __builtin_amdgcn_readlane(sdd, ssp);
+          if (lane == 0) right[__builtin_amdgcn_readlane(spp, ssp)] = (uint16_t)nn;
           node = nn++;
           IFP_T(t7);
           IFP_ACC(17, t6, t7);
@@ -775,11 +796,13 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         sf = middle;
         sl = last;
         sd = depth + 1;
+        spar = me;
       }
       if (lane == sp + 1) {
         sf = first;
         sl = middle - 1;
         sd = depth + 1;
+        spar = -1;
       }
       sp += 2;
       IFP_T(bb1);
@@ -788,23 +811,10 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     }
     if (lane == 0) {
       s_nodes_bad = bad;
-      s_nn = nn;
     }
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
   }
   __syncthreads();
-  // ---- right links from the preorder depths: q is a right child iff the
-  // node before it is at least as deep; its parent is the last node before q
-  // one level up (everything in between is the left sibling's subtree)
-  if (!s_nodes_bad)
-    for (int q = 1 + tid; q < s_nn; q += nb) {
-      const int dq = ndep[q];
-      if (ndep[q - 1] >= dq) {
-        int p = q - 2;
-        while (ndep[p] != dq - 1) p--;
-        right[p] = (uint16_t)q;
-      }
-    }
   }  // valid
   __syncthreads();
   if_stamp(6);

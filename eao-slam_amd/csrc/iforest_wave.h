@@ -202,7 +202,7 @@ namespace eao {
 // the caller has allocated `me` (nn == me + 1) and checked 2 <= cnt,
 // depth < maxDepth. Returns 1 when Node::Build fails (empty right range).
 __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, int cnt, int depth, int maxDepth,
-                                            int me, int& nn, uint2* nodes, uint8_t* ndep) {
+                                            int me, int& nn, uint2* nodes, uint8_t* ndep, uint16_t* right) {
   const int lane = lane_id();
   auto sk64 = [&](int k) { return ((uint64_t)((uint32_t)k ^ 0x80000000u) << 32) | (uint32_t)lane; };
   uint64_t vx = sk64(lane < cnt ? kx : INT_MAX), vy = sk64(lane < cnt ? ky : INT_MAX),
@@ -237,7 +237,11 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
   };
   // pending right children, entry e in lane e: rank sets (6 words), depth |
   // leaf flag (bit 8; then q0 holds the count and no sets are stored)
-  int q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0;
+  int q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0, q7 = 0;  // q7: the parent
+  // right links (the score walk's `right`), written as each right child gets its id
+  auto link = [&](int parent, int child) {
+    if (lane == 0) right[parent] = (uint16_t)child;
+  };
   while (true) {
     // the current node (mX/mY/mZ, count cn, depth d, id node) is not a leaf
     // by count or depth
@@ -274,14 +278,17 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
             mY &= ~ly;
             mZ &= ~lz;
             cn = cr;
+            link(node, nn);
             node = nn++;
             continue;
           }
+          link(node, nn);
           record(nn++, (uint32_t)cr << 2, 0u, d);
         } else {
           if (rleaf) {
             writelane(q0, cr, ssp);
             writelane(q6, d | 256, ssp);
+            writelane(q7, node, ssp);
           } else {
             const uint64_t ux = mX & ~lx, uy = mY & ~ly, uz = mZ & ~lz;
             writelane(q0, (int)(uint32_t)ux, ssp);
@@ -291,6 +298,7 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
             writelane(q4, (int)(uint32_t)uz, ssp);
             writelane(q5, (int)(uint32_t)(uz >> 32), ssp);
             writelane(q6, d, ssp);
+            writelane(q7, node, ssp);
           }
           ssp++;
           mX = lx;  // the left child is next
@@ -308,6 +316,7 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
     while (ssp > 0) {
       ssp--;
       const int e = __builtin_amdgcn_readlane(q6, ssp);
+      link(__builtin_amdgcn_readlane(q7, ssp), nn);
       node = nn++;
       d = e & 255;
       if (e & 256) {

@@ -3,6 +3,8 @@
 // oracle so the decision logic can be debugged without a device. Test
 // infrastructure only -- never part of the product.
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include "../../eao-slam_amd/csrc/assoc.h"
 #include "../../eao-slam_amd/csrc/shard.h"
 #include "../../oracle/oracle.h"
@@ -22,7 +24,9 @@ CamDev make_cam(const eao_camera& c) {
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
                           eao_np_stats* out, hipStream_t, int, const double* const* os_ptr, const float* oth) {
+  static FILE* dump = std::getenv("EAO_HARNESS_DUMP") ? std::fopen(std::getenv("EAO_HARNESS_DUMP"), "w") : nullptr;
   for (int p = 0; p < npairs; p++) {
+    if (dump) std::fprintf(dump, "np %d %d %d\n", npairs, flen[p], olen[p]);
     std::vector<float> pts;
     std::vector<uint8_t> val;
     const double* os = os_ptr ? os_ptr[p] : nullptr;
@@ -41,7 +45,9 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
                                uint32_t seed, const uint32_t* sample, double* scores, hipStream_t, int, int,
                                int, double*, double* scores2) {
+  static FILE* dump = std::getenv("EAO_HARNESS_DUMP") ? std::fopen((std::string(std::getenv("EAO_HARNESS_DUMP")) + ".if").c_str(), "w") : nullptr;
   for (int c = 0; c < nclouds; c++) {
+    if (dump) std::fprintf(dump, "if %d %d\n", nclouds, len[c]);
     if (orc_iforest_scores(pts + 3 * off[c], len[c], trees, seed, sample[c], scores + off[c]))
       for (int i = 0; i < len[c]; i++) scores[off[c] + i] = NAN;  // Build() failed: nothing erased
     if (scores2)
