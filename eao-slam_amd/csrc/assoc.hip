@@ -683,7 +683,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
           const int cn = popc64(mask);
           bool leaf = cn < 2 || d >= maxDepth;
           if (!leaf) {
-            const uint32_t dim = g.lemire(3);
+            const uint32_t dim = g.dim3();
             IFP_T(t1);
             IFP_ACC(12, t0, t1);
             const bool in = (mask >> lane) & 1ull;
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       }
       int* dst = (depth & 1) ? (int*)B0 : (int*)B1;
       IFP_T(bb0);
-      const uint32_t dim = g.lemire(3);
+      const uint32_t dim = g.dim3();
       int mn = INT_MAX, mx = INT_MIN;
       for (int i = first + lane; i <= last; i += 64) {
         const int v = src[dim * psi + i];

@@ -19,7 +19,9 @@ struct WaveRng {
   uint32_t* mt;  // LDS [624]
   int idx;       // next untempered state word (uniform)
   uint32_t buf;  // lane j: draw number (base + j) of the current chunk
-  int bp, blen;  // uniform read position / valid length of buf
+  uint32_t bufd;  // the same draw as uniform_int<uint32>(0, 2) (Lemire), 3 = rejected
+  float buff;     // the same draw as generate_canonical<float, 24>
+  int bp, blen;   // uniform read position / valid length of buf
 
   __device__ void seed(uint32_t s) {
     if (lane_id() == 0) {
@@ -67,6 +69,11 @@ struct WaveRng {
     y ^= (y << 15) & 0xefc60000u;
     y ^= (y >> 18);
     buf = y;
+    // both interpretations of every draw, precomputed off the build's critical chain:
+    // Lemire over range 3 rejects low = y * 3 < 1, i.e. y == 0
+    bufd = y == 0u ? 3u : __umulhi(y, 3u);
+    float r = fmul((float)y, 0x1p-32f);               // == y / 2^32 exactly (power-of-two scale)
+    buff = r >= 1.0f ? __uint_as_float(0x3f7fffffu) : r;  // nextafter(1, 0)
     idx += blen;
     bp = 0;
   }
@@ -87,10 +94,19 @@ struct WaveRng {
     }
     return (uint32_t)(product >> 32);
   }
+  // uniform_int_distribution<uint32_t>(0, 2): lemire(3) from the precomputed lane values
+  __device__ uint32_t dim3() {
+    uint32_t d;
+    do {
+      if (bp >= blen) refill();
+      d = (uint32_t)__builtin_amdgcn_readlane((int)bufd, bp++);
+    } while (d == 3u);
+    return d;
+  }
   // uniform_real_distribution<float>(a, b): generate_canonical<float, 24>
   __device__ float uniform_real(float a, float b) {
-    float ret = fmul((float)next(), 0x1p-32f);  // == x / 2^32 exactly (power-of-two scale)
-    if (ret >= 1.0f) ret = __uint_as_float(0x3f7fffffu);  // nextafter(1, 0)
+    if (bp >= blen) refill();
+    const float ret = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(buff), bp++));
     return fadd(fmul(ret, fsub(b, a)), a);
   }
 };
@@ -217,9 +233,10 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
   const int rz = __builtin_amdgcn_ds_permute(pz << 2, lane);
   // sorted values as floats (-0 folded): min / max / split compare in float
   const float fx = kfloat(sx), fy = kfloat(sy), fz = kfloat(sz);
-  const uint64_t bx = 1ull << px, by = 1ull << py, bz = 1ull << pz;  // item bit of rank r
-  const uint64_t all = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
-  uint64_t mX = all, mY = all, mZ = all;  // valid items hold ranks [0, cnt)
+  // a node is its set of items (bit l = item l); per node only the drawn dimension's
+  // rank set is formed (one ballot through the item permutation) and the left
+  // child's items come back through the inverse one
+  uint64_t S = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
   int d = depth, node = me, cn = cnt, ssp = 0, bad = 0;
   // node records buffered in lanes (lane j = node rb + j): x | depth << 24, split
   int rbx = 0, rby = 0, rb = me;
@@ -235,22 +252,21 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
     writelane(rby, (int)y, id - rb);
     if (id - rb == 63) flush(64);
   };
-  // pending right children, entry e in lane e: rank sets (6 words), depth |
-  // leaf flag (bit 8; then q0 holds the count and no sets are stored)
-  int q0 = 0, q1 = 0, q2 = 0, q3 = 0, q4 = 0, q5 = 0, q6 = 0, q7 = 0;  // q7: the parent
   // right links (the score walk's `right`), written as each right child gets its id
   auto link = [&](int parent, int child) {
     if (lane == 0) right[parent] = (uint16_t)child;
   };
+  // pending right children, entry e in lane e: item set (q0, q1), depth | leaf flag
+  // (bit 8; then q0 holds the count), parent id
+  int q0 = 0, q1 = 0, q2 = 0, q3 = 0;
   while (true) {
-    // the current node (mX/mY/mZ, count cn, depth d, id node) is not a leaf
-    // by count or depth
-    uint32_t x = g.next();
-    while (x * 3u == 0u) x = g.next();  // Lemire rejection for range 3: low < 1
-    const uint32_t dim = __umulhi(x, 3u);
-    const uint64_t md = dim == 0 ? mX : (dim == 1 ? mY : mZ);
+    // the current node (items S, count cn, depth d, id node) is not a leaf by count
+    // or depth
+    const uint32_t dim = g.dim3();
+    const int pk = dim == 0 ? px : (dim == 1 ? py : pz);  // item at rank (lane)
+    const int rk = dim == 0 ? rx : (dim == 1 ? ry : rz);  // rank of item (lane)
     const float fk = dim == 0 ? fx : (dim == 1 ? fy : fz);
-    const int rk = dim == 0 ? rx : (dim == 1 ? ry : rz);
+    const uint64_t md = ballot((S >> pk) & 1ull);  // the node's ranks in this dimension
     const int lo = __builtin_ctzll(md), hi = 63 - __builtin_clzll(md);
     const float mn = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fk), lo));
     const float mx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fk), hi));
@@ -261,22 +277,19 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
       leaf = lm == 0;
       if (!leaf) {
         record(node, dim + 1u, __float_as_uint(split), d);
-        const uint64_t rm = md & ~lm;
-        if (rm == 0) {  // empty right range: Node::Build fails
+        const uint64_t L = ballot((lm >> rk) & 1ull);  // the left items
+        const uint64_t R = S & ~L;
+        if (R == 0) {  // empty right range: Node::Build fails
           bad = 1;
           break;
         }
-        const uint64_t il = ballot((lm >> rk) & 1ull);  // the left items
-        const uint64_t lx = ballot((il & bx) != 0), ly = ballot((il & by) != 0), lz = ballot((il & bz) != 0);
-        const int cl = __builtin_popcountll(lm), cr = cn - cl;
+        const int cl = __builtin_popcountll(L), cr = cn - cl;
         d++;
         const bool lleaf = cl < 2 || d >= maxDepth, rleaf = cr < 2 || d >= maxDepth;
         if (lleaf) {
           record(nn++, (uint32_t)cl << 2, 0u, d);
           if (!rleaf) {  // the right child is next
-            mX &= ~lx;
-            mY &= ~ly;
-            mZ &= ~lz;
+            S = R;
             cn = cr;
             link(node, nn);
             node = nn++;
@@ -287,23 +300,15 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
         } else {
           if (rleaf) {
             writelane(q0, cr, ssp);
-            writelane(q6, d | 256, ssp);
-            writelane(q7, node, ssp);
+            writelane(q2, d | 256, ssp);
           } else {
-            const uint64_t ux = mX & ~lx, uy = mY & ~ly, uz = mZ & ~lz;
-            writelane(q0, (int)(uint32_t)ux, ssp);
-            writelane(q1, (int)(uint32_t)(ux >> 32), ssp);
-            writelane(q2, (int)(uint32_t)uy, ssp);
-            writelane(q3, (int)(uint32_t)(uy >> 32), ssp);
-            writelane(q4, (int)(uint32_t)uz, ssp);
-            writelane(q5, (int)(uint32_t)(uz >> 32), ssp);
-            writelane(q6, d, ssp);
-            writelane(q7, node, ssp);
+            writelane(q0, (int)(uint32_t)R, ssp);
+            writelane(q1, (int)(uint32_t)(R >> 32), ssp);
+            writelane(q2, d, ssp);
           }
+          writelane(q3, node, ssp);
           ssp++;
-          mX = lx;  // the left child is next
-          mY = ly;
-          mZ = lz;
+          S = L;  // the left child is next
           cn = cl;
           node = nn++;
           continue;
@@ -315,21 +320,17 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
     bool found = false;
     while (ssp > 0) {
       ssp--;
-      const int e = __builtin_amdgcn_readlane(q6, ssp);
-      link(__builtin_amdgcn_readlane(q7, ssp), nn);
+      const int e = __builtin_amdgcn_readlane(q2, ssp);
+      link(__builtin_amdgcn_readlane(q3, ssp), nn);
       node = nn++;
       d = e & 255;
       if (e & 256) {
         record(node, (uint32_t)__builtin_amdgcn_readlane(q0, ssp) << 2, 0u, d);
         continue;
       }
-      mX = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q0, ssp) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q1, ssp) << 32);
-      mY = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q2, ssp) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q3, ssp) << 32);
-      mZ = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q4, ssp) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q5, ssp) << 32);
-      cn = __builtin_popcountll(mX);
+      S = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q0, ssp) |
+          ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q1, ssp) << 32);
+      cn = __builtin_popcountll(S);
       found = true;
       break;
     }
