@@ -119,6 +119,24 @@ KERNELS = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_d
            "describe": "k_describe"}
 
 
+PEAK_VALU_LANE_OPS = 78.6e12  # 256 CUs x 4 SIMD-32 x 2.4 GHz x 32 lanes (MI355X_MICROARCH.md)
+
+
+def pmc_valu(kernel, frames):
+    """VALU lane-ops per launch of `kernel` from the committed SQ counter pass
+    (profiles/r02_pmc_sq.txt: SQ_INSTS_VALU wave instructions x 64 lanes) over the same
+    405-frame launch -- a profiled figure of the same launch shape, not a measurement of
+    this run; None for another shape or when the summary is absent."""
+    p = os.path.join(ROOT, "profiles", "r02_pmc_sq.txt")
+    if frames != 405 or not os.path.exists(p):
+        return None
+    for l in open(p):
+        f = l.split()
+        if f[:2] == ["eao::" + kernel.split()[0], "SQ_INSTS_VALU"]:
+            return float(f[-1]) * 64
+    return None
+
+
 def pingpong(n, m):
     """Frame index of step t when m rendered frames are cycled forth and back."""
     p = np.arange(n) % (2 * m - 2) if m > 1 else np.zeros(n, np.int64)
@@ -376,6 +394,7 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": dom_bytes * F, "avg_launch_ms": float(stage[dom])},
             "stages_ms_per_step": {n: float(v) for n, v in zip(STAGES, stage)},
+            "roofline_valu": valu_roof(KERNELS[dom_name], F, float(stage[dom])),
             "extract_ms_per_step": ext_ms,
             "extract_fps": F / (ext_ms * 1e-3),
             "extract_gbs": ab["extract"] * F / (ext_ms * 1e-3) / 1e9,
@@ -406,6 +425,18 @@ def main():
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
     return 0
+
+
+def valu_roof(kernel, frames, ms):
+    """The dominant extraction kernel against the VALU issue roofline: lane-ops per launch
+    (committed SQ_INSTS_VALU pass, profiles/r02_pmc_sq.txt) over this run's launch time."""
+    ops = pmc_valu(kernel, frames)
+    if ops is None:
+        return None
+    ach = ops / (ms * 1e-3)
+    return {"bound": "valu", "kernel": kernel, "achieved": ach / 1e12, "peak": PEAK_VALU_LANE_OPS / 1e12,
+            "unit": "T lane-ops/s", "frac": ach / PEAK_VALU_LANE_OPS, "lane_ops_per_launch": ops,
+            "source": "rocprofv3 --pmc SQ_INSTS_VALU x 64 (profiles/r02_pmc_sq.txt), same 405-frame launch"}
 
 
 def search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc, d_cnt,

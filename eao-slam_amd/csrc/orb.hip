@@ -779,14 +779,19 @@ __global__ __launch_bounds__(256) void k_describe(
     const uint32_t* __restrict__ sel, long long sel_stride, const int* __restrict__ sel_cnt,
     const int2* __restrict__ slot_map, int nslots, int nlevels, const int* __restrict__ umax,
     const int* __restrict__ gk, eao_keypoint_dev* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
-    int* __restrict__ out_cnt, int cap) {
+    int* __restrict__ out_cnt, int cap, int gx) {
   __shared__ uint32_t raw[4][PW][PD];
   __shared__ uint16_t hs[4][PW][HC];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int slot = blockIdx.x * 4 + w;
-  const int f = blockIdx.y;
+  // XCD-aware order (bijective swizzle): blocks b and b + 8 share an XCD, so each group
+  // of blocks takes a contiguous run of (frame, slot group) ids -- a frame's keypoints
+  // then read its level planes through one L2 instead of all eight
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+  const int f = wg / gx, sg = wg - f * gx;
+  const int slot = sg * 4 + w;
   const int* cnts = sel_cnt + f * nlevels;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (sg == 0 && threadIdx.x == 0) {
     int tot = 0;
     for (int i = 0; i < nlevels; i++) tot += max(cnts[i], 0);
     out_cnt[f] = tot;
@@ -1252,10 +1257,10 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   // orientation + blur at the pattern taps + descriptors
   {
     const int nslots = (int)slot_map.size();
-    dim3 g((nslots + 3) / 4, nframes);
-    hipLaunchKernelGGL(k_describe, g, dim3(256), 0, s, d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels,
-                       d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax, d_gk, d_kps, d_desc,
-                       d_counts, out_cap);
+    const int gx = (nslots + 3) / 4;
+    hipLaunchKernelGGL(k_describe, dim3(gx * nframes), dim3(256), 0, s, d_frames, pitch, fstride, d_pyr,
+                       pyr_bytes, d_levels, d_sel, sel_stride, d_sel_cnt, d_slot_map, nslots, nl, d_umax, d_gk,
+                       d_kps, d_desc, d_counts, out_cap, gx);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[4], s));
   EAO_HIP_CHECK(hipGetLastError());
