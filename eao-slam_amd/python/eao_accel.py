@@ -293,6 +293,45 @@ class Matcher:
             v(stream) if stream else None), "eao_match_init_batch_device")
 
 
+class Lines:
+    """Per-frame line detection (line_lbd_detect::detect_raw_lines + filter_lines,
+    reference src/Frame.cc:324-328) on the GPU."""
+
+    def __init__(self, w=640, h=480, max_batch=1, device=0):
+        self.h = ctypes.c_void_p()
+        self.w, self.hh = w, h
+        check(lib().eao_lines_create(device, w, h, max_batch, ctypes.byref(self.h)), "eao_lines_create")
+
+    def close(self):
+        if self.h:
+            lib().eao_lines_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def detect(self, gray, min_length=50.0, cap=4096):
+        """[n][6] float32: (startX, startY, endX, endY, angle, lineLength)."""
+        g8 = np.ascontiguousarray(gray, np.uint8)
+        out = np.zeros((cap, 6), np.float32)
+        n = ctypes.c_int()
+        check(lib().eao_lines_detect(self.h, P(g8), g8.shape[1], ctypes.c_float(min_length), P(out), cap,
+                                     ctypes.byref(n)), "eao_lines_detect")
+        return out[:n.value].copy()
+
+    def debug_maps(self):
+        blur = np.zeros((self.hh, self.w), np.uint8)
+        dx, dy = np.zeros((self.hh, self.w), np.int16), np.zeros((self.hh, self.w), np.int16)
+        code = np.zeros((self.hh, self.w), np.uint16)
+        check(lib().eao_lines_debug_maps(self.h, P(blur), P(dx), P(dy), P(code)), "eao_lines_debug_maps")
+        return blur, dx, dy, code
+
+    def detect_batch_device(self, gray_ptr, nframes, pitch, min_length, lines_ptr, counts_ptr, cap, stream=None):
+        v = ctypes.c_void_p
+        check(lib().eao_lines_detect_batch_device(self.h, v(gray_ptr), nframes, pitch, ctypes.c_float(min_length),
+                                                  v(lines_ptr), v(counts_ptr), cap, v(stream) if stream else None),
+              "eao_lines_detect_batch_device")
+
+
 class Assoc:
     """Object_2D / Object_Map math replacement (reference src/Object.cc, isolation_forest.h)."""
 

@@ -216,6 +216,29 @@ int eao_match_init_batch_device(eao_matcher* m, const eao_camera* cam, int nsear
                                 float* d_prev_matched_xy, int window, int32_t* d_matches12, int32_t* d_nmatches,
                                 void* stream);
 
+/* --- per-frame line detection: replaces line_lbd_detect::detect_raw_lines +
+   filter_lines (src/Frame.cc:324-328; src/line_detect/line_lbd_allclass.cpp:137-214)
+   with the tracker's single octave (Tracking.cc:161-163): GaussianBlur(5x5, sigma 1),
+   EDLineDetector::EDline (src/line_detect/libs/binary_descriptor.cpp:1583-2906) and the
+   keyline endpoint ordering of OctaveKeyLines (:866-887, 1073-1141). A line is
+   (startX, startY, endX, endY, angle, lineLength) -- keylines_to_mat's four columns
+   plus KeyLine::angle / lineLength -- kept when lineLength > min_length (50 in the
+   reference). --------------------------------------------------------------------- */
+typedef struct eao_lines eao_lines;
+int eao_lines_create(int device, int width, int height, int max_batch, eao_lines** out);
+int eao_lines_destroy(eao_lines* l);
+/* batched, HBM-resident: gray frames [n][height][pitch] u8; d_lines [n][cap][6] f32,
+   d_counts[n] (the frame's line count, > cap when truncated; -1 when the reference's
+   EdgeDrawing would fail: more anchors / edge pixels / edges than its arrays hold) */
+int eao_lines_detect_batch_device(eao_lines* l, const uint8_t* d_gray, int nframes, int pitch, float min_length,
+                                  float* d_lines, int32_t* d_counts, int cap, void* stream);
+/* one host frame; returns EAO_E_CAPACITY when more than cap lines (n_out holds the count) */
+int eao_lines_detect(eao_lines* l, const uint8_t* gray, int pitch, float min_length, float* lines, int cap,
+                     int* n_out);
+/* maps of the last eao_lines_detect: blur u8, Sobel dx / dy i16, code u16 = thresholded
+   (|dx| + |dy|) / 4 | 0x8000 when |dx| < |dy| (Horizontal); NULL skips an output */
+int eao_lines_debug_maps(eao_lines* l, uint8_t* blur, int16_t* dx, int16_t* dy, uint16_t* code);
+
 /* --- EAO association: replaces Object_2D / Object_Map math (src/Object.cc) -- */
 typedef struct {
   int32_t verdict; /* 0: m<20, 1: pass, 2: fail -- NoParaDataAssociation return */

@@ -169,6 +169,15 @@ int orc_replay_object(orc_replay* r, int i, int32_t* ints /*8*/, float* floats /
 int orc_replay_lines(orc_replay* r, int n_frames, const int32_t* n_lines, const float* lines);
 int orc_replay_object_points(orc_replay* r, int i, int32_t* ids, int cap);
 
+/* per-frame line detection (lines_ref.cpp): GaussianBlur 5x5 sigma 1 + EDLine maps,
+   edge chains, and detect_raw_lines + filter_lines output (startX, startY, endX, endY,
+   angle, lineLength) per kept line */
+int orc_line_maps(const uint8_t* gray, int w, int h, uint8_t* blur, int16_t* dx, int16_t* dy, int16_t* g,
+                  uint8_t* dir);
+int orc_edge_chains(const uint8_t* gray, int w, int h, uint32_t* xy, int cap_px, uint32_t* sid, int cap_edges,
+                    int* n_px, int* n_edges);
+int orc_edlines(const uint8_t* gray, int w, int h, float min_length, float* out, int cap, int* n_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -318,3 +318,38 @@ class Replay:
             k = lib().orc_replay_object_points(ctypes.c_void_p(self.h), i, P(ids), len(ids))
             pts.append(ids[:k].copy())
         return ints, fl, pts
+
+
+# ---- per-frame line detection (lines_ref.cpp)
+def line_maps(gray):
+    """(blur u8, dx i16, dy i16, g i16, dir u8) of EDLine on GaussianBlur(5x5, 1)."""
+    g8 = np.ascontiguousarray(gray, np.uint8)
+    h, w = g8.shape
+    blur = np.zeros((h, w), np.uint8)
+    dx, dy, gg = (np.zeros((h, w), np.int16) for _ in range(3))
+    dr = np.zeros((h, w), np.uint8)
+    lib().orc_line_maps(P(g8), w, h, P(blur), P(dx), P(dy), P(gg), P(dr))
+    return blur, dx, dy, gg, dr
+
+
+def edge_chains(gray, cap_px=1 << 18, cap_edges=1 << 14):
+    """EdgeDrawing chains: (xy [n_px][2] u32, sid [n_edges + 1] u32)."""
+    g8 = np.ascontiguousarray(gray, np.uint8)
+    h, w = g8.shape
+    xy = np.zeros((cap_px, 2), np.uint32)
+    sid = np.zeros(cap_edges + 1, np.uint32)
+    npx, ne = ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_edge_chains(P(g8), w, h, P(xy), cap_px, P(sid), cap_edges, ctypes.byref(npx), ctypes.byref(ne))
+    assert rc == 0 and npx.value <= cap_px and ne.value <= cap_edges
+    return xy[:npx.value].copy(), sid[:ne.value + 1].copy()
+
+
+def edlines(gray, min_length=50.0, cap=4096):
+    """detect_raw_lines + filter_lines: [n][6] float32 (sx, sy, ex, ey, angle, length)."""
+    g8 = np.ascontiguousarray(gray, np.uint8)
+    h, w = g8.shape
+    out = np.zeros((cap, 6), np.float32)
+    n = ctypes.c_int()
+    rc = lib().orc_edlines(P(g8), w, h, ctypes.c_float(min_length), P(out), cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return out[:n.value].copy()

@@ -1,0 +1,78 @@
+"""GPU per-frame line detection vs the CPU restatement (oracle/lines_ref.cpp).
+
+Reference: src/Frame.cc:324-328 (detect_raw_lines + filter_lines), src/line_detect/
+line_lbd_allclass.cpp:137-214, src/line_detect/libs/binary_descriptor.cpp:796-1148,
+1583-2906 (GaussianBlur 5x5 / EDLineDetector), include/line_lbd/line_descriptor/
+descriptor.hpp:649-844 (nfa). The restatement's parity against the original OpenCV
+build is unpinned (no fixture of the reference holds detected lines; OpenCV is absent):
+these tests pin the GPU to the restatement. Maps and edge chains are integer and must
+match exactly; line endpoints / angle / length are float results of double arithmetic
+with the same operation order and must match exactly too. The only transcendental
+calls (atan2 in the per-pixel direction test, the log-gamma / exp / pow of nfa) are
+device double functions, within an ulp of glibc's: a decision flip needs a value
+within ~1e-15 of its threshold (none occurs on these inputs).
+"""
+import numpy as np
+import pytest
+
+import eao_accel as ea
+import pyoracle as orc
+from tools import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def frames():
+    return synth.line_frames(6, seed=0xEA7)
+
+
+def test_maps_exact(frames):
+    L = ea.Lines()
+    for f in frames[:3]:
+        L.detect(f)
+        blur, dx, dy, code = L.debug_maps()
+        ob, odx, ody, og, odr = orc.line_maps(f)
+        assert np.array_equal(blur, ob)
+        assert np.array_equal(dx, odx) and np.array_equal(dy, ody)
+        assert np.array_equal((code & 0x7fff).astype(np.int16), og)
+        assert np.array_equal((code >> 15).astype(np.uint8) * 255, odr)
+
+
+@pytest.mark.parametrize("min_length", [50.0, 0.0])
+def test_lines_exact(frames, min_length):
+    L = ea.Lines()
+    tot = 0
+    for f in frames:
+        g = L.detect(f, min_length=min_length)
+        o = orc.edlines(f, min_length=min_length)
+        assert g.shape == o.shape, (g.shape, o.shape)
+        assert np.array_equal(g, o), np.abs(g - o).max()
+        tot += len(o)
+    assert tot > 50  # the frames are line-rich
+
+
+def test_lines_textured_and_flat():
+    # the ORB bench frames (procedural texture: few straight edges) and a flat frame (no
+    # anchors, no edges: zero lines, the reference's "detect zero lines" path)
+    L = ea.Lines()
+    fr, _ = synth.frame_stream(2)
+    for f in list(fr) + [np.full((480, 640), 77, np.uint8)]:
+        assert np.array_equal(L.detect(f), orc.edlines(f))
+
+
+def test_lines_batch_device(frames):
+    import torch
+    F = len(frames)
+    dev = torch.device("cuda", 0)
+    L = ea.Lines(max_batch=F)
+    d = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    cap = 256
+    out = torch.zeros((F, cap, 6), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    L.detect_batch_device(d.data_ptr(), F, 640, 50.0, out.data_ptr(), cnt.data_ptr(), cap)
+    torch.cuda.synchronize()
+    ho, hc = out.cpu().numpy(), cnt.cpu().numpy()
+    for t in range(F):
+        o = orc.edlines(frames[t])
+        assert hc[t] == len(o) and np.array_equal(ho[t, :hc[t]], o), t

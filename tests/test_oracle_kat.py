@@ -292,3 +292,26 @@ def test_np_bounds_int32_wrap_q4():
         base = 0.5 * m * (m + n + 1)
         sp = 1.282 * np.sqrt(np.float64(q)) if q >= 0 else np.nan
         assert np.allclose([r["r1"], r["r2"]], [np.float32(base - sp), np.float32(base + sp)], rtol=1e-7, equal_nan=True)
+
+
+def test_line_oracle_properties():
+    """The line restatement on a frame with one bright axis-aligned rectangle: the
+    rectangle's four sides come out (EDLine's border rule only drops lines within 10 px
+    of the image border), each about as long as the side, in the reference's
+    start / end orientation convention (dark side on the left of the direction)."""
+    img = np.full((480, 640), 40, np.uint8)
+    img[149:331, 199:461] = 120  # half-intensity boundary pixels: the gradient peaks on one
+    img[150:330, 200:460] = 200  # pixel row / column, so the edges carry anchors
+    L = orc.edlines(img)
+    assert 3 <= len(L) <= 8
+    lengths = sorted(L[:, 5])
+    assert lengths[-1] > 240  # a 260-px side
+    for sx, sy, ex, ey, ang, ln in L:
+        assert abs(np.hypot(ex - sx, ey - sy) - ln) < 1e-3
+        assert -np.pi <= ang <= np.pi
+    blur, dx, dy, g, d = orc.line_maps(img)
+    # the 8U fixed-point taps cvRound(256 k) of getGaussianKernel(5, 1) are 14, 63, 103,
+    # 63, 14 (sum 257, not renormalised -- the same rule as the 7x7 ORB blur): a flat
+    # region of v blurs to (257^2 v + 2^15) >> 16
+    assert blur[240, 320] == (257 * 257 * 200 + (1 << 15)) >> 16 and blur[20, 20] == (257 * 257 * 40 + (1 << 15)) >> 16
+    assert dx[240, 200] > 0 and dy[150, 300] > 0  # dark -> bright steps

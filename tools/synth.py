@@ -533,3 +533,28 @@ def assoc_stream_config_c(n_frames=1000, seed=0xEA3, K=TUM3_K, w=640, h=480, n_d
         frames.append(dict(T=T, boxes=boxes, ids=obs.astype(np.int32), pos=P[obs], uv=uv,
                            bad=np.zeros(len(obs), np.uint8), kf=(t % kf_every == kf_every - 1)))
     return frames
+
+
+def line_frames(n, w=640, h=480, seed=0xEA7, n_quads=(6, 12)):
+    """Line-rich gray frames for the line detector: a smooth shaded
+    background with mild noise and several solid convex quadrilaterals / thin bars at random
+    angles (the straight object and structure edges EDLine is built for). uint8 [n][h][w]."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    out = np.zeros((n, h, w), np.uint8)
+    for f in range(n):
+        img = 90 + 40 * np.sin(xx / 97.0 + f * 0.05) * np.cos(yy / 131.0) + rng.normal(0, 2.0, (h, w))
+        for _ in range(int(rng.integers(*n_quads))):
+            cx, cy = rng.uniform(40, w - 40), rng.uniform(40, h - 40)
+            a = rng.uniform(0, np.pi)
+            if rng.random() < 0.25:  # a thin bar
+                hw, hh = rng.uniform(60, 220), rng.uniform(2, 5)
+            else:
+                hw, hh = rng.uniform(30, 160), rng.uniform(25, 120)
+            c, s = np.cos(a), np.sin(a)
+            u = (xx - cx) * c + (yy - cy) * s
+            v = -(xx - cx) * s + (yy - cy) * c
+            m = (np.abs(u) <= hw) & (np.abs(v) <= hh)
+            img[m] = rng.uniform(20, 235) + rng.normal(0, 1.5, int(m.sum()))
+        out[f] = np.clip(np.rint(img), 0, 255).astype(np.uint8)
+    return out
