@@ -354,6 +354,7 @@ def main():
     match_ms = float(np.mean(rec["match_ms"]))
     searches = search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc,
                            d_cnt, d_has, d_mpos, match_ms)
+    lines_leg = line_leg(ea, torch, stream, min(F, RENDERED), gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
     n_kps = float(d_cnt.float().mean().item())
     ab = algorithmic_bytes(n_kps)
     dom = int(np.argmax(stage))
@@ -400,6 +401,7 @@ def main():
             "extract_gbs": ab["extract"] * F / (ext_ms * 1e-3) / 1e9,
             "match_ms_per_step": match_ms,
             "searches": searches,
+            "line_detect": lines_leg,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
                                   "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
@@ -425,6 +427,50 @@ def main():
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
     return 0
+
+
+def line_leg(ea, torch, stream, F, gpu, with_cpu=True, reps=3, distinct=48):
+    """Per-frame line detection (detect_raw_lines + filter_lines, Frame.cc:324-328) beside
+    the step: a batch of F line-rich 640x480 frames (tools/synth.line_frames, `distinct`
+    rendered and cycled), HBM-resident, timed with HIP events; the CPU restatement
+    (oracle/lines_ref.cpp, one thread) timed on a few frames, and those frames checked."""
+    from tools import synth
+    dev = torch.device("cuda", gpu)
+    lf = synth.line_frames(min(F, distinct), seed=0xEA7)
+    idx = pingpong(F, len(lf))
+    d = torch.from_numpy(lf).to(dev)[torch.from_numpy(idx).to(dev)].contiguous()
+    L = ea.Lines(W, H, max_batch=F, device=gpu)
+    cap = 256
+    out = torch.zeros((F, cap, 6), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    sp = stream.cuda_stream
+    L.detect_batch_device(d.data_ptr(), F, W, 50.0, out.data_ptr(), cnt.data_ptr(), cap, sp)
+    ms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        L.detect_batch_device(d.data_ptr(), F, W, 50.0, out.data_ptr(), cnt.data_ptr(), cap, sp)
+        e1.record(stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    hc = cnt.cpu().numpy()
+    res = {"frames": F, "ms_per_batch": float(np.mean(ms)), "frames_per_s": F / (np.mean(ms) * 1e-3),
+           "mean_lines": float(hc.mean()), "data": "tools/synth.line_frames (%d rendered, cycled)" % len(lf)}
+    if with_cpu:  # the line detector's CPU baseline: the restatement as checker and timed port
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as orc  # checker / CPU baseline only
+        orc.use_native()  # the same -O3 -march=native build the step's CPU baseline times
+        k = 4
+        t0 = time.perf_counter()
+        ref = [orc.edlines(lf[i]) for i in range(k)]
+        cpu_ms = (time.perf_counter() - t0) * 1e3 / k
+        ho = out.cpu().numpy()
+        ok = all(hc[i] == len(ref[i]) and np.array_equal(ho[i, :hc[i]], ref[i]) for i in range(k))
+        res.update({"cpu_ms_per_frame": cpu_ms, "cpu_kind": "port (oracle/lines_ref.cpp, 1 thread)",
+                    "gpu_over_cpu": (F / (np.mean(ms) * 1e-3)) / (1e3 / cpu_ms), "parity_frames": k,
+                    "parity_bitexact": bool(ok)})
+    L.close()
+    return res
 
 
 def valu_roof(kernel, frames, ms):

@@ -34,10 +34,13 @@ def use_native():
     """Switch to the -O3 -march=native build of the same sources (bench.py's timed CPU
     baseline), compiling it on this machine first; must precede the first lib() call."""
     global LIB_PATH
+    native = os.path.join(HERE, "_build_native", "liboracle.so")
     if _lib is not None:
+        if LIB_PATH == native:
+            return LIB_PATH  # already the native build
         raise RuntimeError("pyoracle: library already loaded")
     subprocess.check_call(["make", "-s", "-j4", "-C", HERE, "native"])
-    LIB_PATH = os.path.join(HERE, "_build_native", "liboracle.so")
+    LIB_PATH = native
     return LIB_PATH
 
 
