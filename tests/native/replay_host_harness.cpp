@@ -73,6 +73,7 @@ AssocEngine::~AssocEngine() {}
 }  // namespace eao
 
 struct eao_assoc { eao::AssocEngine e; };
+extern "C" const char* eao_last_error(void) { return eao::g_err.c_str(); }
 namespace eao { AssocEngine* assoc_engine(eao_assoc* a) { return &a->e; } }
 extern "C" eao_assoc* harness_assoc_create() { auto* a = new eao_assoc(); a->e.dev = 0; return a; }
 // the RCCL exchanger is product-only; the harness shards through

@@ -97,3 +97,49 @@ def test_sharded_replay_world2_matches_oracle(kind, n, flag):
         assert st["exchanges"] > 0
     # both ranks saw the same exchanges
     assert res[0][5]["exchanges"] == res[1][5]["exchanges"]
+
+
+def _worker_capacity(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        H = ctypes.CDLL(HARNESS)
+        H.harness_assoc_create.restype = ctypes.c_void_p
+        H.eao_last_error.restype = ctypes.c_char_p
+        ea._lib = H
+
+        class A:
+            pass
+        a = A()
+        a.h = ctypes.c_void_p(H.harness_assoc_create())
+        g = ea.Replay(a, "iForest")
+        g.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
+        err = None
+        for i, f in enumerate(synth.assoc_stream(12, classes=[39, 56], pts_range=(9000, 9001))):
+            try:
+                g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+            except ea.EaoError as e:
+                err = str(e)
+                break
+        dist.destroy_process_group()
+        q.put((rank, err, None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, None, repr(e)))
+
+
+def test_sharded_capacity_error_reaches_every_rank():
+    """An object over the isolation-forest capacity (9000 points > IF_MAXN): the capacity
+    verdict is taken over the whole batch before the ownership filter, so both ranks fail
+    the same frame with the same error instead of one rank waiting in an exchange."""
+    subprocess.check_call(["make", "-s", "-C", NATIVE])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_capacity, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=300) for _ in procs), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[2] is None for r in res), [r[2] for r in res]
+    assert all(r[1] is not None and "capacity" in r[1] for r in res), [r[1] for r in res]
