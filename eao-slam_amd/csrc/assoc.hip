@@ -448,15 +448,14 @@ __device__ __forceinline__ void if_stamp(int k) {
 
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
 struct IfLds {
-  size_t mt, b0, b1, nodes, right, ndep, shuf, total;
+  size_t mt, b0, b1, nodes, right, shuf, total;
   __host__ __device__ IfLds(int N, int S) {
     mt = 0;
     b0 = al16(624 * 4);
     b1 = b0 + al16(12 * (size_t)S);
     nodes = b1 + al16(12 * (size_t)S);
-    right = nodes + al16(8 * 2 * (size_t)S);
-    ndep = right + al16(2 * 2 * (size_t)S);
-    const size_t build_end = ndep + al16(2 * (size_t)S);
+    right = nodes + al16(8 * (2 * (size_t)S + 2));  // + the two look-ahead ids of rank_subtree
+    const size_t build_end = right + al16(2 * (2 * (size_t)S + 2));
     // sampling scratch (p, head, next, ids) aliases B1 / nodes, dead until the build
     shuf = b1;
     const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
@@ -502,7 +501,6 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   float* B1 = (float*)(smem + L.b1);
   uint2* nodes = (uint2*)(smem + L.nodes);
   uint16_t* right = (uint16_t*)(smem + L.right);
-  uint8_t* ndep = (uint8_t*)(smem + L.ndep);  // node depth, preorder (right links derive from it)
   __shared__ int s_nodes_bad;
 
   const int tr = blockIdx.x, c = blockIdx.y;
@@ -645,7 +643,6 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       // right links for the score walk, written as each right child gets its id
       if (par >= 0 && lane == 0) right[par] = (uint16_t)me;
       const int cnt = last - first + 1;
-      if (lane == 0) ndep[me] = (uint8_t)depth;
       if (cnt < 2 || depth >= maxDepth) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
@@ -659,7 +656,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
         IFP_T(rs0);
         const int nn0 = nn;
-        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, ndep, right);
+        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, right);
         IFP_T(rs1);
         IFP_ACC(21, rs0, rs1);
         IFP_ACC(22, 0ull, 1ull);
@@ -706,10 +703,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
               } else {
                 const uint64_t rmk = mask & ~lm;
                 if (rmk == 0) bad = 1;  // empty right range: Node::Build fails
-                if (lane == 0) {
-                  nodes[node] = make_uint2(dim + 1u, __float_as_uint(split));
-                  ndep[node] = (uint8_t)d;
-                }
+                if (lane == 0) nodes[node] = make_uint2(dim + 1u, __float_as_uint(split));
                 if (lane == ssp) {
                   slo = (int)(uint32_t)rmk;
                   shi = (int)(uint32_t)(rmk >> 32);
@@ -728,10 +722,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
             }
           }
           IFP_T(t6);
-          if (lane == 0) {
-            nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
-            ndep[node] = (uint8_t)d;
-          }
+          if (lane == 0) nodes[node] = make_uint2((uint32_t)cn << 2, 0u);
           if (ssp == 0) break;
           ssp--;
           mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(slo, ssp) |

@@ -214,11 +214,11 @@ namespace eao {
 // from g exactly as the sequential build takes them (dim: Lemire over 3,
 // split: uniform_real(min, max)); leaves (by count or depth) consume none and
 // are recorded without a loop trip. Node records (x = dim + 1 | count << 2,
-// y = split bits) and depths go to nodes / ndep for ids [me, nn), preorder;
+// y = split bits) go to nodes for ids [me, nn), preorder, right links to right;
 // the caller has allocated `me` (nn == me + 1) and checked 2 <= cnt,
 // depth < maxDepth. Returns 1 when Node::Build fails (empty right range).
 __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, int cnt, int depth, int maxDepth,
-                                            int me, int& nn, uint2* nodes, uint8_t* ndep, uint16_t* right) {
+                                            int me, int& nn, uint2* nodes, uint16_t* right) {
   const int lane = lane_id();
   auto sk64 = [&](int k) { return ((uint64_t)((uint32_t)k ^ 0x80000000u) << 32) | (uint32_t)lane; };
   uint64_t vx = sk64(lane < cnt ? kx : INT_MAX), vy = sk64(lane < cnt ? ky : INT_MAX),
@@ -238,26 +238,18 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
   // child's items come back through the inverse one
   uint64_t S = cnt == 64 ? ~0ull : ((1ull << cnt) - 1ull);
   int d = depth, node = me, cn = cnt, ssp = 0, bad = 0;
-  // node records buffered in lanes (lane j = node rb + j): x | depth << 24, split
-  int rbx = 0, rby = 0, rb = me;
-  auto flush = [&](int k) {
-    if (lane < k) {
-      nodes[rb + lane] = make_uint2((uint32_t)rbx & 0xffffffu, (uint32_t)rby);
-      ndep[rb + lane] = (uint8_t)((uint32_t)rbx >> 24);
-    }
-    rb += k;
-  };
-  auto record = [&](int id, uint32_t x, uint32_t y, int dep) {
-    writelane(rbx, (int)(x | ((uint32_t)dep << 24)), id - rb);
-    writelane(rby, (int)y, id - rb);
-    if (id - rb == 63) flush(64);
-  };
-  // right links (the score walk's `right`), written as each right child gets its id
-  auto link = [&](int parent, int child) {
-    if (lane == 0) right[parent] = (uint16_t)child;
+  // Node records and right links go straight to LDS from lane 0 (stores: off the chain).
+  // The loop is written for few taken branches (each costs ~34 cycles on one wave):
+  // both possible leaf-child records are stored unconditionally at ids nn and nn + 1 --
+  // a record at an id that is not (yet) that node's is overwritten later in program
+  // order, since every id up to the final nn gets exactly one real record after it
+  // (the node array has room for the two look-ahead ids) -- and the stack push is an
+  // unconditional writelane whose depth only advances when it is meant.
+  auto put = [&](int id, uint32_t x, uint32_t y) {
+    if (lane == 0) nodes[id] = make_uint2(x, y);
   };
   // pending right children, entry e in lane e: item set (q0, q1), depth | leaf flag
-  // (bit 8; then q0 holds the count), parent id
+  // (bit 8), parent id
   int q0 = 0, q1 = 0, q2 = 0, q3 = 0;
   while (true) {
     // the current node (items S, count cn, depth d, id node) is not a leaf by count
@@ -270,73 +262,62 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
     const int lo = __builtin_ctzll(md), hi = 63 - __builtin_clzll(md);
     const float mn = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fk), lo));
     const float mx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fk), hi));
-    bool leaf = __builtin_bit_cast(int, mn) == __builtin_bit_cast(int, mx);
-    if (!leaf) {
-      const float split = g.uniform_real(mn, mx);
-      const uint64_t lm = md & ballot(fk < split);  // ranks below the split: a prefix
-      leaf = lm == 0;
-      if (!leaf) {
-        record(node, dim + 1u, __float_as_uint(split), d);
-        const uint64_t L = ballot((lm >> rk) & 1ull);  // the left items
-        const uint64_t R = S & ~L;
-        if (R == 0) {  // empty right range: Node::Build fails
-          bad = 1;
-          break;
-        }
-        const int cl = __builtin_popcountll(L), cr = cn - cl;
-        d++;
-        const bool lleaf = cl < 2 || d >= maxDepth, rleaf = cr < 2 || d >= maxDepth;
-        if (lleaf) {
-          record(nn++, (uint32_t)cl << 2, 0u, d);
-          if (!rleaf) {  // the right child is next
-            S = R;
-            cn = cr;
-            link(node, nn);
-            node = nn++;
-            continue;
-          }
-          link(node, nn);
-          record(nn++, (uint32_t)cr << 2, 0u, d);
-        } else {
-          if (rleaf) {
-            writelane(q0, cr, ssp);
-            writelane(q2, d | 256, ssp);
-          } else {
-            writelane(q0, (int)(uint32_t)R, ssp);
-            writelane(q1, (int)(uint32_t)(R >> 32), ssp);
-            writelane(q2, d, ssp);
-          }
-          writelane(q3, node, ssp);
-          ssp++;
-          S = L;  // the left child is next
-          cn = cl;
-          node = nn++;
-          continue;
-        }
-      }
+    const bool eq = __builtin_bit_cast(int, mn) == __builtin_bit_cast(int, mx);
+    // the split draw is read whatever the outcome and consumed only when min != max
+    if (g.bp >= g.blen) g.refill();
+    const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g.buff), g.bp));
+    g.bp += eq ? 0 : 1;
+    const float split = fadd(fmul(r, fsub(mx, mn)), mn);
+    const uint64_t lm = md & ballot(fk < split);  // ranks below the split: a prefix
+    const bool leaf = eq || lm == 0;
+    const uint64_t L = ballot((lm >> rk) & 1ull);  // the left items
+    const uint64_t R = S & ~L;
+    const int cl = __builtin_popcountll(L), cr = cn - cl, d1 = d + 1;
+    const bool lleaf = cl < 2 || d1 >= maxDepth, rleaf = cr < 2 || d1 >= maxDepth;
+    put(node, leaf ? (uint32_t)cn << 2 : dim + 1u, leaf ? 0u : __float_as_uint(split));
+    put(nn, (uint32_t)cl << 2, 0u);      // the left child as a leaf (real when !leaf && lleaf)
+    put(nn + 1, (uint32_t)cr << 2, 0u);  // the right child as a leaf (real when both leaves)
+    if (!leaf && R == 0) {  // empty right range: Node::Build fails
+      bad = 1;
+      break;
     }
-    if (leaf) record(node, (uint32_t)cn << 2, 0u, d);
-    // next pending right child that is not a leaf (leaves are recorded on the way)
+    if (lane == 0 && !leaf && lleaf) right[node] = (uint16_t)(nn + 1);
+    // push the right child when the left one is walked next (case "descend")
+    const bool descend = !leaf && !lleaf;
+    writelane(q0, (int)(uint32_t)R, ssp);
+    writelane(q1, (int)(uint32_t)(R >> 32), ssp);
+    writelane(q2, d1 | (rleaf ? 256 : 0), ssp);
+    writelane(q3, node, ssp);
+    ssp += descend ? 1 : 0;
+    const bool goright = !leaf && lleaf && !rleaf;
+    const int nn0 = nn;
+    nn += leaf ? 0 : (lleaf ? 2 : 1);
+    S = descend ? L : R;
+    cn = descend ? cl : cr;
+    d = d1;
+    node = descend ? nn0 : nn0 + 1;
+    if (descend || goright) continue;
+    // pop: the next pending right child that is not a leaf (leaves recorded on the way)
     bool found = false;
     while (ssp > 0) {
       ssp--;
       const int e = __builtin_amdgcn_readlane(q2, ssp);
-      link(__builtin_amdgcn_readlane(q3, ssp), nn);
-      node = nn++;
-      d = e & 255;
-      if (e & 256) {
-        record(node, (uint32_t)__builtin_amdgcn_readlane(q0, ssp) << 2, 0u, d);
-        continue;
-      }
+      const int par = __builtin_amdgcn_readlane(q3, ssp);
       S = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q0, ssp) |
           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q1, ssp) << 32);
+      if (lane == 0) right[par] = (uint16_t)nn;
+      node = nn++;
+      d = e & 255;
       cn = __builtin_popcountll(S);
+      if (e & 256) {
+        put(node, (uint32_t)cn << 2, 0u);
+        continue;
+      }
       found = true;
       break;
     }
     if (!found) break;
   }
-  flush(nn - rb);
   return bad;
 }
 
