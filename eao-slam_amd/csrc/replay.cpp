@@ -169,11 +169,16 @@ struct Obj {  // Object_Map
   // forest (it was updated earlier in the frame, so it can no longer be associated this
   // frame -- every such effect is a vote or a projected-rect recompute): applied in order
   // when the forest completes, with the pose of their frame (ReplayEngine::associate).
-  enum { DFR_PROJ = 0, DFR_PROJ_IF_NP = 1, DFR_VOTE_IF_NP = 2 };
+  // DFR_T: the t-test step of a later detection (Object.cc:497-620) whose rect overlap
+  // with this object reads the post-forest projected rect; mode 0 a vote for the
+  // detection's associated object, 1 (before the t-test winner, or no winner) a failed
+  // update (rect recompute) if in vT else a vote, 2 (after the winner) a vote
+  enum { DFR_PROJ = 0, DFR_PROJ_IF_NP = 1, DFR_VOTE_IF_NP = 2, DFR_T = 3 };
   struct Dfr {
     int kind;
     Det* det;     // the detection whose NP verdict against this object decides (kinds 1, 2)
-    Obj* target;  // the object that receives the vote (kind 2)
+    Obj* target;  // the object that receives the vote (kinds 2, 3)
+    uint8_t mode = 0, t8 = 0, m10 = 0, m4 = 0;  // DFR_T: mode and the t-test outcomes
   };
   std::vector<Dfr> dfr;
   float dfrT[16];
@@ -212,14 +217,21 @@ void quat_from_R(const double R[3][3], double q[4]) {
   const double nrm = std::sqrt(((q[1] * q[1] + q[3] * q[3]) + (q[2] * q[2] + q[0] * q[0])));
   for (int a = 0; a < 4; a++) q[a] = q[a] / nrm;
 }
-void qrot(const double q[4], const double v[3], double o[3]) {
+// Eigen's q * v: uv = 2 (q.vec x v); v + w uv + q.vec x uv. Scalars, not arrays: g++
+// vectorises the array form into 16-byte reloads of 8-byte stores (store-forward stalls)
+inline void qrot(const double q[4], const double v[3], double o[3]) {
   const double x = q[1], y = q[2], z = q[3], w = q[0];
-  double uv[3] = {y * v[2] - z * v[1], z * v[0] - x * v[2], x * v[1] - y * v[0]};
-  for (int a = 0; a < 3; a++) uv[a] += uv[a];
-  const double c2[3] = {y * uv[2] - z * uv[1], z * uv[0] - x * uv[2], x * uv[1] - y * uv[0]};
-  for (int a = 0; a < 3; a++) o[a] = v[a] + w * uv[a] + c2[a];
+  const double v0 = v[0], v1 = v[1], v2 = v[2];
+  double u0 = y * v2 - z * v1, u1 = z * v0 - x * v2, u2 = x * v1 - y * v0;
+  u0 += u0;
+  u1 += u1;
+  u2 += u2;
+  const double c0 = y * u2 - z * u1, c1 = z * u0 - x * u2, c2 = x * u1 - y * u0;
+  o[0] = v0 + w * u0 + c0;
+  o[1] = v1 + w * u1 + c1;
+  o[2] = v2 + w * u2 + c2;
 }
-void se3_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
+inline void se3_apply(const double q[4], const double t[3], const double v[3], double o[3]) {
   double r[3];
   qrot(q, v, r);
   for (int a = 0; a < 3; a++) o[a] = r[a] + t[a];
@@ -388,7 +400,8 @@ class ReplayEngine {
   int kept_pos = -1;              // the detection being associated
   bool cur_np_done = false;       // ... and whether its NP step has read the cache
   // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
-  double prof[32] = {0};
+  double prof[56] = {0};
+  int phase = 0;
   static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
@@ -775,6 +788,7 @@ class ReplayEngine {
 
   // Object_Map::ComputeMeanAndStandard, Object.cc:967-1198 (min/max replace the sorts)
   void mean_std(Obj* o) {
+    double T0 = now_us();
     for (int a = 0; a < 3; a++) o->sum[a] = 0;
     size_t w = 0;
     for (size_t i = 0; i < o->pts.size(); i++) {
@@ -796,6 +810,7 @@ class ReplayEngine {
         mx[a] = std::max(mx[a], p->pos[a]);
       }
     for (int a = 0; a < 3; a++) o->sd[a] = std::sqrt(s2[a] / (float)n);
+    double T1 = now_us(); prof[32] += T1 - T0;
     if (n == 0) return;
     float c2[3] = {0, 0, 0};
     for (Det* f : o->frames) {
@@ -819,6 +834,7 @@ class ReplayEngine {
     update_pose(o);
     float omn[3] = {INFINITY, INFINITY, INFINITY}, omx[3] = {-INFINITY, -INFINITY, -INFINITY};
     double qi[4], ti[3];  // pose inverse, identical for every point
+    double T2 = now_us(); prof[33] += T2 - T1; prof[36] += n;
     se3_inverse(o->q, o->t, qi, ti);
     for (MapPt* p : o->pts) {
       const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
@@ -830,6 +846,7 @@ class ReplayEngine {
         omx[a] = std::max(omx[a], f);
       }
     }
+    double T3 = now_us(); prof[34] += T3 - T2;
     for (int k = 0; k < 8; k++) {
       const double v[3] = {cx[k] ? omx[0] : omn[0], cy[k] ? omx[1] : omn[1], cz[k] ? omx[2] : omn[2]};
       se3_apply(o->q, o->t, v, o->corner[k]);
@@ -855,6 +872,7 @@ class ReplayEngine {
       dis += std::sqrt(e[0] + e[1] + e[2]);
     }
     o->csd_all = std::sqrt(dis / (float)o->frames.size());
+    prof[35] += now_us() - T3;
   }
 
   bool iforest_applies(const Obj* o) const {
@@ -1157,8 +1175,11 @@ class ReplayEngine {
       int rc = exchange_batch(b);
       if (rc) return rc;
     } else if (b.launched) {
+      Tick tw(&prof[39]);
+      Tick tw2(&prof[42 + phase]);
       EAO_HIP_CHECK(spin_event(b.ev));
     }
+    double tpost = now_us();
     int c = 0;
     while (b.objs[c] != o) c++;
     const size_t n = o->pts.size();
@@ -1184,6 +1205,7 @@ class ReplayEngine {
       }
     }
     o->pts.resize(w);
+    prof[40] += now_us() - tpost;
     if (o->pending == 2) mean_std(o);
     if (o->yaw_due) {  // SampleObjYaw of the launch frame, now that the cuboid is final
       o->yaw_due = false;
@@ -1192,7 +1214,7 @@ class ReplayEngine {
     const eao_np_stats* sps = sworld > 1 ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
     if (!o->dfr.empty()) {  // effects of later same-frame detections, in their order
       for (const Obj::Dfr& d : o->dfr) {
-        if (d.kind != Obj::DFR_PROJ) {
+        if (d.kind == Obj::DFR_PROJ_IF_NP || d.kind == Obj::DFR_VOTE_IF_NP) {
           // NP verdict of (d.det, o) on the post-forest cloud: one of the speculative
           // pairs evaluated behind this forest (kick() includes every later detection)
           int v = -2;
@@ -1209,7 +1231,8 @@ class ReplayEngine {
           }
           if (v == 2) continue;  // fails: the object was not in vNP
         }
-        if (d.kind == Obj::DFR_VOTE_IF_NP) reobj(d.target, o->id);
+        if (d.kind == Obj::DFR_T) t_step_deferred(o, d);
+        else if (d.kind == Obj::DFR_VOTE_IF_NP) reobj(d.target, o->id);
         else proj_with(o, o->dfrT);
       }
       o->dfr.clear();
@@ -1280,10 +1303,29 @@ class ReplayEngine {
     if (ymx > pz.rows) ymx = (float)pz.rows;
     o->proj = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
   }
-  void defer(Obj* o, int kind, Det* f, Obj* target) {
+  void defer(Obj* o, const Obj::Dfr& d) {
     if (o->dfr.empty()) std::memcpy(o->dfrT, pz.T, sizeof(o->dfrT));
-    o->dfr.push_back(Obj::Dfr{kind, f, target});
-    if (kind != Obj::DFR_VOTE_IF_NP) o->proj_dfr = true;
+    o->dfr.push_back(d);
+    if (d.kind != Obj::DFR_VOTE_IF_NP) o->proj_dfr = true;
+  }
+  void defer(Obj* o, int kind, Det* f, Obj* target) { defer(o, Obj::Dfr{kind, f, target}); }
+  // the t-test step's rect part for a held object, at its forest's completion: the rect
+  // read is the one the earlier deferred effects left (they are applied in order)
+  void t_step_deferred(Obj* o, const Obj::Dfr& d) {
+    const Det* f = d.det;
+    int mem = 0;  // 1 vT, 2 vTL
+    if (std::max(ov_iou(f->box, o->proj), ov_iou(f->feat, o->proj)) > 0.25) {
+      mem = (d.t8 || d.m10) ? 1 : 2;
+    } else if (d.m4) {
+      proj_with(o, o->dfrT);  // ComputeProjectRectFrame under the detection's pose
+      if (std::max(ov_iou(f->box, o->proj), ov_iou(f->feat, o->proj)) > 0.25) mem = 2;
+    }
+    if (!mem) return;
+    if (d.mode == 1 && mem == 1) {
+      proj_with(o, o->dfrT);  // DataAssociateUpdate(.., 3) of an updated object: the rect only
+    } else if (d.target && d.target != o) {
+      reobj(d.target, o->id);
+    }
   }
   // an object updated earlier in this frame whose forest has not completed: a later
   // detection's decisions cannot associate it (DataAssociateUpdate returns false), so
@@ -1405,7 +1447,10 @@ class ReplayEngine {
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
-    EAO_HIP_CHECK(spin_event(gpu0_ev));
+    {
+      Tick tw(&prof[41]);
+      EAO_HIP_CHECK(spin_event(gpu0_ev));
+    }
     const int* r = (const int*)(h_out + o_r);
     const uint8_t* ok = h_out + o_ok;
     for (int b = 0; b < nb; b++) {
@@ -1558,7 +1603,9 @@ class ReplayEngine {
       if (Flag == 2 || Flag == 3) defer(o, Obj::DFR_PROJ, f, nullptr);
       return false;
     }
+    phase = 9;
     if (touch(o)) return false;
+    phase = 1;
     if (Flag != 1 && Flag != 4) {
       project_rect_host(o);
       const IRect r1 = o->proj;
@@ -1662,7 +1709,9 @@ class ReplayEngine {
       for (auto& up : objs)
         if (up->cls == f->cls && up->pending) {
           if (!held(up.get())) {
+            phase = 5;
             if ((rc = touch(up.get()))) return rc;
+            phase = 1;
           } else if (up->slot < 0) {
             launch = true;
           }
@@ -1729,7 +1778,9 @@ class ReplayEngine {
       if (!need.empty()) {
         std::vector<Obj*> tl;
         for (int i : need) tl.push_back(objs[i].get());
+        phase = 6;
         rc = flush_list(tl);  // completing a forest publishes its speculative NP pairs
+        phase = 1;
         if (rc) return rc;
         std::vector<int> still;
         for (int i : need)
@@ -1807,7 +1858,9 @@ class ReplayEngine {
         Obj* o = objs[i].get();
         if (f->cls != o->cls || o->bad) continue;
         if (f->pts.size() >= 10 && (int)o->frames.size() > 8) continue;
+        phase = 7;
         if ((rc = proj_read(o))) return rc;
+        phase = 1;
         const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
         if (a >= 0.25 && a > fmax) {
           fmax = a;
@@ -1837,14 +1890,14 @@ class ReplayEngine {
     }
     bool byT = false;
     std::vector<int> vT, vTL;
+    std::vector<std::pair<int, Obj::Dfr>> tdef;  // held objects' deferred t-test parts
     if (flag != "NA" && flag != "IoU" && flag != "NP") {
       for (int i = (int)objs.size() - 1; i >= 0; i--) {
         Obj* o = objs[i].get();
         if (f->cls != o->cls || o->bad) continue;
         const int df = (int)o->frames.size();
         if (df <= 8) continue;
-        if ((rc = proj_read(o))) return rc;
-        const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
+        if (o->pending == 2 && (rc = proj_read(o))) return rc;  // completion recomputes center / csd
         const float dx = std::fabs(o->center[0] - f->pos[0]), dy = std::fabs(o->center[1] - f->pos[1]),
                     dz = std::fabs(o->center[2] - f->pos[2]);
         const float tx = (float)(dx / (o->csd[0] / std::sqrt((double)df)));
@@ -1853,7 +1906,21 @@ class ReplayEngine {
         const float* row = kTTable[std::min(df - 1, 121)];
         if (tx < row[5] && ty < row[5] && tz < row[5]) {
           vT.push_back(i);
-        } else if (a > 0.25) {
+          continue;
+        }
+        if (held(o) && o->pending == 1) {
+          // the rect overlap decides from here on and reads the post-forest rect: a held
+          // object cannot win the step (its update fails), so its part is deferred
+          const Obj::Dfr d{Obj::DFR_T, f, nullptr, 0, (uint8_t)(tx < row[8] && ty < row[8] && tz < row[8]),
+                           (uint8_t)((tx + ty + tz) / 3 < 10), (uint8_t)((tx + ty + tz) / 3 < 4)};
+          tdef.push_back({i, d});
+          continue;
+        }
+        phase = 8;
+        if ((rc = proj_read(o))) return rc;
+        phase = 1;
+        const float a = std::max(ov_iou(RC, o->proj), ov_iou(f->feat, o->proj));
+        if (a > 0.25) {
           if (tx < row[8] && ty < row[8] && tz < row[8])
             vT.push_back(i);
           else if ((a > 0.25) && ((tx + ty + tz) / 3 < 10))
@@ -1874,10 +1941,16 @@ class ReplayEngine {
           if (k != re) reobj(objs[re].get(), objs[k]->id);
         for (int k : vTL)
           if (k != re) reobj(objs[re].get(), objs[k]->id);
+        for (auto& td : tdef) {
+          td.second.target = objs[re].get();
+          defer(objs[td.first].get(), td.second);
+        }
       } else {
+        int won = -1;  // objs index of the winner
         for (size_t i = 0; i < vT.size(); i++) {
           if (update(objs[vT[i]].get(), f, 3)) {
             byT = true;
+            won = vT[i];
             const int tid = vT[i];
             f->method = 3;
             for (size_t j = i + 1; j < vT.size(); j++) reobj(objs[tid].get(), objs[vT[j]]->id);
@@ -1885,6 +1958,11 @@ class ReplayEngine {
               if (k != tid) reobj(objs[tid].get(), objs[k]->id);
             break;
           }
+        }
+        for (auto& td : tdef) {  // vT runs in descending index: before the winner = above it
+          td.second.mode = (won < 0 || td.first > won) ? 1 : 2;
+          td.second.target = won >= 0 ? objs[won].get() : nullptr;
+          defer(objs[td.first].get(), td.second);
         }
       }
     }
@@ -1963,6 +2041,7 @@ class ReplayEngine {
   int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
             const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
     Tick tk(&prof[0]);
+    phase = 4;
     prof[8] += 1;
     cur = fid;
     std::memcpy(pz.T, Tcw, sizeof(pz.T));
@@ -2139,7 +2218,9 @@ class ReplayEngine {
           }
         }
       }
+      phase = 0;
       int rc = frame_start_gpu(recent, pairs, di, oi);
+      phase = 1;
       if (rc) return rc;
       prof[14] += now_us() - tA;
       tA = now_us();
@@ -2167,6 +2248,7 @@ class ReplayEngine {
       }
       if (rc) return rc;
       Tick tke(&prof[30]);
+      phase = 2;
       for (int i = (int)objs.size() - 1; i >= 0; i--) {  // 10.3
         if (flag == "NA") continue;
         Obj* o = objs[i].get();
@@ -2376,6 +2458,8 @@ class ReplayEngine {
   }
 
   void big_to_small(Obj* a, Obj* s) {  // Object.cc:1926-2040
+    Tick tbs(&prof[37]);
+    double tq = now_us();
     size_t w = 0;
     for (size_t i = 0; i < a->pts.size(); i++) {
       const float* P = a->pts[i]->pos;
@@ -2384,6 +2468,7 @@ class ReplayEngine {
       if (!in) a->pts[w++] = a->pts[i];
     }
     a->pts.resize(w);
+    prof[38] += now_us() - tq;
     mean_std(a);
   }
 
@@ -2428,6 +2513,7 @@ class ReplayEngine {
 
   int local_mapping() {
     Tick tk(&prof[1]);
+    phase = 3;
     int rc;
     {
       Tick t0(&prof[24]);
@@ -2452,6 +2538,7 @@ class ReplayEngine {
         if (rc) return rc;
       }
     }
+    Tick tdo(&prof[29]);
     for (size_t i = 0; i < objs.size(); i++) {
       Obj* a = objs[i].get();
       if (a->pts.size() < 10 || a->bad || a->frames.size() < 10) continue;
@@ -2563,8 +2650,8 @@ int eao_replay_profile(eao_replay* r, double* out12) {
 
 int eao_replay_profile_n(eao_replay* r, double* out, int n) {
   if (!r || !out || n < 0) return EAO_E_ARG;
-  std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 32));
-  return std::min(n, 32);
+  std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 56));
+  return std::min(n, 56);
 }
 
 }  // extern "C"

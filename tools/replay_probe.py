@@ -18,7 +18,9 @@ NAMES = {0: "frame", 1: "local_mapping", 2: "#forest_launch", 3: "forest_complet
          5: "np_relaunch", 6: "#frame_start", 7: "frame_start_rt", 8: "#frames", 9: "#spec_np", 10: "#lm_forests", 11: "lm_forest",
          12: "steps1-3", 13: "steps4-9", 14: "frame_start_total", 15: "assoc_loop", 16: "same_cls_flush",
          17: "pending_flush", 18: "kick", 19: "launch", 20: "#retire", 21: "retire", 22: "kick_scan",
-         23: "pack", 24: "lm_flush", 25: "lm_stats", 26: "lm_merge_overlap", 28: "update", 30: "frame_end"}
+         23: "pack", 24: "lm_flush", 25: "lm_stats", 26: "lm_merge_overlap", 28: "update", 29: "lm_overlap", 30: "frame_end",
+         32: "ms_pass12", 33: "ms_pose", 34: "ms_pass3", 35: "ms_corners", 36: "#ms_pts", 37: "big_to_small", 38: "bts_filter",
+         39: "forest_spin", 40: "forest_erase", 41: "fs_spin", 42: "spin_fs", 43: "spin_loop", 44: "spin_end", 45: "spin_lm", 46: "spin_steps1-9", 47: "spin_samecls", 48: "spin_np", 49: "spin_pro", 50: "spin_t", 51: "spin_update"}
 
 if "full" in sys.argv:  # BASELINE configs[2]: the Full list, real detections
     frames, flag = synth.assoc_stream_fr3_real(0, 2582), "Full"
@@ -33,8 +35,8 @@ for rep in range(3):
     t0 = time.perf_counter()
     rp.run(packed)
     dt = time.perf_counter() - t0
-    pr = np.zeros(32)
-    ea.lib().eao_replay_profile_n(rp.h, ea.P(pr), 32)
+    pr = np.zeros(56)
+    ea.lib().eao_replay_profile_n(rp.h, ea.P(pr), 56)
     nf = len(frames)
     print("pass %d: wall %.1f ms (%.0f us/frame)" % (rep, dt * 1e3, dt * 1e6 / nf))
     print("   " + "  ".join("%s=%.0f%s" % (NAMES[k], pr[k] / (1 if NAMES[k][0] == "#" else nf),
