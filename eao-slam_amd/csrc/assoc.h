@@ -56,6 +56,8 @@ class AssocEngine {
                     hipStream_t s, int max_len, int max_sample, int npts_total,
                     double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
                     double* scores2 = nullptr);  // optional second copy of the scores
+  // host (pinned) to device copy as a kernel on stream s (16-byte aligned buffers)
+  int stage_in(void* d_dst, const void* h_src, size_t bytes, hipStream_t s);
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples
   bool iforest_fits(int max_len, int max_sample) const;
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,

@@ -1055,6 +1055,29 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
   return EAO_OK;
 }
 
+// host-to-device staging by the compute queue: 16-byte loads from pinned host memory,
+// grid-stride (a DMA-engine copy costs an engine hand-off on each side of the transfer)
+__global__ __launch_bounds__(256) void k_stage(const unsigned char* __restrict__ src, unsigned char* __restrict__ dst,
+                                               size_t bytes) {
+  const size_t n16 = bytes / 16, stride = (size_t)gridDim.x * blockDim.x;
+  const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (size_t i = t; i < n16; i += stride) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  for (size_t i = 16 * n16 + t; i < bytes; i += stride) dst[i] = src[i];
+}
+
+int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t s) {
+  if (!bytes) return EAO_OK;
+  if (((uintptr_t)dst | (uintptr_t)src) & 15) {
+    set_error("stage_in: buffers must be 16-byte aligned");
+    return EAO_E_ARG;
+  }
+  const size_t blocks = std::min<size_t>(512, (bytes / 16 + 255) / 256 + 1);
+  hipLaunchKernelGGL(k_stage, dim3((unsigned)blocks), dim3(256), 0, s, (const unsigned char*)src, (unsigned char*)dst,
+                     bytes);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
 bool AssocEngine::iforest_fits(int max_len, int max_sample) const {
   return max_len <= IF_MAXN && IfLds(max_len, max_sample).total <= lds_limit;
 }

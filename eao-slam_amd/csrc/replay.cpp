@@ -1430,7 +1430,8 @@ class ReplayEngine {
         oth[nb + k] = th_p[k];
       }
     }
-    EAO_HIP_CHECK(hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, A->stream));
+    rc = A->stage_in(d_in, h_in, in_bytes, A->stream);
+    if (rc) return rc;
     for (int k : wait_slots) EAO_HIP_CHECK(hipStreamWaitEvent(A->stream, ifb[k].ev, 0));
     const int* drm = (const int*)d_in;
     const int* dpm = (const int*)(d_in + o_pm);

@@ -29,3 +29,11 @@ if "--gaps" in sys.argv:  # GPU busy fraction: union of kernel intervals over th
             cur_e = max(cur_e, e)
     busy += cur_e - cur_s
     print("busy %.1f ms of %.1f ms" % (busy / 1e6, (iv[-1][1] - iv[0][0]) / 1e6))
+if "--timeline" in sys.argv:  # a window of dispatches: start offset, duration, gap after the previous end
+    k = int(sys.argv[sys.argv.index("--timeline") + 1])
+    w = rows[len(rows) // 2:len(rows) // 2 + k]
+    t0, pe = w[0][1], w[0][1]
+    for n, s, e, st, gy in w:
+        print("%9.1f us  dur %7.1f  gap %7.1f  stream %d  %s" % ((s - t0) / 1e3, (e - s) / 1e3, (s - pe) / 1e3, st,
+                                                                n.split('(')[0][:40]))
+        pe = max(pe, e)
