@@ -208,6 +208,12 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   // LDS atomic for its base) and the counts m, nvalid, nt
   int mc = fv0 ? 1 : 0, ntk = 0;
   for (int i = t + NPT; i < mt; i += NPT) mc += FV[i] ? 1 : 0;
+  // the rank path below is expected (frame side in a smaller power-of-two class): the
+  // pass only counts, the sort path reloads the object if it is taken after all
+  int Pmt = 256, Pnt = 256;
+  while (Pmt < mt) Pmt <<= 1;
+  while (Pnt < min(ntot, NP_MAXN)) Pnt <<= 1;
+  const bool count_only = 2 * Pmt <= Pmax && Pmt < Pnt;
   for (int i0 = 0; i0 < ntot; i0 += NPT) {
     const int i = i0 + t;
     const bool in = i < ntot;
@@ -221,11 +227,12 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
       keep = kp && OV[i];
     }
     ntk += kp ? 1 : 0;
+    if (keep && (x != x || y != y || z != z)) wpos[3] = 1;  // NaN: only the sort path orders it
     const uint64_t mk = ballot(keep);
     int base = 0;
     if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
     base = __shfl(base, 0, 64);
-    if (keep) {
+    if (keep && !count_only) {
       const int d = base + popc64(mk & lanes_below());
       if (d < Pmax) {
         S[0][d] = x;
@@ -260,13 +267,158 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
-  for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
+  int Pm = 256;
+  while (Pm < m) Pm <<= 1;
+  int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // rank path (the frame side is the smaller): the sample counts of a frame value x need
+  // only r<(x) = #{object values < x} and r<=(x): #{samples < x} = ceil(r< / step)
+  // (sorted[k step] < x iff k step < r<). The m frame values are sorted instead of the
+  // object, and the object is streamed through binary searches into per-bin counts (low
+  // 16 bits: <, high 16 bits: <=; totals <= NP_MAXN) that are prefix-summed: the integer
+  // counts of the sorted-sample search, NaN excepted (NaN takes the sort path)
+  bool rank = count_only && !wpos[3] && 2 * Pm <= Pmax && Pm < P;
+  if (count_only && !rank) wpos[3] = 2;  // the object is reloaded into S below
+  float* D[3] = {dsm, dsm + Pm, dsm + 2 * Pm};
+  int* H = (int*)(dsm + 3 * Pm);  // [3][Pm + 1]
+  if (count_only) {
+    __syncthreads();  // every thread has read wpos
+  }
+  if (rank) {
+    if (t == 0) wpos[0] = 0;
+    for (int i = t; i < 3 * (Pm + 1); i += NPT) H[i] = 0;
+    __syncthreads();
+    bool dnan = false;
+    for (int i0 = 0; i0 < mt; i0 += NPT) {
+      const int i = i0 + t;
+      const bool keep = i < mt && FV[i];
+      float x = 0.f, y = 0.f, z = 0.f;
+      if (keep) {
+        x = F[3 * i];
+        y = F[3 * i + 1];
+        z = F[3 * i + 2];
+        dnan |= x != x || y != y || z != z;
+      }
+      const uint64_t mk = ballot(keep);
+      int base = 0;
+      if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+      base = __shfl(base, 0, 64);
+      if (keep) {
+        const int d = base + popc64(mk & lanes_below());
+        D[0][d] = x;
+        D[1][d] = y;
+        D[2][d] = z;
+      }
+    }
+    for (int i = m + t; i < Pm; i += NPT) D[0][i] = D[1][i] = D[2][i] = INFINITY;
+    if (dnan) wpos[3] = 1;
+    __syncthreads();
+  }
+  if (count_only) {
+    if (wpos[3]) {  // the sort path after all (a NaN, or the sizes): the object reloaded
+      rank = false;
+      __syncthreads();
+      if (t == 0) wpos[0] = 0;
+      __syncthreads();
+      for (int i0 = 0; i0 < ntot; i0 += NPT) {
+        const int i = i0 + t;
+        const bool keep = i < ntot && kept(i) && OV[i];
+        const uint64_t mk = ballot(keep);
+        int base = 0;
+        if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+        base = __shfl(base, 0, 64);
+        if (keep) {
+          const int d = base + popc64(mk & lanes_below());
+          S[0][d] = O[3 * i];
+          S[1][d] = O[3 * i + 1];
+          S[2][d] = O[3 * i + 2];
+        }
+      }
+    }
+  }
+  if (!rank)
+    for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
   __syncthreads();
   NP_STAMP(2);
-  block_sort3_fast(S[0], S[1], S[2], P);
+  block_sort3_fast(rank ? D[0] : S[0], rank ? D[1] : S[1], rank ? D[2] : S[2], rank ? Pm : P);
   NP_STAMP(3);
+  if (rank) {
+    // two object points per thread in flight: 12 independent search chains
+    for (int i0 = t; i0 < ntot; i0 += 2 * NPT) {
+      bool in[2];
+      float v[2][3];
+#pragma unroll
+      for (int u = 0; u < 2; u++) {
+        const int i = i0 + u * NPT;
+        in[u] = i < ntot && kept(i) && OV[i];
+#pragma unroll
+        for (int a = 0; a < 3; a++) v[u][a] = in[u] ? O[3 * i + a] : 0.f;
+      }
+      int lb[2][3], ub[2][3];  // #D < v, #D <= v
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int a = 0; a < 3; a++) lb[u][a] = ub[u][a] = 0;
+      for (int h = Pm >> 1; h > 0; h >>= 1) {
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+#pragma unroll
+          for (int a = 0; a < 3; a++) {
+            lb[u][a] = D[a][lb[u][a] + h - 1] < v[u][a] ? lb[u][a] + h : lb[u][a];
+            ub[u][a] = D[a][ub[u][a] + h - 1] <= v[u][a] ? ub[u][a] + h : ub[u][a];
+          }
+      }
+#pragma unroll
+      for (int u = 0; u < 2; u++)
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+          // Pm - 1 probes cover [0, Pm): the last comparison finishes the count
+          const int l = D[a][lb[u][a]] < v[u][a] ? lb[u][a] + 1 : lb[u][a];
+          const int h = D[a][ub[u][a]] <= v[u][a] ? ub[u][a] + 1 : ub[u][a];
+          int* Ha = H + a * (Pm + 1);
+          // bin 0 (below every frame value) is the hot one: counted per wave; bins >= m
+          // lie past every frame value and are never read
+          const int c0 = popc64(ballot(in[u] && h == 0)) + (popc64(ballot(in[u] && l == 0)) << 16);
+          if (lane == 0 && c0) atomicAdd(&Ha[0], c0);
+          if (!in[u]) continue;
+          if (l == h) {
+            if (l > 0 && l < m) atomicAdd(&Ha[l], 0x10001);
+          } else {
+            if (h > 0 && h < m) atomicAdd(&Ha[h], 1);
+            if (l > 0 && l < m) atomicAdd(&Ha[l], 0x10000);
+          }
+        }
+    }
+    __syncthreads();
+    // inclusive prefix sums of the 3 histograms over [0, m): one wave per axis
+    if (t < 192) {
+      int* Ha = H + (t >> 6) * (Pm + 1);
+      int carry = 0;
+      for (int c0 = 0; c0 < m; c0 += 64) {
+        const int j = c0 + lane;
+        int v = j < m ? Ha[j] : 0;
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(v, o, 64);
+          if (lane >= o) v += u;
+        }
+        if (j < m) Ha[j] = v + carry;
+        carry += __shfl(v, 63, 64);
+      }
+    }
+    __syncthreads();
+    for (int j = t; j < m; j += NPT) {
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        const int v = H[a * (Pm + 1) + j];
+        const int rl = v & 0xffff, rle = v >> 16;
+        const int lo = (rl + step - 1) / step, hi = (rle + step - 1) / step;
+        c9[3 * a] += lo;
+        c9[3 * a + 2] += hi - lo;
+        c9[3 * a + 1] += nsamp - hi;
+      }
+    }
+    goto sums;
+  }
   // rank counts against x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-830)
-  int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int i = t; i < mt; i += NPT) {
     float x[3];
     if (i == t) {
@@ -296,6 +448,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
     }
 #pragma unroll
     for (int a = 0; a < 3; a++) {
+      if (x[a] != x[a]) continue;  // NaN: none of >, <, == holds against any sample
       const int lo = bl[a] + (S[a][bl[a] * step] < x[a] ? 1 : 0);   // #samples < x
       const int hi = bu[a] + (S[a][bu[a] * step] <= x[a] ? 1 : 0);  // #samples <= x
       c9[3 * a] += lo;
@@ -304,6 +457,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
     }
   }
   NP_STAMP(4);
+sums:
   // block sums: wave sums, then one LDS atomic per wave and counter
 #pragma unroll
   for (int k = 0; k < 9; k++) {
@@ -982,7 +1136,8 @@ int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, co
   if (npairs <= 0) return EAO_OK;
   int P = 256;  // k_np_pairs sorts whole 256-element runs
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), sizeof(float) * 3 * P, s, d_fp, d_fv, d_foff,
+  // + 64 B: the rank path's 3 (Pm + 1) bin counters behind its 3 Pm frame values, Pm <= P / 2
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), sizeof(float) * 3 * P + 64, s, d_fp, d_fv, d_foff,
                      d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;

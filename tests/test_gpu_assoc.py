@@ -50,6 +50,44 @@ def test_np_pairs():
             assert np.allclose([g["r1"], g["r2"]], [o["r1"], o["r2"]], rtol=1e-5, atol=1e-5)
 
 
+def test_np_pairs_rank_path():
+    """Large objects against small detections take the rank path of k_np_pairs (the m
+    frame values sorted, the object streamed through binary searches): the counts must
+    equal the sorted-sample search's, with ties (quantised clouds), +-inf coordinates,
+    invalid points and NaN (which falls back to the sort path)."""
+    rng = np.random.default_rng(0x4e50)
+    fs, os_, exp = [], [], []
+    cases = [(30, 8000, None), (100, 5000, 0.05), (250, 600, None), (64, 2048, 0.01), (300, 7000, 0.002),
+             (21, 4000, None), (500, 8192, 0.02), (200, 3000, 0.5), (200, 1200, None), (40, 3000, None),
+             (40, 3000, None)]
+    for k, (m, n, q) in enumerate(cases):
+        f = _cloud(rng, m, [1, 2, 3], 0.1, quant=q)
+        o = _cloud(rng, n, [1, 2, 3] if k % 2 else [1.02, 2, 3.05], 0.1, quant=q)
+        if k == 2:
+            o[:5, 0] = np.inf
+            o[5:9, 1] = -np.inf
+            f[:2, 2] = np.inf
+        if k == 3:
+            f[:10] = o[:10]  # frame values equal to object values
+        fv = (rng.random(m) > 0.05).astype(np.uint8)
+        ov = (rng.random(n) > (0.85 if k == 8 else 0.05)).astype(np.uint8)  # k 8: few valid object points
+        if k == 9:
+            o[7, 1] = np.nan  # a NaN object value: the sort path
+        if k == 10:
+            f[3, 0] = np.nan  # a NaN frame value: the sort path after the frame pass
+        fs.append((f, fv))
+        os_.append((o, ov))
+        exp.append(orc.np_test(f, fv, o, ov))
+    got = ea.Assoc().np_batch(fs, os_)
+    for k, (g, o) in enumerate(zip(got, exp)):
+        info = (k, {x: g[x] for x in ("verdict", "m", "n", "cnt_gt", "cnt_lt", "cnt_eq")},
+                {x: o[x] for x in ("verdict", "m", "n", "cnt_gt", "cnt_lt", "cnt_eq")})
+        assert g["verdict"] == o["verdict"] and g["m"] == o["m"] and g["n"] == o["n"], info
+        assert np.array_equal(g["cnt_gt"], o["cnt_gt"]) and np.array_equal(g["cnt_lt"], o["cnt_lt"]), info
+        assert np.array_equal(g["cnt_eq"], o["cnt_eq"]), info
+        assert np.allclose(g["w"], o["w"], rtol=1e-5, atol=1e-5), info
+
+
 def test_iforest_scores():
     rng = np.random.default_rng(31)
     clouds = []

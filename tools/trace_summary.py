@@ -11,7 +11,7 @@ c = sqlite3.connect(sys.argv[1])
 rows = c.execute("select name, start, end, stream_id, grid_y from kernels order by start").fetchall()
 d = collections.defaultdict(list)
 for n, s, e, st, gy in rows:
-    d[n.split('(')[0]].append(e - s)
+    d[n.split('(')[0] + ("@%d" % st if "--by-stream" in sys.argv else "")].append(e - s)
 print("%d dispatches, span %.1f ms" % (len(rows), (rows[-1][2] - rows[0][1]) / 1e6 if rows else 0))
 for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
     v = np.array(v)
