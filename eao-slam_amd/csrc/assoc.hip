@@ -158,6 +158,9 @@ __device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
 // latency chain (global reads, the sort's barrier phases, the searches) is what
 // costs, so a pair gets a whole CU's worth of waves
 constexpr int NPT = 1024;
+// LDS behind the sort arrays for the rank path: the frame values and 16 counter copies
+// at Pm = 256 (52.5 KB), or 3 Pm values + 3 (Pm + 1) counters, Pm <= P / 4 (6 P bytes)
+constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * (NPT / 64) * 3 * 257 + 64;
 __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
@@ -200,6 +203,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
     f0[2] = F[3 * t + 2];
   }
   if (t < 9) red[t] = 0;
+  if (t == 9) red[9 * 16 - 1] = 0;
   if (t < 4) wpos[t] = 0;
   __syncthreads();
   float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
@@ -208,36 +212,39 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   // LDS atomic for its base) and the counts m, nvalid, nt
   int mc = fv0 ? 1 : 0, ntk = 0;
   for (int i = t + NPT; i < mt; i += NPT) mc += FV[i] ? 1 : 0;
-  // the rank path below is expected (frame side in a smaller power-of-two class): the
-  // pass only counts, the sort path reloads the object if it is taken after all
-  int Pmt = 256, Pnt = 256;
-  while (Pmt < mt) Pmt <<= 1;
-  while (Pnt < min(ntot, NP_MAXN)) Pnt <<= 1;
-  const bool count_only = 2 * Pmt <= Pmax && Pmt < Pnt;
-  for (int i0 = 0; i0 < ntot; i0 += NPT) {
-    const int i = i0 + t;
-    const bool in = i < ntot;
-    float x = 0.f, y = 0.f, z = 0.f;
-    bool kp = false, keep = false;
-    if (in) {
-      x = O[3 * i];
-      y = O[3 * i + 1];
-      z = O[3 * i + 2];
-      kp = kept(i);
-      keep = kp && OV[i];
+  // four chunks' loads in flight before their (LDS-atomic ordered) placement
+  for (int i00 = 0; i00 < ntot; i00 += 4 * NPT) {
+    float x[4], y[4], z[4];
+    bool kp[4], keep[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i00 + u * NPT + t;
+      x[u] = y[u] = z[u] = 0.f;
+      kp[u] = keep[u] = false;
+      if (i < ntot) {
+        x[u] = O[3 * i];
+        y[u] = O[3 * i + 1];
+        z[u] = O[3 * i + 2];
+        kp[u] = kept(i);
+        keep[u] = kp[u] && OV[i];
+      }
     }
-    ntk += kp ? 1 : 0;
-    if (keep && (x != x || y != y || z != z)) wpos[3] = 1;  // NaN: only the sort path orders it
-    const uint64_t mk = ballot(keep);
-    int base = 0;
-    if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
-    base = __shfl(base, 0, 64);
-    if (keep && !count_only) {
-      const int d = base + popc64(mk & lanes_below());
-      if (d < Pmax) {
-        S[0][d] = x;
-        S[1][d] = y;
-        S[2][d] = z;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (i00 + u * NPT >= ntot) break;
+      ntk += kp[u] ? 1 : 0;
+      if (keep[u] && (x[u] != x[u] || y[u] != y[u] || z[u] != z[u])) wpos[3] = 1;  // NaN: the sort path
+      const uint64_t mk = ballot(keep[u]);
+      int base = 0;
+      if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+      base = __shfl(base, 0, 64);
+      if (keep[u]) {
+        const int d = base + popc64(mk & lanes_below());
+        if (d < Pmax) {
+          S[0][d] = x[u];
+          S[1][d] = y[u];
+          S[2][d] = z[u];
+        }
       }
     }
   }
@@ -273,20 +280,20 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   // rank path (the frame side is the smaller): the sample counts of a frame value x need
   // only r<(x) = #{object values < x} and r<=(x): #{samples < x} = ceil(r< / step)
   // (sorted[k step] < x iff k step < r<). The m frame values are sorted instead of the
-  // object, and the object is streamed through binary searches into per-bin counts (low
-  // 16 bits: <, high 16 bits: <=; totals <= NP_MAXN) that are prefix-summed: the integer
-  // counts of the sorted-sample search, NaN excepted (NaN takes the sort path)
-  bool rank = count_only && !wpos[3] && 2 * Pm <= Pmax && Pm < P;
-  if (count_only && !rank) wpos[3] = 2;  // the object is reloaded into S below
-  float* D[3] = {dsm, dsm + Pm, dsm + 2 * Pm};
-  int* H = (int*)(dsm + 3 * Pm);  // [3][Pm + 1]
-  if (count_only) {
-    __syncthreads();  // every thread has read wpos
-  }
+  // object, and the object values (compacted in S above) go through binary searches into
+  // per-bin counts (low 16 bits: <, high 16 bits: <=; totals <= NP_MAXN) that are
+  // prefix-summed: the integer counts of the sorted-sample search, NaN excepted (NaN
+  // takes the sort path). D and the counters live behind S (NP_LDS_EXTRA): with <= 256
+  // frame values the object values crowd few bins, so each wave counts into its own copy
+  const int NH = Pm == 256 ? NPT / 64 : 1, HS = 3 * (Pm + 1);
+  // (below 2048 object values the object's own sort is the cheaper one, np_probe.py)
+  bool rank = !wpos[3] && P >= 2048 && Pm < P && (Pm == 256 || 24 * Pm + 12 <= 6 * Pmax);
+  float* D[3] = {dsm + 3 * Pmax, dsm + 3 * Pmax + Pm, dsm + 3 * Pmax + 2 * Pm};
+  int* H = (int*)(dsm + 3 * Pmax + 3 * Pm);  // [NH][3][Pm + 1]
   if (rank) {
-    if (t == 0) wpos[0] = 0;
-    for (int i = t; i < 3 * (Pm + 1); i += NPT) H[i] = 0;
-    __syncthreads();
+    __syncthreads();  // every thread has read wpos
+    if (t == 0) wpos[3] = 0;
+    for (int i = t; i < NH * HS; i += NPT) H[i] = 0;
     bool dnan = false;
     for (int i0 = 0; i0 < mt; i0 += NPT) {
       const int i = i0 + t;
@@ -300,7 +307,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
       }
       const uint64_t mk = ballot(keep);
       int base = 0;
-      if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
+      if (lane == 0 && mk) base = atomicAdd(&wpos[3], popc64(mk));
       base = __shfl(base, 0, 64);
       if (keep) {
         const int d = base + popc64(mk & lanes_below());
@@ -310,30 +317,9 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
       }
     }
     for (int i = m + t; i < Pm; i += NPT) D[0][i] = D[1][i] = D[2][i] = INFINITY;
-    if (dnan) wpos[3] = 1;
+    if (dnan) red[9 * 16 - 1] = 1;  // (red is zeroed below the 9 sums: slot 143 is free)
     __syncthreads();
-  }
-  if (count_only) {
-    if (wpos[3]) {  // the sort path after all (a NaN, or the sizes): the object reloaded
-      rank = false;
-      __syncthreads();
-      if (t == 0) wpos[0] = 0;
-      __syncthreads();
-      for (int i0 = 0; i0 < ntot; i0 += NPT) {
-        const int i = i0 + t;
-        const bool keep = i < ntot && kept(i) && OV[i];
-        const uint64_t mk = ballot(keep);
-        int base = 0;
-        if (lane == 0 && mk) base = atomicAdd(&wpos[0], popc64(mk));
-        base = __shfl(base, 0, 64);
-        if (keep) {
-          const int d = base + popc64(mk & lanes_below());
-          S[0][d] = O[3 * i];
-          S[1][d] = O[3 * i + 1];
-          S[2][d] = O[3 * i + 2];
-        }
-      }
-    }
+    if (red[9 * 16 - 1]) rank = false;  // a NaN frame value: the sort path (S is intact)
   }
   if (!rank)
     for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
@@ -342,41 +328,41 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   block_sort3_fast(rank ? D[0] : S[0], rank ? D[1] : S[1], rank ? D[2] : S[2], rank ? Pm : P);
   NP_STAMP(3);
   if (rank) {
-    // two object points per thread in flight: 12 independent search chains
-    for (int i0 = t; i0 < ntot; i0 += 2 * NPT) {
+    // the compacted object values from LDS, two per thread in flight: 12 search chains
+    for (int i0 = t; i0 < nvalid; i0 += 2 * NPT) {
       bool in[2];
       float v[2][3];
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int i = i0 + u * NPT;
-        in[u] = i < ntot && kept(i) && OV[i];
+        in[u] = i < nvalid;
 #pragma unroll
-        for (int a = 0; a < 3; a++) v[u][a] = in[u] ? O[3 * i + a] : 0.f;
+        for (int a = 0; a < 3; a++) v[u][a] = in[u] ? S[a][i] : 0.f;
       }
-      int lb[2][3], ub[2][3];  // #D < v, #D <= v
+      int lb[2][3];  // #D < v (the search is LDS-bandwidth bound: one per value and axis)
 #pragma unroll
       for (int u = 0; u < 2; u++)
 #pragma unroll
-        for (int a = 0; a < 3; a++) lb[u][a] = ub[u][a] = 0;
+        for (int a = 0; a < 3; a++) lb[u][a] = 0;
       for (int h = Pm >> 1; h > 0; h >>= 1) {
 #pragma unroll
         for (int u = 0; u < 2; u++)
 #pragma unroll
-          for (int a = 0; a < 3; a++) {
-            lb[u][a] = D[a][lb[u][a] + h - 1] < v[u][a] ? lb[u][a] + h : lb[u][a];
-            ub[u][a] = D[a][ub[u][a] + h - 1] <= v[u][a] ? ub[u][a] + h : ub[u][a];
-          }
+          for (int a = 0; a < 3; a++) lb[u][a] = D[a][lb[u][a] + h - 1] < v[u][a] ? lb[u][a] + h : lb[u][a];
       }
 #pragma unroll
       for (int u = 0; u < 2; u++)
 #pragma unroll
         for (int a = 0; a < 3; a++) {
-          // Pm - 1 probes cover [0, Pm): the last comparison finishes the count
-          const int l = D[a][lb[u][a]] < v[u][a] ? lb[u][a] + 1 : lb[u][a];
-          const int h = D[a][ub[u][a]] <= v[u][a] ? ub[u][a] + 1 : ub[u][a];
-          int* Ha = H + a * (Pm + 1);
-          // bin 0 (below every frame value) is the hot one: counted per wave; bins >= m
-          // lie past every frame value and are never read
+          // Pm - 1 probes cover [0, Pm): the last comparison finishes the count; #D <= v
+          // steps over the frame values equal to v (none, without ties)
+          const float dl = D[a][lb[u][a]];
+          const int l = dl < v[u][a] ? lb[u][a] + 1 : lb[u][a];
+          int h = l;
+          while (h < Pm && D[a][h] == v[u][a]) h++;
+          int* Ha = H + ((t >> 6) % NH) * HS + a * (Pm + 1);
+          // bin 0 (below every frame value) counted per wave; bins >= m lie past every
+          // frame value and are never read
           const int c0 = popc64(ballot(in[u] && h == 0)) + (popc64(ballot(in[u] && l == 0)) << 16);
           if (lane == 0 && c0) atomicAdd(&Ha[0], c0);
           if (!in[u]) continue;
@@ -389,6 +375,14 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
         }
     }
     __syncthreads();
+    if (NH > 1) {  // fold the private copies into copy 0
+      for (int i = t; i < HS; i += NPT) {
+        int v = H[i];
+        for (int k = 1; k < NH; k++) v += H[k * HS + i];
+        H[i] = v;
+      }
+      __syncthreads();
+    }
     // inclusive prefix sums of the 3 histograms over [0, m): one wave per axis
     if (t < 192) {
       int* Ha = H + (t >> 6) * (Pm + 1);
@@ -416,6 +410,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
         c9[3 * a + 1] += nsamp - hi;
       }
     }
+    NP_STAMP(4);
     goto sums;
   }
   // rank counts against x_pt_map_sample = sorted[0], sorted[step], ... (Object.cc:780-830)
@@ -1136,8 +1131,9 @@ int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, co
   if (npairs <= 0) return EAO_OK;
   int P = 256;  // k_np_pairs sorts whole 256-element runs
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
-  // + 64 B: the rank path's 3 (Pm + 1) bin counters behind its 3 Pm frame values, Pm <= P / 2
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), sizeof(float) * 3 * P + 64, s, d_fp, d_fv, d_foff,
+  // the object's sort arrays, then the rank path's frame values and counters (NP_LDS_EXTRA)
+  const size_t lds = sizeof(float) * 3 * P + std::max((size_t)6 * P + 64, NP_LDS_EXTRA);
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), lds, s, d_fp, d_fv, d_foff,
                      d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;

@@ -12,7 +12,8 @@ import eao_accel as ea  # noqa: E402
 
 a = ea.Assoc()
 rng = np.random.default_rng(0)
-for m, n in ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500)):
+for m, n in ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500), (30, 8000), (100, 5000), (300, 7000),
+             (60, 2000)):
     pairs = []
     for _ in range(4):
         f = rng.normal(0, 0.1, (m, 3)).astype(np.float32)
@@ -27,5 +28,5 @@ for m, n in ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500)):
     st = np.zeros(24, np.uint64)
     ea.lib().eao_debug_iforest_stamps(ea.P(st))
     ph = np.diff(st[:6].astype(np.int64))  # EAO_NP_PROF builds (make -C eao-slam_amd prof)
-    print("m=%4d n=%5d 4 pairs: %.1f us/call | cycles count %d compact %d sort %d bounds %d sums %d"
+    print("m=%4d n=%5d 4 pairs: %.1f us/call | cycles count %d frame/pad %d sort %d counts %d sums %d"
           % ((m, n, (time.perf_counter() - t0) / 20 * 1e6) + tuple(int(v) for v in ph)), flush=True)
