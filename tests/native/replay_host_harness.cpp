@@ -2,6 +2,7 @@
 // (eao-slam_amd/csrc/replay.cpp): the three GPU primitives are served by the
 // oracle so the decision logic can be debugged without a device. Test
 // infrastructure only -- never part of the product.
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -69,6 +70,10 @@ int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const flo
   return 0;
 }
 bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }
+int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t) {
+  std::memcpy(dst, src, bytes);  // host "device" memory
+  return EAO_OK;
+}
 AssocEngine::~AssocEngine() {}
 }  // namespace eao
 
