@@ -158,9 +158,10 @@ __device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
 // latency chain (global reads, the sort's barrier phases, the searches) is what
 // costs, so a pair gets a whole CU's worth of waves
 constexpr int NPT = 1024;
-// LDS behind the sort arrays for the rank path: the frame values and 16 counter copies
-// at Pm = 256 (52.5 KB), or 3 Pm values + 3 (Pm + 1) counters, Pm <= P / 4 (6 P bytes)
-constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * (NPT / 64) * 3 * 257 + 64;
+// LDS behind the sort arrays for the rank path (launches with P >= 2048 only): 3 Pm frame
+// values and 3 (Pm + 1) counters, four copies at Pm = 256 (15.4 KB), one at Pm = 512
+constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * 4 * 3 * 257 + 64;
+static_assert(sizeof(float) * 3 * 512 + sizeof(int) * 3 * 513 <= NP_LDS_EXTRA, "rank-path LDS");
 __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
@@ -284,10 +285,11 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   // per-bin counts (low 16 bits: <, high 16 bits: <=; totals <= NP_MAXN) that are
   // prefix-summed: the integer counts of the sorted-sample search, NaN excepted (NaN
   // takes the sort path). D and the counters live behind S (NP_LDS_EXTRA): with <= 256
-  // frame values the object values crowd few bins, so each wave counts into its own copy
-  const int NH = Pm == 256 ? NPT / 64 : 1, HS = 3 * (Pm + 1);
-  // (below 2048 object values the object's own sort is the cheaper one, np_probe.py)
-  bool rank = !wpos[3] && P >= 2048 && Pm < P && (Pm == 256 || 24 * Pm + 12 <= 6 * Pmax);
+  // frame values the object values crowd few bins, so the waves count into four copies
+  const int NH = Pm == 256 ? 4 : 1, HS = 3 * (Pm + 1);
+  // (below 2048 object values the object's own sort is the cheaper one, np_probe.py;
+  // up to 512 frame values the counters fit NP_LDS_EXTRA)
+  bool rank = !wpos[3] && P >= 2048 && Pmax >= 2048 && Pm < P && Pm <= 512;
   float* D[3] = {dsm + 3 * Pmax, dsm + 3 * Pmax + Pm, dsm + 3 * Pmax + 2 * Pm};
   int* H = (int*)(dsm + 3 * Pmax + 3 * Pm);  // [NH][3][Pm + 1]
   if (rank) {
@@ -1132,7 +1134,7 @@ int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, co
   int P = 256;  // k_np_pairs sorts whole 256-element runs
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
   // the object's sort arrays, then the rank path's frame values and counters (NP_LDS_EXTRA)
-  const size_t lds = sizeof(float) * 3 * P + std::max((size_t)6 * P + 64, NP_LDS_EXTRA);
+  const size_t lds = sizeof(float) * 3 * P + (P >= 2048 ? NP_LDS_EXTRA : 64);
   hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), lds, s, d_fp, d_fv, d_foff,
                      d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
