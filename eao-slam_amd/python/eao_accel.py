@@ -293,6 +293,45 @@ class Matcher:
             v(stream) if stream else None), "eao_match_init_batch_device")
 
 
+class Pose:
+    """Optimizer::PoseOptimization replacement (reference src/Optimizer.cc:243-457), monocular edges."""
+
+    def __init__(self, max_kps=4096, max_batch=1, device=0):
+        self.h = ctypes.c_void_p()
+        check(lib().eao_pose_create(device, max_kps, max_batch, ctypes.byref(self.h)), "eao_pose_create")
+
+    def close(self):
+        if self.h:
+            lib().eao_pose_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def optimize(self, cam, Tcw, kps_un, has_mp, mp_pos, inv_level_sigma2, outlier=None):
+        """-> (n_inliers, Tcw_out [4][4] float32, outlier u8[n])."""
+        n = len(kps_un)
+        T = np.ascontiguousarray(Tcw, np.float32)
+        To = np.zeros((4, 4), np.float32)
+        out = np.zeros(n, np.uint8) if outlier is None else np.array(outlier, np.uint8)
+        inv = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        ni = ctypes.c_int32()
+        check(lib().eao_pose_optimization(self.h, ctypes.byref(cam), P(T), n, P(np.ascontiguousarray(kps_un)),
+                                          P(np.ascontiguousarray(has_mp, np.uint8)),
+                                          P(np.ascontiguousarray(mp_pos, np.float32)), P(inv), len(inv), P(To),
+                                          P(out), ctypes.byref(ni)), "eao_pose_optimization")
+        return ni.value, To, out
+
+    def optimize_batch_device(self, cam, nframes, cap, d_T, d_counts, d_kps, d_has, d_pos, inv_level_sigma2,
+                              d_Tout, d_outlier, d_ninl, stream=None):
+        """HBM-resident batch; d_* are device pointers (ints)."""
+        inv = np.ascontiguousarray(inv_level_sigma2, np.float32)
+        v = ctypes.c_void_p
+        check(lib().eao_pose_optimization_batch_device(self.h, ctypes.byref(cam), nframes, cap, v(d_T), v(d_counts),
+                                                       v(d_kps), v(d_has), v(d_pos), P(inv), len(inv), v(d_Tout),
+                                                       v(d_outlier), v(d_ninl), v(stream) if stream else None),
+              "eao_pose_optimization_batch_device")
+
+
 class Lines:
     """Per-frame line detection (line_lbd_detect::detect_raw_lines + filter_lines,
     reference src/Frame.cc:324-328) on the GPU."""

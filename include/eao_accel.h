@@ -366,6 +366,31 @@ int eao_gt_lookup(const double* gt, int m, const double* ts, int n, int32_t* idx
 int eao_undistort_zero(const float* dist, int ndist, const uint8_t* src, int w, int h, int spitch, uint8_t* dst,
                        int dpitch, void* stream);
 
+/* --- pose-only optimisation: replaces Optimizer::PoseOptimization (src/Optimizer.cc:243-457),
+   monocular edges (mvuRight < 0), called at src/Tracking.cc:1106,1699,1741 --- */
+typedef struct eao_pose eao_pose;
+int eao_pose_create(int device, int max_kps, int max_batch, eao_pose** out);
+int eao_pose_destroy(eao_pose* p);
+/* one frame, host buffers: Tcw_in = pFrame->mTcw (4x4 row-major float); kps_un = mvKeysUn;
+   has_mp[i] = mvpMapPoints[i] != NULL; mp_pos[3i..] = its GetWorldPos(); inv_level_sigma2 =
+   mvInvLevelSigma2 (nlevels <= 32). Writes Tcw_out (SetPose), outlier[i] (mvbOutlier) where
+   has_mp[i], and *n_inliers = the function's return value (0 with Tcw_out = Tcw_in when fewer
+   than 3 correspondences, Optimizer.cc:370-371). */
+int eao_pose_optimization(eao_pose* p, const eao_camera* cam, const float* Tcw_in, int n,
+                          const eao_keypoint* kps_un, const uint8_t* has_mp, const float* mp_pos,
+                          const float* inv_level_sigma2, int nlevels, float* Tcw_out, uint8_t* outlier,
+                          int32_t* n_inliers);
+/* batched, HBM-resident: frame f reads d_Tcw_in[f][16], d_counts[f] keypoints of
+   d_kps_un / d_has_mp / d_mp_pos ([nframes][cap], positions [nframes][cap][3]) and writes
+   d_Tcw_out[f][16], d_outlier[f][cap] (has_mp entries), d_n_inliers[f]; asynchronous on
+   `stream` (the handle's stream when NULL). cap <= 8192. */
+int eao_pose_optimization_batch_device(eao_pose* p, const eao_camera* cam, int nframes, int cap,
+                                       const float* d_Tcw_in, const int32_t* d_counts,
+                                       const eao_keypoint* d_kps_un, const uint8_t* d_has_mp,
+                                       const float* d_mp_pos, const float* inv_level_sigma2, int nlevels,
+                                       float* d_Tcw_out, uint8_t* d_outlier, int32_t* d_n_inliers,
+                                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

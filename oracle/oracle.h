@@ -178,6 +178,14 @@ int orc_edge_chains(const uint8_t* gray, int w, int h, uint32_t* xy, int cap_px,
                     int* n_px, int* n_edges);
 int orc_edlines(const uint8_t* gray, int w, int h, float min_length, float* out, int cap, int* n_out);
 
+/* ---- Optimizer::PoseOptimization, monocular edges (src/Optimizer.cc:243-457) ----
+   Tcw 4x4 row-major float (pFrame->mTcw); kps = mvKeysUn; has_mp[i] = mvpMapPoints[i] != 0;
+   mp_pos = GetWorldPos(); outlier[i] (mvbOutlier) written where has_mp[i]. */
+int orc_pose_optimization(const orc_camera* cam, const float* Tcw_in, int n,
+                          const orc_keypoint* kps, const uint8_t* has_mp, const float* mp_pos,
+                          const float* inv_level_sigma2, float* Tcw_out, uint8_t* outlier,
+                          int* n_inliers);
+
 #ifdef __cplusplus
 }
 #endif

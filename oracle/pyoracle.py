@@ -356,3 +356,18 @@ def edlines(gray, min_length=50.0, cap=4096):
     rc = lib().orc_edlines(P(g8), w, h, ctypes.c_float(min_length), P(out), cap, ctypes.byref(n))
     assert rc == 0, rc
     return out[:n.value].copy()
+
+
+def pose_optimization(c, Tcw, kps_un, has_mp, mp_pos, inv_level_sigma2):
+    """Optimizer::PoseOptimization (monocular): -> (n_inliers, Tcw_out [4][4], outlier u8[n])."""
+    n = len(kps_un)
+    To = np.zeros((4, 4), np.float32)
+    out = np.zeros(n, np.uint8)
+    ni = ctypes.c_int()
+    rc = lib().orc_pose_optimization(ctypes.byref(c), P(np.ascontiguousarray(Tcw, np.float32)), n,
+                                     P(np.ascontiguousarray(kps_un)), P(np.ascontiguousarray(has_mp, np.uint8)),
+                                     P(np.ascontiguousarray(mp_pos, np.float32)),
+                                     P(np.ascontiguousarray(inv_level_sigma2, np.float32)), P(To), P(out),
+                                     ctypes.byref(ni))
+    assert rc == 0
+    return ni.value, To, out

@@ -558,3 +558,50 @@ def line_frames(n, w=640, h=480, seed=0xEA7, n_quads=(6, 12)):
             img[m] = rng.uniform(20, 235) + rng.normal(0, 1.5, int(m.sum()))
         out[f] = np.clip(np.rint(img), 0, 255).astype(np.uint8)
     return out
+
+
+def rodrigues(w):
+    """rotation matrix of the axis-angle vector w (float64)."""
+    th = float(np.linalg.norm(w))
+    if th < 1e-12:
+        return np.eye(3)
+    k = np.asarray(w, np.float64) / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * (K @ K)
+
+
+def pose_problem(seed, n=1000, frac_mp=0.7, frac_out=0.1, noise_px=1.0, rot_err=0.02, t_err=0.05,
+                 K=TUM3_K, w=640, h=480, nlevels=8, scale=1.2):
+    """A PoseOptimization input like TrackWithMotionModel's: n keypoints (mvKeysUn) of which
+    frac_mp hold a map point seen at the true pose (level-scaled pixel noise, frac_out gross
+    outliers), and the motion-model prior Tcw = true pose perturbed. Returns
+    (Tcw_prior [4][4] f32, kps structured (x, y, size, angle, response, octave, class_id),
+    has_mp u8[n], mp_pos f32[n][3], inv_level_sigma2 f32[nlevels], Tcw_true)."""
+    fx, fy, cx, cy = K
+    rng = np.random.default_rng(seed)
+    Rt = rodrigues(rng.normal(0, 0.3, 3))
+    tt = rng.normal(0, 0.5, 3)
+    oct_ = rng.integers(0, nlevels, n).astype(np.int32)
+    sc = scale ** oct_.astype(np.float64)
+    u = rng.uniform(0, w, n)
+    v = rng.uniform(0, h, n)
+    z = rng.uniform(0.8, 6.0, n)
+    Xc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    Xw = (Xc - tt) @ Rt  # R^T (Xc - t)
+    obs_u = u + rng.normal(0, noise_px, n) * sc
+    obs_v = v + rng.normal(0, noise_px, n) * sc
+    bad = rng.random(n) < frac_out
+    obs_u[bad] = rng.uniform(0, w, bad.sum())
+    obs_v[bad] = rng.uniform(0, h, bad.sum())
+    kps = np.zeros(n, dtype=[("x", "f4"), ("y", "f4"), ("size", "f4"), ("angle", "f4"), ("response", "f4"),
+                             ("octave", "i4"), ("class_id", "i4")])
+    kps["x"], kps["y"], kps["size"] = obs_u, obs_v, 31 * sc
+    kps["octave"], kps["class_id"] = oct_, -1
+    has = (rng.random(n) < frac_mp).astype(np.uint8)
+    Ttrue = np.eye(4)
+    Ttrue[:3, :3], Ttrue[:3, 3] = Rt, tt
+    Tp = np.eye(4)
+    Tp[:3, :3] = rodrigues(rng.normal(0, rot_err, 3)) @ Rt
+    Tp[:3, 3] = tt + rng.normal(0, t_err, 3)
+    inv = (1.0 / (scale ** (2 * np.arange(nlevels)))).astype(np.float32)
+    return Tp.astype(np.float32), kps, has, Xw.astype(np.float32), inv, Ttrue.astype(np.float32)
