@@ -355,6 +355,7 @@ def main():
     searches = search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc,
                            d_cnt, d_has, d_mpos, match_ms)
     lines_leg = line_leg(ea, torch, stream, min(F, RENDERED), gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
+    pose = pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
     n_kps = float(d_cnt.float().mean().item())
     ab = algorithmic_bytes(n_kps)
     dom = int(np.argmax(stage))
@@ -402,6 +403,7 @@ def main():
             "match_ms_per_step": match_ms,
             "searches": searches,
             "line_detect": lines_leg,
+            "pose_optimization": pose,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
                                   "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
@@ -470,6 +472,80 @@ def line_leg(ea, torch, stream, F, gpu, with_cpu=True, reps=3, distinct=48):
                     "gpu_over_cpu": (F / (np.mean(ms) * 1e-3)) / (1e3 / cpu_ms), "parity_frames": k,
                     "parity_bitexact": bool(ok)})
     L.close()
+    return res
+
+
+def pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=True, reps=3, distinct=64):
+    """Pose-only optimisation (Optimizer::PoseOptimization, Optimizer.cc:243-457; called per
+    frame at Tracking.cc:1106,1699,1741) beside the step: F frames of NFEAT keypoints, 70 %
+    holding a map point, 10 % gross outliers, a perturbed motion-model prior
+    (tools/synth.pose_problem, `distinct` problems cycled), HBM-resident and batched, timed with
+    HIP events; the single-frame host call (the tracker's pattern) timed for its latency; the
+    CPU restatement (oracle/pose_ref.cpp, one thread) timed on a sample and checked."""
+    from tools import synth
+    dev = torch.device("cuda", gpu)
+    probs = [synth.pose_problem(2000 + i, NFEAT) for i in range(min(F, distinct))]
+    idx = pingpong(F, len(probs))
+    T = np.stack([probs[i][0].reshape(16) for i in idx])
+    kp = np.zeros((F, cap), dtype=ea.KP_DTYPE)
+    has = np.zeros((F, cap), np.uint8)
+    pos = np.zeros((F, cap, 3), np.float32)
+    for f, i in enumerate(idx):
+        kp[f, :NFEAT], has[f, :NFEAT], pos[f, :NFEAT] = probs[i][1], probs[i][2], probs[i][3]
+    inv = probs[0][4]
+    cnt = torch.full((F,), NFEAT, dtype=torch.int32, device=dev)
+    d_T = torch.from_numpy(T).to(dev)
+    d_kp = torch.from_numpy(kp.view(np.uint8).reshape(F, cap, 28)).to(dev)
+    d_has, d_pos = torch.from_numpy(has).to(dev), torch.from_numpy(pos).to(dev)
+    d_To = torch.zeros((F, 16), dtype=torch.float32, device=dev)
+    d_out = torch.zeros((F, cap), dtype=torch.uint8, device=dev)
+    d_ni = torch.zeros(F, dtype=torch.int32, device=dev)
+    P = ea.Pose(max_kps=cap, max_batch=F, device=gpu)
+    sp = stream.cuda_stream
+    stream.wait_stream(torch.cuda.current_stream())
+
+    def run():
+        P.optimize_batch_device(ea.camera(), F, cap, d_T.data_ptr(), cnt.data_ptr(), d_kp.data_ptr(),
+                                d_has.data_ptr(), d_pos.data_ptr(), inv, d_To.data_ptr(), d_out.data_ptr(),
+                                d_ni.data_ptr(), sp)
+    run()
+    ms = []
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        run()
+        e1.record(stream)
+        e1.synchronize()
+        ms.append(e0.elapsed_time(e1))
+    Tp, k1, h1, X1, _, _ = probs[0]
+    P.optimize(ea.camera(), Tp, k1, h1, X1, inv)
+    t0 = time.perf_counter()
+    nlat = 20
+    for _ in range(nlat):
+        P.optimize(ea.camera(), Tp, k1, h1, X1, inv)
+    lat_ms = (time.perf_counter() - t0) * 1e3 / nlat
+    To, out, ni = d_To.cpu().numpy(), d_out.cpu().numpy(), d_ni.cpu().numpy()
+    res = {"frames": F, "keypoints": NFEAT, "edges_mean": float(has.sum(1).mean()), "ms_per_batch": float(np.mean(ms)),
+           "frames_per_s": F / (np.mean(ms) * 1e-3), "single_frame_latency_ms": lat_ms,
+           "kernel": "k_pose_opt (one workgroup per frame)",
+           "data": "tools/synth.pose_problem (%d problems cycled)" % len(probs)}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as orc  # checker / CPU baseline only
+        orc.use_native()
+        k = min(32, len(probs))
+        t0 = time.perf_counter()
+        ref = [orc.pose_optimization(orc.cam(), p[0], p[1], p[2], p[3], inv) for p in probs[:k]]
+        cpu_ms = (time.perf_counter() - t0) * 1e3 / k
+        ok = True
+        for f in range(k):
+            h = probs[f][2]
+            ok &= ref[f][0] == int(ni[f]) and np.array_equal(ref[f][2] * h, out[f, :NFEAT] * h)
+            ok &= float(np.abs(ref[f][1] - To[f].reshape(4, 4)).max()) < 1e-5
+        res.update({"cpu_ms_per_frame": cpu_ms, "cpu_kind": "port (oracle/pose_ref.cpp, 1 thread)",
+                    "gpu_over_cpu": (F / (np.mean(ms) * 1e-3)) / (1e3 / cpu_ms), "parity_frames": k,
+                    "parity": bool(ok), "parity_bar": "inliers and outlier flags identical, pose within 1e-5"})
+    P.close()
     return res
 
 
