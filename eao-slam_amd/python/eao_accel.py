@@ -332,6 +332,67 @@ class Pose:
               "eao_pose_optimization_batch_device")
 
 
+class Vocab:
+    """DBoW2 ORB vocabulary on the GPU: ComputeBoW's transform and SearchByBoW
+    (reference Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1139-1271, src/ORBmatcher.cc:159-288).
+    voc: dict with desc [n][32] u8, parent i32, word i32, weight f64, L (tools/synth.vocabulary)."""
+
+    def __init__(self, voc, max_kps=4096, max_batch=1, device=0):
+        self.h = ctypes.c_void_p()
+        self.max_kps = max_kps
+        a = {k: np.ascontiguousarray(voc[k]) for k in ("desc", "parent", "word", "weight")}
+        check(lib().eao_vocab_create(device, len(a["parent"]), P(a["desc"]), P(a["parent"]), P(a["word"]),
+                                     P(a["weight"]), int(voc["L"]), max_kps, max_batch, ctypes.byref(self.h)),
+              "eao_vocab_create")
+
+    def close(self):
+        if self.h and _lib is not None:
+            _lib.eao_vocab_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    __del__ = close
+
+    def transform(self, desc, levelsup=4):
+        """-> (word_ids, word_weights, node_ids, node_start, node_feats)."""
+        n = len(desc)
+        m = max(n, 1)
+        wid, ww = np.zeros(m, np.int32), np.zeros(m, np.float64)
+        nid, ns, nf = np.zeros(m, np.int32), np.zeros(m + 1, np.int32), np.zeros(m, np.int32)
+        nw, nn = ctypes.c_int32(), ctypes.c_int32()
+        check(lib().eao_bow_transform(self.h, n, P(np.ascontiguousarray(desc, np.uint8)), levelsup, P(wid), P(ww),
+                                      ctypes.byref(nw), P(nid), P(ns), P(nf), ctypes.byref(nn)), "eao_bow_transform")
+        k = nn.value
+        return wid[:nw.value].copy(), ww[:nw.value].copy(), nid[:k].copy(), ns[:k + 1].copy(), nf[:ns[k]].copy()
+
+    def search(self, nnratio, check_ori, kf_kps, kf_desc, kf_valid, kf_fv, f_kps, f_desc, f_fv):
+        """SearchByBoW: fv = (node_ids, node_start, node_feats) -> (nmatches, f_match)."""
+        m = np.full(len(f_kps), -1, np.int32)
+        a = [np.ascontiguousarray(x, np.int32) for x in kf_fv]
+        b = [np.ascontiguousarray(x, np.int32) for x in f_fv]
+        n = check(lib().eao_search_by_bow(self.h, ctypes.c_float(nnratio), int(check_ori), len(kf_kps),
+                                          P(np.ascontiguousarray(kf_kps)), P(np.ascontiguousarray(kf_desc, np.uint8)),
+                                          P(np.ascontiguousarray(kf_valid, np.uint8)), len(a[0]), P(a[0]), P(a[1]),
+                                          P(a[2]), len(f_kps), P(np.ascontiguousarray(f_kps)),
+                                          P(np.ascontiguousarray(f_desc, np.uint8)), len(b[0]), P(b[0]), P(b[1]),
+                                          P(b[2]), P(m)), "eao_search_by_bow")
+        return n, m
+
+    def transform_batch_device(self, nframes, cap, d_counts, d_desc, levelsup, d_wid, d_ww, d_nw, d_nid, d_ns, d_nf,
+                               d_nn, stream=None):
+        v = ctypes.c_void_p
+        check(lib().eao_bow_transform_batch_device(self.h, nframes, cap, v(d_counts), v(d_desc), levelsup, v(d_wid),
+                                                   v(d_ww), v(d_nw), v(d_nid), v(d_ns), v(d_nf), v(d_nn),
+                                                   v(stream) if stream else None), "eao_bow_transform_batch_device")
+
+    def search_batch_device(self, nnratio, check_ori, nsearch, cap, kf, fr, d_match, d_nm, stream=None):
+        """kf = (kps, desc, valid, nn, node_ids, node_start, node_feats) device pointers;
+        fr = (n_f, kps, desc, nn, node_ids, node_start, node_feats)."""
+        v = ctypes.c_void_p
+        check(lib().eao_search_by_bow_batch_device(self.h, ctypes.c_float(nnratio), int(check_ori), nsearch, cap,
+                                                   *[v(x) for x in kf], *[v(x) for x in fr], v(d_match), v(d_nm),
+                                                   v(stream) if stream else None), "eao_search_by_bow_batch_device")
+
+
 class Lines:
     """Per-frame line detection (line_lbd_detect::detect_raw_lines + filter_lines,
     reference src/Frame.cc:324-328) on the GPU."""

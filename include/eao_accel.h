@@ -391,6 +391,57 @@ int eao_pose_optimization_batch_device(eao_pose* p, const eao_camera* cam, int n
                                        float* d_Tcw_out, uint8_t* d_outlier, int32_t* d_n_inliers,
                                        void* stream);
 
+/* --- bag of words: Frame::ComputeBoW (src/Frame.cc:516-523 -> DBoW2
+   TemplatedVocabulary::transform(desc, BowVector, FeatureVector, 4), TemplatedVocabulary.h:1139-1271;
+   the ORB vocabulary's TF_IDF weighting + L1 norm) and ORBmatcher::SearchByBoW(KeyFrame*, Frame&,
+   vector<MapPoint*>&) (src/ORBmatcher.cc:159-288), called at src/Tracking.cc (TrackReferenceKeyFrame,
+   Relocalization) --- */
+typedef struct eao_vocab eao_vocab;
+/* the vocabulary as loadFromTextFile leaves it: node descriptors [n_nodes][32], parent[i] in
+   [0, i) (root 0: parent -1), word_id[i] (-1: inner node), weight[i] (idf; 0 = stopped), depth L.
+   n_nodes may be 0 (an empty vocabulary: transforms give empty vectors; searches still work).
+   max_kps <= 4096 features per frame, max_batch frames per batched call. */
+int eao_vocab_create(int device, int n_nodes, const uint8_t* node_desc, const int32_t* parent,
+                     const int32_t* word_id, const double* weight, int L, int max_kps, int max_batch,
+                     eao_vocab** out);
+int eao_vocab_destroy(eao_vocab* v);
+/* transform of one frame's n descriptors: BowVector as (word_ids ascending, word_weights) x
+   *n_words; FeatureVector as CSR: node_ids ascending x *n_nodes, node_start [*n_nodes + 1],
+   node_feats (feature indices, ascending within a node). Arrays hold >= n (+1) entries. */
+int eao_bow_transform(eao_vocab* v, int n, const uint8_t* desc, int levelsup, int32_t* word_ids,
+                      double* word_weights, int32_t* n_words, int32_t* node_ids, int32_t* node_start,
+                      int32_t* node_feats, int32_t* n_nodes);
+/* batched, HBM-resident: frame f reads d_counts[f] descriptors of d_desc [nframes][cap][32] and
+   writes [nframes][cap] word ids / weights / node ids / node features, node starts
+   [nframes][cap + 1] and the counts; asynchronous on `stream`. */
+int eao_bow_transform_batch_device(eao_vocab* v, int nframes, int cap, const int32_t* d_counts,
+                                   const uint8_t* d_desc, int levelsup, int32_t* d_word_ids,
+                                   double* d_word_weights, int32_t* d_n_words, int32_t* d_node_ids,
+                                   int32_t* d_node_start, int32_t* d_node_feats, int32_t* d_n_nodes,
+                                   void* stream);
+/* SearchByBoW(pKF, F, vpMapPointMatches): kf_mp_valid[i] = vpMapPointsKF[i] && !isBad(); the
+   FeatureVectors as eao_bow_transform returns them. f_match[iF] = the keyframe feature whose map
+   point F's feature iF matched (-1: none). Returns nmatches (>= 0) or an EAO_E_* error. */
+int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, const eao_keypoint* kf_kps,
+                      const uint8_t* kf_desc, const uint8_t* kf_mp_valid, int kf_nn,
+                      const int32_t* kf_node_ids, const int32_t* kf_node_start,
+                      const int32_t* kf_node_feats, int n_f, const eao_keypoint* f_kps,
+                      const uint8_t* f_desc, int f_nn, const int32_t* f_node_ids,
+                      const int32_t* f_node_start, const int32_t* f_node_feats, int32_t* f_match);
+/* batched, HBM-resident: search s pairs keyframe slot s with frame slot s ([nsearch][cap]
+   keypoints / descriptors / valid flags / node ids / node features, [nsearch][cap + 1] node starts,
+   per-search node counts d_kf_nn / d_f_nn and frame feature counts d_n_f); writes
+   d_f_match [nsearch][cap] and d_nmatches [nsearch]. */
+int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, int nsearch, int cap,
+                                   const eao_keypoint* d_kf_kps, const uint8_t* d_kf_desc,
+                                   const uint8_t* d_kf_mp_valid, const int32_t* d_kf_nn,
+                                   const int32_t* d_kf_node_ids, const int32_t* d_kf_node_start,
+                                   const int32_t* d_kf_node_feats, const int32_t* d_n_f,
+                                   const eao_keypoint* d_f_kps, const uint8_t* d_f_desc,
+                                   const int32_t* d_f_nn, const int32_t* d_f_node_ids,
+                                   const int32_t* d_f_node_start, const int32_t* d_f_node_feats,
+                                   int32_t* d_f_match, int32_t* d_nmatches, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

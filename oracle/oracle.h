@@ -186,6 +186,24 @@ int orc_pose_optimization(const orc_camera* cam, const float* Tcw_in, int n,
                           const float* inv_level_sigma2, float* Tcw_out, uint8_t* outlier,
                           int* n_inliers);
 
+/* ---- BoW (src/Frame.cc:516-523 -> DBoW2 TemplatedVocabulary::transform, TF_IDF + L1) and
+   ORBmatcher::SearchByBoW(KeyFrame*, Frame&) (src/ORBmatcher.cc:159-288). Vocabulary as arrays:
+   node descriptors [n][32], parent [n] (root 0: -1), word id [n] (-1: inner node), weight [n].
+   FeatureVector as CSR: node_ids ascending, node_start [nn + 1], node_feats. f_match[iF] = the
+   keyframe feature whose map point matched (-1 none). */
+void* orc_vocab_create(int n_nodes, const uint8_t* node_desc, const int32_t* parent,
+                       const int32_t* word_id, const double* weight, int L);
+void orc_vocab_destroy(void* v);
+int orc_bow_transform(void* voc, int n, const uint8_t* desc, int levelsup, int32_t* word_ids,
+                      double* word_weights, int* n_words, int32_t* node_ids, int32_t* node_start,
+                      int32_t* node_feats, int* n_fnodes);
+int orc_search_by_bow(float nnratio, int check_ori, int n_kf, const orc_keypoint* kf_kps,
+                      const uint8_t* kf_desc, const uint8_t* kf_mp_valid, int kf_nn,
+                      const int32_t* kf_node_ids, const int32_t* kf_node_start,
+                      const int32_t* kf_node_feats, int n_f, const orc_keypoint* f_kps,
+                      const uint8_t* f_desc, int f_nn, const int32_t* f_node_ids,
+                      const int32_t* f_node_start, const int32_t* f_node_feats, int32_t* f_match);
+
 #ifdef __cplusplus
 }
 #endif

@@ -371,3 +371,51 @@ def pose_optimization(c, Tcw, kps_un, has_mp, mp_pos, inv_level_sigma2):
                                      ctypes.byref(ni))
     assert rc == 0
     return ni.value, To, out
+
+
+class Vocab:
+    """orc_vocab_create over a tools/synth.vocabulary dict (arrays kept alive here)."""
+
+    def __init__(self, voc):
+        self.voc = {k: np.ascontiguousarray(voc[k]) for k in ("desc", "parent", "word", "weight")}
+        lib().orc_vocab_create.restype = ctypes.c_void_p
+        self.h = ctypes.c_void_p(lib().orc_vocab_create(len(self.voc["parent"]), P(self.voc["desc"]),
+                                                        P(self.voc["parent"]), P(self.voc["word"]),
+                                                        P(self.voc["weight"]), int(voc["L"])))
+
+    def __del__(self):
+        if self.h:
+            lib().orc_vocab_destroy(self.h)
+            self.h = None
+
+
+def bow_transform(voc, desc, levelsup=4):
+    """DBoW2 transform (TF_IDF + L1): -> (word_ids, word_weights, node_ids, node_start, node_feats).
+    voc: a Vocab (or a synth.vocabulary dict, wrapped per call)."""
+    if not isinstance(voc, Vocab):
+        voc = Vocab(voc)
+    n = len(desc)
+    wid = np.zeros(max(n, 1), np.int32)
+    ww = np.zeros(max(n, 1), np.float64)
+    nid = np.zeros(max(n, 1), np.int32)
+    ns = np.zeros(n + 2, np.int32)
+    nf = np.zeros(max(n, 1), np.int32)
+    nw, nn = ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_bow_transform(voc.h, n, P(np.ascontiguousarray(desc, np.uint8)),
+                                 levelsup, P(wid), P(ww), ctypes.byref(nw), P(nid), P(ns), P(nf),
+                                 ctypes.byref(nn))
+    assert rc == 0
+    k = nn.value
+    return wid[:nw.value].copy(), ww[:nw.value].copy(), nid[:k].copy(), ns[:k + 1].copy(), nf[:ns[k]].copy()
+
+
+def search_by_bow(nnratio, check_ori, kf_kps, kf_desc, kf_valid, kf_fv, f_kps, f_desc, f_fv):
+    """SearchByBoW(KF, F): fv = (node_ids, node_start, node_feats); -> (nmatches, f_match)."""
+    m = np.full(len(f_kps), -1, np.int32)
+    a = [np.ascontiguousarray(x, np.int32) for x in kf_fv]
+    b = [np.ascontiguousarray(x, np.int32) for x in f_fv]
+    n = lib().orc_search_by_bow(ctypes.c_float(nnratio), int(check_ori), len(kf_kps), P(np.ascontiguousarray(kf_kps)),
+                                P(np.ascontiguousarray(kf_desc, np.uint8)), P(np.ascontiguousarray(kf_valid, np.uint8)),
+                                len(a[0]), P(a[0]), P(a[1]), P(a[2]), len(f_kps), P(np.ascontiguousarray(f_kps)),
+                                P(np.ascontiguousarray(f_desc, np.uint8)), len(b[0]), P(b[0]), P(b[1]), P(b[2]), P(m))
+    return n, m

@@ -605,3 +605,79 @@ def pose_problem(seed, n=1000, frac_mp=0.7, frac_out=0.1, noise_px=1.0, rot_err=
     Tp[:3, 3] = tt + rng.normal(0, t_err, 3)
     inv = (1.0 / (scale ** (2 * np.arange(nlevels)))).astype(np.float32)
     return Tp.astype(np.float32), kps, has, Xw.astype(np.float32), inv, Ttrue.astype(np.float32)
+
+
+def _flip_bits(rows, nflip, rng):
+    """flip nflip random bit positions (drawn with replacement) of each 32-byte row, in place."""
+    m = len(rows)
+    pos = rng.integers(0, 256, (m, nflip))
+    r = np.repeat(np.arange(m), nflip)
+    np.bitwise_xor.at(rows, (r, (pos >> 3).ravel()), (1 << (pos & 7)).astype(np.uint8).ravel())
+    return rows
+
+
+def vocabulary(K=10, L=4, seed=0xB0, stop_frac=0.02, flips=(48, 24, 12, 6, 4, 3)):
+    """A synthetic DBoW2 ORB vocabulary (the reference's Vocabulary/ORBvoc.bin is a missing
+    blob): a complete K-ary tree of depth L with node ids in breadth-first order (as
+    loadFromTextFile numbers a saveToTextFile vocabulary), child descriptors = the parent's
+    with flips[level] random bits flipped, leaves = words (ids in node order) with TF-IDF
+    weights in (0.5, 5), stop_frac of them stopped (weight 0)."""
+    rng = np.random.default_rng(seed)
+    descs = [rng.integers(0, 256, (1, 32), dtype=np.uint8)]
+    parents = [np.array([-1], np.int32)]
+    levels = [np.zeros(1, np.int32)]
+    first = 0
+    for l in range(1, L + 1):
+        prev = descs[-1]
+        par = np.repeat(np.arange(first, first + len(prev), dtype=np.int32), K)
+        d = np.repeat(prev, K, axis=0)
+        _flip_bits(d, flips[min(l - 1, len(flips) - 1)], rng)
+        first += len(prev)
+        descs.append(d)
+        parents.append(par)
+        levels.append(np.full(len(d), l, np.int32))
+    desc = np.concatenate(descs)
+    parent = np.concatenate(parents)
+    level = np.concatenate(levels)
+    n = len(desc)
+    word = np.full(n, -1, np.int32)
+    leaves = np.nonzero(level == L)[0]
+    word[leaves] = np.arange(len(leaves), dtype=np.int32)
+    weight = np.zeros(n, np.float64)
+    weight[leaves] = rng.uniform(0.5, 5.0, len(leaves))
+    weight[leaves[rng.random(len(leaves)) < stop_frac]] = 0.0
+    return {"desc": desc, "parent": parent, "word": word, "weight": weight, "L": L, "K": K, "leaves": leaves}
+
+
+def bow_features(voc, n, seed=0, flips=6):
+    """n ORB descriptors scattered around random vocabulary leaves (flips random bits each)."""
+    rng = np.random.default_rng(seed)
+    d = voc["desc"][rng.choice(voc["leaves"], n)].copy()
+    return _flip_bits(d, flips, rng)
+
+
+def bow_pair(voc, n_kf=1000, n_f=1000, seed=0, overlap=0.7, valid=0.8):
+    """A keyframe and a frame observing partly the same features: -> (kf_kps, kf_desc, kf_valid,
+    f_kps, f_desc); frame features are re-observations (a few extra bits flipped, the angle
+    rotated by a common in-plane rotation plus noise) of `overlap` of the keyframe's."""
+    rng = np.random.default_rng(seed)
+    kd = bow_features(voc, n_kf, seed)
+    dt = [("x", "f4"), ("y", "f4"), ("size", "f4"), ("angle", "f4"), ("response", "f4"), ("octave", "i4"),
+          ("class_id", "i4")]
+    kk = np.zeros(n_kf, dt)
+    kk["x"], kk["y"] = rng.uniform(0, 640, n_kf), rng.uniform(0, 480, n_kf)
+    kk["angle"] = rng.uniform(0, 360, n_kf)
+    kk["octave"], kk["class_id"] = rng.integers(0, 8, n_kf), -1
+    fd = bow_features(voc, n_f, seed + 7919)
+    fk = np.zeros(n_f, dt)
+    fk["x"], fk["y"] = rng.uniform(0, 640, n_f), rng.uniform(0, 480, n_f)
+    fk["angle"] = rng.uniform(0, 360, n_f)
+    fk["octave"], fk["class_id"] = rng.integers(0, 8, n_f), -1
+    m = int(min(n_kf, n_f) * overlap)
+    src = rng.permutation(n_kf)[:m]
+    dst = rng.permutation(n_f)[:m]
+    fd[dst] = _flip_bits(kd[src].copy(), 8, rng)
+    rot = rng.uniform(0, 360)
+    fk["angle"][dst] = np.mod(kk["angle"][src] - rot + rng.normal(0, 4, m), 360).astype(np.float32)
+    kv = (rng.random(n_kf) < valid).astype(np.uint8)
+    return kk, kd, kv, fk, fd
