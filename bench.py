@@ -356,6 +356,8 @@ def main():
                            d_cnt, d_has, d_mpos, match_ms)
     lines_leg = line_leg(ea, torch, stream, min(F, RENDERED), gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
     pose = pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
+    bow = bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt,
+                  with_cpu=rank == 0 and not args.no_cpu_baseline)
     n_kps = float(d_cnt.float().mean().item())
     ab = algorithmic_bytes(n_kps)
     dom = int(np.argmax(stage))
@@ -404,6 +406,7 @@ def main():
             "searches": searches,
             "line_detect": lines_leg,
             "pose_optimization": pose,
+            "bag_of_words": bow,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
                                   "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
@@ -472,6 +475,89 @@ def line_leg(ea, torch, stream, F, gpu, with_cpu=True, reps=3, distinct=48):
                     "gpu_over_cpu": (F / (np.mean(ms) * 1e-3)) / (1e3 / cpu_ms), "parity_frames": k,
                     "parity_bitexact": bool(ok)})
     L.close()
+    return res
+
+
+def bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt, with_cpu=True, reps=3):
+    """Bag of words beside the step (SURVEY 8f rank 3): Frame::ComputeBoW (DBoW2 transform,
+    levelsup 4, Frame.cc:516-523) of the step's F extracted frames and SearchByBoW
+    (ORBmatcher.cc:159-288) of every frame against its predecessor as the keyframe (F-1
+    searches, 80 % of the keyframe features holding a valid map point), batched and
+    HBM-resident, timed with HIP events; the vocabulary is a synthetic ORB-shaped tree (K=10,
+    L=6, 1.1M nodes: the reference's ORBvoc blob is missing). The CPU restatement
+    (oracle/bow_ref.cpp, one thread) is timed on a sample and checked bit-exact."""
+    from tools import synth
+    dev = torch.device("cuda", gpu)
+    voc = synth.vocabulary(K=10, L=6, seed=0xB0)
+    V = ea.Vocab(voc, max_kps=cap, max_batch=F, device=gpu)
+    rng = np.random.default_rng(0xB1)
+    valid = (rng.random((F, cap)) < 0.8).astype(np.uint8)
+    d_valid = torch.from_numpy(valid).to(dev)
+    z = lambda *s, dt=torch.int32: torch.zeros(s, dtype=dt, device=dev)
+    wid, ww, nw = z(F, cap), z(F, cap, dt=torch.float64), z(F)
+    nid, ns, nf, nn = z(F, cap), z(F, cap + 1), z(F, cap), z(F)
+    S = F - 1
+    match, nm = z(S, cap), z(S)
+    sp = stream.cuda_stream
+    stream.wait_stream(torch.cuda.current_stream())
+
+    def transform():
+        V.transform_batch_device(F, cap, d_cnt.data_ptr(), d_desc.data_ptr(), 4, wid.data_ptr(), ww.data_ptr(),
+                                 nw.data_ptr(), nid.data_ptr(), ns.data_ptr(), nf.data_ptr(), nn.data_ptr(), sp)
+
+    i32 = 4
+    def search():  # keyframe slot s = frame s, frame slot = frame s + 1 (pointer offsets, no copies)
+        kf = (d_kps.data_ptr(), d_desc.data_ptr(), d_valid.data_ptr(), nn.data_ptr(), nid.data_ptr(), ns.data_ptr(),
+              nf.data_ptr())
+        fr = (d_cnt.data_ptr() + i32, d_kps.data_ptr() + cap * 28, d_desc.data_ptr() + cap * 32,
+              nn.data_ptr() + i32, nid.data_ptr() + cap * i32, ns.data_ptr() + (cap + 1) * i32,
+              nf.data_ptr() + cap * i32)
+        V.search_batch_device(0.75, 1, S, cap, kf, fr, match.data_ptr(), nm.data_ptr(), sp)
+    transform()
+    search()
+    tms, sms = [], []
+    for _ in range(reps):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record(stream)
+        transform()
+        e[1].record(stream)
+        search()
+        e[2].record(stream)
+        e[2].synchronize()
+        tms.append(e[0].elapsed_time(e[1]))
+        sms.append(e[1].elapsed_time(e[2]))
+    h = [x.cpu().numpy() for x in (nid, ns, nf, nn, match, nm)]
+    hd = d_desc.cpu().numpy()
+    res = {"frames": F, "searches": S, "vocabulary": "synthetic K=10 L=6 (%d nodes)" % len(voc["parent"]),
+           "transform_ms_per_batch": float(np.mean(tms)), "search_ms_per_batch": float(np.mean(sms)),
+           "transform_frames_per_s": F / (np.mean(tms) * 1e-3), "searches_per_s": S / (np.mean(sms) * 1e-3),
+           "mean_matches": float(h[5].mean()), "kernels": "k_bow_words + k_bow_build; k_bow_search + k_bow_rot"}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as orc  # checker / CPU baseline only
+        orc.use_native()
+        OV = orc.Vocab(voc)
+        k = 16
+        t0 = time.perf_counter()
+        fv = [orc.bow_transform(OV, hd[f, :cnt[f]], 4) for f in range(k + 1)]
+        t_ms = (time.perf_counter() - t0) * 1e3 / (k + 1)
+        t0 = time.perf_counter()
+        sr = [orc.search_by_bow(0.75, 1, kps[s, :cnt[s]], hd[s, :cnt[s]], valid[s, :cnt[s]], fv[s][2:],
+                                kps[s + 1, :cnt[s + 1]], hd[s + 1, :cnt[s + 1]], fv[s + 1][2:]) for s in range(k)]
+        s_ms = (time.perf_counter() - t0) * 1e3 / k
+        ok = True
+        for f in range(k + 1):
+            q = h[3][f]
+            ok &= bool(np.array_equal(h[0][f, :q], fv[f][2]) and np.array_equal(h[1][f, :q + 1], fv[f][3]) and
+                       np.array_equal(h[2][f, :h[1][f, q]], fv[f][4]))
+        for s_ in range(k):
+            ok &= bool(h[5][s_] == sr[s_][0] and np.array_equal(h[4][s_, :cnt[s_ + 1]], sr[s_][1]))
+        res.update({"cpu_transform_ms_per_frame": t_ms, "cpu_search_ms": s_ms,
+                    "cpu_kind": "port (oracle/bow_ref.cpp, 1 thread)", "parity_frames": k + 1,
+                    "parity_bitexact": bool(ok),
+                    "gpu_over_cpu_transform": (F / (np.mean(tms) * 1e-3)) / (1e3 / t_ms),
+                    "gpu_over_cpu_search": (S / (np.mean(sms) * 1e-3)) / (1e3 / s_ms)})
+    V.close()
     return res
 
 
