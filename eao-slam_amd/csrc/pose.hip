@@ -299,6 +299,44 @@ __device__ __forceinline__ double block_sum1(double v, double* red, int& buf) {
   return s;
 }
 
+// DPP row_shr:n of a double (both dwords); lanes shifted in from outside the 16-lane row read 0
+template <int N>
+__device__ __forceinline__ double row_shr(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), 0x110 + N, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x110 + N, 0xF, 0xF, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// the block sum of NV doubles into out[0..NV) (LDS): per 16-lane row a Hillis-Steele scan by
+// DPP (row sum in the row's last lane), the rows' sums to LDS, then thread k < NV adds the
+// block's 4 * NW row sums of value k in row order -- a fixed order, so deterministic. Ends with
+// a barrier: out is then visible to the whole block.
+template <int T, int NV>
+__device__ __forceinline__ void block_sum_rows(double (&v)[NV], double* part, double* out) {
+  constexpr int NR = T / 16;
+#pragma unroll
+  for (int k = 0; k < NV; k++) {
+    v[k] += row_shr<1>(v[k]);
+    v[k] += row_shr<2>(v[k]);
+    v[k] += row_shr<4>(v[k]);
+    v[k] += row_shr<8>(v[k]);
+  }
+  const int r = threadIdx.x >> 4;
+  if ((threadIdx.x & 15) == 15) {
+#pragma unroll
+    for (int k = 0; k < NV; k++) part[k * NR + r] = v[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const double* p = part + threadIdx.x * NR;
+    double s = p[0];
+    for (int q = 1; q < NR; q++) s = s + p[q];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
 template <int EPT>
 struct Edges {
   float ox[EPT], oy[EPT], X[EPT], Y[EPT], Z[EPT], inv[EPT];
@@ -306,9 +344,6 @@ struct Edges {
   uint32_t outl;  // bit k: edge slot k is level 1 (outlier)
 };
 
-__device__ __forceinline__ double huber_rho0(double c, const PoseArgs& a) {
-  return c <= a.dsqr ? c : 2 * sqrt(c) * a.delta - a.dsqr;
-}
 
 // EdgeSE3ProjectXYZOnlyPose::computeError at s; the camera-frame point is returned too
 template <int EPT>
@@ -337,7 +372,9 @@ __global__ void __launch_bounds__(T) k_pose_opt(PoseArgs a, int cap, const float
   __shared__ int s_list[T * EPT];
   __shared__ int s_wcnt[NW];
   __shared__ double s_red[2 * NW * kRed];
-  __shared__ double s_sys[kRed];  // the reduced system: 21 H (lower, packed) | 6 b | chi
+  __shared__ double s_part[kRed * (T / 16)];
+  // two reduced systems (21 H lower packed | 6 b | chi): the current one and a trial's
+  __shared__ double s_sysbuf[2][kRed];
   const int f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int n = min(counts[f], cap);
   const float* T0 = Tin + 16 * f;
@@ -412,11 +449,13 @@ __global__ void __launch_bounds__(T) k_pose_opt(PoseArgs a, int cap, const float
       if (E.idx[k] >= 0 && !((E.outl >> k) & 1)) cnt += 1;
     cnt = block_sum1<T>(cnt, s_red, buf);
     if (cnt > 0) {
-      // ---- SparseOptimizer::optimize(10) with OptimizationAlgorithmLevenberg
-      double x[6] = {0, 0, 0, 0, 0, 0};
-      double lambda = 0, ni = 2;
-      int nbad = 0;
-      for (int it = 0; it < 10; it++) {
+      // ---- SparseOptimizer::optimize(10) with OptimizationAlgorithmLevenberg. A pass at an
+      // estimate gives computeActiveErrors + activeRobustChi2 + buildSystem at once; a trial's
+      // pass is therefore also the next iteration's build when the trial is accepted (solve()
+      // would recompute exactly those errors at exactly that estimate), so each Levenberg
+      // trial costs one pass and only the first iteration has a pass of its own.
+      int cur_buf = 0;
+      auto build_pass = [&](const Se3& at, double* out) {
         double acc[kRed];
 #pragma unroll
         for (int q = 0; q < kRed; q++) acc[q] = 0;
@@ -424,7 +463,7 @@ __global__ void __launch_bounds__(T) k_pose_opt(PoseArgs a, int cap, const float
         for (int k = 0; k < EPT; k++) {
           if (E.idx[k] < 0 || ((E.outl >> k) & 1)) continue;
           double e0, e1, xc, yc, zc;
-          edge_error(E, k, est, a, e0, e1, xc, yc, zc);
+          edge_error(E, k, at, a, e0, e1, xc, yc, zc);
           const double inv = (double)E.inv[k];
           const double c = chi2_of(e0, e1, inv);
           double r1 = 1.0;
@@ -463,68 +502,66 @@ __global__ void __launch_bounds__(T) k_pose_opt(PoseArgs a, int cap, const float
             acc[21 + i] -= ((r1 * J0[i]) * inv) * e0 + ((r1 * J1[i]) * inv) * e1;
           }
         }
-        elast = est;
-        {
-          const double* r = block_partials<T, kRed>(acc, s_red, buf);
-          if (tid < kRed) {
-            double s = r[tid];
-            for (int q = 1; q < NW; q++) s = s + r[q * kRed + tid];
-            s_sys[tid] = s;
-          }
-          __syncthreads();
+        block_sum_rows<T, kRed>(acc, s_part, out);
+      };
+      // one call site for the pass, the solve and the update (register pressure): a flat loop
+      // whose first trip is the first iteration's own pass
+      double x[6] = {0, 0, 0, 0, 0, 0};
+      double lambda = 0, ni = 2, cur = 0, ini = 0;
+      int nbad = 0, it = 0, qn = 0;
+      bool first = true, ok = true;
+      Se3 saved = est;
+      for (;;) {
+        double* target = s_sysbuf[first ? cur_buf : (cur_buf ^ 1)];
+        if (!first) {
+          saved = est;
+          ok = ldlt_solve(s_sysbuf[cur_buf], lambda, x);
+          est = se3_oplus(est, x);
         }
-        double cur = s_sys[27];
-        const double ini = cur;
-        if (it == 0) {
+        build_pass(est, target);
+        elast = est;
+        if (first) {  // iteration 0: computeLambdaInit from the diagonal of H
+          first = false;
+          cur = target[27];
+          ini = cur;
           double md = 0;
 #pragma unroll
-          for (int j = 0; j < 6; j++) md = fmax(fabs(s_sys[j * (j + 3) / 2]), md);
+          for (int j = 0; j < 6; j++) md = fmax(fabs(target[j * (j + 3) / 2]), md);
           lambda = 1e-5 * md;
           ni = 2;
           nbad = 0;
+          qn = 0;
+          continue;
         }
-        double rho = 0;
-        int qn = 0;
-        do {
-          const Se3 saved = est;
-          const bool ok = ldlt_solve(s_sys, lambda, x);
-          est = se3_oplus(est, x);
-          double tc = 0;
+        const double* sys = s_sysbuf[cur_buf];
+        const double tmp = ok ? target[27] : DBL_MAX;
+        double rho = cur - tmp;
+        double scale = 0;
 #pragma unroll
-          for (int k = 0; k < EPT; k++) {
-            if (E.idx[k] < 0 || ((E.outl >> k) & 1)) continue;
-            double e0, e1, xc, yc, zc;
-            edge_error(E, k, est, a, e0, e1, xc, yc, zc);
-            const double c = chi2_of(e0, e1, (double)E.inv[k]);
-            tc += robust ? huber_rho0(c, a) : c;
-          }
-          elast = est;
-          tc = block_sum1<T>(tc, s_red, buf);
-          const double tmp = ok ? tc : DBL_MAX;
-          rho = cur - tmp;
-          double scale = 0;
-#pragma unroll
-          for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + s_sys[21 + j]);
-          scale += 1e-3;
-          rho /= scale;
-          if (rho > 0 && isfinite(tmp)) {
-            double alpha = 1. - pow((2 * rho - 1), 3.0);
-            alpha = fmin(alpha, 2. / 3.);
-            lambda *= fmax(1. / 3., alpha);
-            ni = 2;
-            cur = tmp;
-          } else {
-            lambda *= ni;
-            ni *= 2;
-            est = saved;
-          }
-          qn++;
-        } while (rho < 0 && qn < 10);
+        for (int j = 0; j < 6; j++) scale += x[j] * (lambda * x[j] + sys[21 + j]);
+        scale += 1e-3;
+        rho /= scale;
+        if (rho > 0 && isfinite(tmp)) {
+          double alpha = 1. - pow((2 * rho - 1), 3.0);
+          alpha = fmin(alpha, 2. / 3.);
+          lambda *= fmax(1. / 3., alpha);
+          ni = 2;
+          cur = tmp;
+          cur_buf ^= 1;  // the trial's system is the next iteration's
+        } else {
+          lambda *= ni;
+          ni *= 2;
+          est = saved;
+        }
+        qn++;
+        if (rho < 0 && qn < 10) continue;  // another trial of the same iteration
         if (qn == 10 || rho == 0) break;
         if ((ini - cur) * 1e3 < ini) nbad++;
         else nbad = 0;
         if (nbad >= 3) break;
-        __syncthreads();  // s_sys is rewritten by the next build pass
+        if (++it >= 10) break;
+        ini = cur;  // the next iteration's computeActiveErrors at est: the current system
+        qn = 0;
       }
     }
     // ---- classification (Optimizer.cc:387-415): level-0 edges test the error of the last
@@ -546,7 +583,6 @@ __global__ void __launch_bounds__(T) k_pose_opt(PoseArgs a, int cap, const float
     }
     if (round == 2) robust = false;
     nbad_total = (int)block_sum1<T>(nb, s_red, buf);
-    __syncthreads();  // s_sys reuse across rounds
     if (n0 < 10) break;  // optimizer.edges().size() < 10
   }
 #pragma unroll
