@@ -88,27 +88,27 @@ __device__ __forceinline__ uint32_t pk_max3(uint32_t a, uint32_t b, uint32_t c) 
 }
 
 // The FAST strength (above) for the two vertically adjacent pixels p (low half) and
-// p + RS (high half) at once. A ring byte b is carried as the f16 1024 + b
-// (bits 0x6400 | b: a normal number, exact), so f16 minimum / maximum order
-// the bytes exactly and the 3- then 9-wide arc windows run on both rows per
-// instruction. The arc bounds A, B come out as 0x6400 | value, so
-// S = max(0, v - A, B - v) is taken on their low bytes as integers.
+// p + RS (high half) at once. A ring byte b is carried as the 16-bit pattern 0x00bb, an f16
+// subnormal: the kernels run with f16 denormals preserved (float_denorm_mode_16_64 = 3) and
+// subnormals order as their integer patterns, so f16 minimum / maximum order the bytes exactly
+// and the 3- then 9-wide arc windows run on both rows per instruction (one v_lshl_or per ring
+// pair; an exponent bias would cost a second op). The arc bounds A, B come out as the byte
+// values, so S = max(0, v - A, B - v) is taken on their low bytes as integers.
 // Returns S(row) | S(row + 1) << 16.
 template <int RS>
 __device__ __forceinline__ uint32_t fast_strength_pair(const uint8_t* p) {
   constexpr int off[16] = {3 * RS,  3 * RS + 1,  2 * RS + 2,  RS + 3,  3,  -RS + 3,  -2 * RS + 2,  -3 * RS + 1,
                            -3 * RS, -3 * RS - 1, -2 * RS - 2, -RS - 3, -3, RS - 3,   2 * RS - 2,  3 * RS - 1};
-  constexpr uint32_t BIAS = 0x64006400u;
   uint32_t q[16];
 #pragma unroll
-  for (int k = 0; k < 16; k++) q[k] = ((uint32_t)p[off[k]] | ((uint32_t)p[off[k] + RS] << 16)) | BIAS;
+  for (int k = 0; k < 16; k++) q[k] = (uint32_t)p[off[k]] | ((uint32_t)p[off[k] + RS] << 16);
   uint32_t mn3[16], mx3[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     mn3[k] = pk_min3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
     mx3[k] = pk_max3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
   }
-  uint32_t A = 0x64ff64ffu, B = BIAS;  // 1024 + 255, 1024 + 0
+  uint32_t A = 0x00ff00ffu, B = 0u;  // 255, 0
 #pragma unroll
   for (int k = 0; k < 16; k += 2) {
     const uint32_t a0 = pk_max3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
