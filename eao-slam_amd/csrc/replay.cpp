@@ -1093,7 +1093,8 @@ class ReplayEngine {
       hipStream_t st = if_stream[k % kIfStreams];
       prof[2] += 1;
       Tick tl(&prof[19]);
-      EAO_HIP_CHECK(hipMemcpyAsync(b.d_in, b.h_in, in_bytes, hipMemcpyHostToDevice, st));
+      // compute-queue staging (k_stage), as at the frame start: no DMA-engine hand-off
+      if (int rc0 = A->stage_in(b.d_in, b.h_in, in_bytes, st)) return rc0;
       const int* dm = (const int*)b.d_in;
       // scores go straight to pinned host memory (a device-to-host copy costs
       // ~35 us of round trip per launch on this box) and, for the speculative
