@@ -245,8 +245,8 @@ __global__ __launch_bounds__(256) void k_bow_search(int cap, SearchSlot K, Searc
   }
   if (lo >= Fr.nn[s] || Fr.ids[so + lo] != id) return;
   const int q0 = Fr.start[ss + lo], nq = Fr.start[ss + lo + 1] - q0;
-  if (nq > NODE_MAXF) {
-    if (lane == 0) atomicOr(err, 1);
+  if (nq > NODE_MAXF) {  // reported per search through nmatches (k_bow_rot)
+    if (lane == 0) atomicOr(&err[s], 1);
     return;
   }
   uint8_t* flag = s_flag[w];
@@ -306,13 +306,18 @@ __device__ __forceinline__ int rot_bin(float a_kf, float a_f) {
 __global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict__ n_f, const int* __restrict__ n_kf,
                                                  const eao_keypoint_dev* __restrict__ kkps,
                                                  const eao_keypoint_dev* __restrict__ fkps, int check_ori,
-                                                 int* __restrict__ f_match, int* __restrict__ nmatches) {
+                                                 int* __restrict__ f_match, int* __restrict__ nmatches,
+                                                 const int* __restrict__ err) {
   __shared__ int hist[HISTO_LENGTH];
   __shared__ int keep[HISTO_LENGTH];
   __shared__ int s_cnt;
   const int s = blockIdx.x, t = threadIdx.x;
   const size_t so = (size_t)s * cap;
   const int n = min(n_f[s], cap);
+  if (err[s]) {  // a vocabulary node held more frame features than the search supports
+    if (t == 0) nmatches[s] = EAO_E_CAPACITY;
+    return;
+  }
   if (t < HISTO_LENGTH) hist[t] = 0;
   if (t == 0) s_cnt = 0;
   __syncthreads();
@@ -466,7 +471,7 @@ int eao_vocab_create(int device, int n_nodes, const uint8_t* node_desc, const in
   if ((r = e.alloc(&e.d_i, sizeof(int) * 2 * (3 * K + 8))) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_ww, sizeof(double) * K)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_out, sizeof(int) * (K + 16))) != hipSuccess) return fail(r);
-  if ((r = e.alloc(&e.d_err, sizeof(int))) != hipSuccess) return fail(r);
+  if ((r = e.alloc(&e.d_err, sizeof(int) * B)) != hipSuccess) return fail(r);
   if (n_nodes > 0) {
     if ((r = hipMemcpy(e.d_vdesc, node_desc, 32 * (size_t)n_nodes, hipMemcpyHostToDevice)) != hipSuccess) return fail(r);
     if ((r = hipMemcpy(e.d_cstart, cstart.data(), sizeof(int) * (n_nodes + 1), hipMemcpyHostToDevice)) != hipSuccess)
@@ -559,8 +564,8 @@ int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, i
                                    const int32_t* d_f_nn, const int32_t* d_f_node_ids,
                                    const int32_t* d_f_node_start, const int32_t* d_f_node_feats,
                                    int32_t* d_f_match, int32_t* d_nmatches, void* stream) {
-  if (!v || nsearch < 0 || cap < 1 || cap > v->e.max_kps) {
-    set_error("eao_search_by_bow_batch_device: bad arguments (cap outside [1, max_kps])");
+  if (!v || nsearch < 0 || nsearch > v->e.max_batch || cap < 1 || cap > v->e.max_kps) {
+    set_error("eao_search_by_bow_batch_device: bad arguments (nsearch <= max_batch, cap in [1, max_kps])");
     return EAO_E_ARG;
   }
   if (nsearch == 0) return EAO_OK;
@@ -572,11 +577,11 @@ int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, i
   const SearchSlot F{(const eao_keypoint_dev*)d_f_kps, d_f_desc, nullptr, d_f_nn, d_f_node_ids, d_f_node_start,
                      d_f_node_feats};
   EAO_HIP_CHECK(hipMemsetAsync(d_f_match, 0xff, sizeof(int) * (size_t)nsearch * cap, s));
-  EAO_HIP_CHECK(hipMemsetAsync(e.d_err, 0, sizeof(int), s));
+  EAO_HIP_CHECK(hipMemsetAsync(e.d_err, 0, sizeof(int) * nsearch, s));
   hipLaunchKernelGGL(k_bow_search, dim3((cap + 3) / 4, nsearch), dim3(256), 0, s, cap, K, F, nnratio, d_f_match,
                      e.d_err);
   hipLaunchKernelGGL(k_bow_rot, dim3(nsearch), dim3(256), 0, s, cap, d_n_f, d_kf_nn, K.kps, F.kps, check_ori,
-                     d_f_match, d_nmatches);
+                     d_f_match, d_nmatches, e.d_err);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -634,12 +639,11 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
                                       (const eao_keypoint*)(e.d_kps + K), e.d_desc + 32 * (size_t)K, fI + 3 * K + 4,
                                       fI, fI + K, fI + 2 * K + 1, e.d_out, e.d_out + K, s);
   if (rc) return rc;
-  int nm = 0, err = 0;
+  int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(f_match, e.d_out, sizeof(int) * n_f, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + K, sizeof(int), hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(&err, e.d_err, sizeof(int), hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
-  if (err) {
+  if (nm < 0) {
     set_error("eao_search_by_bow: a vocabulary node holds more than 1024 frame features");
     return EAO_E_CAPACITY;
   }

@@ -431,7 +431,8 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
 /* batched, HBM-resident: search s pairs keyframe slot s with frame slot s ([nsearch][cap]
    keypoints / descriptors / valid flags / node ids / node features, [nsearch][cap + 1] node starts,
    per-search node counts d_kf_nn / d_f_nn and frame feature counts d_n_f); writes
-   d_f_match [nsearch][cap] and d_nmatches [nsearch]. */
+   d_f_match [nsearch][cap] and d_nmatches [nsearch] (EAO_E_CAPACITY for a search in which a
+   vocabulary node holds more than 1024 frame features). nsearch <= max_batch. */
 int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, int nsearch, int cap,
                                    const eao_keypoint* d_kf_kps, const uint8_t* d_kf_desc,
                                    const uint8_t* d_kf_mp_valid, const int32_t* d_kf_nn,

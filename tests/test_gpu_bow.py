@@ -125,3 +125,15 @@ def test_batch_device(orbvoc):
         fk2, fd2 = kps[g2, :n2], desc[g2, :n2]
         no, mo = orc.search_by_bow(0.75, 1, kk, kd, kv, fvs[f], fk2, fd2, fvs[g2])
         assert hn[f] == no and np.array_equal(hm[f, :n2], mo), f
+
+
+def test_search_node_capacity():
+    """a vocabulary node with more than 1024 frame features is reported (EAO_E_CAPACITY),
+    not silently truncated"""
+    voc = synth.vocabulary(K=2, L=2, seed=5, stop_frac=0.0)
+    kk, kd, kv, fk, fd = synth.bow_pair(voc, 3000, 3000, seed=6)
+    V = ea.Vocab(voc, max_kps=4096)
+    kfv, ffv = V.transform(kd, 1)[2:], V.transform(fd, 1)[2:]
+    assert np.diff(ffv[1]).max() > 1024
+    with pytest.raises(ea.EaoError, match="1024"):
+        V.search(0.75, 1, kk, kd, kv, kfv, fk, fd, ffv)
