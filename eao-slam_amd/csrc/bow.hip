@@ -387,9 +387,11 @@ struct VocabEngine {
   double* d_ww = nullptr;             // [max_kps]
   int* d_out = nullptr;               // [max_kps + 16]
   int* d_err = nullptr;
+  int* h_small = nullptr;             // pinned scalars of the single-frame calls
   std::vector<void*> ptrs;
   ~VocabEngine() {
     for (void* p : ptrs) (void)hipFree(p);
+    if (h_small) (void)hipHostFree(h_small);
     if (stream) (void)hipStreamDestroy(stream);
   }
   template <typename Tp>
@@ -472,6 +474,7 @@ int eao_vocab_create(int device, int n_nodes, const uint8_t* node_desc, const in
   if ((r = e.alloc(&e.d_ww, sizeof(double) * K)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_out, sizeof(int) * (K + 16))) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_err, sizeof(int) * B)) != hipSuccess) return fail(r);
+  if ((r = hipHostMalloc((void**)&e.h_small, sizeof(int) * 16, 0)) != hipSuccess) return fail(r);
   if (n_nodes > 0) {
     if ((r = hipMemcpy(e.d_vdesc, node_desc, 32 * (size_t)n_nodes, hipMemcpyHostToDevice)) != hipSuccess) return fail(r);
     if ((r = hipMemcpy(e.d_cstart, cstart.data(), sizeof(int) * (n_nodes + 1), hipMemcpyHostToDevice)) != hipSuccess)
@@ -532,14 +535,15 @@ int eao_bow_transform(eao_vocab* v, int n, const uint8_t* desc, int levelsup, in
   int* d_start = e.d_i + K;
   int* d_feats = e.d_i + 2 * K + 1;
   int* d_wid = e.d_out;
-  EAO_HIP_CHECK(hipMemcpyAsync(d_cnt, &n, sizeof(int), hipMemcpyHostToDevice, s));
+  e.h_small[0] = n;
+  EAO_HIP_CHECK(hipMemcpyAsync(d_cnt, e.h_small, sizeof(int), hipMemcpyHostToDevice, s));
   if (n > 0) EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, desc, 32 * (size_t)n, hipMemcpyHostToDevice, s));
   int rc = eao_bow_transform_batch_device(v, 1, cap, d_cnt, e.d_desc, levelsup, d_wid, e.d_ww, d_cnt + 1, d_ids,
                                           d_start, d_feats, d_cnt + 2, s);
   if (rc) return rc;
-  int hc[3];
-  EAO_HIP_CHECK(hipMemcpyAsync(hc, d_cnt, sizeof(hc), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.h_small + 4, d_cnt, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  const int hc[3] = {e.h_small[4], e.h_small[5], e.h_small[6]};
   *n_words = hc[1];
   *n_nodes = hc[2];
   if (hc[1] > 0) {
@@ -612,7 +616,6 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
     set_error("eao_search_by_bow: a FeatureVector lists more features than the side has");
     return EAO_E_ARG;
   }
-  const int zero = 0;
   if (n_kf > 0) {
     EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, kf_kps, sizeof(eao_keypoint) * n_kf, hipMemcpyHostToDevice, s));
     EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, kf_desc, 32 * (size_t)n_kf, hipMemcpyHostToDevice, s));
@@ -620,8 +623,10 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
   }
   EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, f_kps, sizeof(eao_keypoint) * n_f, hipMemcpyHostToDevice, s));
   EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + 32 * (size_t)K, f_desc, 32 * (size_t)n_f, hipMemcpyHostToDevice, s));
-  auto up_fv = [&](int* base, int nn, const int32_t* ids, const int32_t* st, const int32_t* ft, int nf) -> int {
-    EAO_HIP_CHECK(hipMemcpyAsync(base + 3 * K + 4, &nn, sizeof(int), hipMemcpyHostToDevice, s));
+  auto up_fv = [&](int* base, int nn, const int32_t* ids, const int32_t* st, const int32_t* ft, int nf,
+                   int* hslot) -> int {
+    *hslot = nn;
+    EAO_HIP_CHECK(hipMemcpyAsync(base + 3 * K + 4, hslot, sizeof(int), hipMemcpyHostToDevice, s));
     if (nn > 0) {
       EAO_HIP_CHECK(hipMemcpyAsync(base, ids, sizeof(int) * nn, hipMemcpyHostToDevice, s));
       EAO_HIP_CHECK(hipMemcpyAsync(base + K, st, sizeof(int) * (nn + 1), hipMemcpyHostToDevice, s));
@@ -629,20 +634,20 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
     }
     return EAO_OK;
   };
-  int rc = up_fv(kI, kf_nn, kf_node_ids, kf_node_start, kf_node_feats, kf_nf);
-  if (!rc) rc = up_fv(fI, f_nn, f_node_ids, f_node_start, f_node_feats, f_nf);
+  int rc = up_fv(kI, kf_nn, kf_node_ids, kf_node_start, kf_node_feats, kf_nf, e.h_small);
+  if (!rc) rc = up_fv(fI, f_nn, f_node_ids, f_node_start, f_node_feats, f_nf, e.h_small + 1);
   if (rc) return rc;
-  EAO_HIP_CHECK(hipMemcpyAsync(fI + 3 * K + 5, &n_f, sizeof(int), hipMemcpyHostToDevice, s));
-  (void)zero;
+  e.h_small[2] = n_f;
+  EAO_HIP_CHECK(hipMemcpyAsync(fI + 3 * K + 5, e.h_small + 2, sizeof(int), hipMemcpyHostToDevice, s));
   rc = eao_search_by_bow_batch_device(v, nnratio, check_ori, 1, K, (const eao_keypoint*)e.d_kps, e.d_desc, e.d_valid,
                                       kI + 3 * K + 4, kI, kI + K, kI + 2 * K + 1, fI + 3 * K + 5,
                                       (const eao_keypoint*)(e.d_kps + K), e.d_desc + 32 * (size_t)K, fI + 3 * K + 4,
                                       fI, fI + K, fI + 2 * K + 1, e.d_out, e.d_out + K, s);
   if (rc) return rc;
-  int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(f_match, e.d_out, sizeof(int) * n_f, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + K, sizeof(int), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.h_small + 3, e.d_out + K, sizeof(int), hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  const int nm = e.h_small[3];
   if (nm < 0) {
     set_error("eao_search_by_bow: a vocabulary node holds more than 1024 frame features");
     return EAO_E_CAPACITY;
