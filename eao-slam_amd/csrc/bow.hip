@@ -616,6 +616,23 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
     set_error("eao_search_by_bow: a FeatureVector lists more features than the side has");
     return EAO_E_ARG;
   }
+  // the kernel indexes descriptors / flags / matches with these values and binary-searches the
+  // node ids: every feature index in range, node starts non-decreasing, node ids ascending
+  auto fv_ok = [](int nn, const int32_t* ids, const int32_t* st, const int32_t* ft, int nfeat) {
+    if (nn > 0 && st[0] != 0) return false;
+    for (int i = 0; i < nn; i++)
+      if (st[i + 1] < st[i] || (i > 0 && ids[i] <= ids[i - 1])) return false;
+    const int tot = nn > 0 ? st[nn] : 0;
+    for (int k = 0; k < tot; k++)
+      if (ft[k] < 0 || ft[k] >= nfeat) return false;
+    return true;
+  };
+  if (!fv_ok(kf_nn, kf_node_ids, kf_node_start, kf_node_feats, n_kf) ||
+      !fv_ok(f_nn, f_node_ids, f_node_start, f_node_feats, n_f)) {
+    set_error("eao_search_by_bow: malformed FeatureVector (feature index out of range, node starts "
+              "decreasing or node ids not ascending)");
+    return EAO_E_ARG;
+  }
   if (n_kf > 0) {
     EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, kf_kps, sizeof(eao_keypoint) * n_kf, hipMemcpyHostToDevice, s));
     EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, kf_desc, 32 * (size_t)n_kf, hipMemcpyHostToDevice, s));

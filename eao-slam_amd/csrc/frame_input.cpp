@@ -26,7 +26,7 @@ namespace {
 // `istr >> tmp` with int tmp on one whitespace-separated token: the longest
 // [+-]digits prefix; false (stream failed) when there is none. A token such as
 // "0.824041" yields 0 and leaves ".824041" unread, which fails the next extraction:
-// the row ends there.
+// the row ends there. "12-3" yields 12, then -3.
 bool int_token(const char*& p, const char* end, int& v, bool& stop) {
   while (p < end && (*p == ' ' || *p == '\t' || *p == '\r' || *p == '\v' || *p == '\f')) p++;
   if (p >= end) return false;
@@ -39,7 +39,10 @@ bool int_token(const char*& p, const char* end, int& v, bool& stop) {
   x = neg ? -x : x;
   if (x > INT32_MAX || x < INT32_MIN) return false;  // out of range: failbit, nothing pushed
   v = (int)x;
-  stop = q < end && !(*q == ' ' || *q == '\t' || *q == '\r' || *q == '\v' || *q == '\f');
+  // the row ends when the next character can start no further extraction: "0.82" stops at
+  // '.', but "12-3" reads on (the next `>> int` takes "-3"), as the stream would
+  stop = q < end && !(*q == ' ' || *q == '\t' || *q == '\r' || *q == '\v' || *q == '\f' || *q == '+' ||
+                      *q == '-' || (*q >= '0' && *q <= '9'));
   p = q;
   return true;
 }

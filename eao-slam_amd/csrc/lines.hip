@@ -44,17 +44,26 @@ __device__ __forceinline__ int refl101(int p, int len) {
 }
 
 // ---------------------------------------------------------------- blur
+// CN = 1: gray input. CN = 3 / 4: the colour frame BinaryDescriptor::detectImpl receives
+// (rawImage, Frame.cc:324), converted with COLOR_BGR2GRAY (binary_descriptor.cpp:490-493;
+// OpenCV 3.2 RGB2Gray<uchar> with the BGR coefficient order: (B*1868 + G*9617 + R*4899 +
+// 2^13) >> 14) as the tile is staged -- no gray plane is written or read.
 constexpr int LB_TW = 64, LB_TH = 16;
-__global__ __launch_bounds__(256) void k_line_blur(const uint8_t* __restrict__ gray, int pitch, long long fstride,
+template <int CN>
+__global__ __launch_bounds__(256) void k_line_blur(const uint8_t* __restrict__ img, int pitch, long long fstride,
                                                    int w, int h, int k0, int k1, int k2,
                                                    uint8_t* __restrict__ blur) {
   __shared__ uint8_t in[LB_TH + 4][LB_TW + 4];
   __shared__ int hs[LB_TH + 4][LB_TW];
   const int f = blockIdx.z, x0 = blockIdx.x * LB_TW, y0 = blockIdx.y * LB_TH, t = threadIdx.x;
-  const uint8_t* G = gray + f * fstride;
+  const uint8_t* G = img + f * fstride;
   for (int i = t; i < (LB_TH + 4) * (LB_TW + 4); i += 256) {
     const int r = i / (LB_TW + 4), c = i - r * (LB_TW + 4);
-    in[r][c] = G[(long long)refl101(y0 - 2 + r, h) * pitch + refl101(x0 - 2 + c, w)];
+    const uint8_t* q = G + (long long)refl101(y0 - 2 + r, h) * pitch + (long long)refl101(x0 - 2 + c, w) * CN;
+    if (CN == 1)
+      in[r][c] = q[0];
+    else
+      in[r][c] = (uint8_t)((q[0] * 1868 + q[1] * 9617 + q[2] * 4899 + (1 << 13)) >> 14);
   }
   __syncthreads();
   for (int i = t; i < (LB_TH + 4) * LB_TW; i += 256) {
@@ -575,14 +584,16 @@ struct LineEngine {
   uint32_t *d_anch = nullptr, *d_p1 = nullptr, *d_p2 = nullptr, *d_chain = nullptr, *d_sid = nullptr,
            *d_lscr = nullptr;
   int *d_nanch = nullptr, *d_nedge = nullptr;
-  uint8_t* d_img = nullptr;
+  uint8_t* d_img = nullptr;  // [H][W * 4]: one host frame of up to 4 channels
   float* d_lines = nullptr;
   int* d_nlines = nullptr;
+  int* h_n = nullptr;  // pinned: the single-frame line count
   ~LineEngine() {
     void* p[] = {d_blur, d_dx, d_dy, d_code, d_anch, d_p1, d_p2, d_chain, d_sid, d_lscr, d_nanch, d_nedge, d_img,
                  d_lines, d_nlines};
     for (void* q : p)
       if (q) (void)hipFree(q);
+    if (h_n) (void)hipHostFree(h_n);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -655,8 +666,9 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
       hipMalloc(&e.d_sid, (size_t)(e.ecap + 1) * 4 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_nanch, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_nedge, 4 * (size_t)max_batch) != hipSuccess ||
-      hipMalloc(&e.d_img, (size_t)width * height) != hipSuccess ||
-      hipMalloc(&e.d_lines, sizeof(float) * 6 * 4096) != hipSuccess || hipMalloc(&e.d_nlines, 4) != hipSuccess) {
+      hipMalloc(&e.d_img, (size_t)width * height * 4) != hipSuccess ||
+      hipMalloc(&e.d_lines, sizeof(float) * 6 * 4096) != hipSuccess || hipMalloc(&e.d_nlines, 4) != hipSuccess ||
+      hipHostMalloc((void**)&e.h_n, sizeof(int), 0) != hipSuccess) {
     set_error("eao_lines_create: device allocation failed");
     return fail(EAO_E_HIP);
   }
@@ -669,19 +681,29 @@ int eao_lines_destroy(eao_lines* L) {
   return EAO_OK;
 }
 
-int eao_lines_detect_batch_device(eao_lines* L, const uint8_t* d_gray, int nframes, int pitch, float min_length,
-                                  float* d_lines, int32_t* d_counts, int cap, void* stream) {
-  if (!L || !d_gray || !d_lines || !d_counts || nframes < 1 || cap < 1) return EAO_E_ARG;
+int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int nframes, int pitch, int channels,
+                                        float min_length, float* d_lines, int32_t* d_counts, int cap, void* stream) {
+  if (!L || !d_img || !d_lines || !d_counts || nframes < 1 || cap < 1) return EAO_E_ARG;
   LineEngine& e = L->e;
-  if (nframes > e.B || pitch < e.W) {
-    set_error("eao_lines_detect_batch_device: more frames than max_batch or pitch < width");
+  if (channels != 1 && channels != 3 && channels != 4) {
+    set_error("eao_lines_detect: channels must be 1, 3 or 4");
+    return EAO_E_ARG;
+  }
+  if (nframes > e.B || pitch < e.W * channels) {
+    set_error("eao_lines_detect_batch_device: more frames than max_batch or pitch < width * channels");
     return EAO_E_ARG;
   }
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = stream ? (hipStream_t)stream : e.stream;
   const int W = e.W, H = e.H;
-  hipLaunchKernelGGL(k_line_blur, dim3((W + LB_TW - 1) / LB_TW, (H + LB_TH - 1) / LB_TH, nframes), dim3(256), 0, s,
-                     d_gray, pitch, (long long)pitch * H, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
+  const dim3 bg((W + LB_TW - 1) / LB_TW, (H + LB_TH - 1) / LB_TH, nframes);
+  const long long fs = (long long)pitch * H;
+  if (channels == 1)
+    hipLaunchKernelGGL(k_line_blur<1>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
+  else if (channels == 3)
+    hipLaunchKernelGGL(k_line_blur<3>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
+  else
+    hipLaunchKernelGGL(k_line_blur<4>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
   hipLaunchKernelGGL(k_line_grad, dim3((W * H + 255) / 256, nframes), dim3(256), 0, s, e.d_blur, W, H, e.d_dx,
                      e.d_dy, e.d_code);
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(256), 0, s, e.d_code, W, H, e.d_anch, e.acap, e.d_nanch);
@@ -694,19 +716,25 @@ int eao_lines_detect_batch_device(eao_lines* L, const uint8_t* d_gray, int nfram
   return EAO_OK;
 }
 
-int eao_lines_detect(eao_lines* L, const uint8_t* gray, int pitch, float min_length, float* lines, int cap,
-                     int* n_out) {
-  if (!L || !gray || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
+int eao_lines_detect_batch_device(eao_lines* L, const uint8_t* d_gray, int nframes, int pitch, float min_length,
+                                  float* d_lines, int32_t* d_counts, int cap, void* stream) {
+  return eao_lines_detect_color_batch_device(L, d_gray, nframes, pitch, 1, min_length, d_lines, d_counts, cap, stream);
+}
+
+int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length, float* lines,
+                           int cap, int* n_out) {
+  if (!L || !img || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
   LineEngine& e = L->e;
-  if (pitch < e.W) return EAO_E_ARG;
+  if ((channels != 1 && channels != 3 && channels != 4) || pitch < e.W * channels) return EAO_E_ARG;
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = e.stream;
-  EAO_HIP_CHECK(hipMemcpy2DAsync(e.d_img, e.W, gray, pitch, e.W, e.H, hipMemcpyHostToDevice, s));
-  int rc = eao_lines_detect_batch_device(L, e.d_img, 1, e.W, min_length, e.d_lines, e.d_nlines, 4096, s);
+  const int row = e.W * channels;
+  EAO_HIP_CHECK(hipMemcpy2DAsync(e.d_img, row, img, pitch, row, e.H, hipMemcpyHostToDevice, s));
+  int rc = eao_lines_detect_color_batch_device(L, e.d_img, 1, row, channels, min_length, e.d_lines, e.d_nlines, 4096, s);
   if (rc) return rc;
-  int n = 0;
-  EAO_HIP_CHECK(hipMemcpyAsync(&n, e.d_nlines, 4, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, 4, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  const int n = *e.h_n;
   if (n < 0) {
     set_error("eao_lines_detect: edge arrays overflowed (the reference's EdgeDrawing -1)");
     return EAO_E_CAPACITY;
@@ -715,6 +743,11 @@ int eao_lines_detect(eao_lines* L, const uint8_t* gray, int pitch, float min_len
   const int k = n < cap ? n : cap;
   if (k > 0) EAO_HIP_CHECK(hipMemcpy(lines, e.d_lines, sizeof(float) * 6 * k, hipMemcpyDeviceToHost));
   return n > cap ? EAO_E_CAPACITY : EAO_OK;
+}
+
+int eao_lines_detect(eao_lines* L, const uint8_t* gray, int pitch, float min_length, float* lines, int cap,
+                     int* n_out) {
+  return eao_lines_detect_color(L, gray, pitch, 1, min_length, lines, cap, n_out);
 }
 
 // the intermediate maps of the last eao_lines_detect (frame slot 0): blur [h][w] u8,

@@ -27,6 +27,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -2032,6 +2033,49 @@ class ReplayEngine {
     frame_mean(f);
   }
 
+  // LocalMapping's map-point changes (LocalBundleAdjustment SetWorldPos, MapPointCulling /
+  // KeyFrameCulling SetBadFlag, SearchInNeighbors Replace; LocalMapping.cc:60-80,
+  // MapPoint.cc:73-77,151-220) for the points the replay knows. The object code reads
+  // GetWorldPos() / isBad() live at every later read (Object.cc:967-992), so the arena copy
+  // is rewritten. Replace(pMP) leaves the object holding the old, now bad, pointer -- no
+  // membership moves -- so it arrives here as a bad flag.
+  int update_points(int n, const int32_t* ids, const float* pos, const uint8_t* bad) {
+    // a pending forest's completion (ComputeMeanAndStandard of a new object, deferred
+    // effects) must read the state the reference read when it ran the update: finish
+    // the pending forests before the first change of a known point
+    bool pend = false;
+    for (auto& up : objs) pend |= up->pending != 0;
+    for (int i = 0; pend && i < n; i++) {
+      const MapPt* p = mp_lookup(ids[i]);
+      if (!p) continue;
+      if ((pos && std::memcmp(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3) != 0) ||
+          (bad && p->bad != (bad[i] != 0))) {
+        if (int rc = flush(-1)) return rc;
+        pend = false;
+      }
+    }
+    for (int i = 0; i < n; i++) {
+      MapPt* p = mp_lookup(ids[i]);
+      if (!p) continue;  // never tracked: nothing holds it
+      if (pos) {
+        std::memcpy(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3);
+        p->proj_epoch = 0;
+      }
+      if (bad) p->bad = bad[i] != 0;
+    }
+    return EAO_OK;
+  }
+  // ids of the map points the objects hold (ascending, unique): what a LocalMapping shim
+  // snapshots after BA / culling / fuse
+  int held_points(std::vector<int32_t>& out) const {
+    out.clear();
+    for (const auto& up : objs)
+      for (const MapPt* p : up->pts) out.push_back(p->id);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+    return (int)out.size();
+  }
+
   bool overlap(Obj* a, Obj* b) {  // Object_Map::WhetherOverlap, Object.cc:1906-1922
     const float dx = (float)std::fabs(a->center_c[0] - b->center_c[0]);
     const float dy = (float)std::fabs(a->center_c[1] - b->center_c[1]);
@@ -2564,9 +2608,16 @@ class ReplayEngine {
 
 using namespace eao;
 
+// One handle is reached from the Tracking thread (eao_replay_frame) and the LocalMapping
+// thread (eao_replay_update_points / eao_replay_local_mapping, LocalMapping.cc:86-92):
+// every entry point holds the handle's lock, so the calls are serialised in the order the
+// threads take it (the reference races there; the engine's containers must not).
+// Recursive: eao_replay_run re-enters eao_replay_frame / eao_replay_local_mapping.
 struct eao_replay {
   ReplayEngine r;
+  std::recursive_mutex mu;
 };
+#define EAO_REPLAY_LOCK(r) std::lock_guard<std::recursive_mutex> eao_replay_lk_((r)->mu)
 
 extern "C" {
 
@@ -2590,6 +2641,10 @@ int eao_replay_create(eao_assoc* a, const char* flag, int img_w, int img_h, cons
 }
 
 int eao_replay_destroy(eao_replay* r) {
+  if (r) {
+    r->mu.lock();  // no call of another thread is inside the handle
+    r->mu.unlock();
+  }
   delete r;
   return EAO_OK;
 }
@@ -2600,6 +2655,7 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
   if (!r || !Tcw || n_boxes < 0 || n_pts < 0 || (n_boxes && (!boxes || !det_out)) ||
       (n_pts && (!mp_ids || !mp_pos || !kp_uv)))
     return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   const int rc = r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv,
                             mp_bad, det_out);
@@ -2610,14 +2666,37 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
                    const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
                    const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
                    const uint8_t* mp_bad, const uint8_t* keyframe, int32_t* det_out) {
+  return eao_replay_run_updates(r, n_frames, frame_ids, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv, mp_bad,
+                                keyframe, nullptr, nullptr, nullptr, nullptr, det_out);
+}
+
+int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                           const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                           const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                           const uint8_t* mp_bad, const uint8_t* keyframe, const int32_t* n_upd,
+                           const int32_t* upd_ids, const float* upd_pos, const uint8_t* upd_bad,
+                           int32_t* det_out) {
   if (!r || n_frames < 0 || (n_frames && (!frame_ids || !Tcw || !n_boxes || !n_pts || !keyframe)))
     return EAO_E_ARG;
-  size_t ob = 0, op = 0;
+  if (n_upd) {
+    for (int t = 0; t < n_frames; t++)
+      if (n_upd[t] < 0) return EAO_E_ARG;
+    for (int t = 0; t < n_frames; t++)
+      if (n_upd[t] && !upd_ids) return EAO_E_ARG;
+  }
+  EAO_REPLAY_LOCK(r);
+  size_t ob = 0, op = 0, ou = 0;
   for (int t = 0; t < n_frames; t++) {
     const int rc = eao_replay_frame(r, frame_ids[t], Tcw + 16 * (size_t)t, n_boxes[t], boxes + 5 * ob, n_pts[t],
                                     mp_ids + op, mp_pos + 3 * op, kp_uv + 2 * op, mp_bad ? mp_bad + op : nullptr,
                                     det_out + 4 * ob);
     if (rc < 0) return rc;
+    if (n_upd && n_upd[t]) {  // the frame's map-point record (LocalBA / culling / fuse)
+      const int ru = eao_replay_update_points(r, n_upd[t], upd_ids + ou, upd_pos ? upd_pos + 3 * ou : nullptr,
+                                              upd_bad ? upd_bad + ou : nullptr);
+      if (ru < 0) return ru;
+      ou += (size_t)n_upd[t];
+    }
     if (keyframe[t]) {
       const int rl = eao_replay_local_mapping(r);
       if (rl < 0) return rl;
@@ -2625,11 +2704,32 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
     ob += (size_t)n_boxes[t];
     op += (size_t)n_pts[t];
   }
+  // the stream's last forests complete here, inside the call (no work left pending for a
+  // later reader)
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
+  if (int rc = r->r.flush(-1)) return rc;
   return (int)r->r.objs.size();
+}
+
+int eao_replay_update_points(eao_replay* r, int n, const int32_t* ids, const float* pos, const uint8_t* bad) {
+  if (!r || n < 0 || (n && !ids)) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
+  return r->r.update_points(n, ids, pos, bad);
+}
+
+int eao_replay_held_points(eao_replay* r, int32_t* ids, int cap) {
+  if (!r || cap < 0 || (cap && !ids)) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  std::vector<int32_t> v;
+  const int n = r->r.held_points(v);
+  std::memcpy(ids, v.data(), sizeof(int32_t) * (size_t)std::min(n, cap));
+  return n;
 }
 
 int eao_replay_lines(eao_replay* r, int n_frames, const int32_t* n_lines, const float* lines) {
   if (!r || n_frames < 0 || (n_frames && (!n_lines || !lines))) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   for (int t = 0; t < n_frames; t++) {
     if (n_lines[t] < 0) return EAO_E_ARG;
     r->r.staged_lines.emplace_back(lines, lines + 4 * (size_t)n_lines[t]);
@@ -2640,18 +2740,21 @@ int eao_replay_lines(eao_replay* r, int n_frames, const int32_t* n_lines, const 
 
 int eao_replay_local_mapping(eao_replay* r) {
   if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   return r->r.local_mapping();
 }
 
 int eao_replay_profile(eao_replay* r, double* out12) {
   if (!r || !out12) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   std::memcpy(out12, r->r.prof, sizeof(double) * 24);
   return EAO_OK;
 }
 
 int eao_replay_profile_n(eao_replay* r, double* out, int n) {
   if (!r || !out || n < 0) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 56));
   return std::min(n, 56);
 }
@@ -2682,6 +2785,8 @@ int shard_check(eao_replay* r, int rank, int world) {
 extern "C" {
 
 int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx) {
+  if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   if (int rc = shard_check(r, rank, world)) return rc;
   if (world > 1 && !fn) return EAO_E_ARG;
   r->r.ex.reset(world > 1 ? new CallbackExchanger(fn, ctx) : nullptr);
@@ -2691,6 +2796,8 @@ int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_
 }
 
 int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* unique_id) {
+  if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   if (int rc = shard_check(r, rank, world)) return rc;
   if (!unique_id) return EAO_E_ARG;
   int rc = EAO_OK;
@@ -2704,14 +2811,21 @@ int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* uni
 
 int eao_replay_shard_stats(eao_replay* r, double* out3) {
   if (!r || !out3) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
   std::memcpy(out3, r->r.xstat, sizeof(double) * 3);
   return EAO_OK;
 }
 
-int eao_replay_num_objects(eao_replay* r) { return r ? (int)r->r.objs.size() : EAO_E_ARG; }
+int eao_replay_num_objects(eao_replay* r) {
+  if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  return (int)r->r.objs.size();
+}
 
 int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
-  if (!r || i < 0 || i >= (int)r->r.objs.size() || !ints || !floats) return EAO_E_ARG;
+  if (!r || !ints || !floats) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  if (i < 0 || i >= (int)r->r.objs.size()) return EAO_E_ARG;
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   int rc = r->r.flush(-1);
   if (rc) return rc;
@@ -2744,7 +2858,9 @@ int eao_replay_object(eao_replay* r, int i, int32_t* ints, float* floats) {
 }
 
 int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap) {
-  if (!r || i < 0 || i >= (int)r->r.objs.size()) return EAO_E_ARG;
+  if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  if (i < 0 || i >= (int)r->r.objs.size()) return EAO_E_ARG;
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   int rc = r->r.flush(-1);
   if (rc) return rc;

@@ -4,8 +4,10 @@ This is a thin harness binding used by tests/, bench.py and __graft_entry__;
 the product is the shared library eao-slam_amd/lib/libeao_accel.so. There is
 no fallback: if the library or a gfx950 device is missing, calls raise.
 """
+import atexit
 import ctypes
 import os
+import weakref
 
 import numpy as np
 
@@ -63,6 +65,43 @@ def check(rc, what):
     return rc
 
 
+# Handle lifetime: every handle keeps the destroy function it needs (no lookup through the
+# module at interpreter teardown) and is closed at exit in dependency order (replays before
+# the association engine they return their resources to).
+_open_handles = weakref.WeakSet()
+
+
+class _Handle:
+    _DESTROY = None
+    _EXIT_ORDER = 1
+    h = None
+
+    def _opened(self):
+        self._destroy = getattr(lib(), self._DESTROY)
+        _open_handles.add(self)
+
+    def close(self):
+        h = self.h
+        if h:
+            self.h = ctypes.c_void_p()
+            self._destroy(h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 -- nothing to report to at collection time
+            pass
+
+
+@atexit.register
+def _close_all():
+    for o in sorted(list(_open_handles), key=lambda x: x._EXIT_ORDER):
+        try:
+            o.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def rccl_unique_id():
     """eao_rccl_unique_id: 128-byte RCCL communicator id (one rank creates it)."""
     out = np.zeros(128, np.uint8)
@@ -83,23 +122,19 @@ def camera(w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
     return Camera(w, h, *[float(k) for k in K])
 
 
-class Orb:
+class Orb(_Handle):
     """ORBextractor replacement (reference src/ORBextractor.cc)."""
+    _DESTROY = "eao_orb_destroy"
 
     def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
                  width=640, height=480, max_batch=1, device=0):
         self.p = OrbParams(nfeatures, scale_factor, nlevels, ini_th, min_th, width, height, max_batch)
         self.h = ctypes.c_void_p()
         check(lib().eao_orb_create(ctypes.byref(self.p), device, ctypes.byref(self.h)), "eao_orb_create")
+        self._opened()
         self.nlevels = nlevels
         self.cap = check(lib().eao_orb_frame_capacity(self.h), "eao_orb_frame_capacity")
 
-    def close(self):
-        if self.h:
-            lib().eao_orb_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def scale_tables(self):
         t = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
@@ -167,19 +202,15 @@ def color_to_gray_batch_device(color_ptr, nframes, w, h, pitch, channels, rgb, g
           "eao_color_to_gray_batch_device")
 
 
-class Matcher:
+class Matcher(_Handle):
     """ORBmatcher + Frame grid replacement (reference src/ORBmatcher.cc, src/Frame.cc)."""
+    _DESTROY = "eao_matcher_destroy"
 
     def __init__(self, max_kps=4096, max_batch=2, device=0):
         self.h = ctypes.c_void_p()
         check(lib().eao_matcher_create(device, max_kps, max_batch, ctypes.byref(self.h)), "eao_matcher_create")
+        self._opened()
 
-    def close(self):
-        if self.h:
-            lib().eao_matcher_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def motion(self, cam, Tcw, th, check_ori, last_kps, has_mp, mp_pos, mp_desc, cur_kps, cur_desc, scales):
         cur_match = np.full(len(cur_kps), -1, np.int32)
@@ -293,19 +324,15 @@ class Matcher:
             v(stream) if stream else None), "eao_match_init_batch_device")
 
 
-class Pose:
+class Pose(_Handle):
     """Optimizer::PoseOptimization replacement (reference src/Optimizer.cc:243-457), monocular edges."""
+    _DESTROY = "eao_pose_destroy"
 
     def __init__(self, max_kps=4096, max_batch=1, device=0):
         self.h = ctypes.c_void_p()
         check(lib().eao_pose_create(device, max_kps, max_batch, ctypes.byref(self.h)), "eao_pose_create")
+        self._opened()
 
-    def close(self):
-        if self.h:
-            lib().eao_pose_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def optimize(self, cam, Tcw, kps_un, has_mp, mp_pos, inv_level_sigma2, outlier=None):
         """-> (n_inliers, Tcw_out [4][4] float32, outlier u8[n])."""
@@ -332,10 +359,11 @@ class Pose:
               "eao_pose_optimization_batch_device")
 
 
-class Vocab:
+class Vocab(_Handle):
     """DBoW2 ORB vocabulary on the GPU: ComputeBoW's transform and SearchByBoW
     (reference Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1139-1271, src/ORBmatcher.cc:159-288).
     voc: dict with desc [n][32] u8, parent i32, word i32, weight f64, L (tools/synth.vocabulary)."""
+    _DESTROY = "eao_vocab_destroy"
 
     def __init__(self, voc, max_kps=4096, max_batch=1, device=0):
         self.h = ctypes.c_void_p()
@@ -344,13 +372,8 @@ class Vocab:
         check(lib().eao_vocab_create(device, len(a["parent"]), P(a["desc"]), P(a["parent"]), P(a["word"]),
                                      P(a["weight"]), int(voc["L"]), max_kps, max_batch, ctypes.byref(self.h)),
               "eao_vocab_create")
+        self._opened()
 
-    def close(self):
-        if self.h and _lib is not None:
-            _lib.eao_vocab_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def transform(self, desc, levelsup=4):
         """-> (word_ids, word_weights, node_ids, node_start, node_feats)."""
@@ -393,21 +416,17 @@ class Vocab:
                                                    v(stream) if stream else None), "eao_search_by_bow_batch_device")
 
 
-class Lines:
+class Lines(_Handle):
     """Per-frame line detection (line_lbd_detect::detect_raw_lines + filter_lines,
     reference src/Frame.cc:324-328) on the GPU."""
+    _DESTROY = "eao_lines_destroy"
 
     def __init__(self, w=640, h=480, max_batch=1, device=0):
         self.h = ctypes.c_void_p()
         self.w, self.hh = w, h
         check(lib().eao_lines_create(device, w, h, max_batch, ctypes.byref(self.h)), "eao_lines_create")
+        self._opened()
 
-    def close(self):
-        if self.h:
-            lib().eao_lines_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def detect(self, gray, min_length=50.0, cap=4096):
         """[n][6] float32: (startX, startY, endX, endY, angle, lineLength)."""
@@ -417,6 +436,25 @@ class Lines:
         check(lib().eao_lines_detect(self.h, P(g8), g8.shape[1], ctypes.c_float(min_length), P(out), cap,
                                      ctypes.byref(n)), "eao_lines_detect")
         return out[:n.value].copy()
+
+    def detect_color(self, img, min_length=50.0, cap=4096):
+        """eao_lines_detect_color: the colour frame ([h][w][3 or 4] BGR bytes, rawImage) converted with
+        COLOR_BGR2GRAY inside the blur kernel, as BinaryDescriptor::detectImpl does."""
+        a = np.ascontiguousarray(img, np.uint8)
+        cn = 1 if a.ndim == 2 else a.shape[2]
+        out = np.zeros((cap, 6), np.float32)
+        n = ctypes.c_int()
+        check(lib().eao_lines_detect_color(self.h, P(a), a.shape[1] * cn, cn, ctypes.c_float(min_length), P(out), cap,
+                                           ctypes.byref(n)), "eao_lines_detect_color")
+        return out[:n.value].copy()
+
+    def detect_color_batch_device(self, img_ptr, nframes, pitch, channels, min_length, lines_ptr, counts_ptr, cap,
+                                  stream=None):
+        v = ctypes.c_void_p
+        check(lib().eao_lines_detect_color_batch_device(self.h, v(img_ptr), nframes, pitch, channels,
+                                                        ctypes.c_float(min_length), v(lines_ptr), v(counts_ptr), cap,
+                                                        v(stream) if stream else None),
+              "eao_lines_detect_color_batch_device")
 
     def debug_maps(self):
         blur = np.zeros((self.hh, self.w), np.uint8)
@@ -432,19 +470,15 @@ class Lines:
               "eao_lines_detect_batch_device")
 
 
-class Assoc:
+class Assoc(_Handle):
     """Object_2D / Object_Map math replacement (reference src/Object.cc, isolation_forest.h)."""
+    _DESTROY = "eao_assoc_destroy"
 
     def __init__(self, max_points=65536, device=0):
         self.h = ctypes.c_void_p()
         check(lib().eao_assoc_create(device, max_points, ctypes.byref(self.h)), "eao_assoc_create")
+        self._opened()
 
-    def close(self):
-        if self.h:
-            lib().eao_assoc_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def np_batch(self, frame_sets, obj_sets):
         """frame_sets/obj_sets: lists of (pts (n,3) f32, valid (n,) u8 or None)."""
@@ -488,10 +522,12 @@ class Assoc:
         return rect, ok
 
 
-class Replay:
+class Replay(_Handle):
     """Deterministic association replay on the engine:
     the object section of Tracking::TrackWithMotionModel + LocalMapping object
     maintenance, with NP / iForest / projected rects on the GPU."""
+    _DESTROY = "eao_replay_destroy"
+    _EXIT_ORDER = 0
 
     def __init__(self, assoc, flag="iForest", w=640, h=480, K=(535.4, 539.2, 320.1, 247.6)):
         self.assoc = assoc
@@ -499,13 +535,8 @@ class Replay:
         K4 = np.asarray(K, np.float32)
         check(lib().eao_replay_create(assoc.h, flag.encode(), w, h, P(K4), ctypes.byref(self.h)),
               "eao_replay_create")
+        self._opened()
 
-    def close(self):
-        if self.h:
-            lib().eao_replay_destroy(self.h)
-            self.h = ctypes.c_void_p()
-
-    __del__ = close
 
     def lines(self, sets):
         """Stage frame line segments (eao_replay_lines): a list of (L, 4) arrays, one per upcoming frame."""
@@ -529,6 +560,29 @@ class Replay:
 
     def local_mapping(self):
         check(lib().eao_replay_local_mapping(self.h), "eao_replay_local_mapping")
+
+    def update_points(self, ids, pos=None, bad=None):
+        """eao_replay_update_points: LocalMapping's map-point changes (BA positions, culled /
+        replaced points as bad) for the points the replay holds."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        pos = None if pos is None else np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        bad = None if bad is None else np.ascontiguousarray(bad, np.uint8)
+        check(lib().eao_replay_update_points(self.h, len(ids), P(ids), P(pos), P(bad)), "eao_replay_update_points")
+
+    def held_points(self):
+        n = check(lib().eao_replay_held_points(self.h, None, 0), "eao_replay_held_points")
+        ids = np.zeros(max(1, n), np.int32)
+        n = check(lib().eao_replay_held_points(self.h, P(ids), len(ids)), "eao_replay_held_points")
+        return ids[:n].copy()
+
+    def step(self, fid, f):
+        """One frame of a stream dict (tools/synth): the frame, its map-point record, its local mapping."""
+        out = self.frame(fid, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        if "upd_ids" in f:
+            self.update_points(f["upd_ids"], f["upd_pos"], f["upd_bad"])
+        if f["kf"]:
+            self.local_mapping()
+        return out
 
     ALLGATHER = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -575,13 +629,32 @@ class Replay:
             uv=np.ascontiguousarray(np.concatenate([f["uv"] for f in frames]), np.float32),
             bad=np.ascontiguousarray(np.concatenate([f["bad"] for f in frames]), np.uint8),
             kf=np.array([1 if f["kf"] else 0 for f in frames], np.uint8),
-            lines=[f["lines"] for f in frames] if all("lines" in f for f in frames) else None)
+            lines=[f["lines"] for f in frames] if all("lines" in f for f in frames) else None,
+            **Replay._pack_updates(frames))
+
+    @staticmethod
+    def _pack_updates(frames):
+        """The frames' map-point records (keys upd_ids / upd_pos / upd_bad), if any frame has one."""
+        if not any("upd_ids" in f for f in frames):
+            return {}
+        z = (np.zeros(0, np.int32), np.zeros((0, 3), np.float32), np.zeros(0, np.uint8))
+        rec = [(f["upd_ids"], f["upd_pos"], f["upd_bad"]) if "upd_ids" in f else z for f in frames]
+        return dict(nupd=np.array([len(r[0]) for r in rec], np.int32),
+                    upd_ids=np.ascontiguousarray(np.concatenate([r[0] for r in rec]), np.int32),
+                    upd_pos=np.ascontiguousarray(np.concatenate([np.reshape(r[1], (-1, 3)) for r in rec]), np.float32),
+                    upd_bad=np.ascontiguousarray(np.concatenate([r[2] for r in rec]), np.uint8))
 
     def run(self, pk):
         """eao_replay_run over a packed stream; returns det_out (total boxes x 4)."""
         out = np.zeros((int(pk["nb"].sum()), 4), np.int32)
         if pk.get("lines") is not None:
             self.lines(pk["lines"])
+        if "nupd" in pk:
+            check(lib().eao_replay_run_updates(
+                self.h, pk["n"], P(pk["ids"]), P(pk["T"]), P(pk["nb"]), P(pk["boxes"]), P(pk["npt"]), P(pk["mp"]),
+                P(pk["pos"]), P(pk["uv"]), P(pk["bad"]), P(pk["kf"]), P(pk["nupd"]), P(pk["upd_ids"]),
+                P(pk["upd_pos"]), P(pk["upd_bad"]), P(out)), "eao_replay_run_updates")
+            return out
         check(lib().eao_replay_run(self.h, pk["n"], P(pk["ids"]), P(pk["T"]), P(pk["nb"]), P(pk["boxes"]),
                                    P(pk["npt"]), P(pk["mp"]), P(pk["pos"]), P(pk["uv"]), P(pk["bad"]), P(pk["kf"]),
                                    P(out)), "eao_replay_run")

@@ -13,6 +13,12 @@
  * (inputs resident in HBM) and a hipStream_t passed as void* (NULL = the
  * handle's own stream). All other functions take host pointers.
  *
+ * Streams and scratch: a handle's calls (batched or single-frame) use scratch
+ * owned by the handle, whatever stream they are given. Calls on one handle must
+ * be ordered on one stream (or synchronised by the caller between streams); use
+ * one handle per concurrently used stream. Single-frame calls run on the handle's
+ * own stream and return after it drains.
+ *
  * The engine has NO CPU fallback: without a usable gfx950 device every call
  * returns EAO_E_NODEVICE.
  */
@@ -235,6 +241,18 @@ int eao_lines_detect_batch_device(eao_lines* l, const uint8_t* d_gray, int nfram
 /* one host frame; returns EAO_E_CAPACITY when more than cap lines (n_out holds the count) */
 int eao_lines_detect(eao_lines* l, const uint8_t* gray, int pitch, float min_length, float* lines, int cap,
                      int* n_out);
+/* BinaryDescriptor::detectImpl's own input: the colour frame the EAO Frame ctor hands to
+   detect_raw_lines (rawImage, src/Frame.cc:324; src/Tracking.cc:340,389), channels = 3 or 4
+   interleaved bytes in imread's BGR order, converted with COLOR_BGR2GRAY whatever Camera.RGB says
+   (src/line_detect/libs/binary_descriptor.cpp:490-495; OpenCV 3.2 RGB2Gray<uchar>,
+   (B*1868 + G*9617 + R*4899 + 2^13) >> 14) -- not the tracker's mImGray when mbRGB = 1 (SURVEY
+   Q20). The conversion is fused into the blur kernel's tile load (no gray plane). channels = 1 is
+   eao_lines_detect. pitch in bytes (>= width * channels). */
+int eao_lines_detect_color(eao_lines* l, const uint8_t* img, int pitch, int channels, float min_length,
+                           float* lines, int cap, int* n_out);
+int eao_lines_detect_color_batch_device(eao_lines* l, const uint8_t* d_img, int nframes, int pitch, int channels,
+                                        float min_length, float* d_lines, int32_t* d_counts, int cap,
+                                        void* stream);
 /* maps of the last eao_lines_detect: blur u8, Sobel dx / dy i16, code u16 = thresholded
    (|dx| + |dy|) / 4 | 0x8000 when |dx| < |dy| (Horizontal); NULL skips an output */
 int eao_lines_debug_maps(eao_lines* l, uint8_t* blur, int16_t* dx, int16_t* dy, uint16_t* code);
@@ -309,6 +327,35 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
                    const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
                    const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
                    const uint8_t* mp_bad, const uint8_t* keyframe, int32_t* det_out);
+/* LocalMapping's map-point changes for the points the association holds, applied in place:
+   LocalBundleAdjustment's SetWorldPos (src/Optimizer.cc LocalBundleAdjustment ->
+   src/MapPoint.cc:73-77), MapPointCulling / KeyFrameCulling's SetBadFlag (src/MapPoint.cc:151-167)
+   and SearchInNeighbors' Replace (src/MapPoint.cc:175-220; the object keeps the old, now bad,
+   point: Replace moves no object membership, so a replaced point is passed as bad = 1).
+   pos [n][3] = GetWorldPos(), bad [n] = isBad(); either may be NULL to leave that field. Ids the
+   replay never saw are ignored. The object code re-reads these at every later read
+   (Object_Map::ComputeMeanAndStandard, src/Object.cc:967-992, called by LocalMapping::UpdateObject,
+   src/LocalMapping.cc:772-795; NP tests, projected rects, forests, duplicate checks). The shim
+   calls it from LocalMapping after LocalBA / KeyFrameCulling and before eao_replay_local_mapping
+   (src/LocalMapping.cc:70-90). */
+int eao_replay_update_points(eao_replay* r, int n, const int32_t* ids, const float* pos, const uint8_t* bad);
+/* the ids of the map points the objects hold (ascending, unique): min(count, cap) written,
+   count returned -- the set whose state a LocalMapping shim snapshots for the call above */
+int eao_replay_held_points(eao_replay* r, int32_t* ids, int cap);
+/* eao_replay_run with each frame's map-point record (the trace of SURVEY appendix B extended by
+   LocalMapping's point changes): after frame t, the next n_upd[t] entries of upd_ids / upd_pos /
+   upd_bad are applied as eao_replay_update_points, then eao_replay_local_mapping when keyframe[t].
+   n_upd NULL = no records (eao_replay_run). Every forest of the stream has completed on return. */
+int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                           const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                           const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                           const uint8_t* mp_bad, const uint8_t* keyframe, const int32_t* n_upd,
+                           const int32_t* upd_ids, const float* upd_pos, const uint8_t* upd_bad,
+                           int32_t* det_out);
+/* Threading: every eao_replay_* call holds the handle's lock, so the Tracking thread
+   (eao_replay_frame) and the LocalMapping thread (eao_replay_update_points,
+   eao_replay_local_mapping) may share one handle; the replayed order is the order in which the
+   calls take the lock. */
 int eao_replay_num_objects(eao_replay* r);
 /* ints[8]: id, class, bad, #frames, #points, last add, #co-association votes, #co-views;
    floats[20]: center[3], sigma[3], sigma of frame centers[3], cuboid lenth/width/height,
@@ -432,7 +479,9 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
    keypoints / descriptors / valid flags / node ids / node features, [nsearch][cap + 1] node starts,
    per-search node counts d_kf_nn / d_f_nn and frame feature counts d_n_f); writes
    d_f_match [nsearch][cap] and d_nmatches [nsearch] (EAO_E_CAPACITY for a search in which a
-   vocabulary node holds more than 1024 frame features). nsearch <= max_batch. */
+   vocabulary node holds more than 1024 frame features). nsearch <= max_batch. Preconditions the
+   device path does not check (eao_search_by_bow checks them on the host): node ids ascending,
+   node starts non-decreasing from 0, every listed feature index in [0, count) of its side. */
 int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, int nsearch, int cap,
                                    const eao_keypoint* d_kf_kps, const uint8_t* d_kf_desc,
                                    const uint8_t* d_kf_mp_valid, const int32_t* d_kf_nn,

@@ -1687,6 +1687,23 @@ int orc_replay_local_mapping(orc_replay* r) {
   r->r.local_mapping();
   return 0;
 }
+// LocalMapping's map-point changes (LocalBundleAdjustment SetWorldPos, MapPointCulling /
+// KeyFrameCulling SetBadFlag, SearchInNeighbors Replace -- LocalMapping.cc:60-80,
+// MapPoint.cc:73-77,151-220) for points the replay knows. The object code reads them
+// live: GetWorldPos() / isBad() at every later ComputeMeanAndStandard (Object.cc:967-992),
+// NP test, projected rect, forest and duplicate check. Replace(pMP) leaves the object
+// holding the old, now bad, pointer (no membership transfer), so it is a bad flag here.
+int orc_replay_update_points(orc_replay* r, int n, const int32_t* ids, const float* pos, const uint8_t* bad) {
+  for (int i = 0; i < n; i++) {
+    auto it = r->r.mps.find(ids[i]);
+    if (it == r->r.mps.end()) continue;  // never tracked: no object or detection holds it
+    MapPoint* p = it->second;
+    if (pos)
+      for (int a = 0; a < 3; a++) p->pos[a] = pos[3 * i + a];
+    if (bad) p->bad = bad[i] != 0;
+  }
+  return 0;
+}
 int orc_replay_num_objects(orc_replay* r) { return (int)r->r.objs.size(); }
 int orc_replay_object(orc_replay* r, int i, int32_t* ints, float* floats) {
   if (i < 0 || i >= (int)r->r.objs.size()) return -1;

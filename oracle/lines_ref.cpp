@@ -557,4 +557,22 @@ int orc_edlines(const uint8_t* gray, int w, int h, float min_length, float* out,
   return n > cap ? -2 : 0;
 }
 
+// BinaryDescriptor::detectImpl's input conversion (src/line_detect/libs/binary_descriptor.cpp:490-495):
+// a frame with channels != 1 -- the colour rawImage of the EAO Frame ctor (src/Frame.cc:324,
+// src/Tracking.cc:340,389) -- is converted with COLOR_BGR2GRAY whatever Camera.RGB says (so not
+// the tracker's mImGray when mbRGB): OpenCV 3.2 RGB2Gray<uchar> in the BGR coefficient
+// order, orb_ref.cpp's orc_color_to_gray with rgb = 0. Then orc_edlines on that gray.
+int orc_edlines_color(const uint8_t* img, int w, int h, int pitch, int cn, float min_length, float* out, int cap,
+                      int* n_out) {
+  std::vector<uint8_t> gray((size_t)w * h);
+  if (cn == 1) {
+    for (int y = 0; y < h; y++) std::memcpy(&gray[(size_t)y * w], img + (size_t)y * pitch, w);
+  } else if (cn == 3 || cn == 4) {
+    orc_color_to_gray(img, w, h, pitch, cn, 0, gray.data());
+  } else {
+    return -3;
+  }
+  return orc_edlines(gray.data(), w, h, min_length, out, cap, n_out);
+}
+
 }  // extern "C"

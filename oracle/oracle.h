@@ -160,6 +160,9 @@ int orc_replay_frame(orc_replay* r, int frame_id, const float* Tcw,
                      const uint8_t* mp_bad,
                      int32_t* det_out /* n_boxes*4: outcome, obj id, class, npoints */);
 int orc_replay_local_mapping(orc_replay* r);
+/* map-point changes of LocalMapping (BA positions, culling / replacement as bad flags) for
+   the points with the given ids; pos (n x 3) or bad (n) may be NULL to leave that field */
+int orc_replay_update_points(orc_replay* r, int n, const int32_t* ids, const float* pos, const uint8_t* bad);
 int orc_replay_num_objects(orc_replay* r);
 /* per object summary: id, class, bad, nframes, npts, center[3], std[3], cstd[3],
    cuboid extents lenth/width/height, rmax, last_add, rect_project[4] */
@@ -177,6 +180,10 @@ int orc_line_maps(const uint8_t* gray, int w, int h, uint8_t* blur, int16_t* dx,
 int orc_edge_chains(const uint8_t* gray, int w, int h, uint32_t* xy, int cap_px, uint32_t* sid, int cap_edges,
                     int* n_px, int* n_edges);
 int orc_edlines(const uint8_t* gray, int w, int h, float min_length, float* out, int cap, int* n_out);
+/* the same on the colour frame BinaryDescriptor::detectImpl receives: cn = 3 / 4 bytes per pixel
+   converted with COLOR_BGR2GRAY first (binary_descriptor.cpp:490-495); cn = 1 is gray */
+int orc_edlines_color(const uint8_t* img, int w, int h, int pitch, int cn, float min_length, float* out, int cap,
+                      int* n_out);
 
 /* ---- Optimizer::PoseOptimization, monocular edges (src/Optimizer.cc:243-457) ----
    Tcw 4x4 row-major float (pFrame->mTcw); kps = mvKeysUn; has_mp[i] = mvpMapPoints[i] != 0;

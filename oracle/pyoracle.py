@@ -57,7 +57,7 @@ def lib():
         _lib.orc_extract_match_mt.restype = ctypes.c_double
         _lib.orc_replay_destroy.argtypes = [ctypes.c_void_p]
         for f in ("orc_replay_frame", "orc_replay_local_mapping", "orc_replay_num_objects",
-                  "orc_replay_object", "orc_replay_object_points"):
+                  "orc_replay_object", "orc_replay_object_points", "orc_replay_update_points"):
             getattr(_lib, f).argtypes = None
     return _lib
 
@@ -310,6 +310,22 @@ class Replay:
     def local_mapping(self):
         lib().orc_replay_local_mapping(ctypes.c_void_p(self.h))
 
+    def update_points(self, ids, pos=None, bad=None):
+        """LocalMapping's map-point changes (BA positions, culled / replaced points as bad)."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        pos = None if pos is None else np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        bad = None if bad is None else np.ascontiguousarray(bad, np.uint8)
+        lib().orc_replay_update_points(ctypes.c_void_p(self.h), len(ids), P(ids), P(pos), P(bad))
+
+    def step(self, fid, f):
+        """One frame of a stream dict (synth): the frame, its map-point record, its local mapping."""
+        out = self.frame(fid, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        if "upd_ids" in f:
+            self.update_points(f["upd_ids"], f["upd_pos"], f["upd_bad"])
+        if f["kf"]:
+            self.local_mapping()
+        return out
+
     def objects(self):
         n = lib().orc_replay_num_objects(ctypes.c_void_p(self.h))
         ints = np.zeros((n, 8), np.int32)
@@ -354,6 +370,19 @@ def edlines(gray, min_length=50.0, cap=4096):
     out = np.zeros((cap, 6), np.float32)
     n = ctypes.c_int()
     rc = lib().orc_edlines(P(g8), w, h, ctypes.c_float(min_length), P(out), cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return out[:n.value].copy()
+
+
+def edlines_color(img, min_length=50.0, cap=4096):
+    """The same on the colour frame detectImpl receives ([h][w][3 or 4] BGR bytes, converted with
+    COLOR_BGR2GRAY first; [h][w] is gray)."""
+    a = np.ascontiguousarray(img, np.uint8)
+    h, w = a.shape[:2]
+    cn = 1 if a.ndim == 2 else a.shape[2]
+    out = np.zeros((cap, 6), np.float32)
+    n = ctypes.c_int()
+    rc = lib().orc_edlines_color(P(a), w, h, w * cn, cn, ctypes.c_float(min_length), P(out), cap, ctypes.byref(n))
     assert rc == 0, rc
     return out[:n.value].copy()
 

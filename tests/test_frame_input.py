@@ -35,6 +35,11 @@ def test_yolo_parse_int_semantics_and_order():
     # a short row's missing fields read as 0; a bad token ends the row; CRLF and no final newline
     assert ea.yolo_parse("7 8 9\r\n4 5 x 6\r\n3 1 1 1 1 2").tolist() == [[3, 1, 1, 1, 1, 2], [7, 8, 9, 0, 0, 0],
                                                                        [4, 5, 0, 0, 0, 0]]
+    # a sign right after digits starts the next extraction ("2-3" reads 2, then -3); a lone sign
+    # fails it and ends the row
+    assert ea.yolo_parse("1 2-3 4 5 6\n").tolist() == [[1, 2, -3, 4, 5, 6]]
+    assert ea.yolo_parse("5+3 1 1 1 1\n").tolist() == [[5, 3, 1, 1, 1, 1]]
+    assert ea.yolo_parse("1 2+ 3 4 5 6\n").tolist() == [[1, 2, 0, 0, 0, 0]]
     # std::sort by score, descending; <= 16 equal scores keep the file order (insertion sort)
     rows = [[c, c, 0, 1, 1, 0] for c in range(15)]
     txt = "".join("%d %d %d %d %d 0.5\n" % tuple(r[:5]) for r in rows)

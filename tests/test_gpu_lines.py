@@ -76,3 +76,46 @@ def test_lines_batch_device(frames):
     for t in range(F):
         o = orc.edlines(frames[t])
         assert hc[t] == len(o) and np.array_equal(ho[t, :hc[t]], o), t
+
+
+def color_frames(frames):
+    """BGR frames whose COLOR_BGR2GRAY keeps the edges (B = 255 - g, G = R = g) while the RGB
+    code would give another gray: the conversion order is exercised."""
+    return [np.ascontiguousarray(np.stack([255 - f, f, f], 2)) for f in frames]
+
+
+def test_lines_color_exact(frames):
+    """The EAO Frame ctor hands the colour rawImage to detect_raw_lines; detectImpl converts it
+    with COLOR_BGR2GRAY (binary_descriptor.cpp:490-495). The engine fuses that conversion into
+    the blur: colour in, lines bit-exact with the oracle's BGR2GRAY + EDLine."""
+    L = ea.Lines()
+    tot = 0
+    for c in color_frames(frames):
+        g = L.detect_color(c)
+        o = orc.edlines_color(c)
+        assert g.shape == o.shape and np.array_equal(g, o)
+        blur, _, _, _ = L.debug_maps()
+        assert np.array_equal(blur, orc.line_maps(orc.color_to_gray(c, rgb=False))[0])
+        tot += len(o)
+        # 4-channel (BGRA) input: the same conversion of the first three bytes
+        c4 = np.ascontiguousarray(np.concatenate([c, np.full(c.shape[:2] + (1,), 9, np.uint8)], 2))
+        assert np.array_equal(L.detect_color(c4), o)
+    assert tot > 50
+
+
+def test_lines_color_batch_device(frames):
+    import torch
+    cf = color_frames(frames)
+    F = len(cf)
+    dev = torch.device("cuda", 0)
+    L = ea.Lines(max_batch=F)
+    d = torch.from_numpy(np.ascontiguousarray(np.stack(cf))).to(dev)
+    cap = 256
+    out = torch.zeros((F, cap, 6), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    L.detect_color_batch_device(d.data_ptr(), F, 640 * 3, 3, 50.0, out.data_ptr(), cnt.data_ptr(), cap)
+    torch.cuda.synchronize()
+    ho, hc = out.cpu().numpy(), cnt.cpu().numpy()
+    for t in range(F):
+        o = orc.edlines_color(cf[t])
+        assert hc[t] == len(o) and np.array_equal(ho[t, :hc[t]], o), t

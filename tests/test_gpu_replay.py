@@ -71,3 +71,65 @@ def test_replay_run_stream_matches_per_frame_oracle():
     oi, of, op = o.objects()
     assert np.array_equal(gi, oi)
     assert np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+
+
+def _run_steps(flag, frames, start=1):
+    """frame + map-point record + local mapping per frame, engine vs oracle (step())."""
+    g = ea.Replay(ea.Assoc(), flag)
+    o = orc.Replay(flag)
+    for i, f in enumerate(frames):
+        og, oo = g.step(i + start, f), o.step(i + start, f)
+        assert np.array_equal(og, oo), "frame %d: %s vs %s" % (i, og.tolist(), oo.tolist())
+    gi, gf, gp = g.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi)
+    assert np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert all(np.array_equal(a_, b_) for a_, b_ in zip(gp, op))
+    return g, oi
+
+
+def test_replay_point_updates_fr3_eao_405():
+    """The drop-in boundary's LocalMapping channel: on the fr3 demo stream (real boxes, EAO),
+    every keyframe moves (LocalBA), culls and replaces points the objects hold, most of them
+    not observed by that frame (eao_replay_update_points); ids, statistics and point sets
+    identical to the oracle."""
+    frames = synth.with_point_updates(synth.assoc_stream_fr3_real())
+    held_unobserved = 0
+    g = ea.Replay(ea.Assoc(), "EAO")
+    o = orc.Replay("EAO")
+    for i, f in enumerate(frames):
+        if len(f["upd_ids"]):
+            held = set(g.held_points().tolist())
+            held_unobserved += len((set(f["upd_ids"].tolist()) & held) - set(f["ids"].tolist()))
+        og, oo = g.step(i + 1, f), o.step(i + 1, f)
+        assert np.array_equal(og, oo), "frame %d: %s vs %s" % (i, og.tolist(), oo.tolist())
+    assert held_unobserved > 1000
+    gi, gf, gp = g.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi)
+    assert np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert all(np.array_equal(a_, b_) for a_, b_ in zip(gp, op))
+
+
+def test_replay_point_updates_fr3_full_slice():
+    """Full flag (iForest + lines + yaw + LocalMapping merges) over the first 600 frames of the
+    Full list with the per-keyframe point records."""
+    _run_steps("Full", synth.with_point_updates(synth.assoc_stream_fr3_real(0, 600), seed=0xEA9))
+
+
+def test_replay_run_updates_packed():
+    """eao_replay_run_updates: the recorded stream with its point records in one call."""
+    frames = synth.with_point_updates(synth.assoc_stream_fr3_real()[:200], seed=7)
+    g = ea.Replay(ea.Assoc(), "EAO")
+    det = g.run(ea.Replay.pack(frames))
+    o = orc.Replay("EAO")
+    ref = np.concatenate([o.step(i + 1, f) for i, f in enumerate(frames)])
+    assert np.array_equal(det, ref)
+    gi, gf, _ = g.objects()
+    oi, of, _ = o.objects()
+    assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+
+
+def test_replay_none_flag_fr3_405():
+    """BASELINE configs[0]'s flag (None: no iForest, no yaw) on the fr3 demo stream."""
+    _run_steps("None", synth.assoc_stream_fr3_real())

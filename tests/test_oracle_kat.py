@@ -315,3 +315,19 @@ def test_line_oracle_properties():
     # region of v blurs to (257^2 v + 2^15) >> 16
     assert blur[240, 320] == (257 * 257 * 200 + (1 << 15)) >> 16 and blur[20, 20] == (257 * 257 * 40 + (1 << 15)) >> 16
     assert dx[240, 200] > 0 and dy[150, 300] > 0  # dark -> bright steps
+
+
+def test_line_oracle_color_input():
+    """detectImpl's COLOR_BGR2GRAY (binary_descriptor.cpp:490-495): the colour entry equals the
+    BGR-code conversion followed by the gray detector, and differs from the RGB code's gray."""
+    import pyoracle as orc
+    from tools import synth
+    g = synth.line_frames(1, seed=0xEA7)[0]
+    c = np.ascontiguousarray(np.stack([255 - g, g, g], 2))
+    bgr = orc.color_to_gray(c, rgb=False)
+    assert np.array_equal(orc.edlines_color(c), orc.edlines(bgr))
+    assert np.array_equal(orc.edlines_color(g), orc.edlines(g))
+    assert not np.array_equal(bgr, orc.color_to_gray(c, rgb=True))
+    # OpenCV's fixed-point BGR2GRAY on a few pixels, restated independently
+    b, gg, r = c[..., 0].astype(np.int64), c[..., 1].astype(np.int64), c[..., 2].astype(np.int64)
+    assert np.array_equal(bgr, ((b * 1868 + gg * 9617 + r * 4899 + (1 << 13)) >> 14).astype(np.uint8))

@@ -61,6 +61,15 @@ class _HostReplay(ea.Replay):
     def objects(self):
         return self._with(super().objects)
 
+    def step(self, *a):
+        return self._with(super().step, *a)
+
+    def update_points(self, *a):
+        return self._with(super().update_points, *a)
+
+    def held_points(self):
+        return self._with(super().held_points)
+
     def close(self):
         if self.h:
             self.H.eao_replay_destroy(self.h)
@@ -124,3 +133,91 @@ def test_host_fr3_real_stream_matches_oracle(harness, flag):
     oi, of, op = o.objects()
     assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
     assert all(np.array_equal(x, y) for x, y in zip(gp, op))
+
+
+def _compare(g, o):
+    gi, gf, gp = g.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert all(np.array_equal(x, y) for x, y in zip(gp, op))
+    return oi, of
+
+
+@pytest.mark.parametrize("flag", ["EAO", "Full"])
+def test_host_point_updates_match_oracle(harness, flag):
+    """LocalMapping's map-point record (eao_replay_update_points): at every keyframe points the
+    objects hold -- most of them not observed by that frame -- move (LocalBA), are culled or
+    replaced (bad); ids and statistics identical to the oracle, frame by frame."""
+    frames = synth.with_point_updates(synth.assoc_stream_fr3_real()[:150])
+    g = _HostReplay(harness, flag)
+    o = orc.Replay(flag)
+    held_unobserved = 0
+    for i, f in enumerate(frames):
+        if len(f["upd_ids"]):
+            held = set(g.held_points().tolist())
+            held_unobserved += len((set(f["upd_ids"].tolist()) & held) - set(f["ids"].tolist()))
+        og, oo = g.step(i + 1, f), o.step(i + 1, f)
+        assert np.array_equal(og, oo), (i, og.tolist(), oo.tolist())
+    assert held_unobserved > 100  # the record reaches points no frame re-reported
+    oi, of = _compare(g, o)
+    # the record matters: without it the object statistics come out differently
+    o2 = orc.Replay(flag)
+    for i, f in enumerate(frames):
+        o2.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        if f["kf"]:
+            o2.local_mapping()
+    i2, f2, _ = o2.objects()
+    assert not (np.array_equal(i2, oi) and np.allclose(f2, of, rtol=1e-6, atol=1e-7, equal_nan=True))
+
+
+def test_host_run_updates_matches_oracle(harness):
+    """eao_replay_run_updates (packed stream with the per-frame point records) == the oracle."""
+    frames = synth.with_point_updates(synth.assoc_stream_fr3(60, seed=0xEA6), seed=5)
+    g = _HostReplay(harness, "EAO")
+    det = g._with(ea.Replay.run, g, ea.Replay.pack(frames))
+    o = orc.Replay("EAO")
+    ref = [o.step(i + 1, f) for i, f in enumerate(frames)]
+    assert np.array_equal(det, np.concatenate(ref))
+    _compare(g, o)
+
+
+def test_host_two_threads_share_one_handle(harness):
+    """The Tracking thread replays frames while a LocalMapping thread polls the handle
+    (held_points, update_points with unchanged state, num_objects) with no ordering: the
+    handle's lock keeps the containers whole and the outcome equals the serial oracle."""
+    import threading
+    frames = synth.assoc_stream_fr3_real()[:80]
+    g = _HostReplay(harness, "EAO")
+    stop = threading.Event()
+    errors = []
+
+    H = harness  # called directly: _HostReplay._with swaps a module global, not thread-safe
+
+    def local_mapping_thread():
+        try:
+            buf = np.zeros(1 << 16, np.int32)
+            while not stop.is_set():
+                n = H.eao_replay_held_points(g.h, ea.P(buf), len(buf))
+                assert n >= 0
+                ids = buf[:min(n, 64)].copy()
+                pos = np.zeros((len(ids), 3), np.float32)
+                # an empty record, then a record of nothing the replay knows (ids < 0)
+                assert H.eao_replay_update_points(g.h, 0, ea.P(ids), None, None) == 0
+                neg = -1 - ids
+                assert H.eao_replay_update_points(g.h, len(neg), ea.P(neg), ea.P(pos), None) == 0
+                assert H.eao_replay_num_objects(g.h) >= 0
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = threading.Thread(target=local_mapping_thread)
+    th.start()
+    try:
+        dets = [g.step(i + 1, f) for i, f in enumerate(frames)]
+    finally:
+        stop.set()
+        th.join()
+    assert not errors
+    o = orc.Replay("EAO")
+    ref = [o.step(i + 1, f) for i, f in enumerate(frames)]
+    assert all(np.array_equal(a, b) for a, b in zip(dets, ref))
+    _compare(g, o)

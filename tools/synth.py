@@ -457,6 +457,59 @@ def assoc_stream_fr3_real(start=None, n_frames=None, seed=0xEA1, K=TUM3_K, w=640
     return frames
 
 
+def with_point_updates(frames, seed=0xEA8, move_frac=0.3, sigma=0.004, cull_frac=0.01, replace_frac=0.01,
+                       window=60):
+    """LocalMapping's map-point changes on a replay stream (the trace of SURVEY appendix B plus a
+    per-frame point record, eao_replay_update_points). At every keyframe, among the points seen
+    in the last `window` frames (so most are held by objects but not observed by this frame):
+      * LocalBundleAdjustment moves `move_frac` of them by N(0, sigma) m (SetWorldPos);
+      * MapPointCulling / KeyFrameCulling retire `cull_frac` (SetBadFlag): never tracked again;
+      * SearchInNeighbors replaces `replace_frac` (Replace: the old point turns bad, later
+        observations of it report a fresh id at its position).
+    Later frames observe the points' current state. Returns new frame dicts carrying
+    upd_ids / upd_pos / upd_bad (empty on non-keyframes)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cur, seen, repl, culled = {}, {}, {}, set()
+    next_id = 1 + max(int(f["ids"].max()) for f in frames if len(f["ids"]))
+    out = []
+    for t, f in enumerate(frames):
+        ids, pos, uv = [], [], []
+        for k, i in enumerate(f["ids"].tolist()):
+            while i in repl:
+                i = repl[i]
+            if i in culled:
+                continue
+            if i not in cur:
+                cur[i] = np.asarray(f["pos"][k], np.float32)
+            seen[i] = t
+            ids.append(i)
+            pos.append(cur[i])
+            uv.append(f["uv"][k])
+        g = dict(f, ids=np.asarray(ids, np.int32), pos=np.asarray(pos, np.float32).reshape(-1, 3),
+                 uv=np.asarray(uv, np.float32).reshape(-1, 2), bad=np.zeros(len(ids), np.uint8))
+        uid, upos, ubad = [], [], []
+        if f["kf"]:
+            cand = sorted(i for i, s in seen.items() if s >= t - window and i not in culled and i not in repl)
+            r = rng.random((len(cand), 3))
+            for i, (rm, rc, rr) in zip(cand, r):
+                if rc < cull_frac:
+                    culled.add(i)
+                    uid.append(i), upos.append(cur[i]), ubad.append(1)
+                elif rr < replace_frac:
+                    repl[i] = next_id
+                    cur[next_id] = cur[i] + rng.normal(0, sigma / 4, 3).astype(np.float32)
+                    next_id += 1
+                    uid.append(i), upos.append(cur[i]), ubad.append(1)
+                elif rm < move_frac:
+                    cur[i] = (cur[i] + rng.normal(0, sigma, 3)).astype(np.float32)
+                    uid.append(i), upos.append(cur[i]), ubad.append(0)
+        g["upd_ids"] = np.asarray(uid, np.int32)
+        g["upd_pos"] = np.asarray(upos, np.float32).reshape(-1, 3)
+        g["upd_bad"] = np.asarray(ubad, np.uint8)
+        out.append(g)
+    return out
+
+
 # SURVEY.md §8d input 4 (Config C): 64 objects x 2000 map points, 16 classes,
 # 8 detections per frame each observing m in [50, 300] points of one object
 CONFIG_C_CLASSES = [39, 41, 62, 66, 73, 24, 26, 28, 45, 46, 47, 58, 59, 60, 61, 72]
