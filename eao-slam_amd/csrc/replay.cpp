@@ -46,6 +46,11 @@ static const bool g_spin_wait = [] {
   const char* v = getenv("EAO_BLOCKING_WAIT");  // A/B switch for measurements
   return !(v && v[0] == '1');
 }();
+// A/B switch for measurements: EAO_NO_LOOKAHEAD=1 disables the look-ahead of eao_replay_run
+static const bool g_lookahead = [] {
+  const char* v = getenv("EAO_NO_LOOKAHEAD");
+  return !(v && v[0] == '1');
+}();
 static hipError_t spin_event(hipEvent_t e) {
   if (!g_spin_wait) return hipEventSynchronize(e);
   for (;;) {
@@ -1179,6 +1184,7 @@ class ReplayEngine {
     } else if (b.launched) {
       Tick tw(&prof[39]);
       Tick tw2(&prof[42 + phase]);
+      idle_work(b.ev);
       EAO_HIP_CHECK(spin_event(b.ev));
     }
     double tpost = now_us();
@@ -1452,6 +1458,7 @@ class ReplayEngine {
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
     {
       Tick tw(&prof[41]);
+      idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
       EAO_HIP_CHECK(spin_event(gpu0_ev));
     }
     const int* r = (const int*)(h_out + o_r);
@@ -2013,11 +2020,11 @@ class ReplayEngine {
     for (int a = 0; a < 3; a++) f->pos[a] = f->sum[a] * sc + 0.0f;
   }
 
-  void boxplot(Det* f) {  // Object_2D::RemoveOutliersByBoxPlot, Object.cc:106-158
+  void boxplot(Det* f, const Pose& P) {  // Object_2D::RemoveOutliersByBoxPlot, Object.cc:106-158
     std::vector<float> zc(f->pts.size());
     for (size_t i = 0; i < f->pts.size(); i++) {
       float pc[3];
-      pz.cam(f->pts[i]->pos, pc);
+      P.cam(f->pts[i]->pos, pc);
       zc[i] = pc[2];
     }
     std::vector<float> zs = zc;
@@ -2084,74 +2091,132 @@ class ReplayEngine {
            dz < a->height / 2 + b->height / 2;
   }
 
-  int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
-            const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
-    Tick tk(&prof[0]);
-    phase = 4;
-    prof[8] += 1;
-    cur = fid;
-    std::memcpy(pz.T, Tcw, sizeof(pz.T));
-    epoch++;
-    kept_cur.clear();
-    kept_pos = -1;
-    cur_np_done = true;
-    np_cache.clear();
-    std::vector<Det*> o2;
-    int maxcls = 0;
-    for (int k = 0; k < nb; k++) {
-      std::unique_ptr<Det> f(new Det());
-      f->cls = boxes[5 * k];
-      f->bx = boxes[5 * k + 1];
-      f->by = boxes[5 * k + 2];
-      f->bw = boxes[5 * k + 3];
-      f->bh = boxes[5 * k + 4];
-      f->box = IRect(f->bx, f->by, f->bw, f->bh);
-      f->index = k;
-      f->fid = fid;
-      maxcls = std::max(maxcls, f->cls);
-      o2.push_back(f.get());
-      dets.push_back(std::move(f));
-    }
-    over.assign(objs.size(), 0);
-    double tA = now_us();
-    std::vector<MapPt*> tr(npts);
-    bool pend = false;  // forests still pending from the previous frame read positions / flags
-    for (auto& up : objs) pend |= up->pending != 0;
-    for (int i = 0; pend && i < npts; i++) {
-      auto it = mp_lookup(ids[i]);
-      if (!it) continue;
-      const bool nb_ = bad ? bad[i] != 0 : false;
-      if (std::memcmp(it->pos, pos + 3 * i, sizeof(float) * 3) != 0 || it->bad != nb_) {
-        if (int rc = flush(-1)) return rc;
-        pend = false;
+  // ---- look-ahead (eao_replay_run): steps 1-6 of the next frame -- the frame's own points,
+  // boxes and lines, independent of this frame's association -- run while this frame waits on
+  // the GPU. Only when the next frame leaves every known map point's position and flag as they
+  // stand (so nothing this frame's pending work reads changes), no map-point record comes in
+  // between and the object map is initialised (no InitObjMap in step 9).
+  struct FrameIn {
+    unsigned long fid = 0;
+    const float* T = nullptr;
+    int nb = 0, npts = 0;
+    const int32_t *boxes = nullptr, *ids = nullptr;
+    const float *pos = nullptr, *uv = nullptr;
+    const uint8_t* bad = nullptr;
+  };
+  FrameIn la;            // the next frame's inputs (set by the stream call)
+  bool la_set = false;
+  // steps 1-6 of one frame as a resumable sequence of short steps (a few us each), so idle
+  // time is filled without holding the host past the GPU result it waits for
+  struct Prep {
+    bool active = false;  // being prepared ahead (look-ahead)
+    bool ok = false;      // ... and complete
+    FrameIn in;
+    Pose P;
+    int phase = 0;
+    size_t k = 0;
+    std::vector<MapPt*> tr;
+    std::vector<Det*> o2, kept;
+  } prep, prep_now;
+  // fill a wait on `ev` with the next frame's steps 1-6
+  void idle_work(hipEvent_t ev) {
+    if (!prep.active) {
+      if (!g_lookahead || !la_set || prep.ok || !ini) return;
+      la_set = false;
+      for (int i = 0; i < la.npts; i++) {
+        const MapPt* p = mp_lookup(la.ids[i]);
+        if (!p) continue;
+        if (std::memcmp(p->pos, la.pos + 3 * (size_t)i, sizeof(float) * 3) != 0 ||
+            p->bad != (la.bad ? la.bad[i] != 0 : false))
+          return;  // the next frame changes a known point: it runs in order
       }
+      prep_begin(prep, la);
+      std::memcpy(prep.P.T, la.T, sizeof(prep.P.T));
+      prep.active = true;
+      prof[53] += 1;
     }
-    for (int i = 0; i < npts; i++) {
-      MapPt* p = mappoint(ids[i]);
-      for (int a = 0; a < 3; a++) p->pos[a] = pos[3 * i + a];
-      p->proj_epoch = 0;
-      p->bad = bad ? bad[i] != 0 : false;
-      tr[i] = p;
-    }
-    // STEP 2 AssociateObjAndPoints, Tracking.cc:2434-2468
-    for (int i = 0; i < npts; i++) {
-      MapPt* p = tr[i];
-      if (p->bad) continue;
-      const int px = (int)lrintf(uv[2 * i]), py = (int)lrintf(uv[2 * i + 1]);
-      for (Det* f : o2)
-        if (f->box.contains_i(px, py)) {
-          p->fu = uv[2 * i];
-          p->fv = uv[2 * i + 1];
-          f->pts.push_back(p);
-          for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
+    Tick tk(&prof[52]);
+    while (!prep.ok && hipEventQuery(ev) == hipErrorNotReady) prep.ok = prep_step(prep);
+  }
+  void prep_begin(Prep& s, const FrameIn& in) {
+    s.in = in;
+    s.P = pz;
+    s.phase = 0;
+    s.k = 0;
+    s.ok = false;
+    s.o2.clear();
+    s.kept.clear();
+  }
+
+  // STEPS 1-6 of TrackWithMotionModel's object section for one frame's inputs (pose s.P),
+  // one bounded step per call; true when the frame is ready for step 9 / 10
+  bool prep_step(Prep& s) {
+    const FrameIn& in = s.in;
+    const Pose& P = s.P;
+    std::vector<Det*>& o2 = s.o2;
+    const double tA = now_us();
+    switch (s.phase) {
+      case 0: {
+        for (int k = 0; k < in.nb; k++) {
+          std::unique_ptr<Det> f(new Det());
+          f->cls = in.boxes[5 * k];
+          f->bx = in.boxes[5 * k + 1];
+          f->by = in.boxes[5 * k + 2];
+          f->bw = in.boxes[5 * k + 3];
+          f->bh = in.boxes[5 * k + 4];
+          f->box = IRect(f->bx, f->by, f->bw, f->bh);
+          f->index = k;
+          f->fid = in.fid;
+          o2.push_back(f.get());
+          dets.push_back(std::move(f));
         }
-    }
-    associate_lines(o2);  // STEP 3 AssociateObjAndLines, Tracking.cc:1286
-    prof[12] += now_us() - tA;
-    tA = now_us();
-    for (Det* f : o2) {  // STEP 4
-      frame_mean(f);
-      if (f->pts.size() >= 8) boxplot(f);
+        s.tr.resize(in.npts);
+        for (int i = 0; i < in.npts; i++) {
+          MapPt* p = mappoint(in.ids[i]);
+          for (int a = 0; a < 3; a++) p->pos[a] = in.pos[3 * i + a];
+          p->proj_epoch = 0;
+          p->bad = in.bad ? in.bad[i] != 0 : false;
+          s.tr[i] = p;
+        }
+        s.phase = 1;
+        prof[12] += now_us() - tA;
+        return false;
+      }
+      case 1: {  // STEP 2 AssociateObjAndPoints, Tracking.cc:2434-2468
+        const float* uv = in.uv;
+        for (int i = 0; i < in.npts; i++) {
+          MapPt* p = s.tr[i];
+          if (p->bad) continue;
+          const int px = (int)lrintf(uv[2 * i]), py = (int)lrintf(uv[2 * i + 1]);
+          for (Det* f : o2)
+            if (f->box.contains_i(px, py)) {
+              p->fu = uv[2 * i];
+              p->fv = uv[2 * i + 1];
+              f->pts.push_back(p);
+              for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
+            }
+        }
+        s.phase = 2;
+        prof[12] += now_us() - tA;
+        return false;
+      }
+      case 2:
+        associate_lines(o2);  // STEP 3 AssociateObjAndLines, Tracking.cc:1286
+        s.phase = 3;
+        s.k = 0;
+        prof[12] += now_us() - tA;
+        return false;
+      case 3:  // STEP 4, one detection per step
+        if (s.k < o2.size()) {
+          Det* f = o2[s.k++];
+          frame_mean(f);
+          if (f->pts.size() >= 8) boxplot(f, P);
+        }
+        if (s.k >= o2.size()) s.phase = 4;
+        prof[13] += now_us() - tA;
+        return false;
+      default:
+        break;
     }
     for (Det* f : o2) {  // STEP 5
       const float sc = (float)(1. / (double)f->pts.size());
@@ -2166,8 +2231,8 @@ class ReplayEngine {
       }
       if (xmn < 0) xmn = 0;
       if (ymn < 0) ymn = 0;
-      if (xmx > pz.cols) xmx = (float)pz.cols;
-      if (ymx > pz.rows) ymx = (float)pz.rows;
+      if (xmx > P.cols) xmx = (float)P.cols;
+      if (ymx > P.rows) ymx = (float)P.rows;
       f->feat = rect_trunc(xmn, ymn, xmx - xmn, ymx - ymn);
     }
     // STEP 6 filters, Tracking.cc:1383-1487
@@ -2181,11 +2246,11 @@ class ReplayEngine {
       Det* f = o2[a];
       if (f->bad) continue;
       if (f->cls == 0 || f->cls == 63 || f->cls == 15) f->bad = true;
-      if ((float)f->box.area() / (float)(pz.cols * pz.rows) > 0.5) f->bad = true;
+      if ((float)f->box.area() / (float)(P.cols * P.rows) > 0.5) f->bad = true;
       if (f->pts.size() < 5)
         f->bad = true;
       else if (f->pts.size() < 10 &&
-               (f->bx < 20 || f->by < 20 || f->bx + f->bw > pz.cols - 20 || f->by + f->bh > pz.rows - 20))
+               (f->bx < 20 || f->by < 20 || f->bx + f->bw > P.cols - 20 || f->by + f->bh > P.rows - 20))
         f->bad = true;
       for (size_t b = 0; b < o2.size(); b++) {
         Det* g = o2[b];
@@ -2200,11 +2265,67 @@ class ReplayEngine {
         }
       }
     }
-    std::vector<Det*> kept;
     for (Det* f : o2) {
-      if (!f->bad) kept.push_back(f);
+      if (!f->bad) s.kept.push_back(f);
       else f->method = -1;
     }
+    prof[13] += now_us() - tA;
+    return true;
+  }
+
+  int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
+            const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
+    Tick tk(&prof[0]);
+    phase = 4;
+    prof[8] += 1;
+    cur = fid;
+    std::memcpy(pz.T, Tcw, sizeof(pz.T));
+    epoch++;
+    kept_cur.clear();
+    kept_pos = -1;
+    cur_np_done = true;
+    np_cache.clear();
+    std::vector<Det*> o2, kept;
+    over.assign(objs.size(), 0);
+    if (prep.active) {  // steps 1-6 (partly) ran ahead, while the previous frame waited on the GPU
+      if (prep.in.fid != fid || prep.in.nb != nb) {
+        set_error("replay: look-ahead frame does not match the replayed frame");
+        return EAO_E_STATE;
+      }
+      while (!prep.ok) prep.ok = prep_step(prep);
+      o2.swap(prep.o2);
+      kept.swap(prep.kept);
+      prep.ok = prep.active = false;
+    } else {
+      bool pend = false;  // forests still pending from the previous frame read positions / flags
+      for (auto& up : objs) pend |= up->pending != 0;
+      for (int i = 0; pend && i < npts; i++) {
+        auto it = mp_lookup(ids[i]);
+        if (!it) continue;
+        const bool nb_ = bad ? bad[i] != 0 : false;
+        if (std::memcmp(it->pos, pos + 3 * i, sizeof(float) * 3) != 0 || it->bad != nb_) {
+          if (int rc = flush(-1)) return rc;
+          pend = false;
+        }
+      }
+      FrameIn in;
+      in.fid = fid;
+      in.T = Tcw;
+      in.nb = nb;
+      in.npts = npts;
+      in.boxes = boxes;
+      in.ids = ids;
+      in.pos = pos;
+      in.uv = uv;
+      in.bad = bad;
+      Prep& s = prep_now;
+      prep_begin(s, in);
+      while (!prep_step(s)) {
+      }
+      o2.swap(s.o2);
+      kept.swap(s.kept);
+    }
+    double tA = now_us();
     // STEP 9 InitObjMap, Tracking.cc:2531-2598
     if (!ini) {
       int good = -1;
@@ -2686,7 +2807,24 @@ int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids
   }
   EAO_REPLAY_LOCK(r);
   size_t ob = 0, op = 0, ou = 0;
+  ReplayEngine& E = r->r;
   for (int t = 0; t < n_frames; t++) {
+    // the next frame's inputs, for the look-ahead of steps 1-6 (not across a point record)
+    E.la_set = false;
+    if (t + 1 < n_frames && !(n_upd && n_upd[t])) {
+      ReplayEngine::FrameIn& in = E.la;
+      in.fid = (unsigned long)frame_ids[t + 1];
+      in.T = Tcw + 16 * (size_t)(t + 1);
+      in.nb = n_boxes[t + 1];
+      in.npts = n_pts[t + 1];
+      in.boxes = boxes + 5 * (ob + (size_t)n_boxes[t]);
+      const size_t op1 = op + (size_t)n_pts[t];
+      in.ids = mp_ids + op1;
+      in.pos = mp_pos + 3 * op1;
+      in.uv = kp_uv + 2 * op1;
+      in.bad = mp_bad ? mp_bad + op1 : nullptr;
+      E.la_set = true;
+    }
     const int rc = eao_replay_frame(r, frame_ids[t], Tcw + 16 * (size_t)t, n_boxes[t], boxes + 5 * ob, n_pts[t],
                                     mp_ids + op, mp_pos + 3 * op, kp_uv + 2 * op, mp_bad ? mp_bad + op : nullptr,
                                     det_out + 4 * ob);
@@ -2703,6 +2841,11 @@ int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids
     }
     ob += (size_t)n_boxes[t];
     op += (size_t)n_pts[t];
+  }
+  E.la_set = false;
+  if (E.prep.active) {
+    eao::set_error("replay: look-ahead frame left unconsumed");
+    return EAO_E_STATE;
   }
   // the stream's last forests complete here, inside the call (no work left pending for a
   // later reader)

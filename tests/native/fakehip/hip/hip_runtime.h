@@ -46,6 +46,11 @@ inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) { *e = (hipEv
 inline hipError_t hipEventDestroy(hipEvent_t) { return 0; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return 0; }
 inline hipError_t hipEventSynchronize(hipEvent_t) { return 0; }
-inline hipError_t hipEventQuery(hipEvent_t) { return 0; }
+// every other query reports "not ready", so the engine's idle-time work (the look-ahead of
+// eao_replay_run) runs on the host harness too; the next query completes
+inline hipError_t hipEventQuery(hipEvent_t) {
+  static thread_local unsigned n = 0;
+  return (n++ & 1u) ? (hipError_t)0 : (hipError_t)hipErrorNotReady;
+}
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return 0; }
 inline hipError_t hipMemset(void* p, int v, size_t n) { std::memset(p, v, n); return 0; }

@@ -152,7 +152,7 @@ __global__ void k_bench(const int* keys, int cnt, int reps, unsigned long long* 
 __global__ void k_subtree(const int* keys, int cnt, int maxDepth, int reps, unsigned long long* out) {
   __shared__ uint32_t mts[624];
   __shared__ uint2 nodes[256];
-  __shared__ uint8_t ndep[256];
+  __shared__ uint16_t ndep[256];
   const int lane = threadIdx.x;
   for (int i = lane; i < 624; i += 64) mts[i] = 0x9e3779b9u * (i + 1);
   __syncthreads();
