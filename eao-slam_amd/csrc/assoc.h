@@ -60,6 +60,13 @@ class AssocEngine {
   int stage_in(void* d_dst, const void* h_src, size_t bytes, hipStream_t s);
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples
   bool iforest_fits(int max_len, int max_sample) const;
+  // the frame start's projected rects and NP pairs in one launch (k_rects_np); the inputs
+  // may be pinned host memory read in place
+  int rects_np(const CamDev& cam, const float* T, int nclouds, const float* rpts, const int* roff, const int* rlen,
+               int* rect, uint8_t* ok, const double* const* ros, const float* rth, int npairs, const float* fp,
+               const uint8_t* fv, const int* foff, const int* flen, const float* op, const uint8_t* ov,
+               const int* ooff, const int* olen, eao_np_stats* out, hipStream_t s, int max_olen,
+               const double* const* os_ptr, const float* oth);
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s,
             const double* const* d_os_ptr = nullptr, const float* d_oth = nullptr);

@@ -162,7 +162,7 @@ constexpr int NPT = 1024;
 // values and 3 (Pm + 1) counters, four copies at Pm = 256 (15.4 KB), one at Pm = 512
 constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * 4 * 3 * 257 + 64;
 static_assert(sizeof(float) * 3 * 512 + sizeof(int) * 3 * 513 <= NP_LDS_EXTRA, "rank-path LDS");
-__global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
+__device__ __forceinline__ void np_pair_body(const int p, const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
                                                   const int* __restrict__ flen,
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp,
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   __shared__ int red[9 * 16];
   __shared__ int wpos[4];
-  const int p = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   const float* F = fp + 3 * (long long)foff[p];
   const uint8_t* FV = fv + foff[p];
   const int mt = flen[p];
@@ -492,6 +492,15 @@ sums:
   }
 }
 
+__global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp, const uint8_t* __restrict__ fv,
+                                                  const int* __restrict__ foff, const int* __restrict__ flen,
+                                                  const float* __restrict__ op, const uint8_t* __restrict__ ov,
+                                                  const int* __restrict__ ooff, const int* __restrict__ olen,
+                                                  int Pmax, const double* const* __restrict__ os_ptr,
+                                                  const float* __restrict__ oth, eao_np_stats* __restrict__ out) {
+  np_pair_body(blockIdx.x, fp, fv, foff, flen, op, ov, ooff, olen, Pmax, os_ptr, oth, out);
+}
+
 // ---------------------------------------------------------------- rects
 __device__ __forceinline__ void project_pt(const CamDev& c, const float* T, const float* P, float& u,
                                            float& v) {
@@ -506,16 +515,17 @@ __device__ __forceinline__ void project_pt(const CamDev& c, const float* T, cons
   v = fadd(fmul(fmul(c.fy, pc[1]), invzc), c.cy);
 }
 
-__global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restrict__ Tg,
-                                               const float* __restrict__ pts,
-                                               const int* __restrict__ off,
-                                               const int* __restrict__ len, int* __restrict__ rect,
-                                               uint8_t* __restrict__ ok,
-                                               const double* const* __restrict__ os_ptr,
-                                               const float* __restrict__ oth) {
-  __shared__ float red[4][4];
+// one cloud per workgroup of NB threads (NB / 64 <= 16 waves)
+template <int NB>
+__device__ __forceinline__ void rects_body(const int c, const CamDev& cam, const float* __restrict__ Tg,
+                                           const float* __restrict__ pts, const int* __restrict__ off,
+                                           const int* __restrict__ len, int* __restrict__ rect,
+                                           uint8_t* __restrict__ ok, const double* const* __restrict__ os_ptr,
+                                           const float* __restrict__ oth) {
+  constexpr int NW = NB / 64;
+  __shared__ float red[NW][4];
   __shared__ int s_kept;
-  const int c = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
   int n = len[c];
   const float* P = pts + 3 * (long long)off[c];
   // a pending isolation forest's erasure applied on the fly (as in k_np_pairs)
@@ -527,7 +537,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
   float xmn = INFINITY, xmx = -INFINITY, ymn = INFINITY, ymx = -INFINITY;
   int kept = 0;
   __syncthreads();
-  for (int i = t; i < n; i += 256) {
+  for (int i = t; i < n; i += NB) {
     if (OS && OS[i] > th) continue;
     kept++;
     float u, v;
@@ -553,7 +563,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
   }
   __syncthreads();
   if (t == 0) {
-    for (int k = 1; k < 4; k++) {
+    for (int k = 1; k < NW; k++) {
       xmn = fminf(xmn, red[k][0]);
       xmx = fmaxf(xmx, red[k][1]);
       ymn = fminf(ymn, red[k][2]);
@@ -574,6 +584,36 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
     rect[4 * c + 3] = (int)fsub(ymx, ymn);
     ok[c] = 1;
   }
+}
+
+__global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restrict__ Tg, const float* __restrict__ pts,
+                                               const int* __restrict__ off, const int* __restrict__ len,
+                                               int* __restrict__ rect, uint8_t* __restrict__ ok,
+                                               const double* const* __restrict__ os_ptr,
+                                               const float* __restrict__ oth) {
+  rects_body<256>(blockIdx.x, cam, Tg, pts, off, len, rect, ok, os_ptr, oth);
+}
+
+// the frame start in one launch: workgroups [0, npairs) are NoParaDataAssociation pairs
+// (np_pair_body), the rest the projected rects of the recent objects (rects_body). Inputs
+// may be read straight from pinned host memory (no staging copy on the chain).
+__global__ __launch_bounds__(1024) void k_rects_np(int npairs, const float* __restrict__ fp,
+                                                  const uint8_t* __restrict__ fv, const int* __restrict__ foff,
+                                                  const int* __restrict__ flen, const float* __restrict__ op,
+                                                  const uint8_t* __restrict__ ov, const int* __restrict__ ooff,
+                                                  const int* __restrict__ olen, int Pmax,
+                                                  const double* const* __restrict__ os_ptr,
+                                                  const float* __restrict__ oth, eao_np_stats* __restrict__ out,
+                                                  CamDev cam, const float* __restrict__ Tg,
+                                                  const float* __restrict__ rpts, const int* __restrict__ roff,
+                                                  const int* __restrict__ rlen, int* __restrict__ rect,
+                                                  uint8_t* __restrict__ ok, const double* const* __restrict__ ros,
+                                                  const float* __restrict__ rth) {
+  const int b = blockIdx.x;
+  if (b < npairs)
+    np_pair_body(b, fp, fv, foff, flen, op, ov, ooff, olen, Pmax, os_ptr, oth, out);
+  else
+    rects_body<1024>(b - npairs, cam, Tg, rpts, roff, rlen, rect, ok, ros, rth);
 }
 
 // ---------------------------------------------------------------- iForest
@@ -1124,6 +1164,21 @@ AssocEngine::~AssocEngine() {
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
+}
+
+int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const float* rpts, const int* roff,
+                          const int* rlen, int* rect, uint8_t* ok, const double* const* ros, const float* rth,
+                          int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
+                          const float* op, const uint8_t* ov, const int* ooff, const int* olen, eao_np_stats* out,
+                          hipStream_t s, int max_olen, const double* const* os_ptr, const float* oth) {
+  if (npairs + nclouds <= 0) return EAO_OK;
+  int P = 256;
+  while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
+  const size_t lds = sizeof(float) * 3 * P + (P >= 2048 ? NP_LDS_EXTRA : 64);
+  hipLaunchKernelGGL(k_rects_np, dim3(npairs + nclouds), dim3(NPT), lds, s, npairs, fp, fv, foff, flen, op, ov, ooff,
+                     olen, P, os_ptr, oth, out, cam, T, rpts, roff, rlen, rect, ok, ros, rth);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
 }
 
 int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,

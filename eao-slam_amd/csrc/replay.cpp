@@ -1438,20 +1438,18 @@ class ReplayEngine {
         oth[nb + k] = th_p[k];
       }
     }
-    rc = A->stage_in(d_in, h_in, in_bytes, A->stream);
-    if (rc) return rc;
     for (int k : wait_slots) EAO_HIP_CHECK(hipStreamWaitEvent(A->stream, ifb[k].ev, 0));
-    const int* drm = (const int*)d_in;
-    const int* dpm = (const int*)(d_in + o_pm);
-    const float* dpts = (const float*)(d_in + o_pts);
-    const uint8_t* dval = d_in + o_val;
-    const double* const* dosp = chained ? (const double* const*)(d_in + o_osp) : nullptr;
-    const float* doth = chained ? (const float*)(d_in + o_oth) : nullptr;
-    // results go straight into pinned host memory
-    rc = A->rects(camdev, (const float*)(d_in + o_T), nb, dpts, drm, drm + nb, (int*)(h_out + o_r), h_out + o_ok,
-                  A->stream, dosp, doth);
-    if (rc) return rc;
-    rc = A->np_batch(npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
+    // one launch reads the packed inputs in place from pinned host memory (no staging
+    // kernel on the chain) and writes the results straight back into pinned host memory
+    const unsigned char* din = h_in;
+    const int* drm = (const int*)din;
+    const int* dpm = (const int*)(din + o_pm);
+    const float* dpts = (const float*)(din + o_pts);
+    const uint8_t* dval = din + o_val;
+    const double* const* dosp = chained ? (const double* const*)(din + o_osp) : nullptr;
+    const float* doth = chained ? (const float*)(din + o_oth) : nullptr;
+    rc = A->rects_np(camdev, (const float*)(din + o_T), nb, dpts, drm, drm + nb, (int*)(h_out + o_r), h_out + o_ok,
+                     dosp, doth, npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
                      (eao_np_stats*)h_out, A->stream, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));

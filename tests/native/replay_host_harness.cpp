@@ -69,6 +69,14 @@ int AssocEngine::rects(const CamDev& cam, const float* T, int nclouds, const flo
   }
   return 0;
 }
+int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const float* rpts, const int* roff,
+                          const int* rlen, int* rect, uint8_t* ok, const double* const* ros, const float* rth,
+                          int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
+                          const float* op, const uint8_t* ov, const int* ooff, const int* olen, eao_np_stats* out,
+                          hipStream_t s, int max_olen, const double* const* os_ptr, const float* oth) {
+  rects(cam, T, nclouds, rpts, roff, rlen, rect, ok, s, ros, rth);
+  return np_batch(npairs, fp, fv, foff, flen, op, ov, ooff, olen, out, s, max_olen, os_ptr, oth);
+}
 bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }
 int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t) {
   std::memcpy(dst, src, bytes);  // host "device" memory
