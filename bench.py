@@ -8,13 +8,21 @@ Configs (BASELINE.json):
                  rgb_full_demo.txt, flag Full (iForest + line alignment + EAO).
   --config c     configs[3] "Synthetic 640x480 stream, 64 objects x 2k map-points, assoc
                  sharded via RCCL": the object-sharded association.
+  --config b     configs[4] "Synthetic 1920x1080 stream, 8-level pyramid, 4000 features/frame":
+                 ORB extract + motion match of a 256-frame batch per rank (tools/bench_config_b.py).
 
 One *step* (eao / full) is one pass of the hot path over the whole stream, every input
 resident before timing:
+  0. the frames arrive as 3-channel colour in HBM: cvtColor RGB2GRAY of every frame
+     (mImGray, eao_color_to_gray_batch_device, src/Tracking.cc:349-362);
   1. ORBextractor::operator() of every frame (eao_orb_extract_batch_device,
      src/ORBextractor.cc:1043-1105) -- HBM-resident frames, one batch;
   2. SearchByProjection(CurrentFrame, LastFrame, 15, mono) of every consecutive pair
      (eao_match_motion_batch_device, src/ORBmatcher.cc:1328-1470);
+  2b. the EAO Frame ctor's line detection on every colour frame (detect_raw_lines +
+     filter_lines with detectImpl's COLOR_BGR2GRAY, eao_lines_detect_color_batch_device,
+     src/Frame.cc:324-335) -- the association below consumes the stream's recorded line
+     segments, as the replay trace holds them;
   3. the object-association replay of Tracking.cc:1241-1696 + LocalMapping's object
      maintenance (eao_replay_run: frame by frame, NP test / isolation forest / projected
      rects on the GPU, decisions on the host) over the stream's detections.
@@ -171,13 +179,17 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--config", choices=["eao", "full", "c"], default="eao")
+    ap.add_argument("--config", choices=["eao", "full", "c", "b"], default="eao")
     ap.add_argument("--frames", type=int, default=0, help="override the stream length")
-    ap.add_argument("--cpu-frames", type=int, default=60, help="extract+match single-thread CPU sample")
+    ap.add_argument("--unique", type=int, default=64, help="config b: rendered frames (repeated to --frames)")
+    ap.add_argument("--cpu-frames", type=int, default=None,
+                    help="extract+match single-thread CPU sample (60 frames; 3 at 1080p for config b)")
     ap.add_argument("--cpu-mt-frames", type=int, default=256, help="extract+match all-cores CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
     args = ap.parse_args()
+    if args.cpu_frames is None:
+        args.cpu_frames = 3 if args.config == "b" else 60
     if args.gpus > 1 and "RANK" not in os.environ:
         return launch_ranks(args.gpus, sys.argv[1:])
 
@@ -195,6 +207,13 @@ def main():
     gpu = local % ndev  # ranks beyond the visible devices (a rehearsal on one card) share them
     if args.config == "c":
         return run_config_c(args, rank, world, gpu)
+    if args.config == "b":
+        # BASELINE configs[4]: synthetic 1920x1080, 8 levels, 4000 features, extract + match t vs t-1;
+        # frames are independent units, so N ranks each run a frame shard ("scaling": "weak")
+        from tools import bench_config_b
+        if not args.frames:
+            args.frames = 256
+        return bench_config_b.main(args)
     if world > 1:
         backend = os.environ.get("EAO_DIST_BACKEND", "nccl")  # nccl == RCCL on ROCm
         if backend == "nccl":
@@ -222,7 +241,19 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     assert sptr != 0
-    d_frames = torch.from_numpy(rendered).to(dev)[torch.from_numpy(idx).to(dev)].contiguous()
+    d_render = torch.from_numpy(rendered).to(dev)[torch.from_numpy(idx).to(dev)].contiguous()
+    # the frames as the reference reads them: 3-channel colour (imread's BGR byte order), a
+    # fixed smooth tint per channel over the rendered intensities, resident in HBM. The step
+    # converts them twice, as the reference does: cvtColor RGB2GRAY for the tracker's mImGray
+    # (Camera.RGB = 1, Tracking.cc:349-362) -> ORB; COLOR_BGR2GRAY inside the line
+    # detector's blur (BinaryDescriptor::detectImpl, binary_descriptor.cpp:490-495).
+    yy, xx = torch.meshgrid(torch.arange(H, device=dev), torch.arange(W, device=dev), indexing="ij")
+    tb = (14 * torch.sin(xx.float() / 37.0)).round().to(torch.int16)
+    tr = (11 * torch.cos(yy.float() / 29.0 + xx.float() / 83.0)).round().to(torch.int16)
+    g16 = d_render.to(torch.int16)
+    d_color = torch.stack([(g16 + tb).clamp(0, 255), g16, (g16 - tr).clamp(0, 255)], -1).to(torch.uint8).contiguous()
+    del g16, d_render
+    d_frames = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
 
     orb = ea.Orb(NFEAT, SCALE, NLEV, 20, 7, W, H, max_batch=F, device=gpu)
     cap = orb.cap
@@ -243,6 +274,18 @@ def main():
     d_nm = torch.zeros(F, dtype=i32, device=dev)
     stream.synchronize()
 
+    lines = ea.Lines(W, H, max_batch=F, device=gpu)
+    LCAP = 256
+    d_lines = torch.zeros((F, LCAP, 6), dtype=f32, device=dev)
+    d_lcnt = torch.zeros(F, dtype=i32, device=dev)
+
+    def gray():  # mImGray of every frame (k_gray, RGB2GRAY code on the BGR bytes)
+        ea.color_to_gray_batch_device(d_color.data_ptr(), F, W, H, 3 * W, 3, True, d_frames.data_ptr(), W, gpu, sptr)
+
+    def detect_lines():  # Frame ctor's detect_raw_lines + filter_lines of every frame (Frame.cc:324-335)
+        lines.detect_color_batch_device(d_color.data_ptr(), F, 3 * W, 3, 50.0, d_lines.data_ptr(), d_lcnt.data_ptr(),
+                                        LCAP, sptr)
+
     def extract():
         orb.extract_batch_device(d_frames.data_ptr(), F, W, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(),
                                  cap, sptr)
@@ -255,6 +298,7 @@ def main():
     # -- the map the motion model tracks against: every keypoint of frame t-1 holds a map
     # point on the scene plane (backprojected with the pose, descriptor = its observation's).
     # Built once, untimed: it is map state (an input of SearchByProjection), not an output.
+    gray()
     extract()
     torch.cuda.synchronize()
     cnt = d_cnt.cpu().numpy()
@@ -285,26 +329,33 @@ def main():
         out["replay"] = rp  # object state read back after the timed region
 
     orb.set_timing(True)
+    ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev_m0 = torch.cuda.Event(enable_timing=True)
     ev_m1 = torch.cuda.Event(enable_timing=True)
+    ev_l1 = torch.cuda.Event(enable_timing=True)
     ev_done = torch.cuda.Event()
+
+    def front():  # the frame work of the step on the extraction stream
+        ev_g0.record(stream)
+        gray()
+        ev_g1.record(stream)
+        extract()
+        ev_m0.record(stream)
+        match()
+        ev_m1.record(stream)
+        detect_lines()
+        ev_l1.record(stream)
 
     def step(record):
         out = {}
         th = None
         if args.no_overlap:
-            extract()
-            ev_m0.record(stream)
-            match()
-            ev_m1.record(stream)
+            front()
             associate(out)
         else:
             th = threading.Thread(target=associate, args=(out,))
             th.start()
-            extract()
-            ev_m0.record(stream)
-            match()
-            ev_m1.record(stream)
+            front()
         # wait for the extraction stream only (a device-wide synchronize would also serialise
         # against the association thread's launches), politely: the association thread is
         # the critical path and needs its core
@@ -316,12 +367,14 @@ def main():
         if record is not None:
             record["stage_ms"].append(orb.stage_ms())
             record["match_ms"].append(ev_m0.elapsed_time(ev_m1))
+            record["gray_ms"].append(ev_g0.elapsed_time(ev_g1))
+            record["lines_ms"].append(ev_m1.elapsed_time(ev_l1))
         return out
 
     for _ in range(args.warmup):
         step(None)
 
-    rec = {"stage_ms": [], "match_ms": []}
+    rec = {"stage_ms": [], "match_ms": [], "gray_ms": [], "lines_ms": []}
     eao_dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -331,22 +384,10 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = eao_dist.max_over_ranks(time.perf_counter() - t0, dev)
 
-    # frame input stage (measured beside the step, not in it):
-    # cvtColor(CV_RGB2GRAY) of the stream as 3-channel frames resident in HBM
-    Fg = min(F, 405)
-    d_color = d_frames[:Fg].unsqueeze(-1).repeat(1, 1, 1, 3)
-    d_gray = torch.empty_like(d_frames[:Fg])
-    ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ea.color_to_gray_batch_device(d_color.data_ptr(), Fg, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, gpu, sptr)
-    reps = 10
-    ev_g0.record(stream)
-    for _ in range(reps):
-        ea.color_to_gray_batch_device(d_color.data_ptr(), Fg, W, H, 3 * W, 3, True, d_gray.data_ptr(), W, gpu, sptr)
-    ev_g1.record(stream)
-    torch.cuda.synchronize(dev)
-    gray_ms = ev_g0.elapsed_time(ev_g1) / reps
-    gray_bytes = Fg * W * H * 4  # read 3 B + write 1 B per pixel
-    del d_color, d_gray
+    # frame input stage and per-frame line detection: stages of the step (HIP events on its stream)
+    gray_ms = float(np.mean(rec["gray_ms"]))
+    gray_bytes = F * W * H * 4  # read 3 B + write 1 B per pixel
+    lines_ms = float(np.mean(rec["lines_ms"]))
 
     total_frames = F * args.steps * world
     ms_per_step = 1000.0 * elapsed / args.steps
@@ -354,7 +395,11 @@ def main():
     match_ms = float(np.mean(rec["match_ms"]))
     searches = search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc,
                            d_cnt, d_has, d_mpos, match_ms)
-    lines_leg = line_leg(ea, torch, stream, min(F, RENDERED), gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
+    hl = d_lcnt.cpu().numpy()
+    lines_leg = {"in_step": True, "frames": F, "ms_per_step": lines_ms, "frames_per_s": F / (lines_ms * 1e-3),
+                 "mean_lines": float(hl.mean()), "kernels": "k_line_blur<3> (COLOR_BGR2GRAY fused) + k_line_grad + "
+                 "k_line_anchors + k_edge_draw + k_edlines",
+                 "input": "the step's 3-channel colour frames (rawImage of the EAO Frame ctor, Frame.cc:324)"}
     pose = pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
     bow = bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt,
                   with_cpu=rank == 0 and not args.no_cpu_baseline)
@@ -408,9 +453,9 @@ def main():
             "pose_optimization": pose,
             "bag_of_words": bow,
             "frame_input_stage": {"kernel": "k_gray (cvtColor RGB2GRAY, Tracking.cc:349-362)",
-                                  "frames": Fg, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
+                                  "frames": F, "ms": gray_ms, "achieved_gbs": gray_bytes / (gray_ms * 1e-3) / 1e9,
                                   "frac_hbm_peak": gray_bytes / (gray_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-                                  "note": "measured beside the step (the bench workload is mono frames)"},
+                                  "note": "a stage of the step: colour frames in HBM -> mImGray for the extraction"},
             "mean_keypoints": n_kps,
             "mean_matches": float(d_nm[1:].float().mean().item()),
             "assoc_detections": int(nb.sum()),
@@ -423,7 +468,8 @@ def main():
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"], result["parity"] = cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt,
-                                                                mpos, has, sc, d_desc, d_match, d_nm, out)
+                                                                mpos, has, sc, d_desc, d_match, d_nm, out,
+                                                                d_color, d_lines, d_lcnt)
         result["gpu_over_cpu"] = {"all_cores": result["value"] / result["cpu_baseline"]["value"],
                                   "single_thread": result["value"] / result["cpu_baseline"]["single_thread"]["value"]}
     if world > 1:
@@ -432,50 +478,6 @@ def main():
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
     return 0
-
-
-def line_leg(ea, torch, stream, F, gpu, with_cpu=True, reps=3, distinct=48):
-    """Per-frame line detection (detect_raw_lines + filter_lines, Frame.cc:324-328) beside
-    the step: a batch of F line-rich 640x480 frames (tools/synth.line_frames, `distinct`
-    rendered and cycled), HBM-resident, timed with HIP events; the CPU restatement
-    (oracle/lines_ref.cpp, one thread) timed on a few frames, and those frames checked."""
-    from tools import synth
-    dev = torch.device("cuda", gpu)
-    lf = synth.line_frames(min(F, distinct), seed=0xEA7)
-    idx = pingpong(F, len(lf))
-    d = torch.from_numpy(lf).to(dev)[torch.from_numpy(idx).to(dev)].contiguous()
-    L = ea.Lines(W, H, max_batch=F, device=gpu)
-    cap = 256
-    out = torch.zeros((F, cap, 6), dtype=torch.float32, device=dev)
-    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
-    sp = stream.cuda_stream
-    L.detect_batch_device(d.data_ptr(), F, W, 50.0, out.data_ptr(), cnt.data_ptr(), cap, sp)
-    ms = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        L.detect_batch_device(d.data_ptr(), F, W, 50.0, out.data_ptr(), cnt.data_ptr(), cap, sp)
-        e1.record(stream)
-        e1.synchronize()
-        ms.append(e0.elapsed_time(e1))
-    hc = cnt.cpu().numpy()
-    res = {"frames": F, "ms_per_batch": float(np.mean(ms)), "frames_per_s": F / (np.mean(ms) * 1e-3),
-           "mean_lines": float(hc.mean()), "data": "tools/synth.line_frames (%d rendered, cycled)" % len(lf)}
-    if with_cpu:  # the line detector's CPU baseline: the restatement as checker and timed port
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import pyoracle as orc  # checker / CPU baseline only
-        orc.use_native()  # the same -O3 -march=native build the step's CPU baseline times
-        k = 4
-        t0 = time.perf_counter()
-        ref = [orc.edlines(lf[i]) for i in range(k)]
-        cpu_ms = (time.perf_counter() - t0) * 1e3 / k
-        ho = out.cpu().numpy()
-        ok = all(hc[i] == len(ref[i]) and np.array_equal(ho[i, :hc[i]], ref[i]) for i in range(k))
-        res.update({"cpu_ms_per_frame": cpu_ms, "cpu_kind": "port (oracle/lines_ref.cpp, 1 thread)",
-                    "gpu_over_cpu": (F / (np.mean(ms) * 1e-3)) / (1e3 / cpu_ms), "parity_frames": k,
-                    "parity_bitexact": bool(ok)})
-    L.close()
-    return res
 
 
 def bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt, with_cpu=True, reps=3):
@@ -745,23 +747,38 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu_out):
+def cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt, mpos, has, sc, d_desc, d_match, d_nm, gpu_out,
+                 d_color, d_lines, d_lcnt):
     """Time the oracle (CPU restatement, -O3 -march=native built here) on a bounded sample
     and check the GPU outputs of the same sample against it."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as orc  # checker / CPU baseline only
     orc.use_native()
     F = len(assoc_frames)
     nb = np.cumsum([0] + [len(f["boxes"]) for f in assoc_frames])
     det = gpu_out["det"]
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))  # this job's CPU share (16 on the GPU box)
+    # the job's CPU share: the GPU box grants 16 CPUs per job (OMP_NUM_THREADS / MAX_JOBS = 16) while
+    # nproc reports the whole machine, so the all-cores leg runs on min(16, affinity) threads
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
 
-    # (a) the reference's shape: one thread
+    # (a) the reference's shape: one thread -- per frame cvtColor (mImGray), ORB extraction, the line
+    # detector on the colour frame (EAO Frame ctor), the motion search, the association
     k = min(args.cpu_frames, F)
-    frames_k = d_frames[:k].cpu().numpy()
+    color_k = d_color[:k].cpu().numpy()
+    gpu_gray = d_frames[:k].cpu().numpy()
     desc = d_desc.cpu().numpy()
     match = d_match.cpu().numpy()
     nm = d_nm.cpu().numpy()
+    t0 = time.perf_counter()
+    frames_k = [orc.color_to_gray(color_k[t], rgb=True) for t in range(k)]
+    t_gray = (time.perf_counter() - t0) / k
+    bad_gray = [t for t in range(k) if not np.array_equal(frames_k[t], gpu_gray[t])]
+    t0 = time.perf_counter()
+    olines = [orc.edlines_color(color_k[t]) for t in range(k)]
+    t_lines = (time.perf_counter() - t0) / k
+    gl, gn = d_lines[:k].cpu().numpy(), d_lcnt[:k].cpu().numpy()
+    bad_lines = [t for t in range(k) if not (int(gn[t]) == len(olines[t]) and np.array_equal(gl[t, :gn[t]], olines[t]))]
     t0 = time.perf_counter()
     okps, odesc = [], []
     for t in range(k):
@@ -798,27 +815,40 @@ def cpu_baseline(args, cfg, assoc_frames, d_frames, poses, kps, cnt, mpos, has, 
         gi, gf, _ = gpu_out["replay"].objects()
         ok_obj = bool(np.array_equal(oi, gi) and np.allclose(of, gf, rtol=1e-5, atol=1e-5, equal_nan=True))
 
-    # (b) all cores: extraction + matching frame-parallel, association on one thread beside
+    # (b) all cores: the frame work frame-parallel (cvtColor and the line detector on a thread pool --
+    # ctypes releases the GIL --, extraction + matching on std::threads), association on one thread beside
     km = min(args.cpu_mt_frames, F)
-    frames_m = d_frames[:km].cpu().numpy()
+    color_m = d_color[:km].cpu().numpy()
+    with ThreadPoolExecutor(threads) as pool:
+        t0 = time.perf_counter()
+        frames_m = np.stack(list(pool.map(lambda c: orc.color_to_gray(c, rgb=True), color_m)))
+        t_gray_mt = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        lines_m = list(pool.map(orc.edlines_color, color_m))
+        t_lines_mt = time.perf_counter() - t0
     sec, mk, md, mn, mm, mnm = orc.extract_match_mt(frames_m, poses[:km].reshape(km, 16), has[:km], mpos[:km], sc,
                                                     threads)
     bad_mt = [t for t in range(km) if not (int(mn[t]) == int(cnt[t]) and np.array_equal(mk[t, :mn[t]], kps[t, :mn[t]])
                                            and (t == 0 or np.array_equal(mm[t, :mn[t]], match[t, :mn[t]])))]
-    t_em_mt = sec / km
-    single = 1.0 / (t_ext + t_match + t_assoc)
+    bad_mt += [t for t in range(min(km, k)) if not np.array_equal(lines_m[t], olines[t])]
+    t_em_mt = (sec + t_gray_mt + t_lines_mt) / km
+    single = 1.0 / (t_gray + t_ext + t_lines + t_match + t_assoc)
     allc = 1.0 / max(t_em_mt, t_assoc)  # pipelined: the association thread is the bound
     base = {"value": allc, "unit": "frames/s", "cores": threads, "kind": "port",
             "cpu": cpu_model(), "nproc": os.cpu_count(),
             "sample": "oracle/ CPU restatement (g++ -O3 -march=native -ffp-contract=off, built on this host): "
-                      "extract+match %d frames frame-parallel on %d std::threads (%.2f ms/frame), association replay "
-                      "(%s flag, one thread) over the first %d of %d frames (%.2f ms/frame); frames/s = 1/max of the "
-                      "two (pipelined)" % (km, threads, 1e3 * t_em_mt, cfg["flag"], ka, F, 1e3 * t_assoc),
+                      "cvtColor + line detection + extract + match of %d frames frame-parallel on %d threads (the "
+                      "job's CPU share; %.2f ms/frame), association replay (%s flag, one thread) over the first %d "
+                      "of %d frames (%.2f ms/frame); frames/s = 1/max of the two (pipelined)"
+                      % (km, threads, 1e3 * t_em_mt, cfg["flag"], ka, F, 1e3 * t_assoc),
             "single_thread": {"value": single, "cores": 1,
-                              "sample": "one thread: extract %d frames (%.2f ms/frame), motion-match %d pairs "
-                                        "(%.2f ms/pair), association %d frames (%.2f ms/frame)"
-                                        % (k, 1e3 * t_ext, k - 1, 1e3 * t_match, ka, 1e3 * t_assoc)}}
-    parity = {"frames_checked_extract": k, "keypoints_descriptors_bitexact": not bad_kp,
+                              "sample": "one thread: cvtColor %d frames (%.2f ms/frame), extract (%.2f ms/frame), "
+                                        "line detection (%.2f ms/frame), motion-match %d pairs (%.2f ms/pair), "
+                                        "association %d frames (%.2f ms/frame)"
+                                        % (k, 1e3 * t_gray, 1e3 * t_ext, 1e3 * t_lines, k - 1, 1e3 * t_match, ka,
+                                           1e3 * t_assoc)}}
+    parity = {"frames_checked_extract": k, "gray_bitexact": not bad_gray, "lines_bitexact": not bad_lines,
+              "keypoints_descriptors_bitexact": not bad_kp,
               "match_ids_bitexact": not bad_match, "mismatch_frames": (bad_kp[:5], bad_match[:5]),
               "frames_checked_all_cores_leg": km, "all_cores_leg_identical": not bad_mt,
               "all_cores_leg_mismatch_frames": bad_mt[:5],

@@ -228,6 +228,12 @@ struct SearchSlot {
   const int* feats;      // [nsearch][cap]
 };
 
+// KFKF = false: SearchByBoW(KeyFrame*, Frame&) -- K the keyframe (outer), Fr the frame (inner),
+//   match[iF] = ikf, distance bar <= TH_LOW (ORBmatcher.cc:159-288);
+// KFKF = true: SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2) -- K = KF1 (outer), Fr = KF2 (inner, its map
+//   points checked: Fr.valid), match12[idx1] = idx2, bar < TH_LOW (ORBmatcher.cc:522-655). The inner
+//   side's taken flags are vbMatched2 there, the "already matched" test of the frame here.
+template <bool KFKF>
 __global__ __launch_bounds__(256) void k_bow_search(int cap, SearchSlot K, SearchSlot Fr, float nnratio,
                                                     int* __restrict__ f_match, int* __restrict__ err) {
   __shared__ uint8_t s_flag[4][NODE_MAXF];
@@ -250,7 +256,8 @@ __global__ __launch_bounds__(256) void k_bow_search(int cap, SearchSlot K, Searc
     return;
   }
   uint8_t* flag = s_flag[w];
-  for (int q = lane; q < nq; q += 64) flag[q] = 0;
+  for (int q = lane; q < nq; q += 64)
+    flag[q] = KFKF ? (Fr.valid[so + Fr.feats[so + q0 + q]] ? 0 : 1) : 0;  // !pMP2 || isBad(): never taken
   const int p0 = K.start[ss + j], p1 = K.start[ss + j + 1];
   int* M = f_match + so;
   for (int p = p0; p < p1; p++) {
@@ -283,10 +290,13 @@ __global__ __launch_bounds__(256) void k_bow_search(int cap, SearchSlot K, Searc
         d2 = min(d2, od1);
       }
     }
-    if (d1 <= TH_LOW && (float)d1 < __fmul_rn(nnratio, (float)d2)) {
+    if ((KFKF ? d1 < TH_LOW : d1 <= TH_LOW) && (float)d1 < __fmul_rn(nnratio, (float)d2)) {
       if (lane == 0) {
         flag[p1] = 1;
-        M[Fr.feats[so + q0 + p1]] = ikf;
+        if (KFKF)
+          M[ikf] = Fr.feats[so + q0 + p1];
+        else
+          M[Fr.feats[so + q0 + p1]] = ikf;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -303,7 +313,11 @@ __device__ __forceinline__ int rot_bin(float a_kf, float a_f) {
   return bin;
 }
 
-__global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict__ n_f, const int* __restrict__ n_kf,
+// the rotation check of both searches: KFKF = false iterates the frame's matches (rot = angle(kf) -
+// angle(frame), the histogram of frame indices), KFKF = true KF1's (rot = angle1 - angle2, histogram of
+// idx1); n = the indexed side's feature counts
+template <bool KFKF>
+__global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict__ n_idx,
                                                  const eao_keypoint_dev* __restrict__ kkps,
                                                  const eao_keypoint_dev* __restrict__ fkps, int check_ori,
                                                  int* __restrict__ f_match, int* __restrict__ nmatches,
@@ -313,7 +327,7 @@ __global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict_
   __shared__ int s_cnt;
   const int s = blockIdx.x, t = threadIdx.x;
   const size_t so = (size_t)s * cap;
-  const int n = min(n_f[s], cap);
+  const int n = min(n_idx[s], cap);
   if (err[s]) {  // a vocabulary node held more frame features than the search supports
     if (t == 0) nmatches[s] = EAO_E_CAPACITY;
     return;
@@ -325,7 +339,9 @@ __global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict_
   if (check_ori) {
     for (int i = t; i < n; i += 256) {
       const int k = M[i];
-      if (k >= 0) atomicAdd(&hist[rot_bin(kkps[so + k].angle, fkps[so + i].angle)], 1);
+      if (k >= 0)
+        atomicAdd(&hist[KFKF ? rot_bin(kkps[so + i].angle, fkps[so + k].angle)
+                             : rot_bin(kkps[so + k].angle, fkps[so + i].angle)], 1);
     }
     __syncthreads();
     if (t == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1601-1642)
@@ -357,7 +373,9 @@ __global__ __launch_bounds__(256) void k_bow_rot(int cap, const int* __restrict_
   for (int i = t; i < n; i += 256) {
     const int k = M[i];
     if (k < 0) continue;
-    if (check_ori && !keep[rot_bin(kkps[so + k].angle, fkps[so + i].angle)]) M[i] = -1;
+    if (check_ori && !keep[KFKF ? rot_bin(kkps[so + i].angle, fkps[so + k].angle)
+                                : rot_bin(kkps[so + k].angle, fkps[so + i].angle)])
+      M[i] = -1;
     else c++;
   }
   atomicAdd(&s_cnt, c);
@@ -382,7 +400,7 @@ struct VocabEngine {
   // single-call staging: two sides of a search / one frame of a transform
   eao_keypoint_dev* d_kps = nullptr;  // [2][max_kps]
   uint8_t* d_desc = nullptr;          // [2][max_kps][32]
-  uint8_t* d_valid = nullptr;         // [max_kps]
+  uint8_t* d_valid = nullptr;         // [2][max_kps]
   int* d_i = nullptr;                 // [2][3 * max_kps + 1] node ids | start | feats, + counts
   double* d_ww = nullptr;             // [max_kps]
   int* d_out = nullptr;               // [max_kps + 16]
@@ -469,7 +487,7 @@ int eao_vocab_create(int device, int n_nodes, const uint8_t* node_desc, const in
   if ((r = e.alloc(&e.d_fnode, sizeof(int) * K * B)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_kps, sizeof(eao_keypoint_dev) * 2 * K)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_desc, 64 * K)) != hipSuccess) return fail(r);
-  if ((r = e.alloc(&e.d_valid, K)) != hipSuccess) return fail(r);
+  if ((r = e.alloc(&e.d_valid, 2 * K)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_i, sizeof(int) * 2 * (3 * K + 8))) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_ww, sizeof(double) * K)) != hipSuccess) return fail(r);
   if ((r = e.alloc(&e.d_out, sizeof(int) * (K + 16))) != hipSuccess) return fail(r);
@@ -582,38 +600,71 @@ int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, i
                      d_f_node_feats};
   EAO_HIP_CHECK(hipMemsetAsync(d_f_match, 0xff, sizeof(int) * (size_t)nsearch * cap, s));
   EAO_HIP_CHECK(hipMemsetAsync(e.d_err, 0, sizeof(int) * nsearch, s));
-  hipLaunchKernelGGL(k_bow_search, dim3((cap + 3) / 4, nsearch), dim3(256), 0, s, cap, K, F, nnratio, d_f_match,
-                     e.d_err);
-  hipLaunchKernelGGL(k_bow_rot, dim3(nsearch), dim3(256), 0, s, cap, d_n_f, d_kf_nn, K.kps, F.kps, check_ori,
+  hipLaunchKernelGGL(k_bow_search<false>, dim3((cap + 3) / 4, nsearch), dim3(256), 0, s, cap, K, F, nnratio,
+                     d_f_match, e.d_err);
+  hipLaunchKernelGGL(k_bow_rot<false>, dim3(nsearch), dim3(256), 0, s, cap, d_n_f, K.kps, F.kps, check_ori,
                      d_f_match, d_nmatches, e.d_err);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
 
-int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, const eao_keypoint* kf_kps,
-                      const uint8_t* kf_desc, const uint8_t* kf_mp_valid, int kf_nn,
-                      const int32_t* kf_node_ids, const int32_t* kf_node_start,
-                      const int32_t* kf_node_feats, int n_f, const eao_keypoint* f_kps,
-                      const uint8_t* f_desc, int f_nn, const int32_t* f_node_ids,
-                      const int32_t* f_node_start, const int32_t* f_node_feats, int32_t* f_match) {
-  if (!v || n_kf < 0 || n_f < 0 || n_kf > v->e.max_kps || n_f > v->e.max_kps || kf_nn < 0 || f_nn < 0 ||
-      kf_nn > n_kf || f_nn > n_f || !f_match || (n_kf > 0 && (!kf_kps || !kf_desc || !kf_mp_valid)) ||
-      (n_f > 0 && (!f_kps || !f_desc)) || (kf_nn > 0 && (!kf_node_ids || !kf_node_start || !kf_node_feats)) ||
-      (f_nn > 0 && (!f_node_ids || !f_node_start || !f_node_feats))) {
-    set_error("eao_search_by_bow: bad arguments (sizes outside [0, max_kps] or null buffer)");
+int eao_search_by_bow_kf_batch_device(eao_vocab* v, float nnratio, int check_ori, int nsearch, int cap,
+                                      const int32_t* d_n1, const eao_keypoint* d_kps1, const uint8_t* d_desc1,
+                                      const uint8_t* d_valid1, const int32_t* d_nn1, const int32_t* d_node_ids1,
+                                      const int32_t* d_node_start1, const int32_t* d_node_feats1,
+                                      const eao_keypoint* d_kps2, const uint8_t* d_desc2, const uint8_t* d_valid2,
+                                      const int32_t* d_nn2, const int32_t* d_node_ids2,
+                                      const int32_t* d_node_start2, const int32_t* d_node_feats2,
+                                      int32_t* d_match12, int32_t* d_nmatches, void* stream) {
+  if (!v || nsearch < 0 || nsearch > v->e.max_batch || cap < 1 || cap > v->e.max_kps) {
+    set_error("eao_search_by_bow_kf_batch_device: bad arguments (nsearch <= max_batch, cap in [1, max_kps])");
     return EAO_E_ARG;
   }
-  if (n_f == 0) return 0;
+  if (nsearch == 0) return EAO_OK;
+  VocabEngine& e = v->e;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  hipStream_t s = stream ? (hipStream_t)stream : e.stream;
+  const SearchSlot K1{(const eao_keypoint_dev*)d_kps1, d_desc1, d_valid1, d_nn1, d_node_ids1, d_node_start1,
+                      d_node_feats1};
+  const SearchSlot K2{(const eao_keypoint_dev*)d_kps2, d_desc2, d_valid2, d_nn2, d_node_ids2, d_node_start2,
+                      d_node_feats2};
+  EAO_HIP_CHECK(hipMemsetAsync(d_match12, 0xff, sizeof(int) * (size_t)nsearch * cap, s));
+  EAO_HIP_CHECK(hipMemsetAsync(e.d_err, 0, sizeof(int) * nsearch, s));
+  hipLaunchKernelGGL(k_bow_search<true>, dim3((cap + 3) / 4, nsearch), dim3(256), 0, s, cap, K1, K2, nnratio,
+                     d_match12, e.d_err);
+  hipLaunchKernelGGL(k_bow_rot<true>, dim3(nsearch), dim3(256), 0, s, cap, d_n1, K1.kps, K2.kps, check_ori,
+                     d_match12, d_nmatches, e.d_err);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+// one search of either kind on host buffers: side 1 (keyframe / KF1) and side 2 (frame / KF2)
+// staged into the handle's two slots, the batched path on one search, the result back
+static int search_single(eao_vocab* v, bool kfkf, const char* name, float nnratio, int check_ori, int n1,
+                         const eao_keypoint* kps1, const uint8_t* desc1, const uint8_t* valid1, int nn1,
+                         const int32_t* ids1, const int32_t* st1, const int32_t* ft1, int n2,
+                         const eao_keypoint* kps2, const uint8_t* desc2, const uint8_t* valid2, int nn2,
+                         const int32_t* ids2, const int32_t* st2, const int32_t* ft2, int32_t* out) {
+  if (!v || n1 < 0 || n2 < 0 || n1 > v->e.max_kps || n2 > v->e.max_kps || nn1 < 0 || nn2 < 0 || nn1 > n1 ||
+      nn2 > n2 || !out || (n1 > 0 && (!kps1 || !desc1 || !valid1)) ||
+      (n2 > 0 && (!kps2 || !desc2 || (kfkf && !valid2))) || (nn1 > 0 && (!ids1 || !st1 || !ft1)) ||
+      (nn2 > 0 && (!ids2 || !st2 || !ft2))) {
+    set_error(std::string(name) + ": bad arguments (sizes outside [0, max_kps] or null buffer)");
+    return EAO_E_ARG;
+  }
+  const int n_out = kfkf ? n1 : n2;  // the side the result is indexed by
+  if (n_out == 0) return 0;
   VocabEngine& e = v->e;
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = e.stream;
   const int K = e.max_kps;
-  // staging: side 0 = keyframe, side 1 = frame; the node CSR of side k at d_i + k * (3K + 8)
-  int* kI = e.d_i;
-  int* fI = e.d_i + 3 * K + 8;
-  const int kf_nf = kf_nn > 0 ? kf_node_start[kf_nn] : 0, f_nf = f_nn > 0 ? f_node_start[f_nn] : 0;
-  if (kf_nf > n_kf || f_nf > n_f) {
-    set_error("eao_search_by_bow: a FeatureVector lists more features than the side has");
+  // staging: side 1 and side 2; the node CSR of side k at d_i + k * (3K + 8), then its node and
+  // feature counts
+  int* I1 = e.d_i;
+  int* I2 = e.d_i + 3 * K + 8;
+  const int nf1 = nn1 > 0 ? st1[nn1] : 0, nf2 = nn2 > 0 ? st2[nn2] : 0;
+  if (nf1 > n1 || nf2 > n2) {
+    set_error(std::string(name) + ": a FeatureVector lists more features than the side has");
     return EAO_E_ARG;
   }
   // the kernel indexes descriptors / flags / matches with these values and binary-searches the
@@ -627,23 +678,26 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
       if (ft[k] < 0 || ft[k] >= nfeat) return false;
     return true;
   };
-  if (!fv_ok(kf_nn, kf_node_ids, kf_node_start, kf_node_feats, n_kf) ||
-      !fv_ok(f_nn, f_node_ids, f_node_start, f_node_feats, n_f)) {
-    set_error("eao_search_by_bow: malformed FeatureVector (feature index out of range, node starts "
+  if (!fv_ok(nn1, ids1, st1, ft1, n1) || !fv_ok(nn2, ids2, st2, ft2, n2)) {
+    set_error(std::string(name) + ": malformed FeatureVector (feature index out of range, node starts "
               "decreasing or node ids not ascending)");
     return EAO_E_ARG;
   }
-  if (n_kf > 0) {
-    EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, kf_kps, sizeof(eao_keypoint) * n_kf, hipMemcpyHostToDevice, s));
-    EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, kf_desc, 32 * (size_t)n_kf, hipMemcpyHostToDevice, s));
-    EAO_HIP_CHECK(hipMemcpyAsync(e.d_valid, kf_mp_valid, n_kf, hipMemcpyHostToDevice, s));
+  if (n1 > 0) {
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, kps1, sizeof(eao_keypoint) * n1, hipMemcpyHostToDevice, s));
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc, desc1, 32 * (size_t)n1, hipMemcpyHostToDevice, s));
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_valid, valid1, n1, hipMemcpyHostToDevice, s));
   }
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, f_kps, sizeof(eao_keypoint) * n_f, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + 32 * (size_t)K, f_desc, 32 * (size_t)n_f, hipMemcpyHostToDevice, s));
-  auto up_fv = [&](int* base, int nn, const int32_t* ids, const int32_t* st, const int32_t* ft, int nf,
+  if (n2 > 0) {
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, kps2, sizeof(eao_keypoint) * n2, hipMemcpyHostToDevice, s));
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + 32 * (size_t)K, desc2, 32 * (size_t)n2, hipMemcpyHostToDevice, s));
+    if (kfkf) EAO_HIP_CHECK(hipMemcpyAsync(e.d_valid + K, valid2, n2, hipMemcpyHostToDevice, s));
+  }
+  auto up_fv = [&](int* base, int nn, const int32_t* ids, const int32_t* st, const int32_t* ft, int nf, int n,
                    int* hslot) -> int {
-    *hslot = nn;
-    EAO_HIP_CHECK(hipMemcpyAsync(base + 3 * K + 4, hslot, sizeof(int), hipMemcpyHostToDevice, s));
+    hslot[0] = nn;
+    hslot[1] = n;
+    EAO_HIP_CHECK(hipMemcpyAsync(base + 3 * K + 4, hslot, 2 * sizeof(int), hipMemcpyHostToDevice, s));
     if (nn > 0) {
       EAO_HIP_CHECK(hipMemcpyAsync(base, ids, sizeof(int) * nn, hipMemcpyHostToDevice, s));
       EAO_HIP_CHECK(hipMemcpyAsync(base + K, st, sizeof(int) * (nn + 1), hipMemcpyHostToDevice, s));
@@ -651,25 +705,51 @@ int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, cons
     }
     return EAO_OK;
   };
-  int rc = up_fv(kI, kf_nn, kf_node_ids, kf_node_start, kf_node_feats, kf_nf, e.h_small);
-  if (!rc) rc = up_fv(fI, f_nn, f_node_ids, f_node_start, f_node_feats, f_nf, e.h_small + 1);
+  int rc = up_fv(I1, nn1, ids1, st1, ft1, nf1, n1, e.h_small);
+  if (!rc) rc = up_fv(I2, nn2, ids2, st2, ft2, nf2, n2, e.h_small + 2);
   if (rc) return rc;
-  e.h_small[2] = n_f;
-  EAO_HIP_CHECK(hipMemcpyAsync(fI + 3 * K + 5, e.h_small + 2, sizeof(int), hipMemcpyHostToDevice, s));
-  rc = eao_search_by_bow_batch_device(v, nnratio, check_ori, 1, K, (const eao_keypoint*)e.d_kps, e.d_desc, e.d_valid,
-                                      kI + 3 * K + 4, kI, kI + K, kI + 2 * K + 1, fI + 3 * K + 5,
-                                      (const eao_keypoint*)(e.d_kps + K), e.d_desc + 32 * (size_t)K, fI + 3 * K + 4,
-                                      fI, fI + K, fI + 2 * K + 1, e.d_out, e.d_out + K, s);
+  const eao_keypoint* k1 = (const eao_keypoint*)e.d_kps;
+  const eao_keypoint* k2 = (const eao_keypoint*)(e.d_kps + K);
+  if (kfkf)
+    rc = eao_search_by_bow_kf_batch_device(v, nnratio, check_ori, 1, K, I1 + 3 * K + 5, k1, e.d_desc, e.d_valid,
+                                           I1 + 3 * K + 4, I1, I1 + K, I1 + 2 * K + 1, k2, e.d_desc + 32 * (size_t)K,
+                                           e.d_valid + K, I2 + 3 * K + 4, I2, I2 + K, I2 + 2 * K + 1, e.d_out,
+                                           e.d_out + K, s);
+  else
+    rc = eao_search_by_bow_batch_device(v, nnratio, check_ori, 1, K, k1, e.d_desc, e.d_valid, I1 + 3 * K + 4, I1,
+                                        I1 + K, I1 + 2 * K + 1, I2 + 3 * K + 5, k2, e.d_desc + 32 * (size_t)K,
+                                        I2 + 3 * K + 4, I2, I2 + K, I2 + 2 * K + 1, e.d_out, e.d_out + K, s);
   if (rc) return rc;
-  EAO_HIP_CHECK(hipMemcpyAsync(f_match, e.d_out, sizeof(int) * n_f, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.h_small + 3, e.d_out + K, sizeof(int), hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(out, e.d_out, sizeof(int) * n_out, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.h_small + 4, e.d_out + K, sizeof(int), hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
-  const int nm = e.h_small[3];
+  const int nm = e.h_small[4];
   if (nm < 0) {
-    set_error("eao_search_by_bow: a vocabulary node holds more than 1024 frame features");
+    set_error(std::string(name) + ": a vocabulary node holds more than 1024 features of the second side");
     return EAO_E_CAPACITY;
   }
   return nm;
+}
+
+int eao_search_by_bow(eao_vocab* v, float nnratio, int check_ori, int n_kf, const eao_keypoint* kf_kps,
+                      const uint8_t* kf_desc, const uint8_t* kf_mp_valid, int kf_nn,
+                      const int32_t* kf_node_ids, const int32_t* kf_node_start,
+                      const int32_t* kf_node_feats, int n_f, const eao_keypoint* f_kps,
+                      const uint8_t* f_desc, int f_nn, const int32_t* f_node_ids,
+                      const int32_t* f_node_start, const int32_t* f_node_feats, int32_t* f_match) {
+  return search_single(v, false, "eao_search_by_bow", nnratio, check_ori, n_kf, kf_kps, kf_desc, kf_mp_valid, kf_nn,
+                       kf_node_ids, kf_node_start, kf_node_feats, n_f, f_kps, f_desc, nullptr, f_nn, f_node_ids,
+                       f_node_start, f_node_feats, f_match);
+}
+
+int eao_search_by_bow_kf(eao_vocab* v, float nnratio, int check_ori, int n1, const eao_keypoint* kps1,
+                         const uint8_t* desc1, const uint8_t* valid1, int nn1, const int32_t* node_ids1,
+                         const int32_t* node_start1, const int32_t* node_feats1, int n2, const eao_keypoint* kps2,
+                         const uint8_t* desc2, const uint8_t* valid2, int nn2, const int32_t* node_ids2,
+                         const int32_t* node_start2, const int32_t* node_feats2, int32_t* match12) {
+  return search_single(v, true, "eao_search_by_bow_kf", nnratio, check_ori, n1, kps1, desc1, valid1, nn1, node_ids1,
+                       node_start1, node_feats1, n2, kps2, desc2, valid2, nn2, node_ids2, node_start2, node_feats2,
+                       match12);
 }
 
 }  // extern "C"

@@ -400,6 +400,28 @@ class Vocab(_Handle):
                                           P(b[2]), P(m)), "eao_search_by_bow")
         return n, m
 
+    def search_kf(self, nnratio, check_ori, kps1, desc1, valid1, fv1, kps2, desc2, valid2, fv2):
+        """SearchByBoW(KF1, KF2): fv = (node_ids, node_start, node_feats) -> (nmatches, match12)."""
+        m = np.full(len(kps1), -1, np.int32)
+        a = [np.ascontiguousarray(x, np.int32) for x in fv1]
+        b = [np.ascontiguousarray(x, np.int32) for x in fv2]
+        n = check(lib().eao_search_by_bow_kf(self.h, ctypes.c_float(nnratio), int(check_ori), len(kps1),
+                                             P(np.ascontiguousarray(kps1)), P(np.ascontiguousarray(desc1, np.uint8)),
+                                             P(np.ascontiguousarray(valid1, np.uint8)), len(a[0]), P(a[0]), P(a[1]),
+                                             P(a[2]), len(kps2), P(np.ascontiguousarray(kps2)),
+                                             P(np.ascontiguousarray(desc2, np.uint8)),
+                                             P(np.ascontiguousarray(valid2, np.uint8)), len(b[0]), P(b[0]), P(b[1]),
+                                             P(b[2]), P(m)), "eao_search_by_bow_kf")
+        return n, m
+
+    def search_kf_batch_device(self, nnratio, check_ori, nsearch, cap, d_n1, kf1, kf2, d_match, d_nm, stream=None):
+        """kf1 / kf2: (kps, desc, valid, nn, node_ids, node_start, node_feats) device pointers."""
+        v = ctypes.c_void_p
+        check(lib().eao_search_by_bow_kf_batch_device(self.h, ctypes.c_float(nnratio), int(check_ori), nsearch, cap,
+                                                      v(d_n1), *[v(x) for x in kf1], *[v(x) for x in kf2], v(d_match),
+                                                      v(d_nm), v(stream) if stream else None),
+              "eao_search_by_bow_kf_batch_device")
+
     def transform_batch_device(self, nframes, cap, d_counts, d_desc, levelsup, d_wid, d_ww, d_nw, d_nid, d_ns, d_nf,
                                d_nn, stream=None):
         v = ctypes.c_void_p

@@ -492,6 +492,32 @@ int eao_search_by_bow_batch_device(eao_vocab* v, float nnratio, int check_ori, i
                                    const int32_t* d_f_node_start, const int32_t* d_f_node_feats,
                                    int32_t* d_f_match, int32_t* d_nmatches, void* stream);
 
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+   (src/ORBmatcher.cc:522-655), called by LoopClosing::ComputeSim3 (src/LoopClosing.cc:265). Both sides as
+   eao_search_by_bow's keyframe side: valid1 / valid2[i] = GetMapPointMatches()[i] && !isBad() (the second
+   side's map points are checked too, :576-580), the FeatureVectors as eao_bow_transform returns them.
+   match12[i1] = the KF2 feature whose map point KF1 feature i1 matched (-1: none) -- vpMatches12[i1] is that
+   feature's map point. The distance bar is strict (bestDist1 < TH_LOW), the KF2 features are taken first-wins
+   (vbMatched2), the rotation check histograms idx1. Returns nmatches (>= 0) or an EAO_E_* error. */
+int eao_search_by_bow_kf(eao_vocab* v, float nnratio, int check_ori, int n1, const eao_keypoint* kps1,
+                         const uint8_t* desc1, const uint8_t* valid1, int nn1, const int32_t* node_ids1,
+                         const int32_t* node_start1, const int32_t* node_feats1, int n2, const eao_keypoint* kps2,
+                         const uint8_t* desc2, const uint8_t* valid2, int nn2, const int32_t* node_ids2,
+                         const int32_t* node_start2, const int32_t* node_feats2, int32_t* match12);
+/* batched, HBM-resident: search s pairs KF1 slot s with KF2 slot s ([nsearch][cap] keypoints / descriptors /
+   valid flags / node ids / node features, [nsearch][cap + 1] node starts, node counts d_nn1 / d_nn2, KF1 feature
+   counts d_n1); writes d_match12 [nsearch][cap] and d_nmatches [nsearch] (EAO_E_CAPACITY for a search in which
+   a vocabulary node holds more than 1024 KF2 features). nsearch <= max_batch; the FeatureVector
+   preconditions of eao_search_by_bow_batch_device. */
+int eao_search_by_bow_kf_batch_device(eao_vocab* v, float nnratio, int check_ori, int nsearch, int cap,
+                                      const int32_t* d_n1, const eao_keypoint* d_kps1, const uint8_t* d_desc1,
+                                      const uint8_t* d_valid1, const int32_t* d_nn1, const int32_t* d_node_ids1,
+                                      const int32_t* d_node_start1, const int32_t* d_node_feats1,
+                                      const eao_keypoint* d_kps2, const uint8_t* d_desc2, const uint8_t* d_valid2,
+                                      const int32_t* d_nn2, const int32_t* d_node_ids2,
+                                      const int32_t* d_node_start2, const int32_t* d_node_feats2,
+                                      int32_t* d_match12, int32_t* d_nmatches, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -217,3 +217,76 @@ extern "C" int orc_search_by_bow(float nnratio, int check_ori, int n_kf, const o
   }
   return nmatches;
 }
+
+// ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& vpMatches12)
+// (src/ORBmatcher.cc:522-655; LoopClosing::ComputeSim3, src/LoopClosing.cc:265): the same node
+// walk as the KeyFrame -> Frame search, but the second side's map points are checked too
+// (vpMapPoints2[idx2] && !isBad(), :576-580), its matched flags are vbMatched2 (:534, set at
+// :599, never cleared by the rotation check), the distance bar is strict (bestDist1 < TH_LOW,
+// :594, against <= in the KeyFrame -> Frame search), the result is indexed by the first side
+// (vpMatches12[idx1], :598) and the rotation histogram holds idx1 (:607-613, rot = angle1 -
+// angle2). match12[i1] = the KF2 feature whose map point matched KF1 feature i1 (-1 none).
+extern "C" int orc_search_by_bow_kf(float nnratio, int check_ori, int n1, const orc_keypoint* kps1,
+                                    const uint8_t* desc1, const uint8_t* valid1, int nn1, const int32_t* ids1,
+                                    const int32_t* start1, const int32_t* feats1, int n2, const orc_keypoint* kps2,
+                                    const uint8_t* desc2, const uint8_t* valid2, int nn2, const int32_t* ids2,
+                                    const int32_t* start2, const int32_t* feats2, int32_t* match12) {
+  for (int i = 0; i < n1; i++) match12[i] = -1;
+  std::vector<char> matched2(n2 > 0 ? n2 : 1, 0);
+  int nmatches = 0;
+  std::vector<int> rotHist[HISTO_LENGTH];
+  const float factor = 1.0f / HISTO_LENGTH;
+  int a = 0, b = 0;
+  while (a < nn1 && b < nn2) {
+    if (ids1[a] == ids2[b]) {
+      for (int p = start1[a]; p < start1[a + 1]; p++) {
+        const int idx1 = feats1[p];
+        if (!valid1[idx1]) continue;  // !pMP1 || pMP1->isBad()
+        const uint8_t* d1 = desc1 + 32 * (size_t)idx1;
+        int bestDist1 = 256, bestIdx2 = -1, bestDist2 = 256;
+        for (int q = start2[b]; q < start2[b + 1]; q++) {
+          const int idx2 = feats2[q];
+          if (matched2[idx2] || !valid2[idx2]) continue;
+          const int dist = hamming(d1, desc2 + 32 * (size_t)idx2);
+          if (dist < bestDist1) {
+            bestDist2 = bestDist1;
+            bestDist1 = dist;
+            bestIdx2 = idx2;
+          } else if (dist < bestDist2) {
+            bestDist2 = dist;
+          }
+        }
+        if (bestDist1 < TH_LOW && (float)bestDist1 < nnratio * (float)bestDist2) {
+          match12[idx1] = bestIdx2;
+          matched2[bestIdx2] = 1;
+          if (check_ori) {
+            float rot = kps1[idx1].angle - kps2[bestIdx2].angle;
+            if (rot < 0.0) rot += 360.0f;
+            int bin = (int)std::round(rot * factor);
+            if (bin == HISTO_LENGTH) bin = 0;
+            rotHist[bin].push_back(idx1);
+          }
+          nmatches++;
+        }
+      }
+      a++;
+      b++;
+    } else if (ids1[a] < ids2[b]) {
+      a = (int)(std::lower_bound(ids1 + a, ids1 + nn1, ids2[b]) - ids1);
+    } else {
+      b = (int)(std::lower_bound(ids2 + b, ids2 + nn2, ids1[a]) - ids2);
+    }
+  }
+  if (check_ori) {
+    int i1 = -1, i2 = -1, i3 = -1;
+    three_maxima(rotHist, i1, i2, i3);
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+      if (i == i1 || i == i2 || i == i3) continue;
+      for (int j : rotHist[i]) {
+        match12[j] = -1;
+        nmatches--;
+      }
+    }
+  }
+  return nmatches;
+}

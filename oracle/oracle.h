@@ -211,6 +211,14 @@ int orc_search_by_bow(float nnratio, int check_ori, int n_kf, const orc_keypoint
                       const uint8_t* f_desc, int f_nn, const int32_t* f_node_ids,
                       const int32_t* f_node_start, const int32_t* f_node_feats, int32_t* f_match);
 
+/* ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>&) (src/ORBmatcher.cc:522-655):
+   valid1 / valid2 = GetMapPointMatches()[i] && !isBad(); match12[i1] = matched KF2 feature (-1 none) */
+int orc_search_by_bow_kf(float nnratio, int check_ori, int n1, const orc_keypoint* kps1, const uint8_t* desc1,
+                         const uint8_t* valid1, int nn1, const int32_t* ids1, const int32_t* start1,
+                         const int32_t* feats1, int n2, const orc_keypoint* kps2, const uint8_t* desc2,
+                         const uint8_t* valid2, int nn2, const int32_t* ids2, const int32_t* start2,
+                         const int32_t* feats2, int32_t* match12);
+
 #ifdef __cplusplus
 }
 #endif

@@ -448,3 +448,16 @@ def search_by_bow(nnratio, check_ori, kf_kps, kf_desc, kf_valid, kf_fv, f_kps, f
                                 len(a[0]), P(a[0]), P(a[1]), P(a[2]), len(f_kps), P(np.ascontiguousarray(f_kps)),
                                 P(np.ascontiguousarray(f_desc, np.uint8)), len(b[0]), P(b[0]), P(b[1]), P(b[2]), P(m))
     return n, m
+
+
+def search_by_bow_kf(nnratio, check_ori, kps1, desc1, valid1, fv1, kps2, desc2, valid2, fv2):
+    """SearchByBoW(KF1, KF2): fv = (node_ids, node_start, node_feats); -> (nmatches, match12)."""
+    m = np.full(len(kps1), -1, np.int32)
+    a = [np.ascontiguousarray(x, np.int32) for x in fv1]
+    b = [np.ascontiguousarray(x, np.int32) for x in fv2]
+    n = lib().orc_search_by_bow_kf(ctypes.c_float(nnratio), int(check_ori), len(kps1), P(np.ascontiguousarray(kps1)),
+                                   P(np.ascontiguousarray(desc1, np.uint8)), P(np.ascontiguousarray(valid1, np.uint8)),
+                                   len(a[0]), P(a[0]), P(a[1]), P(a[2]), len(kps2), P(np.ascontiguousarray(kps2)),
+                                   P(np.ascontiguousarray(desc2, np.uint8)), P(np.ascontiguousarray(valid2, np.uint8)),
+                                   len(b[0]), P(b[0]), P(b[1]), P(b[2]), P(m))
+    return n, m

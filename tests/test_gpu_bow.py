@@ -137,3 +137,77 @@ def test_search_node_capacity():
     assert np.diff(ffv[1]).max() > 1024
     with pytest.raises(ea.EaoError, match="1024"):
         V.search(0.75, 1, kk, kd, kv, kfv, fk, fd, ffv)
+
+
+# ---- SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2) (src/ORBmatcher.cc:522-655)
+@pytest.mark.parametrize("check_ori,nnratio", [(1, 0.75), (0, 0.75), (1, 0.9)])
+def test_search_kf_orb_shape(orbvoc, check_ori, nnratio):
+    k1, d1, v1, k2, d2 = synth.bow_pair(orbvoc, 1000, 1000, seed=21)
+    v2 = (np.random.default_rng(22).random(len(k2)) < 0.8).astype(np.uint8)
+    V = ea.Vocab(orbvoc)
+    fv1, fv2 = V.transform(d1)[2:], V.transform(d2)[2:]
+    ng, mg = V.search_kf(nnratio, check_ori, k1, d1, v1, fv1, k2, d2, v2, fv2)
+    no, mo = orc.search_by_bow_kf(nnratio, check_ori, k1, d1, v1, fv1, k2, d2, v2, fv2)
+    assert ng == no and np.array_equal(mg, mo), int((mg != mo).sum())
+    assert no > 100
+
+
+def test_search_kf_dense_nodes_and_edges():
+    voc = synth.vocabulary(K=10, L=4, seed=9)
+    k1, d1, v1, k2, d2 = synth.bow_pair(voc, 1200, 900, seed=23)
+    v2 = (np.random.default_rng(24).random(len(k2)) < 0.7).astype(np.uint8)
+    V = ea.Vocab(voc)
+    fv1, fv2 = V.transform(d1, 3)[2:], V.transform(d2, 3)[2:]
+    g = V.search_kf(0.75, 1, k1, d1, v1, fv1, k2, d2, v2, fv2)
+    o = orc.search_by_bow_kf(0.75, 1, k1, d1, v1, fv1, k2, d2, v2, fv2)
+    assert g[0] == o[0] and np.array_equal(g[1], o[1])
+    assert V.search_kf(0.75, 1, k1, d1, v1, fv1, k2, d2, np.zeros_like(v2), fv2)[0] == 0  # no valid KF2 point
+    e = (np.zeros(0, np.int32), np.zeros(1, np.int32), np.zeros(0, np.int32))
+    assert V.search_kf(0.75, 1, k1, d1, v1, e, k2, d2, v2, fv2)[0] == 0
+
+
+def test_search_kf_batch_device(orbvoc):
+    import torch
+    dev = torch.device("cuda", 0)
+    F, cap = 6, 1024
+    sizes = [1000, 0, 700, 1024, 1, 333]
+    desc = np.zeros((F, cap, 32), np.uint8)
+    kps = np.zeros((F, cap), ea.KP_DTYPE)
+    valid = np.zeros((F, cap), np.uint8)
+    rng = np.random.default_rng(31)
+    for f, n in enumerate(sizes):
+        kk, kd, _, _, _ = synth.bow_pair(orbvoc, max(n, 1), 1, seed=200 + f)
+        desc[f, :n], kps[f, :n], valid[f, :n] = kd[:n], kk[:n], (rng.random(n) < 0.85)
+    # KF2 of search f = KF1 slot f re-observed (bits flipped, angles rotated): share many words
+    desc2, kps2 = desc.copy(), kps.copy()
+    for f, n in enumerate(sizes):
+        desc2[f, :n] = synth._flip_bits(desc[f, :n].copy(), 6, rng)
+        kps2[f, :n]["angle"] = np.mod(kps[f, :n]["angle"] - 40 + rng.normal(0, 3, n), 360).astype(np.float32)
+    valid2 = (rng.random((F, cap)) < 0.85).astype(np.uint8)
+    V = ea.Vocab(orbvoc, max_kps=cap, max_batch=F)
+    fv1 = [orc.bow_transform(orbvoc, desc[f, :n], 4)[2:] for f, n in enumerate(sizes)]
+    fv2 = [orc.bow_transform(orbvoc, desc2[f, :n], 4)[2:] for f, n in enumerate(sizes)]
+
+    def csr(fvs):
+        ids, st, ft, nn = np.zeros((F, cap), np.int32), np.zeros((F, cap + 1), np.int32), \
+            np.zeros((F, cap), np.int32), np.zeros(F, np.int32)
+        for f, (a, b, c) in enumerate(fvs):
+            nn[f] = len(a)
+            ids[f, :len(a)], st[f, :len(b)], ft[f, :len(c)] = a, b, c
+        return ids, st, ft, nn
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    i1, s1, f1, n1 = csr(fv1)
+    i2, s2, f2, n2 = csr(fv2)
+    keep = [t(np.array(sizes, np.int32)), t(kps.view(np.uint8).reshape(F, cap, 28)), t(desc), t(valid), t(n1), t(i1),
+            t(s1), t(f1), t(kps2.view(np.uint8).reshape(F, cap, 28)), t(desc2), t(valid2), t(n2), t(i2), t(s2), t(f2)]
+    match = torch.full((F, cap), -7, dtype=torch.int32, device=dev)
+    nm = torch.zeros(F, dtype=torch.int32, device=dev)
+    V.search_kf_batch_device(0.75, 1, F, cap, keep[0].data_ptr(), tuple(x.data_ptr() for x in keep[1:8]),
+                             tuple(x.data_ptr() for x in keep[8:]), match.data_ptr(), nm.data_ptr())
+    torch.cuda.synchronize()
+    hm, hn = match.cpu().numpy(), nm.cpu().numpy()
+    for f, n in enumerate(sizes):
+        no, mo = orc.search_by_bow_kf(0.75, 1, kps[f, :n], desc[f, :n], valid[f, :n], fv1[f], kps2[f, :n],
+                                      desc2[f, :n], valid2[f, :n], fv2[f])
+        assert hn[f] == no and np.array_equal(hm[f, :n], mo), f
+    assert hn.max() > 100

@@ -10,8 +10,8 @@ src/ORBmatcher.cc:1328-1470), on one HIP stream. Frames are independent units
 data-path collective ("scaling": "weak"); value = all ranks' frames / the max
 over ranks of the timed region.
 
+  python bench.py --config b [--gpus N] [--frames 256] [--steps 5] [--cpu-frames 3]
   python tools/bench_config_b.py [--frames 256] [--steps 5] [--cpu-frames 3]
-  torchrun --nproc-per-node N tools/bench_config_b.py ...
 
 The stream is --unique rendered frames (a smooth camera path) repeated to
 --frames; the pairs across a repeat boundary are pose jumps that match little.
@@ -65,15 +65,20 @@ def algorithmic_bytes(n_kps):
             "describe": l0 + upper + n_kps * 60, "extract": l0 + 2 * upper + n_kps * 60}
 
 
-def main():
+def parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--unique", type=int, default=64, help="rendered frames (repeated to --frames)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--cpu-frames", type=int, default=3)
-    args = ap.parse_args()
+    return ap
 
+
+def main(args=None):
+    """One Config B measurement; `args` as parser() makes them (bench.py --config b passes its own)."""
+    if args is None:
+        args = parser().parse_args()
     rank, world, local = eao_dist.env_rank()
     ndev = torch.cuda.device_count()
     if ndev < 1:
