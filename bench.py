@@ -34,7 +34,8 @@ Inputs: the association runs on the reference's own fr3_long_office detections
 committed in tests/golden/fr3_inputs.npz; the 3-D object clouds, tracked map points and
 line segments are synthesised around them (tools/synth.assoc_stream_fr3_real). The TUM
 images are not available: the extraction frames are procedurally rendered 640x480 views
-(tools/synth.frame_stream; the Full config cycles 405 of them forth and back).
+(tools/synth.frame_stream with office-like straight structure in the texture, so the line
+detector has edges to find; the Full config cycles 405 of them forth and back).
 
 Multi-GPU: `--gpus N` without a torchrun environment starts N rank processes itself
 (before anything touches the GPU). eao / full: every rank replays its own copy of the
@@ -232,7 +233,7 @@ def main():
     if args.frames:
         assoc_frames = assoc_frames[:args.frames]
     F = len(assoc_frames)
-    rendered, rposes = synth.frame_stream(min(F, RENDERED), seed=0xEA0 + rank)
+    rendered, rposes = synth.frame_stream(min(F, RENDERED), seed=0xEA0 + rank, structure=True)
     idx = pingpong(F, len(rendered))
     poses = rposes[idx].astype(np.float32)
     # the extraction / matching stream runs on a dedicated HIP stream (a NULL handle would

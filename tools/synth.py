@@ -28,7 +28,11 @@ def _smooth(a, passes=1):
     return a
 
 
-def texture(seed=0xEA0, size=2048):
+def texture(seed=0xEA0, size=2048, structure=False):
+    """structure=True adds office-like straight structure (posters, screens, shelf and desk edges:
+    large flat rectangles and long bars with sharp edges, own seeded stream) so that views carry
+    the long straight edges the line detector finds; the default texture, which
+    the committed fixtures were made from, is unchanged."""
     rng = np.random.Generator(np.random.PCG64(seed))
     img = np.zeros((size, size), np.float64)
     for octave, amp in ((8, 60.0), (32, 40.0), (128, 25.0)):
@@ -50,6 +54,17 @@ def texture(seed=0xEA0, size=2048):
     img = _smooth(img, 1)
     img = img - img.min()
     img = img * (235.0 / max(img.max(), 1e-9)) + 10.0
+    if structure:  # sharp-edged, painted over the smoothed texture: 50-70 EDLine segments per view
+        srng = np.random.Generator(np.random.PCG64(seed + 0x5157))
+        for _ in range(size * size // 8000):
+            x, y = int(srng.integers(0, size)), int(srng.integers(0, size))
+            if srng.random() < 0.3:  # a long thin bar (shelf / desk / frame edge)
+                w, h = (int(srng.integers(120, 500)), int(srng.integers(4, 10)))
+                if srng.random() < 0.5:
+                    w, h = h, w
+            else:  # a flat panel
+                w, h = int(srng.integers(60, 260)), int(srng.integers(60, 260))
+            img[y:y + h, x:x + w] = srng.uniform(0, 255) + 0.15 * img[y:y + h, x:x + w]
     return np.clip(img, 0, 255).astype(np.uint8)
 
 
@@ -110,8 +125,8 @@ def backproject(Tcw, u, v, depth=2.0, K=TUM3_K):
     return (twc[None, :] + lam[:, None] * d).astype(np.float32)
 
 
-def frame_stream(n, w=640, h=480, seed=0xEA0, step=0.004):
-    tex = texture(seed, 2048 if max(w, h) <= 640 else 4096)
+def frame_stream(n, w=640, h=480, seed=0xEA0, step=0.004, structure=False):
+    tex = texture(seed, 2048 if max(w, h) <= 640 else 4096, structure)
     poses = camera_path(n, seed, step)
     frames = np.stack([render(tex, poses[i], w, h) for i in range(n)])
     return frames, poses
