@@ -11,6 +11,8 @@
 //   shuffle SEED N         std::shuffle of 0..N-1 (uint32)
 //   real SEED N LO HI      N draws of uniform_real_distribution<float>(LO, HI)
 //   iforest N TREES SEED SAMPLE   reads N*3 float32 from stdin, writes N float64
+//   sort5 N                reads N*5 float32 rows, std::sort by row[1] descending (the
+//                          Tracking.cc:64-68 VIC comparator), writes the sorted rows
 #include <algorithm>
 #include <array>
 #include <cmath>
@@ -129,6 +131,13 @@ int main(int argc, char** argv) {
       const double s = std::pow(2.0, -(tot / (double)trees) / c);
       std::fwrite(&s, 8, 1, stdout);
     }
+  } else if (!std::strcmp(m, "sort5")) {
+    std::vector<std::array<float, 5>> rows(std::atoi(argv[2]));
+    for (auto& r : rows)
+      if (std::fread(r.data(), 4, 5, stdin) != 5) return 3;
+    std::sort(rows.begin(), rows.end(),
+              [](const std::array<float, 5>& a, const std::array<float, 5>& b) { return a[1] > b[1]; });
+    for (auto& r : rows) std::fwrite(r.data(), 4, 5, stdout);
   } else {
     return 2;
   }
