@@ -124,26 +124,49 @@ def algorithmic_bytes(n_kps):
 
 
 STAGES = ["pyramid", "fast", "distribute", "describe"]  # the level blur is fused into k_describe
-KERNELS = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
+KERNELS = {"pyramid": "k_resize_tile (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
            "describe": "k_describe"}
 
 
 PEAK_VALU_LANE_OPS = 78.6e12  # 256 CUs x 4 SIMD-32 x 2.4 GHz x 32 lanes (MI355X_MICROARCH.md)
 
 
-def pmc_valu(kernel, frames):
-    """VALU lane-ops per launch of `kernel` from the committed SQ counter pass
-    (profiles/r02_pmc_sq.txt: SQ_INSTS_VALU wave instructions x 64 lanes) over the same
-    405-frame launch -- a profiled figure of the same launch shape, not a measurement of
-    this run; None for another shape or when the summary is absent."""
-    p = os.path.join(ROOT, "profiles", "r02_pmc_sq.txt")
-    if frames != 405 or not os.path.exists(p):
+def _pmc_rows(fname):
+    """(kernel base name, counter, corrected value) rows of a committed tools/pmc_summary.py
+    table; template arguments and the "void" return type are dropped from the name."""
+    p = os.path.join(ROOT, "profiles", fname)
+    if not os.path.exists(p):
         return None
+    rows = []
     for l in open(p):
         f = l.split()
-        if f[:2] == ["eao::" + kernel.split()[0], "SQ_INSTS_VALU"]:
-            return float(f[-1]) * 64
+        if f[:1] == ["void"]:
+            f = f[1:]
+        if len(f) >= 5 and f[0].startswith("eao::"):
+            rows.append((f[0].split("<")[0], f[1], float(f[-1])))
+    return rows
+
+
+def _pmc_value(fname, kernel, counter):
+    rows = _pmc_rows(fname)
+    for k, c, v in rows or []:
+        if k == "eao::" + kernel.split()[0] and c == counter:
+            return v
     return None
+
+
+PMC_FILES = {"fetch": "r03_pmc_fetch.txt", "write": "r03_pmc_write.txt", "sq": "r03_pmc_sq.txt"}
+
+
+def pmc_valu(kernel, frames):
+    """VALU lane-ops per launch of `kernel` from the committed SQ counter pass
+    (profiles/r03_pmc_sq.txt: SQ_INSTS_VALU wave instructions x 64 lanes) over the same
+    405-frame launch -- a profiled figure of the same launch shape, not a measurement of
+    this run; None for another shape or when the summary is absent."""
+    if frames != 405:
+        return None
+    v = _pmc_value(PMC_FILES["sq"], kernel, "SQ_INSTS_VALU")
+    return None if v is None else v * 64
 
 
 def pingpong(n, m):
@@ -160,19 +183,11 @@ def pmc_traffic(kernel, frames):
     measurement of this run; None for another shape or when the summaries are absent."""
     if frames != 405:
         return None, None
-    pairs = [("r02_pmc_fetch.txt", "r02_pmc_write.txt"), ("r01_pmc_fetch_final.txt", "r01_pmc_write_final.txt")]
-    names = next((pr for pr in pairs if all(os.path.exists(os.path.join(ROOT, "profiles", f)) for f in pr)), None)
-    if names is None:
+    vals = [_pmc_value(PMC_FILES[k], kernel, c) for k, c in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE"))]
+    if any(v is None for v in vals):
         return None, None
-    tot, src = 0.0, []
-    for f in names:
-        p = os.path.join(ROOT, "profiles", f)
-        hit = [l.split() for l in open(p) if l.split()[:1] == ["eao::" + kernel.split()[0]]]
-        if not hit:
-            return None, None
-        tot += float(hit[0][-1])
-        src.append("profiles/" + f)
-    return tot, "rocprofv3 --pmc (profiled, committed: %s), same launch shape; not measured in this run" % ", ".join(src)
+    src = ", ".join("profiles/" + PMC_FILES[k] for k in ("fetch", "write"))
+    return sum(vals), "rocprofv3 --pmc (profiled, committed: %s), same launch shape; not measured in this run" % src
 
 
 def main():

@@ -56,6 +56,12 @@ class AssocEngine {
                     hipStream_t s, int max_len, int max_sample, int npts_total,
                     double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
                     double* scores2 = nullptr);  // optional second copy of the scores
+  // sharded forests (shard.h, device form): per launched cloud c the outlier bit mask
+  // (score > threshold, bit k of byte k / 8) written at byte meta[3 c + 2] of d_dst from
+  // the device scores at d_scores + meta[3 c] (meta[3 c + 1] points, th[c] the threshold);
+  // meta / th may be pinned host memory read in place
+  int pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores, unsigned char* d_dst,
+                 hipStream_t s);
   // host (pinned) to device copy as a kernel on stream s (16-byte aligned buffers)
   int stage_in(void* d_dst, const void* h_src, size_t bytes, hipStream_t s);
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples

@@ -1273,6 +1273,34 @@ __global__ __launch_bounds__(256) void k_stage(const unsigned char* __restrict__
   for (size_t i = 16 * n16 + t; i < bytes; i += stride) dst[i] = src[i];
 }
 
+// Outlier bit masks of a sharded forest batch (the record the owner all-gathers, replay.cpp
+// exchange_batch): one thread per mask byte, 8 score tests each (score > th: the erase test of
+// Object.cc:1285-1289, with the exact threshold of k_iforest_sum's scores).
+__global__ __launch_bounds__(256) void k_pack_masks(const int* __restrict__ meta, const float* __restrict__ th,
+                                                    const double* __restrict__ scores,
+                                                    unsigned char* __restrict__ dst) {
+  const int c = blockIdx.y;
+  const int off = meta[3 * c], n = meta[3 * c + 1], out = meta[3 * c + 2];
+  const double t = (double)th[c];
+  const int nbytes = (n + 7) >> 3;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nbytes; j += gridDim.x * blockDim.x) {
+    unsigned v = 0;
+    for (int b = 0; b < 8; b++) {
+      const int k = 8 * j + b;
+      if (k < n && scores[off + k] > t) v |= 1u << b;
+    }
+    dst[out + j] = (unsigned char)v;
+  }
+}
+
+int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
+                            unsigned char* d_dst, hipStream_t s) {
+  if (nclouds <= 0) return EAO_OK;
+  hipLaunchKernelGGL(k_pack_masks, dim3(4, nclouds), dim3(256), 0, s, meta, th, d_scores, d_dst);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
 int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t s) {
   if (!bytes) return EAO_OK;
   if (((uintptr_t)dst | (uintptr_t)src) & 15) {

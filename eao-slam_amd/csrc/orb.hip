@@ -2,9 +2,9 @@
 // ORBextractor::operator() (reference src/ORBextractor.cc:1043-1105).
 //
 // Pipeline per batch of frames (all HBM-resident, one stream):
-//   k_resize      x7  level l from level l-1 (cv::resize INTER_LINEAR 8U,
-//                     fixed point, ORBextractor.cc:1120)
-//   k_fast_band   x1  one 4-wave workgroup per (band of cells <= 512 px, frame):
+//   k_resize_tile x7  level l from level l-1 (cv::resize INTER_LINEAR 8U, fixed
+//                     point, ORBextractor.cc:1120), one workgroup per band of 8 rows
+//   k_fast_band   x1  one 4-wave workgroup per (band of cells <= 258 px, frame):
 //                     band ROI staged in LDS, packed-f16 FAST strength swept
 //                     down 62-column strips, in-cell 3x3 NMS by DPP, iniTh with
 //                     minTh retry for empty cells (ORBextractor.cc:789-829)
@@ -39,33 +39,45 @@ __constant__ int c_pattern[1024] = {
 };
 
 // ---------------------------------------------------------------- resize
-// dst(level l) = resize(src(level l-1)); tables precomputed on the host with
-// OpenCV's coefficient rounding. One thread per output pixel.
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, int spitch,
-                                                long long sstride, uint8_t* __restrict__ dst,
-                                                int dpitch, long long dstride, int dw, int dh,
-                                                const int* __restrict__ xofs,
-                                                const short* __restrict__ ialpha, int xmax,
-                                                const int* __restrict__ yrows,
-                                                const short* __restrict__ ibeta) {
-  const int dx = blockIdx.x * blockDim.x + threadIdx.x;
-  const int dy = blockIdx.y;
+// Row-band tiles: one workgroup makes RESIZE_TR whole output rows (a thread per column,
+// stepping by 256 across the row). A thread walks its column down the band and keeps the
+// last two source rows' horizontal sums in registers, so a source row is read once per
+// band instead of once per output row that uses it (rows are shared ~1.67x at scale 1.2),
+// whole rows keep the reads line-aligned, and the rows a band reads stay in one XCD's L2.
+// Same fixed-point arithmetic as OpenCV's INTER_LINEAR 8U resize (tables on the host).
+constexpr int RESIZE_TR = 8;
+__global__ __launch_bounds__(256) void k_resize_tile(const uint8_t* __restrict__ src, int spitch,
+                                                     long long sstride, uint8_t* __restrict__ dst,
+                                                     int dpitch, long long dstride, int dw, int dh,
+                                                     const int* __restrict__ xofs,
+                                                     const short* __restrict__ ialpha, int xmax,
+                                                     const int* __restrict__ yrows,
+                                                     const short* __restrict__ ibeta) {
+  const int dy0 = blockIdx.y * RESIZE_TR;
   const int f = blockIdx.z;
-  if (dx >= dw) return;
-  const uint8_t* s0 = src + f * sstride + (long long)yrows[2 * dy] * spitch;
-  const uint8_t* s1 = src + f * sstride + (long long)yrows[2 * dy + 1] * spitch;
-  const int sx = xofs[dx];
-  int d0, d1;
-  if (dx < xmax) {
-    const int a0 = ialpha[2 * dx], a1 = ialpha[2 * dx + 1];
-    d0 = s0[sx] * a0 + s0[sx + 1] * a1;
-    d1 = s1[sx] * a0 + s1[sx + 1] * a1;
-  } else {
-    d0 = s0[sx] * 2048;
-    d1 = s1[sx] * 2048;
+  const uint8_t* sf = src + f * sstride;
+  uint8_t* df = dst + f * dstride;
+  const int dy1 = min(dy0 + RESIZE_TR, dh);
+  for (int dx = threadIdx.x; dx < dw; dx += blockDim.x) {
+    const int sx = xofs[dx];
+    const bool two = dx < xmax;
+    const int a0 = two ? ialpha[2 * dx] : 2048, a1 = two ? ialpha[2 * dx + 1] : 0;
+    auto hsum = [&](int r) {
+      const uint8_t* q = sf + (long long)r * spitch + sx;
+      return two ? q[0] * a0 + q[1] * a1 : q[0] * 2048;
+    };
+    int ra = -1, rb = -1, ha = 0, hb = 0;  // the last two source rows and their horizontal sums
+    for (int dy = dy0; dy < dy1; dy++) {
+      const int r0 = yrows[2 * dy], r1 = yrows[2 * dy + 1];
+      int d0, d1;
+      if (r0 == rb) d0 = hb; else if (r0 == ra) d0 = ha; else d0 = hsum(r0);
+      if (r1 == rb) d1 = hb; else if (r1 == ra) d1 = ha; else d1 = hsum(r1);
+      ra = r0; ha = d0;
+      rb = r1; hb = d1;
+      const int v = (d0 * ibeta[2 * dy] + d1 * ibeta[2 * dy + 1] + (1 << 21)) >> 22;
+      df[(long long)dy * dpitch + dx] = (uint8_t)min(max(v, 0), 255);
+    }
   }
-  int v = (d0 * ibeta[2 * dy] + d1 * ibeta[2 * dy + 1] + (1 << 21)) >> 22;
-  dst[f * dstride + (long long)dy * dpitch + dx] = (uint8_t)min(max(v, 0), 255);
 }
 
 // ---------------------------------------------------------------- FAST
@@ -124,8 +136,13 @@ __device__ __forceinline__ uint32_t fast_strength_pair(const uint8_t* p) {
   return (uint32_t)s0 | ((uint32_t)s1 << 16);
 }
 
-// ROI row stride of k_fast_band (bands are <= 512 px wide, + 16-byte alignment slack)
+// ROI row strides of k_fast_band: a band is at most RS - 30 px wide (16-byte alignment
+// slack of the staging loads). Rows of cells are split into bands of balanced width
+// <= FAST_BAND_W, so the narrow stride serves 640x480 and 1920x1080 alike; its smaller
+// LDS block (RS * (2 bh - 6) bytes) lifts the resident waves per CU.
+constexpr int FAST_RS_NARROW = 288;
 constexpr int FAST_RS = 544;
+constexpr int FAST_BAND_W = FAST_RS_NARROW - 30;
 
 // lane l <- lane l-1 (right = false) or l+1 (right = true) across the whole
 // wave (GFX9 DPP wave_shr:1 / wave_shl:1); the missing end lane reads 0
@@ -147,14 +164,14 @@ __device__ __forceinline__ int wave_from_right(int v) { return __builtin_amdgcn_
 //      (S if kept at minTh, else 0) encodes both passes;
 //   3. one wave per cell emits the kept pixels row-major (ballot + popcount),
 //      the iniTh set, or the minTh set when the cell has no iniTh corner.
-__global__ __launch_bounds__(256) void k_fast_band(const uint8_t* __restrict__ frames, int fpitch,
+template <int RS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_fast_band(const uint8_t* __restrict__ frames, int fpitch,
                                                    long long fstride, const uint8_t* __restrict__ pyr,
                                                    long long pstride, const LevelDev* __restrict__ levels,
                                                    const BandDev* __restrict__ bands,
                                                    const CellDev* __restrict__ cells, int iniTh, int minTh,
                                                    uint32_t* __restrict__ cand, long long cand_stride,
                                                    int* __restrict__ cell_cnt, int ncells, int vec_ok) {
-  constexpr int RS = FAST_RS;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ int16_t bnd[64];  // cell detection-window starts (band coords), then the end
   const BandDev B = bands[blockIdx.x];
@@ -1125,11 +1142,17 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
     bands.clear();
     band_w = band_h = 0;
     for (size_t c = 0; c < cells.size();) {
-      size_t e = c;
-      // split long rows: the band ROI stays <= 512 px wide (LDS budget, u16 queue)
-      while (e < cells.size() && cells[e].level == cells[c].level && cells[e].i == cells[c].i &&
-             (e == c || cells[e].x1 - cells[c].x0 <= 512))
-        e++;
+      // the row of cells starting at c, split into the fewest bands of <= FAST_BAND_W px,
+      // with the cells shared out evenly (balanced blocks, narrow LDS rows)
+      size_t row_end = c;
+      while (row_end < cells.size() && cells[row_end].level == cells[c].level && cells[row_end].i == cells[c].i)
+        row_end++;
+      const int row_w = cells[row_end - 1].x1 - cells[c].x0;
+      const size_t nrow = row_end - c;
+      const size_t nb = std::min(nrow, (size_t)((row_w + FAST_BAND_W - 1) / FAST_BAND_W));
+      size_t e = c + (nrow + nb - 1) / nb;
+      // a band of that many cells may still exceed the limit when cell widths differ
+      while (e > c + 1 && cells[e - 1].x1 - cells[c].x0 > FAST_BAND_W) e--;
       BandDev b{};
       b.level = cells[c].level;
       b.ncells = (int16_t)(e - c);
@@ -1218,8 +1241,8 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
     const uint8_t* src = l == 1 ? d_frames : d_pyr + S.plane_off;
     const int spitch = l == 1 ? pitch : S.pitch;
     const long long sstride = l == 1 ? fstride : pyr_bytes;
-    dim3 g((L.w + 255) / 256, L.h, nframes);
-    hipLaunchKernelGGL(k_resize, g, dim3(256), 0, s, src, spitch, sstride, d_pyr + L.plane_off,
+    dim3 g(1, (L.h + RESIZE_TR - 1) / RESIZE_TR, nframes);
+    hipLaunchKernelGGL(k_resize_tile, g, dim3(256), 0, s, src, spitch, sstride, d_pyr + L.plane_off,
                        L.pitch, pyr_bytes, L.w, L.h, d_xofs + L.tab_x, d_ia + 2 * L.tab_x, L.xmax,
                        d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
   }
@@ -1238,10 +1261,12 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
       set_error("orb: FAST cell rows exceed one wave");
       return EAO_E_CAPACITY;
     }
-    size_t lds = (size_t)FAST_RS * (2 * band_h - 6);  // roi, kept strengths of the detection rows
-    hipLaunchKernelGGL(k_fast_band, g, dim3(256), lds, s, d_frames, pitch, fstride, d_pyr, pyr_bytes,
-                       d_levels, d_bands, d_cells, p.ini_th_fast, p.min_th_fast, d_cand, cand_stride,
-                       d_cell_cnt, (int)cells.size(), vec_ok);
+    const bool narrow = band_w + 30 <= FAST_RS_NARROW;
+    const int rs = narrow ? FAST_RS_NARROW : FAST_RS;
+    size_t lds = (size_t)rs * (2 * band_h - 6);  // roi, kept strengths of the detection rows
+    hipLaunchKernelGGL(narrow ? k_fast_band<FAST_RS_NARROW> : k_fast_band<FAST_RS>, g, dim3(256), lds, s,
+                       d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels, d_bands, d_cells, p.ini_th_fast,
+                       p.min_th_fast, d_cand, cand_stride, d_cell_cnt, (int)cells.size(), vec_ok);
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[2], s));
   // quadtree distribution

@@ -444,6 +444,13 @@ class ReplayEngine {
     unsigned char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
     double* contrib = nullptr;  // [50][max_points]
+    // sharded: the per-rank record layout fixed at the launch (mask bytes, speculative
+    // pairs, padded record size) and, in the device form, this rank's record in device
+    // memory, written by the forest batch's own kernels (pack_masks, np_batch)
+    std::vector<size_t> xmb, xnsr;
+    size_t xbytes = 0;
+    unsigned char* d_x = nullptr;
+    size_t cap_x = 0;
   };
   std::vector<IfBatch> ifb;
   hipStream_t if_stream[kIfStreams] = {};
@@ -458,6 +465,11 @@ class ReplayEngine {
   std::vector<unsigned char> xsend, xrecv;
   int owner(const Obj* o) const { return o->id % sworld; }
   bool mine(const Obj* o) const { return sworld == 1 || owner(o) == srank; }
+  // sharded replay: records are exchanged (also at world 1 when an RCCL communicator is
+  // set, which runs the exchange path end to end on one device)
+  bool sharded() const { return (bool)ex; }
+  // device form of the exchange (RCCL): records written and gathered in device memory
+  bool xdev() const { return ex && ex->device_form(); }
   // all-gather xsend (padded to `bytes`) into xrecv [sworld][bytes]
   int exchange(size_t bytes) {
     const double t0 = now_us();
@@ -470,10 +482,21 @@ class ReplayEngine {
     xstat[2] += now_us() - t0;
     return rc;
   }
+  // device form: this rank's `bytes` at d_send (ready behind `ev`) gathered on the GPU;
+  // *recv = the [sworld][bytes] records in pinned host memory
+  int exchange_device(const void* d_send, hipEvent_t ev, size_t bytes, const unsigned char** recv) {
+    const double t0 = now_us();
+    int rc = ex->allgather_device(d_send, ev, bytes, recv);
+    xstat[0] += 1;
+    xstat[1] += (double)bytes;
+    xstat[2] += now_us() - t0;
+    return rc;
+  }
 
   // forest slots, streams and staging outlive the replay: the next replay on
   // the same engine adopts them (allocation is not per replay)
   hipEvent_t gpu0_ev = nullptr;  // frame-start launch completion (spin-waited)
+  bool rn_dev = false;           // rects_np_launch writes its outputs to d_out (device-form exchange)
   struct Pool {
     std::vector<IfBatch> ifb;
     hipStream_t if_stream[kIfStreams] = {};
@@ -538,6 +561,7 @@ class ReplayEngine {
       if (sl.h_out) (void)hipHostFree(sl.h_out);
       if (sl.d_in) (void)hipFree(sl.d_in);
       if (sl.d_out) (void)hipFree(sl.d_out);
+      if (sl.d_x) (void)hipFree(sl.d_x);
       if (sl.contrib) (void)hipFree(sl.contrib);
     }
     for (hipStream_t st : if_stream)
@@ -1027,8 +1051,31 @@ class ReplayEngine {
       const int nl = (int)b.lc.size(), ns = (int)lsp.size();
       for (int c = 0; c < nb; c++) b.objs[c]->slot = k;
       b.left = nb;
-      b.xdone = sworld == 1;
+      b.xdone = !sharded();
       b.launched = nl > 0;
+      if (sharded()) {
+        // the record every rank all-gathers for this batch: per owned object an outlier
+        // bit mask, then the owned speculative NP stats; one padded size for all ranks
+        b.xmb.assign(sworld, 0);
+        b.xnsr.assign(sworld, 0);
+        for (int c = 0; c < nb; c++) b.xmb[owner(b.objs[c])] += (b.objs[c]->pts.size() + 7) / 8;
+        for (size_t q = 0; q < b.sp_obj.size(); q++) b.xnsr[owner(b.objs[b.sp_obj[q]])]++;
+        b.xbytes = 0;
+        for (int r = 0; r < sworld; r++) b.xbytes = std::max(b.xbytes, b.xmb[r] + sizeof(eao_np_stats) * b.xnsr[r]);
+        b.xbytes = std::max<size_t>(al16(b.xbytes), 16);
+        if (xdev() && b.xbytes > b.cap_x) {
+          if (b.d_x) (void)hipFree(b.d_x);
+          b.d_x = nullptr;
+          b.cap_x = std::max(b.xbytes, 2 * b.cap_x);
+          EAO_HIP_CHECK(hipMalloc((void**)&b.d_x, b.cap_x));
+        }
+        if (xdev() && !b.launched) {  // nothing owned: an empty record, ready behind b.ev
+          hipStream_t st = if_stream[k % kIfStreams];
+          if (!b.ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
+          EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st));
+          EAO_HIP_CHECK(hipEventRecord(b.ev, st));
+        }
+      }
       if (!b.launched) continue;
       // in: forest meta [3 nl] | object points [3 np] | object valid [np] | NP meta [4 ns] | th [ns] |
       //     score pointers [ns] | frame points [3 nfp] | frame valid [nfp]
@@ -1041,7 +1088,11 @@ class ReplayEngine {
       const size_t o_osp = al16(o_th + sizeof(float) * ns);
       const size_t o_fp = al16(o_osp + sizeof(double*) * ns);
       const size_t o_fval = o_fp + sizeof(float) * 3 * (size_t)nfp;
-      const size_t in_bytes = ns ? o_fval + nfp : o_pts + sizeof(float) * 3 * (size_t)np;
+      // device-form exchange: the mask packing's meta [3 nl] | thresholds [nl] after the rest
+      const size_t o_pk = al16(ns ? o_fval + nfp : o_pts + sizeof(float) * 3 * (size_t)np);
+      const size_t o_pkth = o_pk + sizeof(int) * 3 * nl;
+      const size_t in_bytes = xdev() ? o_pkth + sizeof(float) * nl
+                                     : ns ? o_fval + nfp : o_pts + sizeof(float) * 3 * (size_t)np;
       b.sp_out = al16(sizeof(double) * np);
       const size_t out_bytes = b.sp_out + sizeof(eao_np_stats) * ns;
       if (in_bytes > b.cap_in) {
@@ -1096,6 +1147,19 @@ class ReplayEngine {
           osp[j] = (const double*)b.d_out + b.loff[c];  // device scores of this forest
         }
       }
+      if (xdev()) {
+        int* pk = (int*)(b.h_in + o_pk);
+        float* pth = (float*)(b.h_in + o_pkth);
+        size_t w = 0;
+        for (int j = 0; j < nl; j++) {
+          Obj* o = b.objs[b.lc[j]];
+          pk[3 * j] = b.loff[b.lc[j]];
+          pk[3 * j + 1] = (int)o->pts.size();
+          pk[3 * j + 2] = (int)w;
+          pth[j] = o->cls == 62 ? 0.65f : 0.6f;
+          w += (o->pts.size() + 7) / 8;
+        }
+      }
       hipStream_t st = if_stream[k % kIfStreams];
       prof[2] += 1;
       Tick tl(&prof[19]);
@@ -1112,11 +1176,18 @@ class ReplayEngine {
       if (ns) {
         const int* spm = (const int*)(b.d_in + o_spm);
         const float* dfp = (const float*)(b.d_in + o_fp);
+        // device-form exchange: the stats go straight into this rank's record
+        eao_np_stats* sp_dst = xdev() ? (eao_np_stats*)(b.d_x + b.xmb[srank]) : (eao_np_stats*)(b.h_out + b.sp_out);
         rc = A->np_batch(ns, dfp, b.d_in + o_fval, spm, spm + ns, (const float*)(b.d_in + o_pts), b.d_in + o_oval,
-                         spm + 2 * ns, spm + 3 * ns, (eao_np_stats*)(b.h_out + b.sp_out), st, max_olen,
-                         (const double* const*)(b.d_in + o_osp), (const float*)(b.d_in + o_th));
+                         spm + 2 * ns, spm + 3 * ns, sp_dst, st, max_olen, (const double* const*)(b.d_in + o_osp),
+                         (const float*)(b.d_in + o_th));
         if (rc) return rc;
         prof[9] += ns;
+      }
+      if (xdev()) {
+        const int* dpk = (const int*)(b.d_in + o_pk);
+        rc = A->pack_masks(nl, dpk, (const float*)(b.d_in + o_pkth), (const double*)b.d_out, b.d_x, st);
+        if (rc) return rc;
       }
       EAO_HIP_CHECK(hipEventRecord(b.ev, st));
     }
@@ -1126,34 +1197,37 @@ class ReplayEngine {
   // completion (no object of the batch has changed since the launch): per
   // owned object an outlier bit mask, then the owned speculative NP stats
   int exchange_batch(IfBatch& b) {
-    if (b.launched) EAO_HIP_CHECK(spin_event(b.ev));
     const int nb = (int)b.objs.size();
     const size_t sb = sizeof(eao_np_stats);
-    std::vector<size_t> mb(sworld, 0), nsr(sworld, 0);
-    for (int c = 0; c < nb; c++) mb[owner(b.objs[c])] += (b.objs[c]->pts.size() + 7) / 8;
-    for (size_t q = 0; q < b.sp_obj.size(); q++) nsr[owner(b.objs[b.sp_obj[q]])]++;
-    size_t bytes = 0;
-    for (int r = 0; r < sworld; r++) bytes = std::max(bytes, mb[r] + sb * nsr[r]);
-    xsend.assign(bytes, 0);
-    size_t w = 0;
-    for (int c : b.lc) {
-      const Obj* o = b.objs[c];
-      const float th = o->cls == 62 ? 0.65f : 0.6f;
-      const double* sc = (const double*)b.h_out + b.loff[c];
-      const size_t n = o->pts.size();
-      for (size_t k = 0; k < n; k++)
-        if (sc[k] > th) xsend[w + k / 8] |= (unsigned char)(1u << (k % 8));
-      w += (n + 7) / 8;
-    }
-    size_t j = 0;
-    for (size_t q = 0; q < b.sp_obj.size(); q++)
-      if (mine(b.objs[b.sp_obj[q]])) {  // launch order = sp_* order restricted to this rank
-        std::memcpy(xsend.data() + w + sb * j, b.h_out + b.sp_out + sb * j, sb);
-        j++;
+    const size_t bytes = b.xbytes;
+    const unsigned char* recv = nullptr;
+    if (xdev()) {
+      // the owner's kernels wrote the record into b.d_x; gathered on the GPU behind b.ev
+      if (int rc = exchange_device(b.d_x, b.ev, bytes, &recv)) return rc;
+    } else {
+      if (b.launched) EAO_HIP_CHECK(spin_event(b.ev));
+      xsend.assign(bytes, 0);
+      size_t w = 0;
+      for (int c : b.lc) {
+        const Obj* o = b.objs[c];
+        const float th = o->cls == 62 ? 0.65f : 0.6f;
+        const double* sc = (const double*)b.h_out + b.loff[c];
+        const size_t n = o->pts.size();
+        for (size_t k = 0; k < n; k++)
+          if (sc[k] > th) xsend[w + k / 8] |= (unsigned char)(1u << (k % 8));
+        w += (n + 7) / 8;
       }
-    if (int rc = exchange(bytes)) return rc;
-    const size_t stride = xrecv.size() / sworld;
-    b.xres = xrecv;
+      size_t j = 0;
+      for (size_t q = 0; q < b.sp_obj.size(); q++)
+        if (mine(b.objs[b.sp_obj[q]])) {  // launch order = sp_* order restricted to this rank
+          std::memcpy(xsend.data() + w + sb * j, b.h_out + b.sp_out + sb * j, sb);
+          j++;
+        }
+      if (int rc = exchange(bytes)) return rc;
+      recv = xrecv.data();
+    }
+    const size_t stride = bytes;
+    b.xres.assign(recv, recv + bytes * sworld);
     b.mask_off.assign(nb, 0);
     b.spst.resize(b.sp_obj.size());
     std::vector<size_t> cm(sworld, 0), cs(sworld, 0);
@@ -1164,7 +1238,7 @@ class ReplayEngine {
     }
     for (size_t q = 0; q < b.sp_obj.size(); q++) {
       const int r = owner(b.objs[b.sp_obj[q]]);
-      std::memcpy(&b.spst[q], b.xres.data() + stride * r + mb[r] + sb * cs[r]++, sb);
+      std::memcpy(&b.spst[q], b.xres.data() + stride * r + b.xmb[r] + sb * cs[r]++, sb);
     }
     b.xdone = true;
     return EAO_OK;
@@ -1192,7 +1266,7 @@ class ReplayEngine {
     while (b.objs[c] != o) c++;
     const size_t n = o->pts.size();
     size_t w = 0;
-    if (sworld > 1) {
+    if (sharded()) {
       const unsigned char* m = b.xres.data() + b.mask_off[c];
       for (size_t k = 0; k < n; k++) {
         if (m[k / 8] >> (k % 8) & 1) {
@@ -1219,7 +1293,7 @@ class ReplayEngine {
       o->yaw_due = false;
       sample_yaw(o, o->yawT);
     }
-    const eao_np_stats* sps = sworld > 1 ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
+    const eao_np_stats* sps = sharded() ? b.spst.data() : (const eao_np_stats*)(b.h_out + b.sp_out);
     if (!o->dfr.empty()) {  // effects of later same-frame detections, in their order
       for (const Obj::Dfr& d : o->dfr) {
         if (d.kind == Obj::DFR_PROJ_IF_NP || d.kind == Obj::DFR_VOTE_IF_NP) {
@@ -1374,7 +1448,7 @@ class ReplayEngine {
     std::vector<int> wait_slots;
     bool chained = false;
     auto inflight = [&](Obj* o, const double*& ptr, float& th) {
-      if (sworld != 1 || !o->pending || o->slot < 0) return;
+      if (sharded() || !o->pending || o->slot < 0) return;
       IfBatch& b = ifb[o->slot];
       if (!b.launched) return;
       int c = 0;
@@ -1396,6 +1470,9 @@ class ReplayEngine {
     const size_t o_r = sizeof(eao_np_stats) * (size_t)npairs, o_ok = o_r + sizeof(int) * 4 * (size_t)nb;
     int rc = stage(in_bytes, o_ok + nb);
     if (rc) return rc;
+    // outputs: pinned host memory (read after the spin), or -- sharded, device-form
+    // exchange -- this rank's record in device memory (d_out), all-gathered by the caller
+    unsigned char* ob = rn_dev ? d_out : h_out;
     int* rmeta = (int*)h_in;
     int* pmeta = (int*)(h_in + o_pm);
     float* pts = (float*)(h_in + o_pts);
@@ -1448,12 +1525,13 @@ class ReplayEngine {
     const uint8_t* dval = din + o_val;
     const double* const* dosp = chained ? (const double* const*)(din + o_osp) : nullptr;
     const float* doth = chained ? (const float*)(din + o_oth) : nullptr;
-    rc = A->rects_np(camdev, (const float*)(din + o_T), nb, dpts, drm, drm + nb, (int*)(h_out + o_r), h_out + o_ok,
+    rc = A->rects_np(camdev, (const float*)(din + o_T), nb, dpts, drm, drm + nb, (int*)(ob + o_r), ob + o_ok,
                      dosp, doth, npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
-                     (eao_np_stats*)h_out, A->stream, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
+                     (eao_np_stats*)ob, A->stream, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
+    if (rn_dev) return EAO_OK;
     {
       Tick tw(&prof[41]);
       idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
@@ -1473,7 +1551,7 @@ class ReplayEngine {
   // owns, then the records are all-gathered and re-assembled in list order
   int rects_np(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
                std::vector<int>& rects, std::vector<eao_np_stats>& stats) {
-    if (sworld == 1) return rects_np_launch(list, pairs, rects, stats);
+    if (!sharded()) return rects_np_launch(list, pairs, rects, stats);
     for (auto& pr : pairs)  // capacity checked on every rank before the owner split (same verdict)
       if (pr.second->pts.size() > (size_t)NP_MAXN) {
         set_error("replay: object exceeds the NP kernel capacity");
@@ -1492,9 +1570,48 @@ class ReplayEngine {
     }
     std::vector<int> R;
     std::vector<eao_np_stats> S;
+    const size_t sb = sizeof(eao_np_stats);
+    if (xdev()) {
+      // device form: the launch writes this rank's record [stats][rects x4][ok] into device
+      // memory (rects_np_launch's own output layout); it is gathered there and only the
+      // gathered records come back
+      size_t bytes = 0;
+      for (int q = 0; q < sworld; q++) bytes = std::max(bytes, sb * npr[q] + (sizeof(int) * 4 + 1) * nl[q]);
+      bytes = std::max<size_t>(al16(bytes), 16);
+      if (int rc = stage(0, bytes)) return rc;
+      int rc;
+      if (L.empty() && P.empty()) {  // nothing owned: an empty record
+        if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
+        EAO_HIP_CHECK(hipMemsetAsync(d_out, 0, bytes, A->stream));
+        EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
+      } else {
+        rn_dev = true;
+        rc = rects_np_launch(L, P, R, S);
+        rn_dev = false;
+        if (rc) return rc;
+      }
+      idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
+      const unsigned char* recv = nullptr;
+      if ((rc = exchange_device(d_out, gpu0_ev, bytes, &recv))) return rc;
+      std::vector<int> il(sworld, 0), ip(sworld, 0);
+      rects.assign(5 * list.size(), 0);
+      stats.resize(pairs.size());
+      for (size_t b = 0; b < list.size(); b++) {
+        const int q = owner(list[b]);
+        const unsigned char* rec = recv + bytes * q;
+        const int i = il[q]++;
+        std::memcpy(&rects[5 * b], rec + sb * npr[q] + sizeof(int) * 4 * i, sizeof(int) * 4);
+        rects[5 * b + 4] = rec[sb * npr[q] + sizeof(int) * 4 * nl[q] + i];
+      }
+      for (size_t k = 0; k < pairs.size(); k++) {
+        const int q = owner(pairs[k].second);
+        std::memcpy(&stats[k], recv + bytes * q + sb * ip[q]++, sb);
+      }
+      return EAO_OK;
+    }
     int rc = rects_np_launch(L, P, R, S);
     if (rc) return rc;
-    const size_t rb = sizeof(int) * 5, sb = sizeof(eao_np_stats);
+    const size_t rb = sizeof(int) * 5;
     size_t bytes = 0;
     for (int q = 0; q < sworld; q++) bytes = std::max(bytes, rb * nl[q] + sb * npr[q]);
     xsend.assign(bytes, 0);
@@ -1533,7 +1650,7 @@ class ReplayEngine {
     // one rank: the launch is queued behind those forests on the GPU (erasure applied on
     // the fly, rects_np_launch) and the host completes them afterwards, so the host never
     // waits twice; sharded, the forests complete first (their outcome is all-gathered)
-    if (sworld > 1)
+    if (sharded())
       if (int rc = complete_pending()) return rc;
     std::vector<int> rects;
     std::vector<eao_np_stats> st;
@@ -1544,7 +1661,7 @@ class ReplayEngine {
     }
     // completion before the results are applied: a deferred projected-rect recompute of
     // the previous frame must not overwrite this frame's step 10.1 rect
-    if (sworld == 1)
+    if (!sharded())
       if (int rc = complete_pending()) return rc;
     for (size_t b = 0; b < list.size(); b++)
       if (rects[5 * b + 4]) list[b]->proj = IRect(rects[5 * b], rects[5 * b + 1], rects[5 * b + 2], rects[5 * b + 3]);

@@ -6,14 +6,30 @@
 // result records are all-gathered so that every rank applies the same
 // outcome. The exchanger is the one collective of that data path.
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstddef>
 
 namespace eao {
 
 struct Exchanger {
   virtual ~Exchanger() {}
-  // all-gather of host buffers: recv[r * bytes, (r + 1) * bytes) = rank r's send
+  // host form (the gloo callback of eao_replay_shard_callback): all-gather of host
+  // buffers, recv[r * bytes, (r + 1) * bytes) = rank r's send
   virtual int allgather(const void* send, void* recv, size_t bytes) = 0;
+  // device form (RCCL): the records are gathered from device memory into device memory.
+  // d_send holds this rank's `bytes` once `ready` has completed (the kernels that wrote
+  // it were recorded on it); the collective waits for that event on the GPU, and the
+  // [world][bytes] result is copied to the host once: *h_recv points at it (pinned,
+  // valid until the next exchange).
+  virtual bool device_form() const { return false; }
+  virtual int allgather_device(const void* d_send, hipEvent_t ready, size_t bytes, const unsigned char** h_recv) {
+    (void)d_send;
+    (void)ready;
+    (void)bytes;
+    (void)h_recv;
+    return -1;
+  }
 };
 
 // RCCL over xGMI (shard_rccl.cpp): a communicator of `world` ranks on device `dev`

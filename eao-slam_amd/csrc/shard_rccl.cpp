@@ -1,10 +1,12 @@
 // shard_rccl.cpp -- RCCL exchanger of the sharded association.
 //
-// One communicator per replay; each exchange is a single ncclAllGather of
-// the ranks' fixed-size result records over xGMI. The records are a few KB
-// (64-byte NP statistics, 20-byte projected rects, per-point outlier bit
-// masks), so the exchange is latency bound; it runs on its own non-blocking
-// stream through pinned host staging.
+// One communicator per replay; each exchange is a single ncclAllGather of the
+// ranks' fixed-size result records over xGMI. The records (64-byte NP
+// statistics, 17-byte projected rects, per-point outlier bit masks) are written
+// by the engine's kernels straight into device memory; the collective reads
+// them there after a GPU-side wait on the producing stream's event, gathers into
+// device memory, and only the gathered records the host's decisions need come
+// back, in one copy. The exchange is latency bound (a few KB).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -32,16 +34,14 @@ struct RcclExchanger : Exchanger {
   int dev = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
-  unsigned char *h_send = nullptr, *h_recv = nullptr, *d_send = nullptr, *d_recv = nullptr;
+  unsigned char *h_recv = nullptr, *d_recv = nullptr;
   size_t cap = 0;  // bytes per rank
 
   ~RcclExchanger() override {
     if (stream) (void)hipStreamSynchronize(stream);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
-    if (h_send) (void)hipHostFree(h_send);
     if (h_recv) (void)hipHostFree(h_recv);
-    if (d_send) (void)hipFree(d_send);
     if (d_recv) (void)hipFree(d_recv);
   }
   int init(int d, int rank, int w, const void* uid) {
@@ -60,28 +60,28 @@ struct RcclExchanger : Exchanger {
     // every pointer is released and cleared before reallocating, so a failed
     // allocation below never leaves the destructor a stale pointer to free again
     if (stream) EAO_HIP_CHECK(hipStreamSynchronize(stream));
-    if (h_send) (void)hipHostFree(h_send);
     if (h_recv) (void)hipHostFree(h_recv);
-    if (d_send) (void)hipFree(d_send);
     if (d_recv) (void)hipFree(d_recv);
-    h_send = h_recv = d_send = d_recv = nullptr;
+    h_recv = d_recv = nullptr;
     cap = 0;
-    EAO_HIP_CHECK(hipHostMalloc((void**)&h_send, c, 0));
     EAO_HIP_CHECK(hipHostMalloc((void**)&h_recv, c * world, 0));
-    EAO_HIP_CHECK(hipMalloc((void**)&d_send, c));
     EAO_HIP_CHECK(hipMalloc((void**)&d_recv, c * world));
     cap = c;
     return EAO_OK;
   }
-  int allgather(const void* send, void* recv, size_t bytes) override {
-    if (bytes == 0) return EAO_OK;
+  int allgather(const void*, void*, size_t) override {
+    set_error("rccl exchanger: records are exchanged from device memory (allgather_device)");
+    return EAO_E_ARG;
+  }
+  bool device_form() const override { return true; }
+  int allgather_device(const void* d_send, hipEvent_t ready, size_t bytes, const unsigned char** out) override {
+    if (bytes == 0) return EAO_E_ARG;
     if (int rc = grow(bytes)) return rc;
-    std::memcpy(h_send, send, bytes);
-    EAO_HIP_CHECK(hipMemcpyAsync(d_send, h_send, bytes, hipMemcpyHostToDevice, stream));
+    if (ready) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready, 0));
     EAO_NCCL_CHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
     EAO_HIP_CHECK(hipMemcpyAsync(h_recv, d_recv, bytes * world, hipMemcpyDeviceToHost, stream));
     EAO_HIP_CHECK(hipStreamSynchronize(stream));
-    std::memcpy(recv, h_recv, bytes * world);
+    *out = h_recv;
     return EAO_OK;
   }
 };
@@ -100,9 +100,17 @@ Exchanger* make_rccl_exchanger(int dev, int rank, int world, const void* unique_
 
 }  // namespace eao
 
-// one-rank RCCL exchange self-test: a world-1 communicator from a fresh unique id,
-// one all-gather of a byte pattern through the replay's exchanger (pinned staging,
-// H2D, ncclAllGather, D2H, stream sync), result compared with the pattern
+namespace {
+__global__ void k_selftest_pattern(unsigned char* d, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = (unsigned char)(i * 131 + 7);
+}
+}  // namespace
+
+// one-rank RCCL exchange self-test: a world-1 communicator from a fresh unique id, one
+// all-gather of a byte pattern through the replay's exchanger in its device form (the
+// pattern in device memory, ready behind an event; ncclAllGather device to device; one
+// copy back), result compared with the pattern
 extern "C" int eao_rccl_selftest(int device, int bytes) {
   if (bytes <= 0) return EAO_E_ARG;
   if (!eao_device_ok(device)) {
@@ -114,20 +122,39 @@ extern "C" int eao_rccl_selftest(int device, int bytes) {
   int rc = 0;
   eao::Exchanger* x = eao::make_rccl_exchanger(device, 0, 1, uid, &rc);
   if (!x) return rc;
-  // the requested size, then one past the initial 4 KB staging (grow() reallocates)
+  unsigned char* d_send = nullptr;
+  hipEvent_t ev = nullptr;
+  // the requested size, then one past the initial 4 KB (grow() reallocates)
   for (size_t n : {(size_t)bytes, (size_t)bytes + 4097}) {
-    std::string send(n, '\0'), recv(n, '\1');
+    std::string send(n, '\0');
     for (size_t i = 0; i < n; i++) send[i] = (char)(i * 131 + 7);
-    rc = x->allgather(send.data(), &recv[0], n);
-    if (!rc && recv != send) {
+    if (d_send) (void)hipFree(d_send);
+    d_send = nullptr;
+    if (hipMalloc((void**)&d_send, n) != hipSuccess ||
+        (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess)) {
+      eao::set_error("eao_rccl_selftest: test buffer setup failed");
+      rc = EAO_E_HIP;
+      break;
+    }
+    // the pattern is written on the device (as the engine's kernels write their records)
+    hipLaunchKernelGGL(k_selftest_pattern, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d_send, n);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(ev, 0) != hipSuccess) {
+      eao::set_error("eao_rccl_selftest: pattern kernel failed");
+      rc = EAO_E_HIP;
+      break;
+    }
+    const unsigned char* recv = nullptr;
+    rc = x->allgather_device(d_send, ev, n, &recv);
+    if (!rc && std::memcmp(recv, send.data(), n) != 0) {
       eao::set_error("eao_rccl_selftest: gathered bytes differ");
       rc = EAO_E_HIP;
     }
     if (rc) break;
   }
+  if (d_send) (void)hipFree(d_send);
+  if (ev) (void)hipEventDestroy(ev);
   delete x;
-  if (rc) return rc;
-  return EAO_OK;
+  return rc;
 }
 
 extern "C" int eao_rccl_unique_id(uint8_t* out) {

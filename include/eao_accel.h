@@ -371,12 +371,18 @@ int eao_replay_object_points(eao_replay* r, int i, int32_t* ids, int cap);
    rank o.id % world and the result records are all-gathered. Call before the
    first frame.
    eao_replay_shard_rccl: RCCL communicator (one device per rank, xGMI);
-     unique_id = 128 bytes from eao_rccl_unique_id on one rank, broadcast.
-   eao_replay_shard_callback: the all-gather is the caller's (e.g. gloo). */
+     unique_id = 128 bytes from eao_rccl_unique_id on one rank, broadcast. The
+     records stay in device memory: the kernels write them, ncclAllGather reads
+     them there behind a GPU-side event wait, and only the gathered records come
+     back (one copy per exchange). World 1 is allowed and runs the whole exchange
+     path on one device.
+   eao_replay_shard_callback: the all-gather is the caller's (e.g. gloo), on host
+     buffers; world 1 disables sharding. */
 typedef int (*eao_allgather_fn)(void* ctx, const void* send, void* recv, size_t bytes_per_rank);
 int eao_rccl_unique_id(uint8_t* out128);
 /* One-rank self-test of the RCCL exchanger of eao_replay_shard_rccl: a world-1 communicator,
-   all-gathers of `bytes` and bytes + 4097 (staging regrowth), results compared. 0 = ok. */
+   device-to-device all-gathers of a kernel-written pattern of `bytes` and bytes + 4097
+   (buffer regrowth), results compared. 0 = ok. */
 int eao_rccl_selftest(int device, int bytes);
 int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* unique_id128);
 int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx);

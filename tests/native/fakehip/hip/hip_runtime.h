@@ -54,3 +54,4 @@ inline hipError_t hipEventQuery(hipEvent_t) {
 }
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return 0; }
 inline hipError_t hipMemset(void* p, int v, size_t n) { std::memset(p, v, n); return 0; }
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) { std::memset(p, v, n); return 0; }

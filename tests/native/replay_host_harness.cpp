@@ -89,12 +89,56 @@ struct eao_assoc { eao::AssocEngine e; };
 extern "C" const char* eao_last_error(void) { return eao::g_err.c_str(); }
 namespace eao { AssocEngine* assoc_engine(eao_assoc* a) { return &a->e; } }
 extern "C" eao_assoc* harness_assoc_create() { auto* a = new eao_assoc(); a->e.dev = 0; return a; }
-// the RCCL exchanger is product-only; the harness shards through
-// eao_replay_shard_callback (gloo from Python)
+// The RCCL exchanger is product-only. In its place eao_replay_shard_rccl gets a
+// device-form exchanger over the all-gather callback set by harness_set_device_exchange
+// (gloo from Python): "device" memory is host memory here, so the replay's device-form
+// code paths (records written by pack_masks / np_batch / rects_np into device buffers,
+// gathered from there) run on the CPU against the oracle.
 namespace eao {
-Exchanger* make_rccl_exchanger(int, int, int, const void*, int* rc) {
-  set_error("harness: no RCCL");
-  *rc = -3;
-  return nullptr;
+namespace {
+eao_allgather_fn g_dev_fn = nullptr;
+void* g_dev_ctx = nullptr;
+struct DeviceLoopExchanger : Exchanger {
+  int world;
+  std::vector<unsigned char> recv;
+  explicit DeviceLoopExchanger(int w) : world(w) {}
+  int allgather(const void*, void*, size_t) override {
+    set_error("harness device exchanger: host form called");
+    return EAO_E_ARG;
+  }
+  bool device_form() const override { return true; }
+  int allgather_device(const void* d_send, hipEvent_t, size_t bytes, const unsigned char** out) override {
+    recv.assign(bytes * world, 0xcd);
+    if (world == 1) {
+      std::memcpy(recv.data(), d_send, bytes);
+    } else if (!g_dev_fn || g_dev_fn(g_dev_ctx, d_send, recv.data(), bytes)) {
+      set_error("harness device exchanger: all-gather failed");
+      return EAO_E_ARG;
+    }
+    *out = recv.data();
+    return EAO_OK;
+  }
+};
+}  // namespace
+Exchanger* make_rccl_exchanger(int, int, int world, const void*, int* rc) {
+  *rc = 0;
+  return new DeviceLoopExchanger(world);
+}
+int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
+                            unsigned char* d_dst, hipStream_t) {
+  for (int c = 0; c < nclouds; c++) {
+    const int off = meta[3 * c], n = meta[3 * c + 1], out = meta[3 * c + 2];
+    for (int j = 0; j < (n + 7) / 8; j++) {
+      unsigned v = 0;
+      for (int b = 0; b < 8 && 8 * j + b < n; b++)
+        if (d_scores[off + 8 * j + b] > (double)th[c]) v |= 1u << b;
+      d_dst[out + j] = (unsigned char)v;
+    }
+  }
+  return EAO_OK;
 }
 }  // namespace eao
+extern "C" void harness_set_device_exchange(eao_allgather_fn fn, void* ctx) {
+  eao::g_dev_fn = fn;
+  eao::g_dev_ctx = ctx;
+}

@@ -123,8 +123,26 @@ def test_config_c_sharded_world2_matches_oracle(mode):
 
 
 def test_rccl_exchanger_world1():
-    """The RCCL exchanger of eao_replay_shard_rccl on a world-1 communicator: pinned staging,
-    H2D, ncclAllGather, D2H and the stream sync run, the staging regrows past 4 KB, and the
-    gathered bytes equal the sent ones (shard_rccl.cpp)."""
+    """The RCCL exchanger of eao_replay_shard_rccl on a world-1 communicator, device form: a
+    pattern written by a kernel, the GPU-side wait on its event, ncclAllGather device to
+    device, one copy back; the buffers regrow past 4 KB; gathered bytes == sent (shard_rccl.cpp)."""
     ea.rccl_selftest(0, 1000)
     ea.rccl_selftest(0, 64)
+
+
+def test_config_c_rccl_world1_device_records_match_oracle():
+    """The sharded replay's whole exchange path on one device: a world-1 RCCL communicator
+    (eao_replay_shard_rccl), every forest batch's outlier masks packed by k_pack_masks and its
+    speculative NP stats written into device records, the frame start's rects / NP stats
+    written into a device record, all of them all-gathered device to device over RCCL; ids,
+    points and statistics identical to the oracle."""
+    frames = synth.assoc_stream_config_c(N_FRAMES)
+    g = ea.Replay(ea.Assoc(), "EAO")
+    g.shard(0, 1, unique_id=ea.rccl_unique_id())
+    outs = []
+    for i, f in enumerate(frames):
+        outs.append(g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
+        if f["kf"]:
+            g.local_mapping()
+    _check(outs, g.objects(), _oracle(frames))
+    assert g.shard_stats()["exchanges"] > N_FRAMES

@@ -35,7 +35,24 @@ def _stream(kind, n):
     return synth.assoc_stream_config_c(n) if kind == "C" else synth.assoc_stream(n)
 
 
-def _worker(rank, world, port, flag, kind, n, q):
+def _device_exchange(H, world):
+    """The harness's stand-in for the RCCL exchanger (device form) over gloo: the replay
+    writes its records into "device" buffers and gathers them from there."""
+    gather = eao_dist.allgather_bytes_gloo() if world > 1 else None
+
+    def fn(ctx, send, recv, nbytes):
+        try:
+            data = gather(ctypes.string_at(send, nbytes))
+            ctypes.memmove(recv, data, len(data))
+            return 0
+        except Exception:  # noqa: BLE001 -- reported through the C status
+            return -1
+    cb = ea.Replay.ALLGATHER(fn)
+    H.harness_set_device_exchange(cb, None)
+    return cb
+
+
+def _worker(rank, world, port, flag, kind, n, q, form="host"):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -48,7 +65,11 @@ def _worker(rank, world, port, flag, kind, n, q):
         a = A()
         a.h = ctypes.c_void_p(H.harness_assoc_create())
         g = ea.Replay(a, flag)
-        g.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
+        if form == "device":
+            keep = _device_exchange(H, world)  # noqa: F841 -- the callback must outlive the replay
+            g.shard(rank, world, unique_id=bytes(128))
+        else:
+            g.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
         outs = []
         for i, f in enumerate(_stream(kind, n)):
             outs.append(g.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"]))
@@ -72,14 +93,18 @@ def _oracle(flag, kind, n):
     return outs, o.objects()
 
 
-@pytest.mark.parametrize("kind,n,flag", [("C", 40, "EAO"), ("fr3", 60, "iForest"), ("fr3", 30, "NP")])
-def test_sharded_replay_world2_matches_oracle(kind, n, flag):
+@pytest.mark.parametrize("kind,n,flag,form,world", [("C", 40, "EAO", "host", 2), ("fr3", 60, "iForest", "host", 2),
+                                                   ("fr3", 30, "NP", "host", 2), ("C", 40, "EAO", "device", 2),
+                                                   ("fr3", 40, "EAO", "device", 2), ("C", 30, "EAO", "device", 1)])
+def test_sharded_replay_world2_matches_oracle(kind, n, flag, form, world):
+    """form "device": the RCCL exchanger's device form (records written by the kernels into
+    device buffers, gathered from there); world 1 runs the whole exchange path on one rank."""
     orc.lib()
     subprocess.check_call(["make", "-s", "-C", NATIVE])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, flag, kind, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, flag, kind, n, q, form)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=600) for _ in procs), key=lambda r: r[0])
@@ -96,7 +121,7 @@ def test_sharded_replay_world2_matches_oracle(kind, n, flag):
         assert pts == [p.tolist() for p in rp]
         assert st["exchanges"] > 0
     # both ranks saw the same exchanges
-    assert res[0][5]["exchanges"] == res[1][5]["exchanges"]
+    assert res[0][5]["exchanges"] == res[-1][5]["exchanges"]
 
 
 def _worker_capacity(rank, world, port, q):

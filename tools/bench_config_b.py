@@ -187,7 +187,7 @@ def main(args=None):
         dom_bytes = ab.get(names[dom], ab["extract"])
         ach = dom_bytes * F / (stage[dom] * 1e-3) / 1e9
         ext_ms = float(stage.sum())
-        kern = {"pyramid": "k_resize (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
+        kern = {"pyramid": "k_resize_tile (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
                 "describe": "k_describe"}
         result = {
             "metric": "frames/sec (ORB extract+match) on 1920x1080, 4000 features, 8 levels",
