@@ -439,7 +439,9 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
                                                    int* __restrict__ sel_cnt, int nlevels) {
   __shared__ QShared<QCAP> S;
   constexpr int QOS = QShared<QCAP>::QOS;
-  const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+  // grid (frames, levels): workgroups are dispatched x fastest, so every frame's level-0
+  // quadtree (the longest walk) starts first and the shorter levels fill in behind it
+  const int l = blockIdx.y, f = blockIdx.x, lane = threadIdx.x;
   const LevelDev& L = levels[l];
   const uint32_t* C = cand + f * cand_stride;
   // ping-pong halves of this (frame, level): [2 cand_off, 2 cand_off + 2 cand_cap) of the frame area
@@ -1271,7 +1273,7 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[2], s));
   // quadtree distribution
   {
-    dim3 g(nl, nframes);
+    dim3 g(nframes, nl);
     int need = 0;
     for (int l = 0; l < nl; l++) need = std::max(need, levels[l].nfeat + 4 * levels[l].nIni + 16);
     auto kd = need <= 256 ? k_distribute<256> : need <= 512 ? k_distribute<512> : k_distribute<1024>;
