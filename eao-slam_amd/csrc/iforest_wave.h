@@ -223,7 +223,17 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
   auto sk64 = [&](int k) { return ((uint64_t)((uint32_t)k ^ 0x80000000u) << 32) | (uint32_t)lane; };
   uint64_t vx = sk64(lane < cnt ? kx : INT_MAX), vy = sk64(lane < cnt ? ky : INT_MAX),
            vz = sk64(lane < cnt ? kz : INT_MAX);
-  wave_sort3(vx, vy, vz);
+  // the items sit in lanes [0, cnt): a bitonic network over the next power of two >= cnt
+  // lanes sorts them (lanes beyond hold INT_MAX keys whatever order they end in, and no
+  // node ever contains them); 6 / 10 / 15 steps instead of 21 for cnt <= 8 / 16 / 32
+  if (cnt > 32)
+    wave_sort3(vx, vy, vz);
+  else if (cnt > 16)
+    bitonic_sort3<32>(vx, vy, vz);
+  else if (cnt > 8)
+    bitonic_sort3<16>(vx, vy, vz);
+  else
+    bitonic_sort3<8>(vx, vy, vz);
   // rank r (this lane): sorted key s*, item p*; item l (this lane): rank r*
   const int sx = (int)((uint32_t)(vx >> 32) ^ 0x80000000u), px = (int)(uint32_t)vx;
   const int sy = (int)((uint32_t)(vy >> 32) ^ 0x80000000u), py = (int)(uint32_t)vy;
