@@ -433,6 +433,7 @@ class ReplayEngine {
     // launch list (the owned objects), their offsets in the packed clouds
     std::vector<int> lc, loff;
     bool launched = false;
+    uint64_t seq = 0;       // launch order (if_seq at the launch)
     unsigned long fid = 0;  // frame of the launch (speculative NP stats belong to it)
     // sharded: the all-gathered outcome, an outlier bit mask per object
     // (mask_off into xres) and the speculative NP stats in sp_* order
@@ -454,6 +455,10 @@ class ReplayEngine {
   };
   std::vector<IfBatch> ifb;
   hipStream_t if_stream[kIfStreams] = {};
+  // the batch whose launch is the last work queued on each forest stream (-1: other work
+  // or none): a launch that waits on that batch alone can queue behind it on its stream
+  int if_tail[kIfStreams] = {-1, -1, -1, -1};
+  uint64_t if_seq = 0;
   int if_next = 0;
   int pend_err = 0;
 
@@ -1071,6 +1076,7 @@ class ReplayEngine {
         }
         if (xdev() && !b.launched) {  // nothing owned: an empty record, ready behind b.ev
           hipStream_t st = if_stream[k % kIfStreams];
+          if_tail[k % kIfStreams] = -1;
           if (!b.ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
           EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st));
           EAO_HIP_CHECK(hipEventRecord(b.ev, st));
@@ -1161,6 +1167,8 @@ class ReplayEngine {
         }
       }
       hipStream_t st = if_stream[k % kIfStreams];
+      b.seq = ++if_seq;
+      if_tail[k % kIfStreams] = k;
       prof[2] += 1;
       Tick tl(&prof[19]);
       // compute-queue staging (k_stage), as at the frame start: no DMA-engine hand-off
@@ -1515,7 +1523,20 @@ class ReplayEngine {
         oth[nb + k] = th_p[k];
       }
     }
-    for (int k : wait_slots) EAO_HIP_CHECK(hipStreamWaitEvent(A->stream, ifb[k].ev, 0));
+    // queued behind the latest of those forests on its own stream when that batch is the
+    // stream's last work (in-queue order: no cross-queue event wait on the chain, which
+    // costs 10-25 us between the forest's end and this launch's start); the others, if
+    // any, through event waits
+    hipStream_t ls = A->stream;
+    int lk = -1;
+    for (int k : wait_slots)
+      if (if_tail[k % kIfStreams] == k && (lk < 0 || ifb[k].seq > ifb[lk].seq)) lk = k;
+    if (lk >= 0) {
+      ls = if_stream[lk % kIfStreams];
+      if_tail[lk % kIfStreams] = -1;
+    }
+    for (int k : wait_slots)
+      if (k != lk) EAO_HIP_CHECK(hipStreamWaitEvent(ls, ifb[k].ev, 0));
     // one launch reads the packed inputs in place from pinned host memory (no staging
     // kernel on the chain) and writes the results straight back into pinned host memory
     const unsigned char* din = h_in;
@@ -1527,10 +1548,10 @@ class ReplayEngine {
     const float* doth = chained ? (const float*)(din + o_oth) : nullptr;
     rc = A->rects_np(camdev, (const float*)(din + o_T), nb, dpts, drm, drm + nb, (int*)(ob + o_r), ob + o_ok,
                      dosp, doth, npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
-                     (eao_np_stats*)ob, A->stream, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
+                     (eao_np_stats*)ob, ls, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
-    EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
+    EAO_HIP_CHECK(hipEventRecord(gpu0_ev, ls));
     if (rn_dev) return EAO_OK;
     {
       Tick tw(&prof[41]);
