@@ -12,6 +12,9 @@ namespace eao {
 
 constexpr int NP_MAXN = 8192;   // object points per NP pair handled in LDS
 constexpr int IF_MAXN = 7168;   // points per isolation-forest cloud (tree + sample in LDS)
+constexpr int IF_CTL = 256;     // CalculateC(leaf size) table entries staged in the forest kernel's LDS
+constexpr int IF_TAB_N = 4096;  // cloud sizes covered by the forest's sample table (k_iforest_sample)
+constexpr int IF_TAB_TW = 5;    // generator states per tree in the table: after 1 .. IF_TAB_TW twists
 constexpr int IF_LDS = 160 * 1024;  // LDS per workgroup on gfx950
 
 class AssocEngine {
@@ -31,6 +34,14 @@ class AssocEngine {
   double* d_contrib = nullptr;   // [max_trees][max_points] path length per (tree, point)
   double* d_ctab = nullptr;      // [IF_MAXN + 1] CalculateC(n) table (leaf sizes, sample sizes)
   uint32_t cached_seed = 0, cached_trees = 0;
+  // the sample table (k_iforest_sample): for n in [2, tab_n], sample n / 2, of (cached_seed,
+  // cached_trees); built with the generator states, tab_n = 0 until then
+  int tab_n = 0;
+  uint16_t* d_tab_ids = nullptr;      // per n, per tree: n / 2 sample ids
+  long long* d_tab_off = nullptr;     // [IF_TAB_N + 1] offset of size n's block in d_tab_ids
+  int* d_tab_D = nullptr;             // [IF_TAB_N + 1][trees] draws taken by the shuffle (-1: not covered)
+  uint32_t* d_tab_states = nullptr;   // [trees][IF_TAB_TW][624] states after 1 .. IF_TAB_TW twists
+  int iforest_table(uint32_t seed, uint32_t trees, hipStream_t s);
   size_t lds_limit = 0;
   double* d_scores = nullptr;    // [max_points]
   // the erase decision of IsolationForestDeleteOutliers, score > th (th = 0.6f, or 0.65f

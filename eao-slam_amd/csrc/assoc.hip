@@ -13,6 +13,7 @@
 //   k_iforest_sum  one thread per point: path lengths summed in tree order,
 //                  score 2^(-E[h]/c(psi)) (isolation_forest.h:499-530)
 #include <hip/hip_runtime.h>
+#include <cstring>
 
 #include <algorithm>
 #include <climits>
@@ -639,86 +640,38 @@ __device__ __forceinline__ void if_stamp(int k) {
 
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
 struct IfLds {
-  size_t mt, b0, b1, nodes, right, shuf, total;
+  size_t mt, b0, b1, nodes, shuf, ct, total;
   __host__ __device__ IfLds(int N, int S) {
     mt = 0;
     b0 = al16(624 * 4);
     b1 = b0 + al16(12 * (size_t)S);
     nodes = b1 + al16(12 * (size_t)S);
-    right = nodes + al16(8 * (2 * (size_t)S + 2));  // + the two look-ahead ids of rank_subtree
-    const size_t build_end = right + al16(2 * (2 * (size_t)S + 2));
+    const size_t build_end = nodes + al16(8 * (2 * (size_t)S + 2));  // + rank_subtree's two look-ahead ids
     // sampling scratch (p, head, next, ids) aliases B1 / nodes, dead until the build
     shuf = b1;
     const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
                             al16(2 * (size_t)S);
-    total = build_end > shuf_end ? build_end : shuf_end;
+    ct = build_end > shuf_end ? build_end : shuf_end;  // CalculateC of leaf sizes < IF_CTL
+    total = ct + 8 * IF_CTL;
   }
 };
 
 #define IF_END 0xffffu
 
-// One workgroup (16 waves) per (tree, cloud): IsolationTree::Build of
-// isolation_forest.h:165-224,300-345 by wave 0 -- the libstdc++-11 draw stream
-// replicated exactly -- then every wave walks the cloud's points through the
-// tree (GetAnomalyScores' PathLength, :499-530); k_iforest_sum adds the
-// per-(tree, point) path lengths in tree order.
-//
-// Sampling: std::shuffle of ids [0, n) (paired Lemire draws, stl_algo.h) is a
-// Fisher-Yates sequence of positions p_j <= j.  The draws are taken 64 at a
-// time in parallel; the swaps are not replayed: with v_j = j before step j
-// the final content of position k is the last step that wrote k,
+// IsolationTree::Build's sample (isolation_forest.h:300-330): std::shuffle of ids [0, n)
+// (paired Lemire draws, stl_algo.h) is a Fisher-Yates sequence of positions p_j <= j.  The
+// draws are taken 64 at a time in parallel; the swaps are not replayed: with v_j = j before
+// step j the final content of position k is the last step that wrote k,
 //   final(k)   = max{ j > k : p_j = k }   or else  f(p_k, k)  (k if p_k = k)
 //   f(q, t)    = max{ j in (q, t) : p_j = q } or else f(p_q, q) (q if p_q = q, 0 at q = 0)
-// resolved per thread from per-position writer lists.  Only the sample's set
-// matters to the build (min/max, counts and membership are order-free), so
-// the sampled coordinates are gathered straight into LDS and partitioned
-// between two ping-pong buffers by depth parity; a node of <= 64 items builds
-// its whole subtree in registers (one item per lane, children as lane masks).
-//
-// mt_init: per tree, the mt19937 state after seeding and the first twist
-// (the seeds are fixed per forest, so it is computed once on the host).
-__global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__ pts,
-                                                      const int* __restrict__ off,
-                                                      const int* __restrict__ len,
-                                                      const uint32_t* __restrict__ mt_init,
-                                                      const uint32_t* __restrict__ sample,
-                                                      int maxN, int maxS, int npts_total,
-                                                      const double* __restrict__ ctab,
-                                                      double* __restrict__ contrib) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const IfLds L(maxN, maxS);
-  uint32_t* mts = (uint32_t*)(smem + L.mt);
-  float* B0 = (float*)(smem + L.b0);
-  float* B1 = (float*)(smem + L.b1);
-  uint2* nodes = (uint2*)(smem + L.nodes);
-  uint16_t* right = (uint16_t*)(smem + L.right);
-  __shared__ int s_nodes_bad;
-
-  const int tr = blockIdx.x, c = blockIdx.y;
-  // the wave index is wave-uniform: readfirstlane tells the compiler, so the
-  // one-wave phases below branch on scalars and keep their state in SGPRs
-  const int tid = threadIdx.x, lane = tid & 63, nb = blockDim.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int n = len[c];
-  const int psi = (int)sample[c];
-  const float* P = pts + 3 * (long long)off[c];
-  double* out = contrib + (long long)tr * npts_total + off[c];
-  const bool valid = !(n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe);
-  if (tid == 0) s_nodes_bad = valid ? 0 : 1;
-  if (valid) {
-  uint16_t* p = (uint16_t*)(smem + L.shuf);
-  uint32_t* head = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
-  uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
-  uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
-  if_stamp(0);
-  for (int i = tid; i < 624; i += nb) mts[i] = mt_init[624 * tr + i];
+// resolved per thread from per-position writer lists.  ids[k] <- final(k), k < psi.  Every
+// thread of the block takes part; g (wave 0's generator, state in LDS) is left after the
+// shuffle's draws; p / head / nxt are LDS scratch of n entries; ends before a barrier.
+__device__ __forceinline__ void if_sample(WaveRng& g, int n, int psi, uint16_t* p, uint32_t* head, uint16_t* nxt,
+                                          uint16_t* ids, int tid, int nb, int wave, int lane) {
   for (int q = tid; q < n; q += nb) head[q] = IF_END;
   __syncthreads();
   if_stamp(1);
-  WaveRng g;  // used by wave 0 only
-  g.mt = mts;
-  g.idx = 0;  // state already twisted once
-  g.bp = g.blen = 0;
   if (wave == 0) {
     // ---- shuffle draws: positions p[j], j = 1..n-1
     const bool even = (n % 2) == 0;
@@ -786,6 +739,82 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     }
     ids[k] = (uint16_t)id;
   }
+}
+
+
+// One workgroup (16 waves) per (tree, cloud): IsolationTree::Build of
+// isolation_forest.h:165-224,300-345 by wave 0 -- the libstdc++-11 draw stream
+// replicated exactly -- then every wave walks the cloud's points through the
+// tree (GetAnomalyScores' PathLength, :499-530); k_iforest_sum adds the
+// per-(tree, point) path lengths in tree order.
+//
+// The sample (if_sample) is taken from the engine's table when the cloud's size is
+// covered (sample = n / 2, as IsolationForestDeleteOutliers asks), else drawn here.
+// Only the sample's set matters to the build (min/max, counts and membership are
+// order-free), so the sampled coordinates are gathered straight into LDS and
+// partitioned between two ping-pong buffers by depth parity; a node of <= 64 items
+// builds its whole subtree in registers (one item per lane, children as lane masks).
+//
+// mt_init: per tree, the mt19937 state after seeding and the first twist
+// (the seeds are fixed per forest, so it is computed once on the host).
+__global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__ pts,
+                                                      const int* __restrict__ off,
+                                                      const int* __restrict__ len,
+                                                      const uint32_t* __restrict__ mt_init,
+                                                      const uint32_t* __restrict__ sample,
+                                                      int maxN, int maxS, int npts_total,
+                                                      const double* __restrict__ ctab,
+                                                      double* __restrict__ contrib, int tab_n,
+                                                      const uint16_t* __restrict__ tab_ids,
+                                                      const long long* __restrict__ tab_off,
+                                                      const int* __restrict__ tab_D,
+                                                      const uint32_t* __restrict__ tab_states) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const IfLds L(maxN, maxS);
+  uint32_t* mts = (uint32_t*)(smem + L.mt);
+  float* B0 = (float*)(smem + L.b0);
+  float* B1 = (float*)(smem + L.b1);
+  uint2* nodes = (uint2*)(smem + L.nodes);
+  double* ctl = (double*)(smem + L.ct);
+  __shared__ int s_nodes_bad;
+
+  const int tr = blockIdx.x, c = blockIdx.y;
+  // the wave index is wave-uniform: readfirstlane tells the compiler, so the
+  // one-wave phases below branch on scalars and keep their state in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, nb = blockDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = len[c];
+  const int psi = (int)sample[c];
+  const float* P = pts + 3 * (long long)off[c];
+  double* out = contrib + (long long)tr * npts_total + off[c];
+  const bool valid = !(n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe);
+  if (tid == 0) s_nodes_bad = valid ? 0 : 1;
+  const bool tab = valid && n <= tab_n && psi == n / 2 && tab_D[(size_t)n * gridDim.x + tr] >= 0;  // uniform
+  if (valid) {
+  uint16_t* p = (uint16_t*)(smem + L.shuf);
+  uint32_t* head = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
+  uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
+  uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
+  if_stamp(0);
+  for (int i = tid; i < IF_CTL; i += nb) ctl[i] = ctab[i];
+  WaveRng g;  // used by wave 0 only
+  g.mt = mts;
+  g.idx = 0;  // state already twisted once
+  g.tw = 0;
+  g.bp = g.blen = 0;
+  const uint16_t* sid = ids;  // the sample: LDS, or the precomputed table
+  if (tab) {
+    // the sample and the generator after the shuffle depend only on (n, tree): taken from the
+    // engine's table (k_iforest_sample), the build continues at draw D of this tree's stream
+    const int D = tab_D[(size_t)n * gridDim.x + tr];
+    const uint32_t* st = tab_states + ((size_t)tr * IF_TAB_TW + D / 624) * 624;
+    for (int i = tid; i < 624; i += nb) mts[i] = st[i];
+    g.idx = D % 624;
+    sid = tab_ids + tab_off[n] + (size_t)tr * psi;
+  } else {
+    for (int i = tid; i < 624; i += nb) mts[i] = mt_init[624 * tr + i];
+    if_sample(g, n, psi, p, head, nxt, ids, tid, nb, wave, lane);
+  }
   __syncthreads();
   if_stamp(4);
   {
@@ -794,7 +823,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       float v[4][3];
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const float* q = P + 3 * (size_t)ids[k + u * nb];
+        const float* q = P + 3 * (size_t)sid[k + u * nb];
         v[u][0] = q[0];
         v[u][1] = q[1];
         v[u][2] = q[2];
@@ -807,7 +836,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       }
     }
     for (; k < psi; k += nb) {
-      const float* q = P + 3 * (size_t)ids[k];
+      const float* q = P + 3 * (size_t)sid[k];
       ((int*)B0)[k] = fkey(q[0]);
       ((int*)B0)[psi + k] = fkey(q[1]);
       ((int*)B0)[2 * psi + k] = fkey(q[2]);
@@ -832,7 +861,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       const int par = __builtin_amdgcn_readlane(spar, sp);
       const int me = nn++;
       // right links for the score walk, written as each right child gets its id
-      if (par >= 0 && lane == 0) right[par] = (uint16_t)me;
+      if (par >= 0 && lane == 0) set_right(nodes, par, me);
       const int cnt = last - first + 1;
       if (cnt < 2 || depth >= maxDepth) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
@@ -847,7 +876,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
         IFP_T(rs0);
         const int nn0 = nn;
-        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes, right);
+        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes);
         IFP_T(rs1);
         IFP_ACC(21, rs0, rs1);
         IFP_ACC(22, 0ull, 1ull);
@@ -919,7 +948,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
           mask = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(slo, ssp) |
                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(shi, ssp) << 32);
           d = __builtin_amdgcn_readlane(sdd, ssp);
-          if (lane == 0) right[__builtin_amdgcn_readlane(spp, ssp)] = (uint16_t)nn;
+          if (lane == 0) set_right(nodes, __builtin_amdgcn_readlane(spp, ssp), nn);
           node = nn++;
           IFP_T(t7);
           IFP_ACC(17, t6, t7);
@@ -1030,7 +1059,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
         const uint32_t d = nd[u].x & 3u;
         if (d != 0u) {
           const float v = d == 1u ? x[u][0] : (d == 2u ? x[u][1] : x[u][2]);
-          k[u] = v < __uint_as_float(nd[u].y) ? k[u] + 1 : (int)right[k[u]];
+          k[u] = v < __uint_as_float(nd[u].y) ? k[u] + 1 : (int)(nd[u].x >> 16);
           depth[u]++;
         }
       }
@@ -1045,10 +1074,45 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int i = i0 + u * nb;
-      if (i < n) out[i] = (double)depth[u] + ctab[nd[u].x >> 2];
+      const uint32_t lc = nd[u].x >> 2;  // leaf size
+      if (i < n) out[i] = (double)depth[u] + (lc < IF_CTL ? ctl[lc] : ctab[lc]);
     }
   }
   if_stamp(7);
+}
+
+// The sample table of the engine (AssocEngine::iforest_table): for every cloud size n in
+// [2, tab_n] and tree, the ids of if_sample with sample n / 2 (at tab_ids + tab_off[n] +
+// tree * (n / 2)) and D = the draws its shuffle takes from the tree's stream (tab_D[n][tree]).
+// Both depend on (n, tree) only -- a constant of the forest's seeds, like mt_init.
+__global__ __launch_bounds__(256) void k_iforest_sample(const uint32_t* __restrict__ mt_init, int n0, int tab_n,
+                                                        const long long* __restrict__ tab_off,
+                                                        uint16_t* __restrict__ tab_ids, int* __restrict__ tab_D) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int n = n0 + blockIdx.y, tr = blockIdx.x;
+  if (n > tab_n) return;  // whole workgroup
+  const int psi = n / 2;
+  const int tid = threadIdx.x, lane = tid & 63, nb = blockDim.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  uint32_t* mts = (uint32_t*)smem;
+  uint16_t* p = (uint16_t*)(smem + al16(624 * 4));
+  uint32_t* head = (uint32_t*)((unsigned char*)p + al16(2 * (size_t)n));
+  uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
+  uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
+  for (int i = tid; i < 624; i += nb) mts[i] = mt_init[624 * tr + i];
+  WaveRng g;
+  g.mt = mts;
+  g.idx = 0;
+  g.tw = 0;
+  g.bp = g.blen = 0;
+  if_sample(g, n, psi, p, head, nxt, ids, tid, nb, wave, lane);
+  __syncthreads();
+  uint16_t* dst = tab_ids + tab_off[n] + (size_t)tr * psi;
+  for (int k = tid; k < psi; k += nb) dst[k] = ids[k];
+  if (tid == 0) {  // wave 0 holds the generator
+    const int D = 624 * g.tw + g.idx - (g.blen - g.bp);
+    tab_D[(size_t)n * gridDim.x + tr] = D / 624 < IF_TAB_TW ? D : -1;
+  }
 }
 
 // score = 2^(-E[h(x)] / c(psi)), E[h] summed over the trees in order (GetAnomalyScores,
@@ -1160,7 +1224,8 @@ int AssocEngine::init(int device, int mp) {
 
 AssocEngine::~AssocEngine() {
   if (replay_pool && replay_pool_free) replay_pool_free(replay_pool);
-  void* ptrs[] = {d_pts, d_valid, d_meta, d_np, d_rect, d_ok, d_T, d_mtinit, d_scores, d_contrib, d_ctab};
+  void* ptrs[] = {d_pts,    d_valid,   d_meta,       d_np,      d_rect,    d_ok,        d_T,        d_mtinit,
+                  d_scores, d_contrib, d_ctab,       d_tab_ids, d_tab_off, d_tab_D, d_tab_states};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -1230,6 +1295,52 @@ static void forest_states(uint32_t seed, uint32_t trees, std::vector<uint32_t>& 
   }
 }
 
+// The per-tree generator states (mt_init) of a forest seed and the sample table of
+// k_iforest_sample: built once per (seed, trees), synchronously (forest batches on other
+// streams read them right after). ~0.4 GB of HBM for IF_TAB_N = 4096.
+int AssocEngine::iforest_table(uint32_t seed, uint32_t trees, hipStream_t s) {
+  std::vector<uint32_t> st;
+  forest_states(seed, trees, st);
+  EAO_HIP_CHECK(hipMemcpyAsync(d_mtinit, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, s));
+  // states after 1 .. IF_TAB_TW twists of every tree's generator
+  std::vector<uint32_t> tw((size_t)trees * IF_TAB_TW * 624);
+  for (uint32_t t = 0; t < trees; t++) {
+    uint32_t mt[624];
+    std::memcpy(mt, st.data() + (size_t)624 * t, sizeof(mt));
+    for (int k = 0; k < IF_TAB_TW; k++) {
+      if (k) mt_twist(mt);
+      std::memcpy(tw.data() + ((size_t)t * IF_TAB_TW + k) * 624, mt, sizeof(mt));
+    }
+  }
+  std::vector<long long> off(IF_TAB_N + 1, 0);
+  for (int n = 3; n <= IF_TAB_N; n++) off[n] = off[n - 1] + (long long)trees * ((n - 1) / 2);
+  const long long tot = off[IF_TAB_N] + (long long)trees * (IF_TAB_N / 2);
+  if (trees != cached_trees || !d_tab_ids) {
+    void* old[] = {d_tab_ids, d_tab_off, d_tab_D, d_tab_states};
+    for (void* q : old)
+      if (q) (void)hipFree(q);
+    EAO_HIP_CHECK(hipMalloc(&d_tab_ids, sizeof(uint16_t) * (size_t)tot));
+    EAO_HIP_CHECK(hipMalloc(&d_tab_off, sizeof(long long) * off.size()));
+    EAO_HIP_CHECK(hipMalloc(&d_tab_D, sizeof(int) * (size_t)(IF_TAB_N + 1) * trees));
+    EAO_HIP_CHECK(hipMalloc(&d_tab_states, sizeof(uint32_t) * tw.size()));
+  }
+  EAO_HIP_CHECK(hipMemcpyAsync(d_tab_off, off.data(), sizeof(long long) * off.size(), hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(d_tab_states, tw.data(), sizeof(uint32_t) * tw.size(), hipMemcpyHostToDevice, s));
+  EAO_HIP_CHECK(hipMemsetAsync(d_tab_D, 0xff, sizeof(int) * (size_t)(IF_TAB_N + 1) * trees, s));  // -1
+  for (int n0 = 2; n0 <= IF_TAB_N; n0 += 256) {  // LDS sized per range of n: more workgroups per CU
+    const size_t n1 = std::min(n0 + 255, IF_TAB_N);
+    const size_t lds = al16(624 * 4) + al16(2 * n1) + al16(4 * n1) + al16(2 * n1) + al16(2 * (n1 / 2));
+    hipLaunchKernelGGL(k_iforest_sample, dim3(trees, (unsigned)(n1 - n0 + 1)), dim3(256), lds, s, d_mtinit, n0,
+                       IF_TAB_N, (const long long*)d_tab_off, d_tab_ids, d_tab_D);
+    EAO_HIP_CHECK(hipGetLastError());
+  }
+  EAO_HIP_CHECK(hipStreamSynchronize(s));  // the host vectors are pageable; other streams read the table next
+  cached_seed = seed;
+  cached_trees = trees;
+  tab_n = IF_TAB_N;
+  return EAO_OK;
+}
+
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len,
                                uint32_t trees, uint32_t seed, const uint32_t* d_sample,
                                double* scores, hipStream_t s, int maxN, int maxS, int npts_total,
@@ -1245,16 +1356,12 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     set_error("iforest: cloud exceeds the LDS-resident tree capacity");
     return EAO_E_CAPACITY;
   }
-  if (seed != cached_seed || trees != cached_trees) {
-    std::vector<uint32_t> st;
-    forest_states(seed, trees, st);
-    EAO_HIP_CHECK(hipMemcpyAsync(d_mtinit, st.data(), sizeof(uint32_t) * st.size(), hipMemcpyHostToDevice, s));
-    EAO_HIP_CHECK(hipStreamSynchronize(s));  // st is pageable and about to go out of scope
-    cached_seed = seed;
-    cached_trees = trees;
+  if (seed != cached_seed || trees != cached_trees || !tab_n) {
+    if (int rc = iforest_table(seed, trees, s)) return rc;
   }
   hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(1024), L.total, s, pts, off, len,
-                     d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib);
+                     d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n, d_tab_ids, d_tab_off,
+                     d_tab_D, d_tab_states);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,

@@ -99,8 +99,9 @@ int eao_orb_extract(eao_orb* h, const uint8_t* gray, int w, int hh, int stride, 
   int rc = e.run(e.d_img, 1, w, e.d_out_kps, e.d_out_desc, e.d_out_cnt, e.cap, e.stream);
   if (rc) return rc;
   int n = 0;
-  EAO_HIP_CHECK(hipMemcpyAsync(&n, e.d_out_cnt, sizeof(int), hipMemcpyDeviceToHost, e.stream));
+  // the stream's work is complete before the count is read (no async copy into a stack variable)
   EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
+  EAO_HIP_CHECK(hipMemcpy(&n, e.d_out_cnt, sizeof(int), hipMemcpyDeviceToHost));
   *n_out = n;
   if (n > cap) {
     set_error("eao_orb_extract: output capacity too small");

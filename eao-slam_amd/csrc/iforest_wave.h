@@ -18,6 +18,7 @@ namespace eao {
 struct WaveRng {
   uint32_t* mt;  // LDS [624]
   int idx;       // next untempered state word (uniform)
+  int tw;        // twists since the state the generator started from (draw count = 624 tw + idx - unread)
   uint32_t buf;  // lane j: draw number (base + j) of the current chunk
   uint32_t bufd;  // the same draw as uniform_int<uint32>(0, 2) (Lemire), 3 = rejected
   float buff;     // the same draw as generate_canonical<float, 24>
@@ -33,6 +34,7 @@ struct WaveRng {
       }
     }
     idx = 624;
+    tw = -1;
     bp = blen = 0;
     WAVE_FENCE();
   }
@@ -58,6 +60,7 @@ struct WaveRng {
     }
     WAVE_FENCE();
     idx = 0;
+    tw++;
   }
   __device__ void refill() {
     if (idx >= 624) twist();
@@ -152,6 +155,14 @@ __device__ __forceinline__ void wave_minmax_key(int& mn, int& mx) {
 
 __host__ __device__ __forceinline__ size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// tree node record in LDS: x = dim + 1 (bits 0-1) | right child id << 16 for a split,
+// count << 2 for a leaf (count < 16384); y = the split's float bits. The right link is
+// written later, into the upper half of x (a 16-bit store after the record's own store),
+// so the score walk reads one record per level.
+__device__ __forceinline__ void set_right(uint2* nodes, int id, int link) {
+  ((uint16_t*)nodes)[4 * id + 1] = (uint16_t)link;
+}
+
 // lane l <- lane l ^ J (J a power of two < 64): DPP within quads, swizzle
 // within 32, permlane swaps across rows / halves (gfx950)
 template <int J>
@@ -213,12 +224,13 @@ namespace eao {
 // come from one ballot each through the item permutation. Draws are taken
 // from g exactly as the sequential build takes them (dim: Lemire over 3,
 // split: uniform_real(min, max)); leaves (by count or depth) consume none and
-// are recorded without a loop trip. Node records (x = dim + 1 | count << 2,
-// y = split bits) go to nodes for ids [me, nn), preorder, right links to right;
+// are recorded without a loop trip. Node records (x = dim + 1 | right child id << 16 for
+// a split, count << 2 for a leaf; y = split bits) go to nodes for ids [me, nn), preorder;
+// a right link is a 16-bit store into the upper half of x once the right child has its id;
 // the caller has allocated `me` (nn == me + 1) and checked 2 <= cnt,
 // depth < maxDepth. Returns 1 when Node::Build fails (empty right range).
 __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, int cnt, int depth, int maxDepth,
-                                            int me, int& nn, uint2* nodes, uint16_t* right) {
+                                            int me, int& nn, uint2* nodes) {
   const int lane = lane_id();
   auto sk64 = [&](int k) { return ((uint64_t)((uint32_t)k ^ 0x80000000u) << 32) | (uint32_t)lane; };
   uint64_t vx = sk64(lane < cnt ? kx : INT_MAX), vy = sk64(lane < cnt ? ky : INT_MAX),
@@ -291,7 +303,7 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
       bad = 1;
       break;
     }
-    if (lane == 0 && !leaf && lleaf) right[node] = (uint16_t)(nn + 1);
+    if (lane == 0 && !leaf && lleaf) set_right(nodes, node, nn + 1);
     // push the right child when the left one is walked next (case "descend")
     const bool descend = !leaf && !lleaf;
     writelane(q0, (int)(uint32_t)R, ssp);
@@ -315,7 +327,7 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
       const int par = __builtin_amdgcn_readlane(q3, ssp);
       S = (uint64_t)(uint32_t)__builtin_amdgcn_readlane(q0, ssp) |
           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(q1, ssp) << 32);
-      if (lane == 0) right[par] = (uint16_t)nn;
+      if (lane == 0) set_right(nodes, par, nn);
       node = nn++;
       d = e & 255;
       cn = __builtin_popcountll(S);

@@ -1428,8 +1428,9 @@ int eao_match_local(eao_matcher* m, const eao_camera* cam, float th, float nnrat
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  // the stream's work is complete before the count is read (no async copy into a stack variable)
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  EAO_HIP_CHECK(hipMemcpy(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost));
   return nm;
 }
 
@@ -1480,8 +1481,9 @@ int eao_match_keyframe(eao_matcher* m, const eao_camera* cam, const float* Tcw, 
   EAO_HIP_CHECK(hipGetLastError());
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  // the stream's work is complete before the count is read (no async copy into a stack variable)
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  EAO_HIP_CHECK(hipMemcpy(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost));
   return nm;
 }
 
@@ -1514,8 +1516,9 @@ int eao_match_init(eao_matcher* m, const eao_camera* cam, float nnratio, int che
   int nm = 0;
   EAO_HIP_CHECK(hipMemcpyAsync(matches12, e.d_out, sizeof(int) * n1, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipMemcpyAsync(prev_matched_xy, e.d_f, sizeof(float) * 2 * n1, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost, s));
+  // the stream's work is complete before the count is read (no async copy into a stack variable)
   EAO_HIP_CHECK(hipStreamSynchronize(s));
+  EAO_HIP_CHECK(hipMemcpy(&nm, e.d_out + 2 * K, sizeof(int), hipMemcpyDeviceToHost));
   return nm;
 }
 

@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <array>
 #include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -408,6 +409,19 @@ class ReplayEngine {
   // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
   double prof[56] = {0};
   int phase = 0;
+  // development trace (EAO_REPLAY_TRACE=<file>): host events on the steady clock (ns, the
+  // clock rocprofv3's kernel timestamps use), written at destruction -- tools/replay_timeline.py
+  struct TraceEv {
+    int64_t t;
+    int32_t ev, a, b, c;
+  };
+  std::vector<TraceEv> trace;
+  const char* trace_path = std::getenv("EAO_REPLAY_TRACE");
+  void tr(int ev, int a = 0, int b = 0, int c = 0) {
+    if (!trace_path) return;
+    trace.push_back({std::chrono::duration_cast<std::chrono::nanoseconds>(
+                         std::chrono::steady_clock::now().time_since_epoch()).count(), ev, a, b, c});
+  }
   static double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
   }
@@ -542,6 +556,11 @@ class ReplayEngine {
   ~ReplayEngine() {
     for (hipStream_t st : if_stream)
       if (st) (void)hipStreamSynchronize(st);
+    if (trace_path && !trace.empty())
+      if (FILE* f = std::fopen(trace_path, "ab")) {
+        std::fwrite(trace.data(), sizeof(TraceEv), trace.size(), f);
+        std::fclose(f);
+      }
     if (gpu0_ev) (void)hipEventDestroy(gpu0_ev);
     if (A && !A->replay_pool && !ifb.empty()) {
       Pool* p = new Pool();
@@ -1198,6 +1217,7 @@ class ReplayEngine {
         if (rc) return rc;
       }
       EAO_HIP_CHECK(hipEventRecord(b.ev, st));
+      tr(5, k, nl, maxN);
     }
     return EAO_OK;
   }
@@ -1266,8 +1286,10 @@ class ReplayEngine {
     } else if (b.launched) {
       Tick tw(&prof[39]);
       Tick tw2(&prof[42 + phase]);
+      tr(6, o->slot, phase);
       idle_work(b.ev);
       EAO_HIP_CHECK(spin_event(b.ev));
+      tr(7, o->slot, phase);
     }
     double tpost = now_us();
     int c = 0;
@@ -1552,12 +1574,14 @@ class ReplayEngine {
     if (rc) return rc;
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, ls));
+    tr(2, lk, (int)wait_slots.size(), npairs);
     if (rn_dev) return EAO_OK;
     {
       Tick tw(&prof[41]);
       idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
       EAO_HIP_CHECK(spin_event(gpu0_ev));
     }
+    tr(3);
     const int* r = (const int*)(h_out + o_r);
     const uint8_t* ok = h_out + o_ok;
     for (int b = 0; b < nb; b++) {
@@ -2412,6 +2436,7 @@ class ReplayEngine {
   int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
             const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
     Tick tk(&prof[0]);
+    tr(1, (int)fid);
     phase = 4;
     prof[8] += 1;
     cur = fid;
@@ -2540,6 +2565,7 @@ class ReplayEngine {
       }
       kept_pos = (int)kept.size();
       cur_np_done = true;
+      tr(4);
       prof[15] += now_us() - tA;
       tA = now_us();
       {
@@ -2816,6 +2842,11 @@ class ReplayEngine {
 
   int local_mapping() {
     Tick tk(&prof[1]);
+    tr(8);
+    struct TrEnd {
+      ReplayEngine* r;
+      ~TrEnd() { r->tr(9); }
+    } tr_end{this};
     phase = 3;
     int rc;
     {

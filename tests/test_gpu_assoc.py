@@ -103,6 +103,31 @@ def test_iforest_scores():
         assert np.array_equal(g > 0.6, o > 0.6)
 
 
+def test_iforest_sample_table_and_drawn_paths():
+    """The engine takes a forest's sample from its table (k_iforest_sample) when the cloud
+    has at most IF_TAB_N = 4096 points and the sample is n / 2, and draws it in the kernel
+    otherwise: both must equal the restatement. Sizes around the shuffle's 624-draw twists
+    (n / 2 near 624 and 1248), odd sizes, the table's last size, one beyond it, and other
+    sample sizes."""
+    rng = np.random.default_rng(0x7AB)
+    sizes = (1247, 1248, 1249, 2495, 2497, 4095, 4096, 4097, 5001)
+    clouds = []
+    for n in sizes:
+        c = _cloud(rng, n, [0, 0, 2], 0.05)
+        c[: n // 25] += rng.uniform(-0.5, 0.5, (n // 25, 3)).astype(np.float32)
+        clouds.append(c)
+    a = ea.Assoc(max_points=40000)
+    for c, g in zip(clouds, a.iforest(clouds)):  # sample n / 2: table up to 4096, drawn beyond
+        o = orc.iforest(c)
+        assert np.allclose(g, o, rtol=1e-5, atol=1e-9), len(c)
+        assert np.array_equal(g > 0.6, o > 0.6), len(c)
+    sub = clouds[:4]
+    samples = [len(c) // 3 for c in sub]  # drawn in the kernel whatever the size
+    for c, m, g in zip(sub, samples, a.iforest(sub, samples=samples)):
+        o = orc.iforest(c, sample=m)
+        assert np.allclose(g, o, rtol=1e-5, atol=1e-9), (len(c), m)
+
+
 def test_project_rects(frames):
     _, poses = frames
     rng = np.random.default_rng(41)

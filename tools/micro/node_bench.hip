@@ -166,7 +166,7 @@ __global__ void k_subtree(const int* keys, int cnt, int maxDepth, int reps, unsi
   const unsigned long long t0 = clock64();
   for (int r = 0; r < reps; r++) {
     int nn = 1;
-    bad |= rank_subtree(g, kx, ky, kz, cnt, 0, maxDepth, 0, nn, nodes, ndep);
+    bad |= rank_subtree(g, kx, ky, kz, cnt, 0, maxDepth, 0, nn, nodes);
     total += nn;
   }
   const unsigned long long t1 = clock64();
