@@ -203,6 +203,7 @@ def main():
     ap.add_argument("--cpu-mt-frames", type=int, default=256, help="extract+match all-cores CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
+    ap.add_argument("--poll", action="store_true", help="A/B: poll the extraction stream while the association runs")
     args = ap.parse_args()
     if args.cpu_frames is None:
         args.cpu_frames = 3 if args.config == "b" else 60
@@ -372,14 +373,16 @@ def main():
             th = threading.Thread(target=associate, args=(out,))
             th.start()
             front()
-        # wait for the extraction stream only (a device-wide synchronize would also serialise
-        # against the association thread's launches), politely: the association thread is
-        # the critical path and needs its core
+        # the association thread is the critical path: the main thread makes no HIP call while it
+        # runs (it joins it first), then waits for the extraction stream only (a device-wide
+        # synchronize would also serialise against other streams)
         ev_done.record(stream)
-        while not ev_done.query():
-            time.sleep(2e-4)
+        if args.poll:
+            while not ev_done.query():
+                time.sleep(2e-4)
         if th is not None:
             th.join()
+        ev_done.synchronize()
         if record is not None:
             record["stage_ms"].append(orb.stage_ms())
             record["match_ms"].append(ev_m0.elapsed_time(ev_m1))

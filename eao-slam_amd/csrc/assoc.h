@@ -14,6 +14,8 @@ constexpr int NP_MAXN = 8192;   // object points per NP pair handled in LDS
 constexpr int IF_MAXN = 7168;   // points per isolation-forest cloud (tree + sample in LDS)
 constexpr int IF_CTL = 256;     // CalculateC(leaf size) table entries staged in the forest kernel's LDS
 constexpr int IF_TAB_N = 4096;  // cloud sizes covered by the forest's sample table (k_iforest_sample)
+constexpr int IF_JSLOTS = 16;   // forest kernel: rank subtrees prepared ahead by helper waves (slots)
+constexpr int IF_HELPERS = 3;   // ... and the helper waves (1..3: the other SIMDs of wave 0's CU)
 constexpr int IF_TAB_TW = 5;    // generator states per tree in the table: after 1 .. IF_TAB_TW twists
 constexpr int IF_LDS = 160 * 1024;  // LDS per workgroup on gfx950
 

@@ -640,8 +640,8 @@ __device__ __forceinline__ void if_stamp(int k) {
 
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
 struct IfLds {
-  size_t mt, b0, b1, nodes, shuf, ct, total;
-  __host__ __device__ IfLds(int N, int S) {
+  size_t mt, b0, b1, nodes, shuf, ct, js, jq, total;
+  __host__ __device__ IfLds(int N, int S, int J = 0) {  // J helper job slots
     mt = 0;
     b0 = al16(624 * 4);
     b1 = b0 + al16(12 * (size_t)S);
@@ -652,7 +652,9 @@ struct IfLds {
     const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
                             al16(2 * (size_t)S);
     ct = build_end > shuf_end ? build_end : shuf_end;  // CalculateC of leaf sizes < IF_CTL
-    total = ct + 8 * IF_CTL;
+    js = ct + 8 * IF_CTL;                          // helper waves' prepared subtrees
+    jq = js + sizeof(RankSlot) * J;                // the subtree job list
+    total = jq + al16(4 * ((size_t)S / 8 + 4));
   }
 };
 
@@ -768,15 +770,21 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
                                                       const uint16_t* __restrict__ tab_ids,
                                                       const long long* __restrict__ tab_off,
                                                       const int* __restrict__ tab_D,
-                                                      const uint32_t* __restrict__ tab_states) {
+                                                      const uint32_t* __restrict__ tab_states, int jslots) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const IfLds L(maxN, maxS);
+  const IfLds L(maxN, maxS, jslots);
   uint32_t* mts = (uint32_t*)(smem + L.mt);
   float* B0 = (float*)(smem + L.b0);
   float* B1 = (float*)(smem + L.b1);
   uint2* nodes = (uint2*)(smem + L.nodes);
   double* ctl = (double*)(smem + L.ct);
   __shared__ int s_nodes_bad;
+  // rank-subtree preparation by helper waves: wave 0 posts jobs (jq[j] = first | cnt << 16 |
+  // buffer parity << 23 | slot << 24), waves 1..IF_HELPERS take them in order (s_take), sort the
+  // items into slot RS[slot] and publish s_done[slot] = j + 1
+  __shared__ int s_post, s_take, s_stop, s_done[IF_JSLOTS];
+  RankSlot* RS = (RankSlot*)(smem + L.js);
+  int* jq = (int*)(smem + L.jq);
 
   const int tr = blockIdx.x, c = blockIdx.y;
   // the wave index is wave-uniform: readfirstlane tells the compiler, so the
@@ -797,6 +805,8 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
   if_stamp(0);
   for (int i = tid; i < IF_CTL; i += nb) ctl[i] = ctab[i];
+  if (tid < jslots) s_done[tid] = 0;
+  if (tid == 0) s_post = s_take = s_stop = 0;
   WaveRng g;  // used by wave 0 only
   g.mt = mts;
   g.idx = 0;  // state already twisted once
@@ -852,13 +862,30 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     const int maxDepth = (int)ceil(log2((double)psi));
     int sf = 0, sl = psi - 1, sd = 0;  // lane 0 = root
     int spar = -1;                     // parent id of a pending right child, else -1
+    int sjob = -1;                     // helper job of a rank-space entry (j | slot << 16), else -1
     int sp = 1, nn = 0, bad = 0;
+    uint32_t fslot = (1u << jslots) - 1u;  // free job slots
+    int njob = 0;
+    const int maxjob = psi / 8 + 4;
+    // a child of 8..64 items that will be built in rank space: its sort goes to a helper now
+    auto post = [&](int f, int c, int d) -> int {
+      if (c < 8 || c > 64 || d >= maxDepth || fslot == 0u || njob >= maxjob) return -1;
+      const int slot = __builtin_ctz(fslot);
+      fslot &= ~(1u << slot);
+      const int j = njob++;
+      if (lane == 0) {
+        jq[j] = f | (c << 16) | ((d & 1) << 23) | (slot << 24);
+        __hip_atomic_store(&s_post, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return j | (slot << 16);
+    };
     while (sp > 0 && !bad) {
       sp--;
       const int first = __builtin_amdgcn_readlane(sf, sp);
       const int last = __builtin_amdgcn_readlane(sl, sp);
       const int depth = __builtin_amdgcn_readlane(sd, sp);
       const int par = __builtin_amdgcn_readlane(spar, sp);
+      const int job = __builtin_amdgcn_readlane(sjob, sp);
       const int me = nn++;
       // right links for the score walk, written as each right child gets its id
       if (par >= 0 && lane == 0) set_right(nodes, par, me);
@@ -870,13 +897,32 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       const int* src = (depth & 1) ? (const int*)B1 : K0;
       if (cnt >= 8 && cnt <= 64) {
         // whole subtree in rank space (iforest_wave.h rank_subtree)
-        const bool has = lane < cnt;
-        const int kx = has ? src[first + lane] : INT_MAX;
-        const int ky = has ? src[psi + first + lane] : INT_MAX;
-        const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
         IFP_T(rs0);
+        RankTab tb;
+        bool ready = false;
+        if (job >= 0) {  // prepared by a helper wave (bounded wait; sorted here after it)
+          const int j = job & 0xffff, slot = job >> 16;
+          for (int w = 0; w < 4096; w++) {
+            if (__hip_atomic_load(&s_done[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == j + 1) {
+              ready = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (ready) {
+            tb = rank_load(&RS[slot]);
+            fslot |= 1u << slot;  // (a slot whose job timed out stays taken: its helper may still write it)
+          }
+        }
+        if (!ready) {
+          const bool has = lane < cnt;
+          const int kx = has ? src[first + lane] : INT_MAX;
+          const int ky = has ? src[psi + first + lane] : INT_MAX;
+          const int kz = has ? src[2 * psi + first + lane] : INT_MAX;
+          tb = rank_prep(kx, ky, kz, cnt);
+        }
         const int nn0 = nn;
-        bad |= rank_subtree(g, kx, ky, kz, cnt, depth, maxDepth, me, nn, nodes);
+        bad |= rank_build(g, tb, cnt, depth, maxDepth, me, nn, nodes);
         IFP_T(rs1);
         IFP_ACC(21, rs0, rs1);
         IFP_ACC(22, 0ull, 1ull);
@@ -1002,18 +1048,22 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       if (nr == 0) bad = 1;  // right range empty: Node::Build returns false
       if (lane == 0) nodes[me] = make_uint2(dim + 1u, __float_as_uint(split));
       const int middle = first + nl;
+      // helper jobs for rank-space children, the left one first (it is built first)
+      const int jl = post(first, nl, depth + 1), jr = post(middle, nr, depth + 1);
       // push right, then left: the left subtree is built (and draws) first
       if (lane == sp) {
         sf = middle;
         sl = last;
         sd = depth + 1;
         spar = me;
+        sjob = jr;
       }
       if (lane == sp + 1) {
         sf = first;
         sl = middle - 1;
         sd = depth + 1;
         spar = -1;
+        sjob = jl;
       }
       sp += 2;
       IFP_T(bb1);
@@ -1022,8 +1072,39 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     }
     if (lane == 0) {
       s_nodes_bad = bad;
+      __hip_atomic_store(&s_stop, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
+  } else if (wave <= IF_HELPERS) {
+    // helper: take posted subtree jobs in order, sort their items into the job's slot
+    while (true) {
+      int j = -1;
+      while (true) {
+        if (__hip_atomic_load(&s_stop, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        const int tk = __hip_atomic_load(&s_take, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (tk < __hip_atomic_load(&s_post, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+          int got = -1;
+          if (lane == 0) got = atomicCAS(&s_take, tk, tk + 1) == tk ? tk : -1;
+          got = __builtin_amdgcn_readfirstlane(got);
+          if (got >= 0) {
+            j = got;
+            break;
+          }
+          continue;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (j < 0) break;
+      const int e = jq[j];
+      const int f = e & 0xffff, c = (e >> 16) & 0x7f, slot = (e >> 24) & 0xff;
+      const int* src = ((e >> 23) & 1) ? (const int*)B1 : (const int*)B0;
+      const bool has = lane < c;
+      const int kx = has ? src[f + lane] : INT_MAX;
+      const int ky = has ? src[psi + f + lane] : INT_MAX;
+      const int kz = has ? src[2 * psi + f + lane] : INT_MAX;
+      rank_store(&RS[slot], rank_prep(kx, ky, kz, c));
+      if (lane == 0) __hip_atomic_store(&s_done[slot], j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
   __syncthreads();
   }  // valid
@@ -1351,7 +1432,6 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     set_error("iforest: too many trees, clouds or points per call");
     return EAO_E_CAPACITY;
   }
-  const IfLds L(maxN, maxS);
   if (!iforest_fits(maxN, maxS)) {
     set_error("iforest: cloud exceeds the LDS-resident tree capacity");
     return EAO_E_CAPACITY;
@@ -1359,9 +1439,13 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
   if (seed != cached_seed || trees != cached_trees || !tab_n) {
     if (int rc = iforest_table(seed, trees, s)) return rc;
   }
+  // helper job slots: as many as the LDS left by the tree allows (up to IF_JSLOTS)
+  int jslots = IF_JSLOTS;
+  while (jslots > 0 && IfLds(maxN, maxS, jslots).total > lds_limit) jslots--;
+  const IfLds L(maxN, maxS, jslots);
   hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(1024), L.total, s, pts, off, len,
                      d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n, d_tab_ids, d_tab_off,
-                     d_tab_D, d_tab_states);
+                     d_tab_D, d_tab_states, jslots);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,

@@ -229,8 +229,45 @@ namespace eao {
 // a right link is a 16-bit store into the upper half of x once the right child has its id;
 // the caller has allocated `me` (nn == me + 1) and checked 2 <= cnt,
 // depth < maxDepth. Returns 1 when Node::Build fails (empty right range).
-__device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, int cnt, int depth, int maxDepth,
-                                            int me, int& nn, uint2* nodes) {
+// per dimension: the sorted key at rank (lane), the item at rank (lane), the rank of item (lane)
+struct RankTab {
+  int sx, sy, sz, px, py, pz, rx, ry, rz;
+};
+// LDS image of a RankTab (the forest kernel's helper waves prepare subtrees ahead of wave 0)
+struct RankSlot {
+  int s[3][64];
+  uint8_t p[3][64], r[3][64];
+};
+__device__ __forceinline__ void rank_store(RankSlot* S, const RankTab& t) {
+  const int l = lane_id();
+  S->s[0][l] = t.sx;
+  S->s[1][l] = t.sy;
+  S->s[2][l] = t.sz;
+  S->p[0][l] = (uint8_t)t.px;
+  S->p[1][l] = (uint8_t)t.py;
+  S->p[2][l] = (uint8_t)t.pz;
+  S->r[0][l] = (uint8_t)t.rx;
+  S->r[1][l] = (uint8_t)t.ry;
+  S->r[2][l] = (uint8_t)t.rz;
+}
+__device__ __forceinline__ RankTab rank_load(const RankSlot* S) {
+  const int l = lane_id();
+  RankTab t;
+  t.sx = S->s[0][l];
+  t.sy = S->s[1][l];
+  t.sz = S->s[2][l];
+  t.px = S->p[0][l];
+  t.py = S->p[1][l];
+  t.pz = S->p[2][l];
+  t.rx = S->r[0][l];
+  t.ry = S->r[1][l];
+  t.rz = S->r[2][l];
+  return t;
+}
+
+// the subtree's items sorted once per dimension (rank_subtree's preparation; it depends on the
+// items only, not on the draw stream)
+__device__ __forceinline__ RankTab rank_prep(int kx, int ky, int kz, int cnt) {
   const int lane = lane_id();
   auto sk64 = [&](int k) { return ((uint64_t)((uint32_t)k ^ 0x80000000u) << 32) | (uint32_t)lane; };
   uint64_t vx = sk64(lane < cnt ? kx : INT_MAX), vy = sk64(lane < cnt ? ky : INT_MAX),
@@ -253,6 +290,14 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
   const int rx = __builtin_amdgcn_ds_permute(px << 2, lane);
   const int ry = __builtin_amdgcn_ds_permute(py << 2, lane);
   const int rz = __builtin_amdgcn_ds_permute(pz << 2, lane);
+  return RankTab{sx, sy, sz, px, py, pz, rx, ry, rz};
+}
+
+__device__ __forceinline__ int rank_build(WaveRng& g, const RankTab& tb, int cnt, int depth, int maxDepth, int me,
+                                          int& nn, uint2* nodes) {
+  const int lane = lane_id();
+  const int sx = tb.sx, sy = tb.sy, sz = tb.sz, px = tb.px, py = tb.py, pz = tb.pz, rx = tb.rx, ry = tb.ry,
+            rz = tb.rz;
   // sorted values as floats (-0 folded): min / max / split compare in float
   const float fx = kfloat(sx), fy = kfloat(sy), fz = kfloat(sz);
   // a node is its set of items (bit l = item l); per node only the drawn dimension's
@@ -341,6 +386,11 @@ __device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, 
     if (!found) break;
   }
   return bad;
+}
+
+__device__ __forceinline__ int rank_subtree(WaveRng& g, int kx, int ky, int kz, int cnt, int depth, int maxDepth,
+                                            int me, int& nn, uint2* nodes) {
+  return rank_build(g, rank_prep(kx, ky, kz, cnt), cnt, depth, maxDepth, me, nn, nodes);
 }
 
 }  // namespace eao
