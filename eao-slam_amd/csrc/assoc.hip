@@ -29,7 +29,7 @@ namespace eao {
 // in-kernel phase stamps (workgroup 0 of k_np_pairs: slots 0-7 under EAO_NP_PROF;
 // workgroup (0,0) of k_iforest_tree: slots 0-7, 10), read through
 // eao_debug_iforest_stamps: development instrumentation, a few SALU ops
-__device__ unsigned long long g_if_stamp[24];
+__device__ unsigned long long g_if_stamp[32];
 #ifdef EAO_NP_PROF
 #define NP_STAMP(k)                                                                   \
   if (blockIdx.x == 0 && threadIdx.x == 0) {                                          \
@@ -1004,41 +1004,55 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       int* dst = (depth & 1) ? (int*)B0 : (int*)B1;
       IFP_T(bb0);
       const uint32_t dim = g.dim3();
+      IFP_T(bq1);
       int mn = INT_MAX, mx = INT_MIN;
       for (int i = first + lane; i <= last; i += 64) {
         const int v = src[dim * psi + i];
         mn = min(mn, v);
         mx = max(mx, v);
       }
+      IFP_T(bq2);
       wave_minmax_key(mn, mx);
+      IFP_T(bq3);
       if (mn == mx) {
         if (lane == 0) nodes[me] = make_uint2((uint32_t)cnt << 2, 0u);
         continue;
       }
       const float split = g.uniform_real(kfloat(mn), kfloat(mx));
       const int ks = fkey(split);
+      IFP_T(bq4);
+      IFP_ACC(24, bb0, bq1);
+      IFP_ACC(25, bq1, bq2);
+      IFP_ACC(26, bq2, bq3);
+      IFP_ACC(27, bq3, bq4);
+      IFP_ACC(28, 0ull, (unsigned long long)cnt);
       int nl = 0, nr = 0;
+      // branch-free but for the stores: the loads read a clamped index (lanes past the range
+      // reload the last item), both destinations are computed and selected
+      const uint64_t below = lanes_below();
+      int ii = min(first + lane, last);
+      int x = src[ii], y = src[psi + ii], z = src[2 * psi + ii];
       for (int c0 = first; c0 <= last; c0 += 64) {
         const int i = c0 + lane;
         const bool in = i <= last;
-        int x = 0, y = 0, z = 0;
-        if (in) {
-          x = src[i];
-          y = src[psi + i];
-          z = src[2 * psi + i];
-        }
+        // the next chunk's loads go out before this chunk's stores (software pipeline)
+        ii = min(i + 64, last);
+        const int x2 = src[ii], y2 = src[psi + ii], z2 = src[2 * psi + ii];
         const int v = dim == 0 ? x : (dim == 1 ? y : z);
         const bool lft = in && v < ks;
         const uint64_t ml = ballot(lft), mr = ballot(in && !lft);
+        const int dl = first + nl + popc64(ml & below), dr = last - (nr + popc64(mr & below));
+        const int dd = lft ? dl : dr;
         if (in) {
-          const int dd = lft ? first + nl + popc64(ml & lanes_below())
-                             : last - (nr + popc64(mr & lanes_below()));
           dst[dd] = x;
           dst[psi + dd] = y;
           dst[2 * psi + dd] = z;
         }
         nl += popc64(ml);
         nr += popc64(mr);
+        x = x2;
+        y = y2;
+        z = z2;
       }
       WAVE_FENCE();
       if (nl == 0) {  // middle == first
@@ -1067,6 +1081,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
       }
       sp += 2;
       IFP_T(bb1);
+      IFP_ACC(29, bq4, bb1);
       IFP_ACC(18, bb0, bb1);
       IFP_ACC(19, 0ull, 1ull);
     }
@@ -1656,9 +1671,9 @@ int eao_iforest_erase_threshold(float th, double* x0) {
   return EAO_OK;
 }
 
-int eao_debug_iforest_stamps(uint64_t* out12) {
-  if (!out12) return EAO_E_ARG;
-  EAO_HIP_CHECK(hipMemcpyFromSymbol(out12, HIP_SYMBOL(g_if_stamp), sizeof(uint64_t) * 24));
+int eao_debug_iforest_stamps(uint64_t* out32) {
+  if (!out32) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_if_stamp), sizeof(uint64_t) * 32));
   return EAO_OK;
 }
 

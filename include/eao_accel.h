@@ -390,8 +390,9 @@ int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_
 int eao_replay_shard_stats(eao_replay* r, double* out3);
 
 /* development instrumentation: s_memtime stamps of the last isolation-forest
-   tree launch (workgroup (0,0)): [0..7] phase boundaries, [10] node count. */
-int eao_debug_iforest_stamps(uint64_t* out12);
+   tree launch (workgroup (0,0)), 32 entries: [0..7] phase boundaries, [10] node count,
+   [12..29] sub-step cycle sums of EAO_IF_PROF builds. */
+int eao_debug_iforest_stamps(uint64_t* out32);
 /* wall-clock profile of a replay (us): [0] frame total, [1] local mapping,
    [2]/[3] iForest launches / time, [4]/[5] NP launches / time,
    [6]/[7] rect launches / time, [8] frames, [12..15] frame sections. */

@@ -25,7 +25,7 @@ for m, n in ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500), (30, 80
     t0 = time.perf_counter()
     for _ in range(20):
         a.np_batch(fs, os_)
-    st = np.zeros(24, np.uint64)
+    st = np.zeros(32, np.uint64)
     ea.lib().eao_debug_iforest_stamps(ea.P(st))
     ph = np.diff(st[:6].astype(np.int64))  # EAO_NP_PROF builds (make -C eao-slam_amd prof)
     print("m=%4d n=%5d 4 pairs: %.1f us/call | cycles count %d frame/pad %d sort %d counts %d sums %d"
