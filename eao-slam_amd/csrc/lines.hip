@@ -14,10 +14,12 @@
 //                   scan order (w outer, h inner, step 2), chunked count + block scan + write
 //   k_edge_draw     one wave per frame: the anchor walks (edge map as an LDS bitmap), the
 //                   kept chains assembled by the whole wave
-//   k_edlines       one wave per frame: least-squares fits and normal-equation sums as
-//                   wave reductions (integer data, exact in double), the extension walk
-//                   in wave-uniform control flow, LineValidation_'s per-pixel directions
-//                   in parallel, nfa, endpoints, ordering and the length filter
+//   k_edlines       8 waves per frame, a wave per chain (chains are independent): least-
+//                   squares fits and normal-equation sums as wave reductions (integer data,
+//                   exact in double), the extension walk in wave-uniform control flow,
+//                   LineValidation_'s per-pixel directions in parallel, nfa, endpoints,
+//                   ordering and the length filter; the chains' lines then placed in chain
+//                   order by a block scan of the per-chain counts
 // The walks are sequential per frame by the reference's definition (each anchor's chain
 // depends on the edge map left by all earlier ones); frames run concurrently.
 #include <hip/hip_runtime.h>
@@ -35,6 +37,7 @@ namespace eao {
 constexpr int LN_HORIZ = 0x8000;  // code bit: dirImg_ == Horizontal (|dx| < |dy|)
 constexpr int LN_UP = 1, LN_RIGHT = 2, LN_DOWN = 3, LN_LEFT = 4;
 constexpr int LN_GRAD_TH = 80, LN_ANCHOR_TH = 8, LN_MIN_LEN = 15, LN_TRY = 6, LN_SKIP = 2;
+constexpr int LN_WAVES = 8;  // k_edlines: waves per frame (chains are independent)
 constexpr double LN_FIT_ERR = 1.6;
 
 __device__ __forceinline__ int refl101(int p, int len) {
@@ -351,7 +354,7 @@ __device__ __forceinline__ uint32_t px_y(uint32_t p) { return p >> 16; }
 // (cv::gemm's double accumulation), as LeastSquaresLineFit_'s ATA / ATV
 __device__ void fit_block(const uint32_t* P, uint32_t s, uint32_t e, bool horiz, float* ata, float* atv) {
   double s00 = 0, s01 = 0, t0 = 0, t1 = 0;
-  for (uint32_t i = s + threadIdx.x; i < e; i += 64) {
+  for (uint32_t i = s + lane_id(); i < e; i += 64) {
     const uint32_t p = P[i];
     const double u = (double)(horiz ? px_x(p) : px_y(p)), v = (double)(horiz ? px_y(p) : px_x(p));
     s00 += u * u;
@@ -376,13 +379,16 @@ __device__ __forceinline__ void solve2(const float* ata, const float* atv, doubl
 }
 
 // one wave per frame: chains Q / S -> lines out [cap][6] (sx, sy, ex, ey, angle, length)
-__global__ __launch_bounds__(64) void k_edlines(const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi,
-                                                const int16_t* __restrict__ dyi, int W, int H,
-                                                const uint32_t* __restrict__ chains, const uint32_t* __restrict__ sid,
-                                                const int* __restrict__ nedge, int pcap, int ecap,
-                                                uint32_t* __restrict__ lscratch, float min_length,
-                                                float* __restrict__ out, int* __restrict__ nout, int cap) {
-  const int f = blockIdx.x, lane = threadIdx.x;
+__global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __restrict__ code,
+                                                          const int16_t* __restrict__ dxi,
+                                                          const int16_t* __restrict__ dyi, int W, int H,
+                                                          const uint32_t* __restrict__ chains,
+                                                          const uint32_t* __restrict__ sid,
+                                                          const int* __restrict__ nedge, int pcap, int ecap,
+                                                          uint32_t* __restrict__ lscratch,
+                                                          uint32_t* __restrict__ ccount, float min_length,
+                                                          float* __restrict__ out, int* __restrict__ nout, int cap) {
+  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint16_t* C = code + (long long)f * W * H;
   const int16_t* DX = dxi + (long long)f * W * H;
   const int16_t* DY = dyi + (long long)f * W * H;
@@ -390,18 +396,23 @@ __global__ __launch_bounds__(64) void k_edlines(const uint16_t* __restrict__ cod
   const uint32_t* S = sid + (long long)f * (ecap + 1);
   uint32_t* L = lscratch + (long long)f * 2 * pcap;
   float* O = out + (long long)f * cap * 6;
+  int* CNT = (int*)(ccount + (long long)f * pcap);  // lines kept per chain
   const int ne = nedge[f];
-  if (ne < 0) {
-    if (lane == 0) nout[f] = -1;
+  if (ne < 0) {  // the whole workgroup
+    if (threadIdx.x == 0) nout[f] = -1;
     return;
   }
   const double logNT = 2.0 * (log10((double)W) + log10((double)H));
   auto horiz_at = [&](uint32_t p) { return (C[px_y(p) * W + px_x(p)] & LN_HORIZ) != 0; };
-  uint32_t offL = 0;
-  int nl = 0;
-  for (int e = 0; e < ne; e++) {
+  // chains are independent: wave w takes chains w, w + nw, ...; a chain's line pixels use its
+  // own stretch of the scratch [S[e], S[e + 1]), and its kept lines are parked at the start
+  // of that stretch (record k at 6 k: below the next line's pixels, see the store) until the
+  // block places every chain's lines in chain order
+  for (int e = wave; e < ne; e += nw) {
     uint32_t s = S[e];
     const uint32_t end = S[e + 1];
+    uint32_t offL = s;
+    int nl = 0;
     double le2[2] = {0, 0};
     float ata[4], atv[2];
     while (end > s + LN_MIN_LEN) {
@@ -553,14 +564,16 @@ __global__ __launch_bounds__(64) void k_edlines(const uint16_t* __restrict__ cod
         if (d >= 0.25 * M_PI && d < 0.75 * M_PI && ddy < 0) change = true;
         if (((d >= 0.75 * M_PI && d < M_PI) || (d >= -M_PI && d < -0.75 * M_PI)) && ddx > 0) change = true;
         if (length > min_length) {
-          if (nl < cap && lane == 0) {
-            float* o = O + 6 * (long long)nl;
-            o[0] = change ? ep[2] : ep[0];
-            o[1] = change ? ep[3] : ep[1];
-            o[2] = change ? ep[0] : ep[2];
-            o[3] = change ? ep[1] : ep[3];
-            o[4] = direction;
-            o[5] = length;
+          // record nl of this chain at L[S[e] + 6 nl]: every earlier kept line of the chain
+          // spans >= LN_MIN_LEN - 3 > 6 pixels, so the record lies below this line's start
+          // (or, for nl = 0, over this line's own pixels, read above)
+          if (lane < 6) {
+            const float v = lane == 0 ? (change ? ep[2] : ep[0])
+                          : lane == 1 ? (change ? ep[3] : ep[1])
+                          : lane == 2 ? (change ? ep[0] : ep[2])
+                          : lane == 3 ? (change ? ep[1] : ep[3])
+                          : lane == 4 ? direction : length;
+            L[S[e] + 6 * nl + lane] = __float_as_uint(v);
           }
           nl++;
         }
@@ -568,8 +581,38 @@ __global__ __launch_bounds__(64) void k_edlines(const uint16_t* __restrict__ cod
         offL = lineStart;
       }
     }
+    if (lane == 0) CNT[e] = nl;
   }
-  if (lane == 0) nout[f] = nl;
+  __syncthreads();
+  // the chains' lines in chain order: a block scan of the per-chain counts; a chain's thread
+  // copies its records (lines past cap are counted, not stored, as the reference's nl)
+  __shared__ int wsum[16], carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < ne; c0 += blockDim.x) {
+    const int i = c0 + threadIdx.x;
+    const int v = i < ne ? CNT[i] : 0;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(x, o, 64);
+      if (lane >= o) x += u;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = carry;
+    for (int w = 0; w < wave; w++) before += wsum[w];
+    const int base = before + x - v;
+    if (i < ne) {
+      const uint32_t* R = L + S[i];
+      for (int j = 0; j < v; j++)
+        if (base + j < cap)
+          for (int q = 0; q < 6; q++) O[6 * (long long)(base + j) + q] = __uint_as_float(R[6 * j + q]);
+    }
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) carry = base + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) nout[f] = carry;
 }
 
 // ================================================================ host
@@ -710,8 +753,10 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   const size_t lds = (size_t)(W * H + 31) / 32 * 4;
   hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), lds, s, e.d_code, W, H, e.d_anch, e.d_nanch, e.acap,
                      e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
-  hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64), 0, s, e.d_code, e.d_dx, e.d_dy, W, H, e.d_chain, e.d_sid,
-                     e.d_nedge, e.pcap, e.ecap, e.d_lscr, min_length, d_lines, d_counts, cap);
+  // (the parts scratch P1 is dead after k_edge_draw: it holds the per-chain line counts)
+  hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
+                     e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_p1, min_length, d_lines, d_counts,
+                     cap);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
