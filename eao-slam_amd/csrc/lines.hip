@@ -159,8 +159,25 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
                      WalkState& st, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap) {
   const int lane = threadIdx.x;
   int idx = (int)(y * W + x);
+  const int lastIdx = W * H - 1;
+  // the pixel and its 8 neighbours in one round of loads (indices clamped to the plane: at a
+  // border the walk stops before reading a neighbour), issued as soon as the step's pixel is
+  // known (the end of the previous step), not two dependent rounds per step
+  int c;
+  uint8_t nUL, nU, nUR, nL, nR, nDL, nD, nDR;
+  auto load9 = [&](int i) {
+    c = C[i];
+    nUL = (uint8_t)C[max(i - W - 1, 0)];
+    nU = (uint8_t)C[max(i - W, 0)];
+    nUR = (uint8_t)C[max(i - W + 1, 0)];
+    nL = (uint8_t)C[max(i - 1, 0)];
+    nR = (uint8_t)C[min(i + 1, lastIdx)];
+    nDL = (uint8_t)C[min(i + W - 1, lastIdx)];
+    nD = (uint8_t)C[min(i + W, lastIdx)];
+    nDR = (uint8_t)C[min(i + W + 1, lastIdx)];
+  };
+  load9(idx);
   while (true) {
-    const int c = C[idx];
     if ((c & 0x7fff) == 0 || ((bits[idx >> 5] >> (idx & 31)) & 1u)) break;
     if (off >= cap) return false;
     if (lane == 0) {
@@ -175,7 +192,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
       st.lastY = y;
       if (lastDir == LN_RIGHT || should == LN_RIGHT) {
         if (x == (uint32_t)W - 1 || y == 0 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = (uint8_t)C[idx - W + 1], g2 = (uint8_t)C[idx + 1], g3 = (uint8_t)C[idx + W + 1];
+        const uint8_t g1 = nUR, g2 = nR, g3 = nDR;
         if (g1 >= g2 && g1 >= g3) {
           x++;
           y--;
@@ -188,7 +205,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
         lastDir = LN_RIGHT;
       } else if (lastDir == LN_LEFT || should == LN_LEFT) {
         if (x == 0 || y == 0 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = (uint8_t)C[idx - W - 1], g2 = (uint8_t)C[idx - 1], g3 = (uint8_t)C[idx + W - 1];
+        const uint8_t g1 = nUL, g2 = nL, g3 = nDL;
         if (g1 >= g2 && g1 >= g3) {
           x--;
           y--;
@@ -206,7 +223,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
       st.lastY = y;
       if (lastDir == LN_DOWN || should == LN_DOWN) {
         if (x == 0 || x == (uint32_t)W - 1 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = (uint8_t)C[idx + W + 1], g2 = (uint8_t)C[idx + W], g3 = (uint8_t)C[idx + W - 1];
+        const uint8_t g1 = nDR, g2 = nD, g3 = nDL;
         if (g1 >= g2 && g1 >= g3) {
           x++;
           y++;
@@ -219,7 +236,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
         lastDir = LN_DOWN;
       } else if (lastDir == LN_UP || should == LN_UP) {
         if (x == 0 || x == (uint32_t)W - 1 || y == 0) break;
-        const uint8_t g1 = (uint8_t)C[idx - W + 1], g2 = (uint8_t)C[idx - W], g3 = (uint8_t)C[idx - W - 1];
+        const uint8_t g1 = nUR, g2 = nU, g3 = nUL;
         if (g1 >= g2 && g1 >= g3) {
           x++;
           y--;
@@ -234,6 +251,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
     }
     idx = (int)(y * W + x);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    load9(idx);
   }
   return true;
 }
