@@ -10,8 +10,9 @@
 //                   (taps cvRound(k * 256), REFLECT_101, columns (s + 2^15) >> 16)
 //   k_line_grad     one thread per pixel: Sobel 3x3 (REFLECT_101) dx, dy; code =
 //                   thresholded |dx| + |dy| over 4 (cvRound) | Horizontal bit
-//   k_line_anchors  one workgroup per frame: the anchors in the reference's column-major
-//                   scan order (w outer, h inner, step 2), chunked count + block scan + write
+//   k_line_anchors  one workgroup per frame, a thread per candidate column: the anchors in the
+//                   reference's column-major scan order (w outer, h inner, step 2) from a
+//                   block scan of the per-column counts, rows walked with coalesced reads
 //   k_edge_draw     one wave per frame: the anchor walks (edge map as an LDS bitmap), the
 //                   kept chains assembled by the whole wave
 //   k_edlines       8 waves per frame, a wave per chain (chains are independent): least-
@@ -115,37 +116,51 @@ __device__ __forceinline__ bool is_anchor(const uint16_t* C, int W, int x, int y
   if (c & LN_HORIZ) return g >= (C[i - W] & 0x7fff) + LN_ANCHOR_TH && g >= (C[i + W] & 0x7fff) + LN_ANCHOR_TH;
   return g >= (C[i - 1] & 0x7fff) + LN_ANCHOR_TH && g >= (C[i + 1] & 0x7fff) + LN_ANCHOR_TH;
 }
-__global__ __launch_bounds__(256) void k_line_anchors(const uint16_t* __restrict__ code, int W, int H,
+// A thread per candidate column (x = 1 + 2 t, up to blockDim.x columns per pass): the anchors
+// of one column are consecutive in the reference's column-major order, so a block scan of
+// the per-column counts in thread order places every column; the column's rows are walked in
+// order, adjacent threads reading adjacent pixels (coalesced).
+__global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict__ code, int W, int H,
                                                       uint32_t* __restrict__ anchors, int acap,
                                                       int* __restrict__ nanchor) {
-  __shared__ int part[256];
-  const int f = blockIdx.x, t = threadIdx.x;
+  __shared__ int wsum[8], base;
+  const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint16_t* C = code + (long long)f * W * H;
-  const int nw = (W - 2 + 1) / 2, nh = (H - 2 + 1) / 2, n = nw * nh;
-  const int per = (n + 255) / 256, k0 = t * per, k1 = min(n, k0 + per);
-  int c = 0;
-  for (int k = k0; k < k1; k++) c += is_anchor(C, W, 1 + 2 * (k / nh), 1 + 2 * (k % nh)) ? 1 : 0;
-  part[t] = c;
-  __syncthreads();
-  if (t == 0) {
-    int run = 0;
-    for (int i = 0; i < 256; i++) {
-      const int v = part[i];
-      part[i] = run;
-      run += v;
-    }
-    nanchor[f] = run;
-  }
-  __syncthreads();
-  int o = part[t];
   uint32_t* A = anchors + (long long)f * acap;
-  for (int k = k0; k < k1; k++) {
-    const int x = 1 + 2 * (k / nh), y = 1 + 2 * (k % nh);
-    if (is_anchor(C, W, x, y)) {
-      if (o < acap) A[o] = (uint32_t)x | ((uint32_t)y << 16);
-      o++;
+  const int nw = (W - 2 + 1) / 2, nh = (H - 2 + 1) / 2;
+  if (t == 0) base = 0;
+  __syncthreads();
+  for (int x0 = 0; x0 < nw; x0 += blockDim.x) {
+    const int col = x0 + t, x = 1 + 2 * col;
+    int c = 0;
+    if (col < nw)
+      for (int j = 0; j < nh; j++) c += is_anchor(C, W, x, 1 + 2 * j) ? 1 : 0;
+    int v = c;  // inclusive scan over the block's columns
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o, 64);
+      if (lane >= o) v += u;
     }
+    if (lane == 63) wsum[wave] = v;
+    __syncthreads();
+    int o = base + v - c;
+    for (int w = 0; w < wave; w++) o += wsum[w];
+    if (col < nw)
+      for (int j = 0; j < nh; j++) {
+        const int y = 1 + 2 * j;
+        if (is_anchor(C, W, x, y)) {
+          if (o < acap) A[o] = (uint32_t)x | ((uint32_t)y << 16);
+          o++;
+        }
+      }
+    __syncthreads();
+    if (t == blockDim.x - 1) {
+      int tot = 0;
+      for (int w = 0; w < (int)(blockDim.x >> 6); w++) tot += wsum[w];
+      base += tot;
+    }
+    __syncthreads();
   }
+  if (t == 0) nanchor[f] = base;
 }
 
 // ---------------------------------------------------------------- edge drawing
@@ -767,7 +782,7 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
     hipLaunchKernelGGL(k_line_blur<4>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
   hipLaunchKernelGGL(k_line_grad, dim3((W * H + 255) / 256, nframes), dim3(256), 0, s, e.d_blur, W, H, e.d_dx,
                      e.d_dy, e.d_code);
-  hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(256), 0, s, e.d_code, W, H, e.d_anch, e.acap, e.d_nanch);
+  hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_code, W, H, e.d_anch, e.acap, e.d_nanch);
   const size_t lds = (size_t)(W * H + 31) / 32 * 4;
   hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), lds, s, e.d_code, W, H, e.d_anch, e.d_nanch, e.acap,
                      e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
