@@ -170,28 +170,54 @@ struct WalkState {
   uint32_t lastX, lastY;
 };
 // one walk from (x, y); appends packed (y << 16 | x) to P[off..]; false on overflow
+// The walk reads the gradient code through a 64 x 64 tile of it cached in LDS, reloaded
+// (centred on the step's pixel, rows clamped to the plane) when the pixel's 3 x 3
+// neighbourhood leaves it: one round of coalesced loads per ~30 steps instead of one
+// global round trip per step.
+constexpr int LN_TS = 64;
+struct CodeTile {
+  uint16_t* t;  // LDS [LN_TS][LN_TS]
+  int x0, y0;   // origin in the plane (x0 = -LN_TS: empty)
+};
+__device__ __forceinline__ void tile_cover(const uint16_t* __restrict__ C, int W, int H, CodeTile& T, int x, int y) {
+  const int ax = max(x - 1, 0), bx = min(x + 1, W - 1), ay = max(y - 1, 0), by = min(y + 1, H - 1);
+  if (ax >= T.x0 && bx < T.x0 + LN_TS && ay >= T.y0 && by < T.y0 + LN_TS) return;  // uniform
+  T.x0 = min(max(x - LN_TS / 2, 0), max(W - LN_TS, 0));
+  T.y0 = min(max(y - LN_TS / 2, 0), max(H - LN_TS, 0));
+  const int lane = lane_id(), cx = min(T.x0 + lane, W - 1);
+  for (int r0 = 0; r0 < LN_TS; r0 += 16) {  // 16 row loads in flight per lane
+    uint16_t v[16];
+#pragma unroll
+    for (int r = 0; r < 16; r++) v[r] = C[min(T.y0 + r0 + r, H - 1) * W + cx];
+#pragma unroll
+    for (int r = 0; r < 16; r++) T.t[(r0 + r) * LN_TS + lane] = v[r];
+  }
+}
+__device__ __forceinline__ int tile_at(const CodeTile& T, int x, int y) {  // inside the plane
+  return T.t[(y - T.y0) * LN_TS + (x - T.x0)];
+}
 __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bits, uint32_t x, uint32_t y, int lastDir,
-                     WalkState& st, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap) {
+                     WalkState& st, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap, CodeTile& T) {
   const int lane = threadIdx.x;
   int idx = (int)(y * W + x);
-  const int lastIdx = W * H - 1;
-  // the pixel and its 8 neighbours in one round of loads (indices clamped to the plane: at a
-  // border the walk stops before reading a neighbour), issued as soon as the step's pixel is
-  // known (the end of the previous step), not two dependent rounds per step
+  // the pixel and its 8 neighbours from the tile (neighbour coordinates clamped to the plane:
+  // at a border the walk stops before using a neighbour)
   int c;
   uint8_t nUL, nU, nUR, nL, nR, nDL, nD, nDR;
-  auto load9 = [&](int i) {
-    c = C[i];
-    nUL = (uint8_t)C[max(i - W - 1, 0)];
-    nU = (uint8_t)C[max(i - W, 0)];
-    nUR = (uint8_t)C[max(i - W + 1, 0)];
-    nL = (uint8_t)C[max(i - 1, 0)];
-    nR = (uint8_t)C[min(i + 1, lastIdx)];
-    nDL = (uint8_t)C[min(i + W - 1, lastIdx)];
-    nD = (uint8_t)C[min(i + W, lastIdx)];
-    nDR = (uint8_t)C[min(i + W + 1, lastIdx)];
+  auto load9 = [&](int, int xx, int yy) {
+    tile_cover(C, W, H, T, xx, yy);
+    const int xl = max(xx - 1, 0), xr = min(xx + 1, W - 1), yu = max(yy - 1, 0), yd = min(yy + 1, H - 1);
+    c = tile_at(T, xx, yy);
+    nUL = (uint8_t)tile_at(T, xl, yu);
+    nU = (uint8_t)tile_at(T, xx, yu);
+    nUR = (uint8_t)tile_at(T, xr, yu);
+    nL = (uint8_t)tile_at(T, xl, yy);
+    nR = (uint8_t)tile_at(T, xr, yy);
+    nDL = (uint8_t)tile_at(T, xl, yd);
+    nD = (uint8_t)tile_at(T, xx, yd);
+    nDR = (uint8_t)tile_at(T, xr, yd);
   };
-  load9(idx);
+  load9(idx, (int)x, (int)y);
   while (true) {
     if ((c & 0x7fff) == 0 || ((bits[idx >> 5] >> (idx & 31)) & 1u)) break;
     if (off >= cap) return false;
@@ -266,7 +292,7 @@ __device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bit
     }
     idx = (int)(y * W + x);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    load9(idx);
+    load9(idx, (int)x, (int)y);
   }
   return true;
 }
@@ -282,6 +308,7 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ c
   const int f = blockIdx.x, lane = threadIdx.x;
   const uint16_t* C = code + (long long)f * W * H;
   const int nb = (W * H + 31) / 32;
+  CodeTile T{(uint16_t*)(bits + ((nb + 3) & ~3)), -LN_TS, -LN_TS};
   for (int i = lane; i < nb; i += 64) bits[i] = 0;
   __syncthreads();
   const uint32_t* A = anchors + (long long)f * acap;
@@ -304,13 +331,13 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ c
     }
     const bool horiz = (C[idx] & LN_HORIZ) != 0;
     uint32_t o1 = 0, o2 = 0;
-    if (!walk(C, W, H, bits, x, y, horiz ? LN_RIGHT : LN_DOWN, st, P1, o1, (uint32_t)pcap)) {
+    if (!walk(C, W, H, bits, x, y, horiz ? LN_RIGHT : LN_DOWN, st, P1, o1, (uint32_t)pcap, T)) {
       fail = true;
       break;
     }
     if (lane == 0) atomicAnd(&bits[idx >> 5], ~(1u << (idx & 31)));  // the second part walks the anchor again
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (!walk(C, W, H, bits, x, y, horiz ? LN_LEFT : LN_UP, st, P2, o2, (uint32_t)pcap)) {
+    if (!walk(C, W, H, bits, x, y, horiz ? LN_LEFT : LN_UP, st, P2, o2, (uint32_t)pcap, T)) {
       fail = true;
       break;
     }
@@ -783,7 +810,7 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   hipLaunchKernelGGL(k_line_grad, dim3((W * H + 255) / 256, nframes), dim3(256), 0, s, e.d_blur, W, H, e.d_dx,
                      e.d_dy, e.d_code);
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_code, W, H, e.d_anch, e.acap, e.d_nanch);
-  const size_t lds = (size_t)(W * H + 31) / 32 * 4;
+  const size_t lds = (size_t)(((W * H + 31) / 32 + 3) & ~3) * 4 + sizeof(uint16_t) * LN_TS * LN_TS;
   hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), lds, s, e.d_code, W, H, e.d_anch, e.d_nanch, e.acap,
                      e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
   // (the parts scratch P1 is dead after k_edge_draw: it holds the per-chain line counts)
