@@ -78,6 +78,28 @@ def test_lines_batch_device(frames):
         assert hc[t] == len(o) and np.array_equal(ho[t, :hc[t]], o), t
 
 
+def test_lines_batch_device_small_cap(frames):
+    """Lines past the caller's capacity are counted, not stored (the reference's nl keeps
+    counting): with k_edlines's chains on separate waves, the block scan that places each
+    chain's lines in chain order must stop storing at cap and still report the full count."""
+    import torch
+    F = len(frames)
+    dev = torch.device("cuda", 0)
+    L = ea.Lines(max_batch=F)
+    d = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    cap = 5
+    out = torch.full((F * cap + 4, 6), -7.0, dtype=torch.float32, device=dev)  # frame t: rows [t cap, t cap + cap)
+    cnt = torch.zeros(F, dtype=torch.int32, device=dev)
+    L.detect_batch_device(d.data_ptr(), F, 640, 50.0, out.data_ptr(), cnt.data_ptr(), cap)
+    torch.cuda.synchronize()
+    ho, hc = out.cpu().numpy(), cnt.cpu().numpy()
+    assert (ho[F * cap:] == -7.0).all()  # nothing written past the last frame's cap
+    for t in range(F):
+        o = orc.edlines(frames[t])
+        assert hc[t] == len(o) and len(o) > cap, t  # the frames hold more lines than cap
+        assert np.array_equal(ho[t * cap:(t + 1) * cap], o[:cap]), t
+
+
 def color_frames(frames):
     """BGR frames whose COLOR_BGR2GRAY keeps the edges (B = 255 - g, G = R = g) while the RGB
     code would give another gray: the conversion order is exercised."""
