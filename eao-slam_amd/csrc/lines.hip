@@ -734,8 +734,10 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
     set_error("no usable gfx950 device (the engine has no CPU fallback)");
     return EAO_E_NODEVICE;
   }
-  if ((size_t)(width * height + 31) / 32 * 4 > 160 * 1024) {
-    set_error("eao_lines_create: the per-frame edge bitmap exceeds the LDS");
+  // the same dynamic LDS k_edge_draw is launched with: the edge bitmap (16-byte padded) +
+  // the gradient-code tile
+  if ((size_t)(((width * height + 31) / 32 + 3) & ~3) * 4 + sizeof(uint16_t) * LN_TS * LN_TS > 160 * 1024) {
+    set_error("eao_lines_create: the per-frame edge bitmap and code tile exceed the LDS");
     return EAO_E_CAPACITY;
   }
   eao_lines* L = new eao_lines();

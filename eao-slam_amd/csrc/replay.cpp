@@ -603,6 +603,8 @@ class ReplayEngine {
       const size_t c = std::max(in_bytes, 2 * cap_in);
       if (h_in) (void)hipHostFree(h_in);
       if (d_in) (void)hipFree(d_in);
+      h_in = d_in = nullptr;
+      cap_in = 0;
       EAO_HIP_CHECK(hipHostMalloc((void**)&h_in, c, 0));
       EAO_HIP_CHECK(hipMalloc((void**)&d_in, c));
       cap_in = c;
@@ -611,6 +613,8 @@ class ReplayEngine {
       const size_t c = std::max(out_bytes, 2 * cap_out);
       if (h_out) (void)hipHostFree(h_out);
       if (d_out) (void)hipFree(d_out);
+      h_out = d_out = nullptr;
+      cap_out = 0;
       EAO_HIP_CHECK(hipHostMalloc((void**)&h_out, c, 0));
       EAO_HIP_CHECK(hipMalloc((void**)&d_out, c));
       cap_out = c;
@@ -670,9 +674,14 @@ class ReplayEngine {
 
   // Tracking::AssociateObjAndLines (Tracking.cc:2472-2527) for the detections whose
   // lines SampleObjYaw can read (yaw-sampled classes); the frame's staged line set
-  void associate_lines(const std::vector<Det*>& o2) {
+  // `taken`: the consumed line set is kept there (a discarded look-ahead puts it back)
+  void associate_lines(const std::vector<Det*>& o2, std::vector<float>* taken = nullptr, bool* took = nullptr) {
     const std::vector<float>* fl = staged_next < staged_lines.size() ? &staged_lines[staged_next] : nullptr;
     if (fl) staged_next++;
+    if (fl && taken) {
+      *taken = *fl;
+      *took = true;
+    }
     std::vector<double> all, in, ang;
     if (fl && yaw_on()) {
       all.assign(fl->begin(), fl->end());
@@ -1079,19 +1088,22 @@ class ReplayEngine {
       b.launched = nl > 0;
       if (sharded()) {
         // the record every rank all-gathers for this batch: per owned object an outlier
-        // bit mask, then the owned speculative NP stats; one padded size for all ranks
+        // bit mask, then (from the next 16-byte boundary) the owned speculative NP stats;
+        // one padded size for all ranks
         b.xmb.assign(sworld, 0);
         b.xnsr.assign(sworld, 0);
         for (int c = 0; c < nb; c++) b.xmb[owner(b.objs[c])] += (b.objs[c]->pts.size() + 7) / 8;
         for (size_t q = 0; q < b.sp_obj.size(); q++) b.xnsr[owner(b.objs[b.sp_obj[q]])]++;
         b.xbytes = 0;
-        for (int r = 0; r < sworld; r++) b.xbytes = std::max(b.xbytes, b.xmb[r] + sizeof(eao_np_stats) * b.xnsr[r]);
+        for (int r = 0; r < sworld; r++) b.xbytes = std::max(b.xbytes, al16(b.xmb[r]) + sizeof(eao_np_stats) * b.xnsr[r]);
         b.xbytes = std::max<size_t>(al16(b.xbytes), 16);
         if (xdev() && b.xbytes > b.cap_x) {
           if (b.d_x) (void)hipFree(b.d_x);
           b.d_x = nullptr;
-          b.cap_x = std::max(b.xbytes, 2 * b.cap_x);
-          EAO_HIP_CHECK(hipMalloc((void**)&b.d_x, b.cap_x));
+          const size_t c = std::max(b.xbytes, 2 * b.cap_x);
+          b.cap_x = 0;  // raised only once the allocation exists
+          EAO_HIP_CHECK(hipMalloc((void**)&b.d_x, c));
+          b.cap_x = c;
         }
         if (xdev() && !b.launched) {  // nothing owned: an empty record, ready behind b.ev
           hipStream_t st = if_stream[k % kIfStreams];
@@ -1123,16 +1135,22 @@ class ReplayEngine {
       if (in_bytes > b.cap_in) {
         if (b.h_in) (void)hipHostFree(b.h_in);
         if (b.d_in) (void)hipFree(b.d_in);
-        b.cap_in = std::max(in_bytes, 2 * b.cap_in);
-        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_in, b.cap_in, 0));
-        EAO_HIP_CHECK(hipMalloc((void**)&b.d_in, b.cap_in));
+        b.h_in = b.d_in = nullptr;
+        const size_t c = std::max(in_bytes, 2 * b.cap_in);
+        b.cap_in = 0;  // raised only once both allocations exist
+        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_in, c, 0));
+        EAO_HIP_CHECK(hipMalloc((void**)&b.d_in, c));
+        b.cap_in = c;
       }
       if (out_bytes > b.cap_out) {
         if (b.h_out) (void)hipHostFree(b.h_out);
         if (b.d_out) (void)hipFree(b.d_out);
-        b.cap_out = std::max(out_bytes, 2 * b.cap_out);
-        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_out, b.cap_out, 0));
-        EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, b.cap_out));
+        b.h_out = b.d_out = nullptr;
+        const size_t c = std::max(out_bytes, 2 * b.cap_out);
+        b.cap_out = 0;
+        EAO_HIP_CHECK(hipHostMalloc((void**)&b.h_out, c, 0));
+        EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, c));
+        b.cap_out = c;
       }
       int* meta = (int*)b.h_in;
       float* pts = (float*)(b.h_in + o_pts);
@@ -1204,7 +1222,7 @@ class ReplayEngine {
         const int* spm = (const int*)(b.d_in + o_spm);
         const float* dfp = (const float*)(b.d_in + o_fp);
         // device-form exchange: the stats go straight into this rank's record
-        eao_np_stats* sp_dst = xdev() ? (eao_np_stats*)(b.d_x + b.xmb[srank]) : (eao_np_stats*)(b.h_out + b.sp_out);
+        eao_np_stats* sp_dst = xdev() ? (eao_np_stats*)(b.d_x + al16(b.xmb[srank])) : (eao_np_stats*)(b.h_out + b.sp_out);
         rc = A->np_batch(ns, dfp, b.d_in + o_fval, spm, spm + ns, (const float*)(b.d_in + o_pts), b.d_in + o_oval,
                          spm + 2 * ns, spm + 3 * ns, sp_dst, st, max_olen, (const double* const*)(b.d_in + o_osp),
                          (const float*)(b.d_in + o_th));
@@ -1245,6 +1263,7 @@ class ReplayEngine {
           if (sc[k] > th) xsend[w + k / 8] |= (unsigned char)(1u << (k % 8));
         w += (n + 7) / 8;
       }
+      w = al16(w);  // the stats start 16-byte aligned (the device form stores them as structs)
       size_t j = 0;
       for (size_t q = 0; q < b.sp_obj.size(); q++)
         if (mine(b.objs[b.sp_obj[q]])) {  // launch order = sp_* order restricted to this rank
@@ -1266,7 +1285,7 @@ class ReplayEngine {
     }
     for (size_t q = 0; q < b.sp_obj.size(); q++) {
       const int r = owner(b.objs[b.sp_obj[q]]);
-      std::memcpy(&b.spst[q], b.xres.data() + stride * r + b.xmb[r] + sb * cs[r]++, sb);
+      std::memcpy(&b.spst[q], b.xres.data() + stride * r + al16(b.xmb[r]) + sb * cs[r]++, sb);
     }
     b.xdone = true;
     return EAO_OK;
@@ -2277,7 +2296,21 @@ class ReplayEngine {
     size_t k = 0;
     std::vector<MapPt*> tr;
     std::vector<Det*> o2, kept;
+    bool took_lines = false;  // step 3 consumed a staged line set (kept in `lines`)
+    std::vector<float> lines;
   } prep, prep_now;
+  // drop a look-ahead that will not be consumed (a failed stream call, or a frame call that
+  // does not continue the stream): its detections stay unreferenced, a line set it consumed
+  // goes back to the front of the staged sets, and the frame runs in order when it comes
+  void discard_lookahead() {
+    if (prep.active && prep.took_lines) {
+      staged_lines.insert(staged_lines.begin() + (ptrdiff_t)staged_next, std::move(prep.lines));
+    }
+    prep.active = prep.ok = prep.took_lines = false;
+    prep.o2.clear();
+    prep.kept.clear();
+    la_set = false;
+  }
   // fill a wait on `ev` with the next frame's steps 1-6
   void idle_work(hipEvent_t ev) {
     if (!prep.active) {
@@ -2304,6 +2337,7 @@ class ReplayEngine {
     s.phase = 0;
     s.k = 0;
     s.ok = false;
+    s.took_lines = false;
     s.o2.clear();
     s.kept.clear();
   }
@@ -2361,7 +2395,7 @@ class ReplayEngine {
         return false;
       }
       case 2:
-        associate_lines(o2);  // STEP 3 AssociateObjAndLines, Tracking.cc:1286
+        associate_lines(o2, &s == &prep ? &s.lines : nullptr, &s.took_lines);  // STEP 3, Tracking.cc:1286
         s.phase = 3;
         s.k = 0;
         prof[12] += now_us() - tA;
@@ -2448,11 +2482,8 @@ class ReplayEngine {
     np_cache.clear();
     std::vector<Det*> o2, kept;
     over.assign(objs.size(), 0);
+    if (prep.active && (prep.in.fid != fid || prep.in.nb != nb)) discard_lookahead();  // not the stream's next
     if (prep.active) {  // steps 1-6 (partly) ran ahead, while the previous frame waited on the GPU
-      if (prep.in.fid != fid || prep.in.nb != nb) {
-        set_error("replay: look-ahead frame does not match the replayed frame");
-        return EAO_E_STATE;
-      }
       while (!prep.ok) prep.ok = prep_step(prep);
       o2.swap(prep.o2);
       kept.swap(prep.kept);
@@ -2928,11 +2959,9 @@ int eao_replay_create(eao_assoc* a, const char* flag, int img_w, int img_h, cons
   return EAO_OK;
 }
 
+// The caller joins every other thread that uses the handle first (eao_accel.h): a lock
+// taken here could not keep a late caller out of a freed handle.
 int eao_replay_destroy(eao_replay* r) {
-  if (r) {
-    r->mu.lock();  // no call of another thread is inside the handle
-    r->mu.unlock();
-  }
   delete r;
   return EAO_OK;
 }
@@ -2958,6 +2987,13 @@ int eao_replay_run(eao_replay* r, int n_frames, const int32_t* frame_ids, const 
                                 keyframe, nullptr, nullptr, nullptr, nullptr, det_out);
 }
 
+static int replay_stream(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                         const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                         const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                         const uint8_t* mp_bad, const uint8_t* keyframe, const int32_t* n_upd,
+                         const int32_t* upd_ids, const float* upd_pos, const uint8_t* upd_bad,
+                         int32_t* det_out);
+
 int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
                            const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
                            const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
@@ -2973,6 +3009,20 @@ int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids
       if (n_upd[t] && !upd_ids) return EAO_E_ARG;
   }
   EAO_REPLAY_LOCK(r);
+  ReplayEngine& E = r->r;
+  E.discard_lookahead();
+  const int rc = replay_stream(r, n_frames, frame_ids, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv, mp_bad,
+                               keyframe, n_upd, upd_ids, upd_pos, upd_bad, det_out);
+  if (rc < 0) E.discard_lookahead();  // an aborted stream leaves no look-ahead behind
+  return rc;
+}
+
+static int replay_stream(eao_replay* r, int n_frames, const int32_t* frame_ids, const float* Tcw,
+                         const int32_t* n_boxes, const int32_t* boxes, const int32_t* n_pts,
+                         const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                         const uint8_t* mp_bad, const uint8_t* keyframe, const int32_t* n_upd,
+                         const int32_t* upd_ids, const float* upd_pos, const uint8_t* upd_bad,
+                         int32_t* det_out) {
   size_t ob = 0, op = 0, ou = 0;
   ReplayEngine& E = r->r;
   for (int t = 0; t < n_frames; t++) {

@@ -355,7 +355,10 @@ int eao_replay_run_updates(eao_replay* r, int n_frames, const int32_t* frame_ids
 /* Threading: every eao_replay_* call holds the handle's lock, so the Tracking thread
    (eao_replay_frame) and the LocalMapping thread (eao_replay_update_points,
    eao_replay_local_mapping) may share one handle; the replayed order is the order in which the
-   calls take the lock. */
+   calls take the lock. eao_replay_destroy takes no lock: the caller joins every other thread
+   that uses the handle before destroying it.
+   A stream call that fails part-way returns < 0 and drops the next frame's look-ahead state;
+   a later eao_replay_frame / eao_replay_run continues from the last completed frame. */
 int eao_replay_num_objects(eao_replay* r);
 /* ints[8]: id, class, bad, #frames, #points, last add, #co-association votes, #co-views;
    floats[20]: center[3], sigma[3], sigma of frame centers[3], cuboid lenth/width/height,
@@ -397,7 +400,7 @@ int eao_debug_iforest_stamps(uint64_t* out32);
    [2]/[3] iForest launches / time, [4]/[5] NP launches / time,
    [6]/[7] rect launches / time, [8] frames, [12..15] frame sections. */
 int eao_replay_profile(eao_replay* r, double* out24);
-/* The same wall-clock profile, up to n (<= 32) slots; returns the number copied. */
+/* The same wall-clock profile, up to n (<= 56) slots; returns the number copied. */
 int eao_replay_profile_n(eao_replay* r, double* out, int n);
 
 /* ---- frame input stage (src/Tracking.cc:340-554) ---- */
