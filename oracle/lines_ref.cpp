@@ -29,8 +29,16 @@ namespace {
 
 constexpr int kHorizontal = 255, kVertical = 0;  // binary_descriptor.cpp:58-59
 constexpr int kUp = 1, kRight = 2, kDown = 3, kLeft = 4;
-constexpr int kGradTh = 80, kAnchorTh = 8, kScan = 2, kMinLineLen = 15;  // EDLineDetector(), :1518-1524
-constexpr double kFitErrTh = 1.6;
+// EDLineDetector's knobs; the defaults are EDLineDetector() (:1518-1524), the detector the EAO
+// Frame runs. Other values serve only the pinning of this restatement against the Edge Drawing
+// library's own outputs (tests/test_oracle_ed_pin.py).
+struct EdParams {
+  int grad_th = 80, anchor_th = 8, scan = 2, min_line_len = 15;
+  double fit_err_th = 1.6;
+  int gdiv = 4;  // gImg_ = thresholded |dx| + |dy| divided by this (EdgeDrawing, :1650-1662)
+  int validate = 1;  // 0: keep every fitted segment (bValidate_ = false, :2590-2600)
+};
+const EdParams kDefaultParams{};
 constexpr int kTryTime = 6, kSkip = 2;  // :64-65
 
 inline int reflect101(int p, int len) {
@@ -117,7 +125,7 @@ struct Maps {
   std::vector<uint8_t> dir;        // dirImg_: 255 = Horizontal
 };
 
-void compute_maps(const uint8_t* gray, int w, int h, Maps& M) {
+void compute_maps(const uint8_t* gray, int w, int h, Maps& M, const EdParams& P = kDefaultParams) {
   M.w = w;
   M.h = h;
   const size_t n = (size_t)w * h;
@@ -154,8 +162,9 @@ void compute_maps(const uint8_t* gray, int w, int h, Maps& M) {
       M.dx[i] = (int16_t)gx;
       M.dy[i] = (int16_t)gy;
       const int ax = gx < 0 ? -gx : gx, ay = gy < 0 ? -gy : gy, s = ax + ay;
-      const int t = s > kGradTh + 1 ? s : 0;
-      M.g[i] = (int16_t)round_half_even((double)((float)t * 0.25f));
+      const int t = s > P.grad_th + 1 ? s : 0;
+      M.g[i] = P.gdiv == 4 ? (int16_t)round_half_even((double)((float)t * 0.25f))
+                           : (int16_t)std::min(t / P.gdiv, 32767);
       M.dir[i] = ax < ay ? kHorizontal : kVertical;
     }
 }
@@ -165,22 +174,23 @@ struct Chains {
 };
 
 // EdgeDrawing, binary_descriptor.cpp:1583-2381
-int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
+int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out,
+                 const EdParams& P = kDefaultParams) {
   const int W = M.w, H = M.h;
   const uint32_t pixelNum = (uint32_t)W * H;
   const uint32_t edgePixelArraySize = pixelNum / 5, maxNumOfEdge = edgePixelArraySize / 20;
   const int16_t* pg = M.g.data();
   const uint8_t* pd = M.dir.data();
   std::vector<uint32_t> ax, ay;
-  for (int w = 1; w < W - 1; w += kScan)
-    for (int h = 1; h < H - 1; h += kScan) {
+  for (int w = 1; w < W - 1; w += P.scan)
+    for (int h = 1; h < H - 1; h += P.scan) {
       const int i = h * W + w;
       if (pd[i] == kHorizontal) {
-        if (pg[i] >= pg[i - W] + kAnchorTh && pg[i] >= pg[i + W] + kAnchorTh) {
+        if (pg[i] >= pg[i - W] + P.anchor_th && pg[i] >= pg[i + W] + P.anchor_th) {
           ax.push_back(w);
           ay.push_back(h);
         }
-      } else if (pg[i] >= pg[i - 1] + kAnchorTh && pg[i] >= pg[i + 1] + kAnchorTh) {
+      } else if (pg[i] >= pg[i - 1] + P.anchor_th && pg[i] >= pg[i + 1] + P.anchor_th) {
         ax.push_back(w);
         ay.push_back(h);
       }
@@ -196,6 +206,9 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
   uint32_t offF = 0, offS = 0, offPS = 0;
   uint32_t lastX = 0, lastY = 0;  // persist across walks and anchors, as in the reference
   // one walk from (x, y) with initial direction dir0, pixels appended to (X, Y, off)
+  // the walk reads gImg_ as unsigned char (gValue1..3, :1643, 1746-2000): /4 values above 255
+  // wrap; the unscaled (gdiv 1) pinning variant compares the full values, as ED does
+  auto gv = [&](int i) { return P.gdiv == 4 ? (int)(uint8_t)pg[i] : (int)pg[i]; };
   auto walk = [&](uint32_t x, uint32_t y, int lastDir, std::vector<uint32_t>& X, std::vector<uint32_t>& Y,
                   uint32_t& off) -> bool {
     int idx = (int)(y * W + x);
@@ -211,7 +224,7 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
         lastY = y;
         if (lastDir == kRight || should == kRight) {
           if (x == (uint32_t)W - 1 || y == 0 || y == (uint32_t)H - 1) break;
-          const uint8_t g1 = (uint8_t)pg[idx - W + 1], g2 = (uint8_t)pg[idx + 1], g3 = (uint8_t)pg[idx + W + 1];
+          const int g1 = gv(idx - W + 1), g2 = gv(idx + 1), g3 = gv(idx + W + 1);
           if (g1 >= g2 && g1 >= g3) {
             x++;
             y--;
@@ -224,7 +237,7 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
           lastDir = kRight;
         } else if (lastDir == kLeft || should == kLeft) {
           if (x == 0 || y == 0 || y == (uint32_t)H - 1) break;
-          const uint8_t g1 = (uint8_t)pg[idx - W - 1], g2 = (uint8_t)pg[idx - 1], g3 = (uint8_t)pg[idx + W - 1];
+          const int g1 = gv(idx - W - 1), g2 = gv(idx - 1), g3 = gv(idx + W - 1);
           if (g1 >= g2 && g1 >= g3) {
             x--;
             y--;
@@ -242,7 +255,7 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
         lastY = y;
         if (lastDir == kDown || should == kDown) {
           if (x == 0 || x == (uint32_t)W - 1 || y == (uint32_t)H - 1) break;
-          const uint8_t g1 = (uint8_t)pg[idx + W + 1], g2 = (uint8_t)pg[idx + W], g3 = (uint8_t)pg[idx + W - 1];
+          const int g1 = gv(idx + W + 1), g2 = gv(idx + W), g3 = gv(idx + W - 1);
           if (g1 >= g2 && g1 >= g3) {
             x++;
             y++;
@@ -255,7 +268,7 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
           lastDir = kDown;
         } else if (lastDir == kUp || should == kUp) {
           if (x == 0 || x == (uint32_t)W - 1 || y == 0) break;
-          const uint8_t g1 = (uint8_t)pg[idx - W + 1], g2 = (uint8_t)pg[idx - W], g3 = (uint8_t)pg[idx - W - 1];
+          const int g1 = gv(idx - W + 1), g2 = gv(idx - W), g3 = gv(idx - W - 1);
           if (g1 >= g2 && g1 >= g3) {
             x++;
             y--;
@@ -284,7 +297,7 @@ int edge_drawing(const Maps& M, Chains& E, std::vector<uint32_t>* anchors_out) {
     sS[offPS] = offS;
     if (!walk(x, y, horiz ? kLeft : kUp, sX, sY, offS)) return -1;
     const int lenF = (int)(offF - fS[offPS]), lenS = (int)(offS - sS[offPS]);
-    if (lenF + lenS < kMinLineLen + 1) {  // short edge, dropped (its pixels stay marked)
+    if (lenF + lenS < P.min_line_len + 1) {  // short edge, dropped (its pixels stay marked)
       offF = fS[offPS];
       offS = sS[offPS];
     } else {
@@ -348,7 +361,7 @@ struct Line {
 };
 
 // EDline(image, lines), binary_descriptor.cpp:2383-2630, with LineValidation_ (:2793-2874)
-int edline(const Maps& M, const Chains& E, std::vector<Line>& out) {
+int edline(const Maps& M, const Chains& E, std::vector<Line>& out, const EdParams& P = kDefaultParams) {
   const int W = M.w, H = M.h;
   out.clear();
   const uint32_t nEdges = (uint32_t)E.sid.size() - 1;
@@ -364,24 +377,24 @@ int edline(const Maps& M, const Chains& E, std::vector<Line>& out) {
     const uint32_t end = E.sid[e + 1];
     double lineEq[2] = {0, 0};
     Fit F{};
-    while (end > s + kMinLineLen) {
+    while (end > s + P.min_line_len) {
       double fitErr = 0;
-      while (end > s + kMinLineLen) {  // an initial segment of minLineLen_ pixels
+      while (end > s + P.min_line_len) {  // an initial segment of minLineLen_ pixels
         const bool horiz = dirAt(ex[s], ey[s]) == kHorizontal;
         const uint32_t* u = horiz ? ex : ey;
         const uint32_t* v = horiz ? ey : ex;
-        fit_block(u, v, s, s + kMinLineLen, F.ata, F.atv);
+        fit_block(u, v, s, s + P.min_line_len, F.ata, F.atv);
         solve(F, lineEq);
         double err = 0;
-        for (uint32_t i = s; i < s + kMinLineLen; i++) {
+        for (uint32_t i = s; i < s + P.min_line_len; i++) {
           const double c = (double)v[i] - (double)u[i] * lineEq[0] - lineEq[1];
           err += c * c;
         }
         fitErr = std::sqrt(err);
-        if (fitErr <= kFitErrTh) break;
+        if (fitErr <= P.fit_err_th) break;
         s += kSkip;
       }
-      if (fitErr > kFitErrTh) break;
+      if (fitErr > P.fit_err_th) break;
       lineStart = offL;
       const bool horiz = dirAt(ex[s], ey[s]) == kHorizontal;
       double coef1 = 0;
@@ -391,7 +404,7 @@ int edline(const Maps& M, const Chains& E, std::vector<Line>& out) {
         tryTimes++;
         if (first) {
           first = false;
-          for (int i = 0; i < kMinLineLen; i++) {
+          for (int i = 0; i < P.min_line_len; i++) {
             lx[offL] = ex[s];
             ly[offL++] = ey[s++];
           }
@@ -411,7 +424,7 @@ int edline(const Maps& M, const Chains& E, std::vector<Line>& out) {
                                  : std::fabs(ex[s] - lineEq[0] * ey[s] - lineEq[1]) * coef1;
           lx[offL] = ex[s];
           ly[offL++] = ey[s++];
-          if (d > kFitErrTh) {
+          if (d > P.fit_err_th) {
             if (++outliers > 3) break;
           } else {
             outliers = 0;
@@ -456,7 +469,9 @@ int edline(const Maps& M, const Chains& E, std::vector<Line>& out) {
           if (std::fabs(std::fabs(direction) - M_PI * 0.5) < 0.15)
             if (std::fabs(le[2]) < 10 || std::fabs(W - std::fabs(le[2])) < 10) reject = true;
         }
-        if (!reject) {
+        if (!P.validate) {
+          ok = true;
+        } else if (!reject) {
           int k = 0;
           for (int i = 0; i < n; i++) {
             const double dd = std::fabs(direction - pdir[i]);
@@ -518,6 +533,47 @@ int orc_edge_chains(const uint8_t* gray, int w, int h, uint32_t* xy, int cap_px,
   }
   for (int i = 0; i < std::min(*n_edges + 1, cap_edges + 1); i++) sid[i] = E.sid[i];
   return 0;
+}
+
+// The restatement under other knobs, for its pinning against the Edge Drawing library's own
+// outputs (Thirdparty/EDTest/ED-EdgeMap.pgm, EDLinesTest/LineSegments.txt):
+// ip = {gradient threshold, anchor threshold, scan interval, min line length, gdiv, validate}.
+static EdParams ed_params(const int* ip, double fit_err) {
+  EdParams P;
+  P.grad_th = ip[0];
+  P.anchor_th = ip[1];
+  P.scan = ip[2];
+  P.min_line_len = ip[3];
+  P.gdiv = ip[4];
+  P.fit_err_th = fit_err;
+  P.validate = ip[5];
+  return P;
+}
+// the kept edge chains' pixels as a 255 / 0 map (EDTest/main.cpp:65-72 draws ED's segments so)
+int orc_ed_edge_map(const uint8_t* gray, int w, int h, const int* ip, double fit_err, uint8_t* map, int* n_chains) {
+  const EdParams P = ed_params(ip, fit_err);
+  Maps M;
+  compute_maps(gray, w, h, M, P);
+  Chains E;
+  if (edge_drawing(M, E, nullptr, P) != 1) return -1;
+  std::memset(map, 0, (size_t)w * h);
+  for (size_t i = 0; i < E.x.size(); i++) map[(size_t)E.y[i] * w + E.x[i]] = 255;
+  *n_chains = (int)E.sid.size() - 1;
+  return 0;
+}
+// EDline's segments (endpoints x1, y1, x2, y2 as fitted, no length filter or reordering)
+int orc_ed_segments(const uint8_t* gray, int w, int h, const int* ip, double fit_err, float* out, int cap,
+                    int* n_out) {
+  const EdParams P = ed_params(ip, fit_err);
+  Maps M;
+  compute_maps(gray, w, h, M, P);
+  Chains E;
+  if (edge_drawing(M, E, nullptr, P) != 1) return -1;
+  std::vector<Line> L;
+  edline(M, E, L, P);
+  *n_out = (int)L.size();
+  for (int i = 0; i < std::min(*n_out, cap); i++) std::memcpy(out + 4 * (size_t)i, L[i].ep, sizeof(float) * 4);
+  return *n_out > cap ? -2 : 0;
 }
 
 // detect_raw_lines (octave 0) + filter_lines(length > min_length) + keylines_to_mat:

@@ -179,6 +179,12 @@ int orc_line_maps(const uint8_t* gray, int w, int h, uint8_t* blur, int16_t* dx,
                   uint8_t* dir);
 int orc_edge_chains(const uint8_t* gray, int w, int h, uint32_t* xy, int cap_px, uint32_t* sid, int cap_edges,
                     int* n_px, int* n_edges);
+/* the restatement under other EDLineDetector knobs (ip = grad th, anchor th, scan, min line
+   length, gradient divisor, validate): kept chains as a 255/0 map, and EDline's raw segments -- only for
+   pinning against the Edge Drawing library's outputs (tests/test_oracle_ed_pin.py) */
+int orc_ed_edge_map(const uint8_t* gray, int w, int h, const int* ip, double fit_err, uint8_t* map, int* n_chains);
+int orc_ed_segments(const uint8_t* gray, int w, int h, const int* ip, double fit_err, float* out, int cap,
+                    int* n_out);
 int orc_edlines(const uint8_t* gray, int w, int h, float min_length, float* out, int cap, int* n_out);
 /* the same on the colour frame BinaryDescriptor::detectImpl receives: cn = 3 / 4 bytes per pixel
    converted with COLOR_BGR2GRAY first (binary_descriptor.cpp:490-495); cn = 1 is gray */

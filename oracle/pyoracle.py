@@ -363,6 +363,30 @@ def edge_chains(gray, cap_px=1 << 18, cap_edges=1 << 14):
     return xy[:npx.value].copy(), sid[:ne.value + 1].copy()
 
 
+def ed_edge_map(gray, grad_th, anchor_th, scan, min_line_len, gdiv, fit_err=1.6):
+    """The restatement's kept EdgeDrawing chains as a 255/0 map under other knobs (pinning only)."""
+    g8 = np.ascontiguousarray(gray, np.uint8)
+    h, w = g8.shape
+    ip = np.array([grad_th, anchor_th, scan, min_line_len, gdiv, 1], np.int32)
+    m = np.zeros((h, w), np.uint8)
+    n = ctypes.c_int()
+    rc = lib().orc_ed_edge_map(P(g8), w, h, P(ip), ctypes.c_double(fit_err), P(m), ctypes.byref(n))
+    assert rc == 0, rc
+    return m, n.value
+
+
+def ed_segments(gray, grad_th, anchor_th, scan, min_line_len, gdiv, fit_err=1.6, validate=1, cap=1 << 14):
+    """EDline's raw segments [n][4] (x1, y1, x2, y2) under other knobs (pinning only)."""
+    g8 = np.ascontiguousarray(gray, np.uint8)
+    h, w = g8.shape
+    ip = np.array([grad_th, anchor_th, scan, min_line_len, gdiv, validate], np.int32)
+    out = np.zeros((cap, 4), np.float32)
+    n = ctypes.c_int()
+    rc = lib().orc_ed_segments(P(g8), w, h, P(ip), ctypes.c_double(fit_err), P(out), cap, ctypes.byref(n))
+    assert rc == 0, rc
+    return out[:n.value].copy()
+
+
 def edlines(gray, min_length=50.0, cap=4096):
     """detect_raw_lines + filter_lines: [n][6] float32 (sx, sy, ex, ey, angle, length)."""
     g8 = np.ascontiguousarray(gray, np.uint8)
