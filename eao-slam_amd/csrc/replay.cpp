@@ -3083,7 +3083,7 @@ int eao_replay_held_points(eao_replay* r, int32_t* ids, int cap) {
   EAO_REPLAY_LOCK(r);
   std::vector<int32_t> v;
   const int n = r->r.held_points(v);
-  std::memcpy(ids, v.data(), sizeof(int32_t) * (size_t)std::min(n, cap));
+  if (n > 0 && cap > 0) std::memcpy(ids, v.data(), sizeof(int32_t) * (size_t)std::min(n, cap));
   return n;
 }
 

@@ -25,7 +25,8 @@ NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
 def harness():
     orc.lib()
     subprocess.check_call(["make", "-s", "-C", NATIVE])
-    H = ctypes.CDLL(os.path.join(NATIVE, "_build", "libreplay_host.so"))
+    # EAO_HARNESS_SO: a sanitizer build of the same harness (tests/test_replay_sanitizers.py)
+    H = ctypes.CDLL(os.environ.get("EAO_HARNESS_SO") or os.path.join(NATIVE, "_build", "libreplay_host.so"))
     H.harness_assoc_create.restype = ctypes.c_void_p
     return H
 
