@@ -203,6 +203,8 @@ def main():
     ap.add_argument("--cpu-mt-frames", type=int, default=256, help="extract+match all-cores CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
+    ap.add_argument("--shard", action="store_true",
+                    help="config c: the object-sharded exchange path also at world 1 (one-rank RCCL communicator)")
     ap.add_argument("--poll", action="store_true", help="A/B: poll the extraction stream while the association runs")
     args = ap.parse_args()
     if args.cpu_frames is None:
@@ -896,29 +898,38 @@ def run_config_c(args, rank, world, gpu):
     packed = ea.Replay.pack(frames)
     assoc = ea.Assoc(device=gpu)
 
+    # --shard: the sharded path at any world size, world 1 included (a one-rank RCCL
+    # communicator: every record is written, gathered and read back through the exchange)
+    sharded = world > 1 or args.shard
+
     def make():
         rp = ea.Replay(assoc, "EAO")
-        if world > 1:
-            if exch == "gloo":
+        if sharded:
+            if exch == "gloo" and world > 1:
                 rp.shard(rank, world, allgather=eao_dist.allgather_bytes_gloo())
             else:
-                uid = eao_dist.broadcast_bytes(ea.rccl_unique_id() if rank == 0 else None)
+                uid = ea.rccl_unique_id() if world == 1 else \
+                    eao_dist.broadcast_bytes(ea.rccl_unique_id() if rank == 0 else None)
                 rp.shard(rank, world, unique_id=uid)
         return rp
 
     for _ in range(args.warmup):
-        make().run(packed)
-    elapsed, det, rp = 0.0, None, None
+        w = make()
+        w.run(packed)
+        w.close()
+    # one replay per timed step, set up (communicators included) before the timed region
+    reps = [make() for _ in range(args.steps)]
+    det = None
     eao_dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        if rp is not None:
-            rp.close()
-        rp = make()
+    for rp in reps:
         det = rp.run(packed)
     eao_dist.barrier()
     elapsed = eao_dist.max_over_ranks(time.perf_counter() - t0)
-    st = rp.shard_stats() if world > 1 else {"exchanges": 0, "bytes_per_rank": 0.0, "exchange_us": 0.0}
+    rp = reps[-1]
+    for r in reps[:-1]:
+        r.close()
+    st = rp.shard_stats() if sharded else {"exchanges": 0, "bytes_per_rank": 0.0, "exchange_us": 0.0}
     prof = np.zeros(24, np.float64)
     ea.lib().eao_replay_profile(rp.h, ea.P(prof))
     result = None
@@ -933,7 +944,8 @@ def run_config_c(args, rank, world, gpu):
                     "16 classes, %.1f boxes and %.0f map points per frame)"
                     % (np.mean(nb), np.mean([len(f["ids"]) for f in frames])),
             "config": {"workload": "Config C association (BASELINE configs[3]), %d frames" % nfr,
-                       "parallelism": "objects%d" % world, "exchange": exch if world > 1 else None},
+                       "parallelism": "objects%d" % world,
+                       "exchange": (exch if world > 1 else "rccl") if sharded else None},
             "exchange": {"count": st["exchanges"], "bytes_per_rank_per_exchange":
                          st["bytes_per_rank"] / max(1, st["exchanges"]),
                          "us_per_exchange": st["exchange_us"] / max(1, st["exchanges"]),

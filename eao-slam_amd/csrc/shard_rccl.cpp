@@ -34,11 +34,13 @@ struct RcclExchanger : Exchanger {
   int dev = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // the gathered records' copy-back
   unsigned char *h_recv = nullptr, *d_recv = nullptr;
   size_t cap = 0;  // bytes per rank
 
   ~RcclExchanger() override {
     if (stream) (void)hipStreamSynchronize(stream);
+    if (done) (void)hipEventDestroy(done);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
     if (h_recv) (void)hipHostFree(h_recv);
@@ -80,7 +82,16 @@ struct RcclExchanger : Exchanger {
     if (ready) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready, 0));
     EAO_NCCL_CHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
     EAO_HIP_CHECK(hipMemcpyAsync(h_recv, d_recv, bytes * world, hipMemcpyDeviceToHost, stream));
-    EAO_HIP_CHECK(hipStreamSynchronize(stream));
+    // the replay thread spins on the copy's event, as on its own launches: a blocking
+    // synchronisation may park the thread and pay a wake-up per exchange
+    if (!done) EAO_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    EAO_HIP_CHECK(hipEventRecord(done, stream));
+    for (;;) {
+      const hipError_t r = hipEventQuery(done);
+      if (r == hipSuccess) break;
+      if (r != hipErrorNotReady) EAO_HIP_CHECK(r);
+      __builtin_ia32_pause();
+    }
     *out = h_recv;
     return EAO_OK;
   }

@@ -64,6 +64,46 @@ def test_config_c_unsharded_matches_oracle():
     _check(outs, g.objects(), _oracle(frames))
 
 
+def _digest(frames):
+    import zlib
+    h = 0
+    for f in frames:
+        for k in ("T", "boxes", "ids", "pos", "uv", "bad"):
+            h = zlib.crc32(np.ascontiguousarray(f[k]).tobytes(), h)
+        h = zlib.crc32(bytes([1 if f["kf"] else 0]), h)
+    return h
+
+
+@pytest.mark.parametrize("mode", ["unsharded", "rccl_world1"])
+def test_config_c_200_frames_at_scale(mode):
+    """BASELINE configs[3] at the config's scale: the first 200 frames of the 1000-frame
+    stream against the committed oracle outputs (tools/make_config_c_golden.py) -- ids of every
+    detection, object point sets (CRC of the sorted ids), integer fields identical, statistics
+    within 1e-5 -- with the objects' clouds reaching the config's size (>= 1500 points; the
+    forests and NP tests run on clouds of up to ~1800 points). Also through the sharded exchange
+    at world 1 (one-rank RCCL communicator: records written, gathered and read in device memory)."""
+    import zlib
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "replay_config_c_200.npz"))
+    frames = synth.assoc_stream_config_c(int(g["n_stream"]))[:int(g["n_frames"])]
+    assert _digest(frames) == int(g["digest"]), "generated inputs differ from the fixture's"
+    rp = ea.Replay(ea.Assoc(), "EAO")
+    if mode == "rccl_world1":
+        rp.shard(0, 1, unique_id=ea.rccl_unique_id())
+    det = rp.run(ea.Replay.pack(frames))
+    bad = np.nonzero((det != g["det_out"]).any(1))[0]
+    assert not len(bad), "first differing detection %d: %s vs %s" % (bad[0], det[bad[0]], g["det_out"][bad[0]])
+    ints, fl, pts = rp.objects()
+    assert np.array_equal(ints, g["obj_ints"])
+    assert np.allclose(fl, g["obj_floats"], rtol=1e-5, atol=1e-5, equal_nan=True)
+    crc = np.array([zlib.crc32(np.sort(p).astype(np.int32).tobytes()) for p in pts], np.uint32)
+    assert np.array_equal(np.array([len(p) for p in pts]), g["obj_pts_len"]) and np.array_equal(crc, g["obj_pts_crc"])
+    assert ints[:, 4].max() >= 1500
+    if mode == "rccl_world1":
+        st = rp.shard_stats()
+        assert st["exchanges"] > 200
+    rp.close()
+
+
 def _worker(rank, world, port, mode, q):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

@@ -34,7 +34,8 @@ def stream_digest(frames):
     h = 0
     for f in frames:
         for k in ("T", "boxes", "ids", "pos", "uv", "bad", "lines"):
-            h = zlib.crc32(np.ascontiguousarray(f[k]).tobytes(), h)
+            if k in f:  # (streams without line sets: Config C)
+                h = zlib.crc32(np.ascontiguousarray(f[k]).tobytes(), h)
         h = zlib.crc32(bytes([1 if f["kf"] else 0]), h)
     return np.uint32(h)
 
