@@ -326,6 +326,65 @@ bool pos_key(const float* p, PosKey& k) {
   return true;
 }
 
+// min / max of v[0..n) exactly as the sequential std::min / std::max scan from (mn, mx) would
+// leave them: eight independent lanes (the scan's select keeps NaNs out, as the scan does), and
+// the sequential scan again when a result is zero (the one case where the lanes' tie order could
+// pick the other sign of zero)
+void minmax_scan(const float* v, size_t n, float& mn, float& mx) {
+  float a[8], b[8];
+  for (int k = 0; k < 8; k++) {
+    a[k] = mn;
+    b[k] = mx;
+  }
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8)
+    for (int k = 0; k < 8; k++) {
+      a[k] = v[i + k] < a[k] ? v[i + k] : a[k];
+      b[k] = b[k] < v[i + k] ? v[i + k] : b[k];
+    }
+  float m0 = a[0], m1 = b[0];
+  for (int k = 1; k < 8; k++) {
+    m0 = a[k] < m0 ? a[k] : m0;
+    m1 = m1 < b[k] ? b[k] : m1;
+  }
+  for (; i < n; i++) {
+    m0 = v[i] < m0 ? v[i] : m0;
+    m1 = m1 < v[i] ? v[i] : m1;
+  }
+  if (m0 == 0.0f || m1 == 0.0f) {
+    float s0 = mn, s1 = mx;
+    for (size_t j = 0; j < n; j++) {
+      s0 = std::min(s0, v[j]);
+      s1 = std::max(s1, v[j]);
+    }
+    m0 = s0;
+    m1 = s1;
+  }
+  mn = m0;
+  mx = m1;
+}
+
+// ComputeMeanAndStandard's cuboid pass: every position through the inverse object pose
+// (Eigen's q * v + t in double), rounded to float. Gathered input, one point per iteration with no
+// dependence between points: vectorised (AVX2 clone where the host has it), bit-identical per point
+__attribute__((target_clones("avx2", "default")))
+void se3_batch(const double qi[4], const double ti[3], size_t n, const float* __restrict__ px,
+               const float* __restrict__ py, const float* __restrict__ pz, float* __restrict__ ox,
+               float* __restrict__ oy, float* __restrict__ oz) {
+  const double x = qi[1], y = qi[2], z = qi[3], w = qi[0], t0 = ti[0], t1 = ti[1], t2 = ti[2];
+  for (size_t i = 0; i < n; i++) {
+    const double v0 = px[i], v1 = py[i], v2 = pz[i];
+    double u0 = y * v2 - z * v1, u1 = z * v0 - x * v2, u2 = x * v1 - y * v0;
+    u0 += u0;
+    u1 += u1;
+    u2 += u2;
+    const double c0 = y * u2 - z * u1, c1 = z * u0 - x * u2, c2 = x * u1 - y * u0;
+    ox[i] = (float)((v0 + w * u0 + c0) + t0);
+    oy[i] = (float)((v1 + w * u1 + c1) + t1);
+    oz[i] = (float)((v2 + w * u2 + c2) + t2);
+  }
+}
+
 }  // namespace
 
 class ReplayEngine {
@@ -850,14 +909,29 @@ class ReplayEngine {
   }
 
   // Object_Map::ComputeMeanAndStandard, Object.cc:967-1198 (min/max replace the sorts)
+  // ComputeMeanAndStandard scratch: the object's positions gathered once per call (SoA), and
+  // their images under the inverse cuboid pose
+  std::vector<float> ms_p[3], ms_t[3];
   void mean_std(Obj* o) {
     double T0 = now_us();
     for (int a = 0; a < 3; a++) o->sum[a] = 0;
+    const size_t n0 = o->pts.size();
+    for (int a = 0; a < 3; a++)
+      if (ms_p[a].size() < n0) {
+        ms_p[a].resize(n0 + n0 / 2 + 64);
+        ms_t[a].resize(n0 + n0 / 2 + 64);
+      }
+    float* px = ms_p[0].data();
+    float* py = ms_p[1].data();
+    float* pz = ms_p[2].data();
     size_t w = 0;
-    for (size_t i = 0; i < o->pts.size(); i++) {
+    for (size_t i = 0; i < n0; i++) {
       MapPt* p = o->pts[i];
       if (p->bad) continue;
       for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
+      px[w] = p->pos[0];
+      py[w] = p->pos[1];
+      pz[w] = p->pos[2];
       o->pts[w++] = p;
     }
     o->pts.resize(w);
@@ -866,12 +940,15 @@ class ReplayEngine {
     for (int a = 0; a < 3; a++) o->center[a] = o->sum[a] * sc + 0.0f;
     float s2[3] = {0, 0, 0};
     float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (MapPt* p : o->pts)
-      for (int a = 0; a < 3; a++) {
-        s2[a] += (p->pos[a] - o->center[a]) * (p->pos[a] - o->center[a]);
-        mn[a] = std::min(mn[a], p->pos[a]);
-        mx[a] = std::max(mx[a], p->pos[a]);
+    {
+      const float c0 = o->center[0], c1 = o->center[1], c2 = o->center[2];
+      for (size_t i = 0; i < n; i++) {  // the three sums in point order (float, as the reference)
+        s2[0] += (px[i] - c0) * (px[i] - c0);
+        s2[1] += (py[i] - c1) * (py[i] - c1);
+        s2[2] += (pz[i] - c2) * (pz[i] - c2);
       }
+      for (int a = 0; a < 3; a++) minmax_scan(ms_p[a].data(), n, mn[a], mx[a]);
+    }
     for (int a = 0; a < 3; a++) o->sd[a] = std::sqrt(s2[a] / (float)n);
     double T1 = now_us(); prof[32] += T1 - T0;
     if (n == 0) return;
@@ -899,16 +976,8 @@ class ReplayEngine {
     double qi[4], ti[3];  // pose inverse, identical for every point
     double T2 = now_us(); prof[33] += T2 - T1; prof[36] += n;
     se3_inverse(o->q, o->t, qi, ti);
-    for (MapPt* p : o->pts) {
-      const double v[3] = {p->pos[0], p->pos[1], p->pos[2]};
-      double r[3];
-      se3_apply(qi, ti, v, r);
-      for (int a = 0; a < 3; a++) {
-        const float f = (float)r[a];
-        omn[a] = std::min(omn[a], f);
-        omx[a] = std::max(omx[a], f);
-      }
-    }
+    se3_batch(qi, ti, n, px, py, pz, ms_t[0].data(), ms_t[1].data(), ms_t[2].data());
+    for (int a = 0; a < 3; a++) minmax_scan(ms_t[a].data(), n, omn[a], omx[a]);
     double T3 = now_us(); prof[34] += T3 - T2;
     for (int k = 0; k < 8; k++) {
       const double v[3] = {cx[k] ? omx[0] : omn[0], cy[k] ? omx[1] : omn[1], cz[k] ? omx[2] : omn[2]};
