@@ -367,7 +367,13 @@ void minmax_scan(const float* v, size_t n, float& mn, float& mx) {
 // ComputeMeanAndStandard's cuboid pass: every position through the inverse object pose
 // (Eigen's q * v + t in double), rounded to float. Gathered input, one point per iteration with no
 // dependence between points: vectorised (AVX2 clone where the host has it), bit-identical per point
-__attribute__((target_clones("avx2", "default")))
+// (host code: the device compilation pass of this file sees no clones)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define EAO_HOST_CLONES
+#else
+#define EAO_HOST_CLONES __attribute__((target_clones("avx2", "default")))
+#endif
+EAO_HOST_CLONES
 void se3_batch(const double qi[4], const double ti[3], size_t n, const float* __restrict__ px,
                const float* __restrict__ py, const float* __restrict__ pz, float* __restrict__ ox,
                float* __restrict__ oy, float* __restrict__ oz) {
