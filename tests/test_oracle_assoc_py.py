@@ -133,3 +133,37 @@ def test_full_slice_with_localmapping_merges():
 @pytest.mark.parametrize("flag", ["None", "NP", "IoU", "NA"])
 def test_other_flags_short_stream(flag):
     _run_both(flag, synth.assoc_stream(16, lines=True))
+
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("name", ["replay_fr3_demo_eao", "replay_fr3_full"])
+def test_independent_restatement_over_whole_streams(name):
+    """The pure-Python restatement's outputs over the WHOLE streams (all 405 EAO frames, all 2582
+    Full frames; tools/make_assoc_py_golden.py, minutes of pure Python, hence fixtures) equal the
+    C++ oracle's fixtures that the engine's GPU tests compare against (tests/test_gpu_fr3.py):
+    every detection's outcome and object id, the object records and their point sets."""
+    c = np.load(os.path.join(GOLDEN, name + ".npz"))
+    p = np.load(os.path.join(GOLDEN, name + "_py.npz"))
+    assert int(c["digest"]) == int(p["digest"]) and c["flag"] == p["flag"]
+    bad = np.nonzero((c["det_out"] != p["det_out"]).any(1))[0]
+    assert not len(bad), "first differing detection %d" % (bad[0] if len(bad) else -1)
+    assert np.array_equal(c["obj_ints"], p["obj_ints"])
+    assert np.allclose(c["obj_floats"], p["obj_floats"], rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert np.array_equal(c["obj_pts_len"], p["obj_pts_len"]) and np.array_equal(c["obj_pts_crc"], p["obj_pts_crc"])
+
+
+def test_cpp_oracle_reproduces_demo_fixture():
+    """The C++ oracle as built now still writes the committed demo fixture (so the fixture the
+    engine and the Python restatement are held to is the oracle's current output)."""
+    import zlib
+    g = np.load(os.path.join(GOLDEN, "replay_fr3_demo_eao.npz"))
+    frames = synth.assoc_stream_fr3_real()
+    o = orc.Replay("EAO")
+    det = np.concatenate([o.step(i + 1, f) for i, f in enumerate(frames)])
+    assert np.array_equal(det, g["det_out"])
+    ints, fl, pts = o.objects()
+    assert np.array_equal(ints, g["obj_ints"]) and np.allclose(fl, g["obj_floats"], rtol=1e-5, atol=1e-5, equal_nan=True)
+    crc = np.array([zlib.crc32(np.sort(q).astype(np.int32).tobytes()) for q in pts], np.uint32)
+    assert np.array_equal(crc, g["obj_pts_crc"])
