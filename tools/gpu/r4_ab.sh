@@ -7,6 +7,10 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_assoc.py -x -v --timeout 12
 EAO_FAST_ROWS=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r4_ab_orb_rows.log 2>&1 &&
 timeout -k 10 200 python -u tools/orb_stages.py --reps 10 > gpurun_out/r4_ab_orb_stages_base.log 2>&1 &&
 EAO_FAST_ROWS=1 timeout -k 10 200 python -u tools/orb_stages.py --reps 10 > gpurun_out/r4_ab_orb_stages_rows.log 2>&1 &&
+EAO_FAST_XCD=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4_ab_orb_xcd.log 2>&1 &&
+EAO_FAST_XCD=1 timeout -k 10 200 python -u tools/orb_stages.py --reps 10 > gpurun_out/r4_ab_orb_stages_xcd.log 2>&1 &&
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r4_ab_pmc_fetch_base -o run -- python3 tools/pmc_extract.py > gpurun_out/r4_ab_pmc_fetch_base.log 2>&1 &&
+EAO_FAST_XCD=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r4_ab_pmc_fetch_xcd -o run -- python3 tools/pmc_extract.py > gpurun_out/r4_ab_pmc_fetch_xcd.log 2>&1 &&
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4_ab_replay.log 2>&1 &&
 timeout -k 10 300 bash tools/ab_probe.sh eao-slam_amd/lib/ab/base/libeao_accel.so eao-slam_amd/lib/libeao_accel.so > gpurun_out/r4_ab_probe.log 2>&1 &&
 timeout -k 10 120 python -u tools/micro/if_probe.py > gpurun_out/r4_ab_ifprobe_new.log 2>&1 &&
