@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <chrono>
 #include <cstdio>
@@ -52,6 +53,48 @@ static const bool g_lookahead = [] {
   const char* v = getenv("EAO_NO_LOOKAHEAD");
   return !(v && v[0] == '1');
 }();
+// Outputs written straight into pinned host memory (frame-start stats / rects, forest scores,
+// speculative NP stats) are pre-filled with patterns no kernel writes (a NaN payload the
+// hardware never produces; a byte no flag takes), and the host waits until every word it needs
+// has been overwritten -- or until the launch's event completes, whichever comes first: the
+// data lands a few microseconds before the command processor's end-of-kernel signal.
+// EAO_SENTINEL_WAIT=0 waits on the events only (A/B switch).
+static hipError_t spin_event_plain(hipEvent_t e) {
+  for (;;) {
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    __builtin_ia32_pause();
+  }
+}
+static const bool g_sentinel = [] {
+  const char* v = getenv("EAO_SENTINEL_WAIT");
+  return !(v && v[0] == '0');
+}();
+static constexpr uint32_t kSent32 = 0x7FBADBADu;          // int / float words
+static constexpr uint64_t kSent64 = 0x7FF4DEADBEEFCAFEull;  // double words
+static constexpr uint8_t kSent8 = 0xAB;                    // flag bytes
+static inline uint32_t ld32(const void* p) { return __atomic_load_n((const uint32_t*)p, __ATOMIC_RELAXED); }
+static inline uint64_t ld64(const void* p) { return __atomic_load_n((const uint64_t*)p, __ATOMIC_RELAXED); }
+static inline uint8_t ld8(const void* p) { return __atomic_load_n((const uint8_t*)p, __ATOMIC_RELAXED); }
+static void fill32(void* p, size_t words) {
+  uint32_t* q = (uint32_t*)p;
+  for (size_t i = 0; i < words; i++) q[i] = kSent32;
+}
+static void fill64(void* p, size_t words) {
+  uint64_t* q = (uint64_t*)p;
+  for (size_t i = 0; i < words; i++) q[i] = kSent64;
+}
+// wait for `ready()` (sentinels overwritten) or the event, whichever comes first
+template <class Ready>
+static hipError_t spin_ready(hipEvent_t e, Ready&& ready) {
+  if (!g_sentinel || !g_spin_wait) return g_spin_wait ? spin_event_plain(e) : hipEventSynchronize(e);
+  for (;;) {
+    if (ready()) return hipSuccess;
+    const hipError_t r = hipEventQuery(e);
+    if (r != hipErrorNotReady) return r;
+    __builtin_ia32_pause();
+  }
+}
 static hipError_t spin_event(hipEvent_t e) {
   if (!g_spin_wait) return hipEventSynchronize(e);
   for (;;) {
@@ -1227,6 +1270,10 @@ class ReplayEngine {
         EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, c));
         b.cap_out = c;
       }
+      if (g_sentinel && !sharded()) {  // scores and speculative stats pre-filled (spin_ready)
+        fill64(b.h_out, (size_t)np);
+        fill32(b.h_out + b.sp_out, (size_t)ns * (sizeof(eao_np_stats) / 4));
+      }
       int* meta = (int*)b.h_in;
       float* pts = (float*)(b.h_in + o_pts);
       for (int j = 0; j < nl; j++) {
@@ -1381,8 +1428,32 @@ class ReplayEngine {
       Tick tw(&prof[39]);
       Tick tw2(&prof[42 + phase]);
       tr(6, o->slot, phase);
-      idle_work(b.ev);
-      EAO_HIP_CHECK(spin_event(b.ev));
+      // this object's scores and its speculative NP stats written (the batch's other objects
+      // and kernels may still run) -- or the batch's event
+      int c0 = 0;
+      while (b.objs[c0] != o) c0++;
+      const size_t s0 = (size_t)b.loff[c0], s1 = s0 + o->pts.size();
+      size_t si = s0, qi = 0;
+      const size_t nsw = sizeof(eao_np_stats) / 4;
+      auto ready = [&]() -> bool {
+        for (; si < s1; si++)
+          if (ld64(b.h_out + 8 * si) == kSent64) return false;
+        for (; qi < b.sp_obj.size(); qi++) {
+          if (b.sp_obj[qi] != c0) continue;
+          const unsigned char* st = b.h_out + b.sp_out + sizeof(eao_np_stats) * qi;  // unsharded: launch order
+          for (size_t w = 0; w < nsw; w++)
+            if (ld32(st + 4 * w) == kSent32) return false;
+        }
+        return true;
+      };
+      if (sharded()) {  // outputs come from the exchange; no sentinels there
+        idle_work(b.ev);
+        EAO_HIP_CHECK(spin_event(b.ev));
+      } else {
+        idle_work(b.ev, ready);
+        EAO_HIP_CHECK(spin_ready(b.ev, ready));
+        std::atomic_thread_fence(std::memory_order_acquire);
+      }
       tr(7, o->slot, phase);
     }
     double tpost = now_us();
@@ -1597,6 +1668,10 @@ class ReplayEngine {
     // outputs: pinned host memory (read after the spin), or -- sharded, device-form
     // exchange -- this rank's record in device memory (d_out), all-gathered by the caller
     unsigned char* ob = rn_dev ? d_out : h_out;
+    if (!rn_dev && g_sentinel) {  // outputs pre-filled with patterns the kernel never writes
+      fill32(h_out, (size_t)npairs * (sizeof(eao_np_stats) / 4) + 4 * (size_t)nb);
+      std::memset(h_out + o_ok, kSent8, (size_t)nb);
+    }
     int* rmeta = (int*)h_in;
     int* pmeta = (int*)(h_in + o_pm);
     float* pts = (float*)(h_in + o_pts);
@@ -1672,8 +1747,26 @@ class ReplayEngine {
     if (rn_dev) return EAO_OK;
     {
       Tick tw(&prof[41]);
-      idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
-      EAO_HIP_CHECK(spin_event(gpu0_ev));
+      // every stats word, every ok byte, and the rect words of the ok rects written (scanned
+      // from where the last scan stopped)
+      const size_t nsw = (size_t)npairs * (sizeof(eao_np_stats) / 4);
+      size_t ws = 0;
+      int wb = 0;
+      auto ready = [&]() -> bool {
+        for (; ws < nsw; ws++)
+          if (ld32(h_out + 4 * ws) == kSent32) return false;
+        for (; wb < nb; wb++) {
+          const uint8_t okb = ld8(h_out + o_ok + wb);
+          if (okb == kSent8) return false;
+          if (okb)
+            for (int q = 0; q < 4; q++)
+              if (ld32(h_out + o_r + 4 * (4 * (size_t)wb + q)) == kSent32) return false;
+        }
+        return true;
+      };
+      idle_work(gpu0_ev, ready);  // the next frame's steps 1-6, while the GPU is busy
+      EAO_HIP_CHECK(spin_ready(gpu0_ev, ready));
+      std::atomic_thread_fence(std::memory_order_acquire);
     }
     tr(3);
     const int* r = (const int*)(h_out + o_r);
@@ -2386,8 +2479,12 @@ class ReplayEngine {
     prep.kept.clear();
     la_set = false;
   }
-  // fill a wait on `ev` with the next frame's steps 1-6
+  // fill a wait on `ev` with the next frame's steps 1-6 (until the event, or `ready()`)
   void idle_work(hipEvent_t ev) {
+    idle_work(ev, [] { return false; });
+  }
+  template <class Ready>
+  void idle_work(hipEvent_t ev, Ready&& ready) {
     if (!prep.active) {
       if (!g_lookahead || !la_set || prep.ok || !ini) return;
       la_set = false;
@@ -2404,7 +2501,7 @@ class ReplayEngine {
       prof[53] += 1;
     }
     Tick tk(&prof[52]);
-    while (!prep.ok && hipEventQuery(ev) == hipErrorNotReady) prep.ok = prep_step(prep);
+    while (!prep.ok && !(g_sentinel && ready()) && hipEventQuery(ev) == hipErrorNotReady) prep.ok = prep_step(prep);
   }
   void prep_begin(Prep& s, const FrameIn& in) {
     s.in = in;

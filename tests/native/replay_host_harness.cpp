@@ -142,3 +142,4 @@ extern "C" void harness_set_device_exchange(eao_allgather_fn fn, void* ctx) {
   eao::g_dev_fn = fn;
   eao::g_dev_ctx = ctx;
 }
+extern "C" void harness_set_events_never(int v) { fake_events_never() = v; }

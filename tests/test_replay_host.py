@@ -222,3 +222,21 @@ def test_host_two_threads_share_one_handle(harness):
     ref = [o.step(i + 1, f) for i, f in enumerate(frames)]
     assert all(np.array_equal(a, b) for a, b in zip(dets, ref))
     _compare(g, o)
+
+
+def test_host_outputs_complete_without_events(harness):
+    """The unsharded waits end on the outputs themselves: with every event query reporting
+    "not ready" (harness_set_events_never), the fr3 stream still completes -- each frame start
+    and forest completion sees its sentinel-prefilled outputs overwritten (replay.cpp
+    spin_ready) -- with the oracle's ids and statistics."""
+    frames = synth.assoc_stream_fr3_real()[:120]
+    harness.harness_set_events_never(1)
+    try:
+        g = _HostReplay(harness, "EAO")
+        det = g._with(ea.Replay.run, g, ea.Replay.pack(frames))
+        o = orc.Replay("EAO")
+        ref = np.concatenate([o.step(i + 1, f) for i, f in enumerate(frames)])
+        assert np.array_equal(det, ref)
+        _compare(g, o)
+    finally:
+        harness.harness_set_events_never(0)
