@@ -103,6 +103,36 @@ def test_iforest_scores():
         assert np.array_equal(g > 0.6, o > 0.6)
 
 
+def test_iforest_mask_path_boundaries():
+    """The forest kernel's mask path (nodes of more than 64 items as slot bits over a sample of
+    at most 1024 items): samples just above 64 (one / two slots), at 1024 (16 slots), clouds with
+    ties and duplicated points (min == max in a dimension, equal keys across a split), a cloud of
+    one repeated point (the root is a leaf) and a flat cloud (one dimension constant), in one
+    launch and alone; the same scores as the restatement."""
+    rng = np.random.default_rng(0x3A5C)
+    clouds = []
+    for n in (129, 130, 131, 257, 1024, 2047, 2048):
+        c = _cloud(rng, n, [0, 0, 2], 0.05)
+        c[: max(1, n // 30)] += rng.uniform(-0.5, 0.5, (max(1, n // 30), 3)).astype(np.float32)
+        clouds.append(c)
+    lat = np.round(_cloud(rng, 600, [0, 0, 2], 0.05) * 50) / 50  # many equal keys
+    clouds.append(lat.astype(np.float32))
+    dup = _cloud(rng, 300, [0, 0, 2], 0.05)
+    dup[100:] = dup[:200]  # every point twice or three times
+    clouds.append(dup)
+    clouds.append(np.tile(np.float32([[0.1, -0.2, 2.0]]), (400, 1)))  # one point repeated
+    flat = _cloud(rng, 500, [0, 0, 2], 0.05)
+    flat[:, 1] = 0.25  # a constant dimension
+    clouds.append(flat)
+    a = ea.Assoc(max_points=40000)
+    for batch in (clouds, [[c] for c in clouds]):
+        got = a.iforest(batch) if isinstance(batch[0], np.ndarray) else [a.iforest(b)[0] for b in batch]
+        for c, g in zip(clouds, got):
+            o = orc.iforest(c)
+            assert np.allclose(g, o, rtol=1e-5, atol=1e-9, equal_nan=True), len(c)
+            assert np.array_equal(g > 0.6, o > 0.6), len(c)
+
+
 def test_iforest_sample_table_and_drawn_paths():
     """The engine takes a forest's sample from its table (k_iforest_sample) when the cloud
     has at most IF_TAB_N = 4096 points and the sample is n / 2, and draws it in the kernel
