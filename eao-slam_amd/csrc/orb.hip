@@ -136,57 +136,6 @@ __device__ __forceinline__ uint32_t fast_strength_pair(const uint8_t* p) {
   return (uint32_t)s0 | ((uint32_t)s1 << 16);
 }
 
-// The same strengths for the pixel rows a, a + 1 (and a + 2, a + 3) from whole ROI rows: a lane
-// reads the 12 aligned bytes around its window [x - 3, x + 4] of each row a - 3 .. a + 4 (+ 2)
-// once, realigns them to L = cols x-3..x, H = cols x+1..x+4 (two v_alignbyte), and builds every
-// packed ring pair with one v_perm_b32 from the two rows it spans -- 3 LDS dword reads per row
-// shared by both pairs of a trip instead of 2 byte reads per ring pixel and pixel row.
-// rows: realigned L / H of rows a - 3 + i, i = 0..7 (the pair a, a + 1).
-__device__ __forceinline__ uint32_t fast_strength_rows(const uint32_t* L, const uint32_t* H) {
-  constexpr int dy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
-  constexpr int dx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
-  uint32_t q[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    const int j = dx[k] + 3, i = dy[k] + 3, jj = j & 3;
-    const uint32_t* X = j < 4 ? L : H;
-    // byte jj of row a + dy -> bits 0-7, of row a + 1 + dy -> bits 16-23, zeros elsewhere
-    q[k] = __builtin_amdgcn_perm(X[i + 1], X[i], (uint32_t)jj | 0x0c00u | ((uint32_t)(4 + jj) << 16) | 0x0c000000u);
-  }
-  uint32_t mn3[16], mx3[16];
-#pragma unroll
-  for (int k = 0; k < 16; k++) {
-    mn3[k] = pk_min3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
-    mx3[k] = pk_max3(q[k], q[(k + 1) & 15], q[(k + 2) & 15]);
-  }
-  uint32_t A = 0x00ff00ffu, B = 0u;  // 255, 0
-#pragma unroll
-  for (int k = 0; k < 16; k += 2) {
-    const uint32_t a0 = pk_max3(mx3[k], mx3[(k + 3) & 15], mx3[(k + 6) & 15]);
-    const uint32_t a1 = pk_max3(mx3[k + 1], mx3[(k + 4) & 15], mx3[(k + 7) & 15]);
-    const uint32_t b0 = pk_min3(mn3[k], mn3[(k + 3) & 15], mn3[(k + 6) & 15]);
-    const uint32_t b1 = pk_min3(mn3[k + 1], mn3[(k + 4) & 15], mn3[(k + 7) & 15]);
-    A = pk_min3(A, a0, a1);
-    B = pk_max3(B, b0, b1);
-  }
-  const int v0 = (int)(L[3] >> 24), v1 = (int)(L[4] >> 24);
-  const int s0 = max(0, max(v0 - (int)(A & 0xff), (int)(B & 0xff) - v0));
-  const int s1 = max(0, max(v1 - (int)((A >> 16) & 0xff), (int)((B >> 16) & 0xff) - v1));
-  return (uint32_t)s0 | ((uint32_t)s1 << 16);
-}
-// realigned window [x - 3, x + 4] of nrow rows starting at row r0 of the ROI (row stride RS):
-// `w` = the 4-byte aligned address at or below column x - 3 of row r0, `sh` = the misalignment
-template <int RS, int NROW>
-__device__ __forceinline__ void fast_rows(const uint8_t* w, int sh, uint32_t (&L)[NROW], uint32_t (&H)[NROW]) {
-#pragma unroll
-  for (int r = 0; r < NROW; r++) {
-    const uint32_t* d = (const uint32_t*)(w + r * RS);
-    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
-    L[r] = __builtin_amdgcn_alignbyte(d1, d0, (uint32_t)sh);
-    H[r] = __builtin_amdgcn_alignbyte(d2, d1, (uint32_t)sh);
-  }
-}
-
 // ROI row strides of k_fast_band: a band is at most RS - 30 px wide (16-byte alignment
 // slack of the staging loads). Rows of cells are split into bands of balanced width
 // <= FAST_BAND_W, so the narrow stride serves 640x480 and 1920x1080 alike; its smaller
@@ -215,7 +164,7 @@ __device__ __forceinline__ int wave_from_right(int v) { return __builtin_amdgcn_
 //      (S if kept at minTh, else 0) encodes both passes;
 //   3. one wave per cell emits the kept pixels row-major (ballot + popcount),
 //      the iniTh set, or the minTh set when the cell has no iniTh corner.
-template <int RS, int ROWS>
+template <int RS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_fast_band(const uint8_t* __restrict__ frames, int fpitch,
                                                    long long fstride, const uint8_t* __restrict__ pyr,
                                                    long long pstride, const LevelDev* __restrict__ levels,
@@ -289,26 +238,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
     // thresholded at minTh (rows >= y1 read as 0), with the in-window left /
     // right neighbours. Row a + 1 = y1 reads one ROI row past the band, which
     // is still inside the LDS allocation (the F area) and is masked.
-    // ROWS: the whole-row gather (fast_strength_rows); the lane's window start x - 3, clamped
-    // for the halo lanes whose strengths are not used
-    const int xw = max(x - 3, 0);
-    const int wsh = (int)(((uintptr_t)(roi + xw)) & 3);
-    const uint8_t* wbase = roi + xw - wsh;
     auto strengths = [&](int a, bool two, uint32_t& spa, uint32_t& spb) {
       spa = spb = 0;
       if (!(inx && a < y1)) return;
-      if (ROWS) {
-        uint32_t L8[8], H8[8];
-        fast_rows<RS, 8>(wbase + (a - 3) * RS, wsh, L8, H8);
-        spa = fast_strength_rows(L8, H8);
-        if (two) {
-          fast_rows<RS, 8>(wbase + (a - 1) * RS, wsh, L8, H8);
-          spb = fast_strength_rows(L8, H8);
-        }
-      } else {
-        spa = fast_strength_pair<RS>(roi + a * RS + x);
-        if (two) spb = fast_strength_pair<RS>(roi + (a + 2) * RS + x);
-      }
+      spa = fast_strength_pair<RS>(roi + a * RS + x);
+      if (two) spb = fast_strength_pair<RS>(roi + (a + 2) * RS + x);
     };
     auto pair_from = [&](uint32_t sp, int a, int (&Sv)[2], int (&Lv)[2], int (&Rv)[2]) {
       int s0 = (int)(sp & 0xffffu), s1 = (int)(sp >> 16);
@@ -1351,16 +1285,12 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
     const bool narrow = band_w + 30 <= FAST_RS_NARROW;
     const int rs = narrow ? FAST_RS_NARROW : FAST_RS;
     size_t lds = (size_t)rs * (2 * band_h - 6);  // roi, kept strengths of the detection rows
-    // EAO_FAST_ROWS=1: the whole-row ring gather (A/B switch while it is measured)
-    static const bool rows = [] {
-      const char* v = getenv("EAO_FAST_ROWS");
-      return v && v[0] == '1';
-    }();
-    auto kf = narrow ? (rows ? k_fast_band<FAST_RS_NARROW, 1> : k_fast_band<FAST_RS_NARROW, 0>)
-                     : (rows ? k_fast_band<FAST_RS, 1> : k_fast_band<FAST_RS, 0>);
-    static const int xcd = [] {  // EAO_FAST_XCD=1: XCD-aware band order (A/B switch while measured)
+    auto kf = narrow ? k_fast_band<FAST_RS_NARROW> : k_fast_band<FAST_RS>;
+    // XCD-aware band order (k_fast_band): FETCH 611 -> 363 MB per 405-frame launch, time unchanged
+    // (profiles/r04_ab_fast.txt); EAO_FAST_XCD=0 restores the row-major order (A/B switch)
+    static const int xcd = [] {
       const char* v = getenv("EAO_FAST_XCD");
-      return v && v[0] == '1' ? 1 : 0;
+      return v && v[0] == '0' ? 0 : 1;
     }();
     hipLaunchKernelGGL(kf, g, dim3(256), lds, s,
                        d_frames, pitch, fstride, d_pyr, pyr_bytes, d_levels, d_bands, d_cells, p.ini_th_fast,
