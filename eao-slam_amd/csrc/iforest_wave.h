@@ -63,8 +63,9 @@ struct WaveRng {
     tw++;
   }
   __device__ void refill() {
+    idx = __builtin_amdgcn_readfirstlane(idx);  // uniform state: keep it scalar
     if (idx >= 624) twist();
-    blen = min(64, 624 - idx);
+    blen = __builtin_amdgcn_readfirstlane(min(64, 624 - idx));
     const int l = lane_id();
     uint32_t y = l < blen ? mt[idx + l] : 0u;
     y ^= (y >> 11);
@@ -77,7 +78,7 @@ struct WaveRng {
     bufd = y == 0u ? 3u : __umulhi(y, 3u);
     float r = fmul((float)y, 0x1p-32f);               // == y / 2^32 exactly (power-of-two scale)
     buff = r >= 1.0f ? __uint_as_float(0x3f7fffffu) : r;  // nextafter(1, 0)
-    idx += blen;
+    idx = __builtin_amdgcn_readfirstlane(idx + blen);
     bp = 0;
   }
   __device__ uint32_t next() {
@@ -101,6 +102,9 @@ struct WaveRng {
   __device__ uint32_t dim3() {
     uint32_t d;
     do {
+      // the read position is wave-uniform: readfirstlane keeps it (and the refill test) scalar
+      bp = __builtin_amdgcn_readfirstlane(bp);
+      blen = __builtin_amdgcn_readfirstlane(blen);
       if (bp >= blen) refill();
       d = (uint32_t)__builtin_amdgcn_readlane((int)bufd, bp++);
     } while (d == 3u);
@@ -108,6 +112,8 @@ struct WaveRng {
   }
   // uniform_real_distribution<float>(a, b): generate_canonical<float, 24>
   __device__ float uniform_real(float a, float b) {
+    bp = __builtin_amdgcn_readfirstlane(bp);
+    blen = __builtin_amdgcn_readfirstlane(blen);
     if (bp >= blen) refill();
     const float ret = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(buff), bp++));
     return fadd(fmul(ret, fsub(b, a)), a);
@@ -331,6 +337,8 @@ __device__ __forceinline__ int rank_build(WaveRng& g, const RankTab& tb, int cnt
     const float mx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, fk), hi));
     const bool eq = __builtin_bit_cast(int, mn) == __builtin_bit_cast(int, mx);
     // the split draw is read whatever the outcome and consumed only when min != max
+    g.bp = __builtin_amdgcn_readfirstlane(g.bp);
+    g.blen = __builtin_amdgcn_readfirstlane(g.blen);
     if (g.bp >= g.blen) g.refill();
     const float r = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(g.buff), g.bp));
     g.bp += eq ? 0 : 1;

@@ -12,7 +12,11 @@ EAO_FAST_XCD=1 timeout -k 10 200 python -u tools/orb_stages.py --reps 10 > gpuru
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r4_ab_pmc_fetch_base -o run -- python3 tools/pmc_extract.py > gpurun_out/r4_ab_pmc_fetch_base.log 2>&1 &&
 EAO_FAST_XCD=1 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r4_ab_pmc_fetch_xcd -o run -- python3 tools/pmc_extract.py > gpurun_out/r4_ab_pmc_fetch_xcd.log 2>&1 &&
 timeout -k 10 400 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4_ab_replay.log 2>&1 &&
-timeout -k 10 300 bash tools/ab_probe.sh eao-slam_amd/lib/ab/base/libeao_accel.so eao-slam_amd/lib/libeao_accel.so > gpurun_out/r4_ab_probe.log 2>&1 &&
+for r in 1 2; do
+  EAO_ACCEL_LIB=eao-slam_amd/lib/ab/base/libeao_accel.so timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" | sed "s/^/base /" &&
+  EAO_SENTINEL_WAIT=0 timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" | sed "s/^/forest /" &&
+  timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" | sed "s/^/forest+sentinel /" || break
+done > gpurun_out/r4_ab_probe.log 2>&1 &&
 timeout -k 10 120 python -u tools/micro/if_probe.py > gpurun_out/r4_ab_ifprobe_new.log 2>&1 &&
 EAO_ACCEL_LIB=eao-slam_amd/lib/ab/base/libeao_accel.so timeout -k 10 120 python -u tools/micro/if_probe.py > gpurun_out/r4_ab_ifprobe_base.log 2>&1 &&
 echo "== kernarg A/B" > gpurun_out/r4_ab_kernarg.log &&
