@@ -638,6 +638,10 @@ __device__ __forceinline__ void if_stamp(int k) {
 }
 
 
+// CalculateC entries staged in LDS: every leaf size of a sample of S (a leaf holds at most S
+// items) when that fits, else the first IF_CTL
+__host__ __device__ inline int if_ctl_n(int S) { return S < 2048 ? S + 1 : IF_CTL; }
+
 // dynamic LDS carve of k_iforest_tree for clouds of <= N points, samples <= S
 struct IfLds {
   size_t mt, b0, b1, nodes, shuf, ct, js, jq, total;
@@ -651,8 +655,8 @@ struct IfLds {
     shuf = b1;
     const size_t shuf_end = shuf + al16(2 * (size_t)N) + al16(4 * (size_t)N) + al16(2 * (size_t)N) +
                             al16(2 * (size_t)S);
-    ct = build_end > shuf_end ? build_end : shuf_end;  // CalculateC of leaf sizes < IF_CTL
-    js = ct + 8 * IF_CTL;                          // helper waves' prepared subtrees
+    ct = build_end > shuf_end ? build_end : shuf_end;  // CalculateC of leaf sizes < if_ctl_n(S)
+    js = ct + 8 * (size_t)if_ctl_n(S);             // helper waves' prepared subtrees
     jq = js + sizeof(RankSlot) * J;                // the subtree job list
     total = jq + al16(4 * ((size_t)S / 8 + 4));
   }
@@ -773,6 +777,7 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
                                                       const uint32_t* __restrict__ tab_states, int jslots) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const IfLds L(maxN, maxS, jslots);
+  const int ctl_n = if_ctl_n(maxS);  // CalculateC entries staged in LDS
   uint32_t* mts = (uint32_t*)(smem + L.mt);
   float* B0 = (float*)(smem + L.b0);
   float* B1 = (float*)(smem + L.b1);
@@ -798,13 +803,26 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
   const bool valid = !(n <= 0 || psi <= 0 || psi > n || n > maxN || psi > maxS || n > 0xfffe);
   if (tid == 0) s_nodes_bad = valid ? 0 : 1;
   const bool tab = valid && n <= tab_n && psi == n / 2 && tab_D[(size_t)n * gridDim.x + tr] >= 0;  // uniform
+  // the score walk (after the build) is done by the waves that neither build nor sort: they load
+  // their points now, so the loads' latency hides behind the sample gather and the build
+  constexpr int SW0 = IF_HELPERS + 1, SWT = 1024 - 64 * SW0;  // first scoring wave, scoring threads
+  const int st = tid - 64 * SW0;
+  float sx[4][3];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int i = st + u * SWT;
+    const bool ld = valid && st >= 0 && i < n;
+    sx[u][0] = ld ? P[3 * i] : 0.f;
+    sx[u][1] = ld ? P[3 * i + 1] : 0.f;
+    sx[u][2] = ld ? P[3 * i + 2] : 0.f;
+  }
   if (valid) {
   uint16_t* p = (uint16_t*)(smem + L.shuf);
   uint32_t* head = (uint32_t*)(smem + L.shuf + al16(2 * (size_t)n));
   uint16_t* nxt = (uint16_t*)((unsigned char*)head + al16(4 * (size_t)n));
   uint16_t* ids = (uint16_t*)((unsigned char*)nxt + al16(2 * (size_t)n));
   if_stamp(0);
-  for (int i = tid; i < IF_CTL; i += nb) ctl[i] = ctab[i];
+  for (int i = tid; i < ctl_n; i += nb) ctl[i] = ctab[i];
   if (tid < jslots) s_done[tid] = 0;
   if (tid == 0) s_post = s_take = s_stop = 0;
   WaveRng g;  // used by wave 0 only
@@ -1130,48 +1148,71 @@ __global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__
     for (int i = tid; i < n; i += nb) out[i] = __longlong_as_double(0x7ff8000000000000ll);
   } else
 
-  // four independent walks per thread in flight (LDS latency-bound chains)
-  for (int i0 = tid; i0 < n; i0 += 4 * nb) {
-    float x[4][3];
-    int k[4], depth[4];
-    uint2 nd[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = min(i0 + u * nb, n - 1);
-      x[u][0] = P[3 * i];
-      x[u][1] = P[3 * i + 1];
-      x[u][2] = P[3 * i + 2];
-      k[u] = 0;
-      depth[u] = 0;
-    }
-    const uint2 root = nodes[0];
-#pragma unroll
-    for (int u = 0; u < 4; u++) nd[u] = root;
-    bool any = (root.x & 3u) != 0u;
-    while (any) {
-      any = false;
+  {
+    // one walk: depth of the leaf it ends in + CalculateC(leaf size) (the staged table: every
+    // leaf size of the sample when it fits); four walks per thread in flight
+    auto walk4 = [&](const float (&x)[4][3], const bool (&act)[4], const int (&idx)[4]) {
+      int k[4], depth[4];
+      uint2 nd[4];
+      const uint2 root = nodes[0];
+      bool any = false;
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const uint32_t d = nd[u].x & 3u;
-        if (d != 0u) {
-          const float v = d == 1u ? x[u][0] : (d == 2u ? x[u][1] : x[u][2]);
-          k[u] = v < __uint_as_float(nd[u].y) ? k[u] + 1 : (int)(nd[u].x >> 16);
-          depth[u]++;
+        k[u] = 0;
+        depth[u] = 0;
+        nd[u] = act[u] ? root : make_uint2(0u, 0u);  // inactive: a finished walk
+        any |= (nd[u].x & 3u) != 0u;
+      }
+      while (any) {
+        any = false;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t d = nd[u].x & 3u;
+          if (d != 0u) {
+            const float v = d == 1u ? x[u][0] : (d == 2u ? x[u][1] : x[u][2]);
+            k[u] = v < __uint_as_float(nd[u].y) ? k[u] + 1 : (int)(nd[u].x >> 16);
+            depth[u]++;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if ((nd[u].x & 3u) != 0u) {
+            nd[u] = nodes[k[u]];
+            any |= (nd[u].x & 3u) != 0u;
+          }
         }
       }
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        if ((nd[u].x & 3u) != 0u) {
-          nd[u] = nodes[k[u]];
-          any |= (nd[u].x & 3u) != 0u;
-        }
+        const uint32_t lc = nd[u].x >> 2;  // leaf size
+        if (act[u]) out[idx[u]] = (double)depth[u] + (lc < (uint32_t)ctl_n ? ctl[lc] : ctab[lc]);
       }
-    }
+    };
+    if (st >= 0) {  // the prefetched points: indices st + u * SWT
+      bool act[4];
+      int idx[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * nb;
-      const uint32_t lc = nd[u].x >> 2;  // leaf size
-      if (i < n) out[i] = (double)depth[u] + (lc < IF_CTL ? ctl[lc] : ctab[lc]);
+      for (int u = 0; u < 4; u++) {
+        idx[u] = st + u * SWT;
+        act[u] = idx[u] < n;
+      }
+      walk4(sx, act, idx);
+    }
+    // points beyond the prefetched 4 * SWT (clouds of more than 3072 points): every thread
+    for (int i0 = 4 * SWT + tid; i0 < n; i0 += 4 * nb) {
+      float x[4][3];
+      bool act[4];
+      int idx[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        idx[u] = i0 + u * nb;
+        act[u] = idx[u] < n;
+        const int i = min(idx[u], n - 1);
+        x[u][0] = P[3 * i];
+        x[u][1] = P[3 * i + 1];
+        x[u][2] = P[3 * i + 2];
+      }
+      walk4(x, act, idx);
     }
   }
   if_stamp(7);
