@@ -6,15 +6,15 @@
 // ordering (:866-887, 1073-1141); lines longer than min_length are kept.
 //
 // Pipeline per batch of HBM-resident gray frames:
-//   k_line_blur     64x16 output tiles: the 8U fixed-point separable 5-tap Gaussian
-//                   (taps cvRound(k * 256), REFLECT_101, columns (s + 2^15) >> 16)
-//   k_line_grad     one thread per pixel: Sobel 3x3 (REFLECT_101) dx, dy; code =
-//                   thresholded |dx| + |dy| over 4 (cvRound) | Horizontal bit
-//   k_line_anchors  one workgroup per frame, a thread per candidate column: the anchors in the
+//   k_line_maps     64x32 output tiles through LDS: (COLOR_BGR2GRAY,) the 8U fixed-point
+//                   separable 5-tap Gaussian, Sobel 3x3 dx, dy, code = thresholded |dx| + |dy|
+//                   over 4 (cvRound) | Horizontal bit, and the walk's move bytes
+//   k_line_anchors  one workgroup per frame, a thread per candidate column (the candidates tested
+//                   in k_line_maps, one row mask per column and band): the anchors in the
 //                   reference's column-major scan order (w outer, h inner, step 2) from a
-//                   block scan of the per-column counts, rows walked with coalesced reads
-//   k_edge_draw     one wave per frame: the anchor walks (edge map as an LDS bitmap), the
-//                   kept chains assembled by the whole wave
+//                   block scan of the per-column counts
+//   k_edge_draw     one wave per frame: the anchor walks over the move bytes (edge map as an
+//                   LDS bitmap), the kept chains assembled by the whole wave
 //   k_edlines       8 waves per frame, a wave per chain (chains are independent): least-
 //                   squares fits and normal-equation sums as wave reductions (integer data,
 //                   exact in double), the extension walk in wave-uniform control flow,
@@ -41,100 +41,234 @@ constexpr int LN_GRAD_TH = 80, LN_ANCHOR_TH = 8, LN_MIN_LEN = 15, LN_TRY = 6, LN
 constexpr int LN_WAVES = 8;  // k_edlines: waves per frame (chains are independent)
 constexpr double LN_FIT_ERR = 1.6;
 
-__device__ __forceinline__ int refl101(int p, int len) {
-  if (len == 1) return 0;
-  while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;
-  return p;
+// ---------------------------------------------------------------- move bytes
+// A walk step (:1746-2000) depends on the pixel only: whether it is an edge pixel (gImg_ > 0),
+// its direction (dirImg_), and, for each of the two directions a walk can take through it, which
+// of the three forward neighbours has the largest gImg_ byte (the reference's if-chain, ties
+// included) or that the image border ends the walk there. k_line_maps evaluates this once per
+// pixel into a byte, so a step of the sequential walk is two LDS reads (the
+// byte through a tile cache, the edge-map bit) and a few scalar operations:
+//   bit 7: gImg_ > 0   bit 6: Horizontal
+//   bits 2-3: the step when walking RIGHT (Horizontal) / DOWN (Vertical)
+//   bits 4-5: the step when walking LEFT (Horizontal) / UP (Vertical)
+//   step: 0 straight, 1 the g1 diagonal, 2 the g3 diagonal, 3 at the border: stop after the pixel
+// (a Horizontal pixel is only ever left RIGHT or LEFT, a Vertical one DOWN or UP). Rows have
+// the pitch MP (a multiple of 16) so the tile loads are aligned 16-byte loads.
+constexpr int LM_EDGE = 0x80, LM_HORIZ = 0x40;
+__device__ __forceinline__ int ln_pick(int g1, int g2, int g3) {
+  return (g1 >= g2 && g1 >= g3) ? 1 : ((g3 >= g2 && g3 >= g1) ? 2 : 0);
 }
 
-// ---------------------------------------------------------------- blur
-// CN = 1: gray input. CN = 3 / 4: the colour frame BinaryDescriptor::detectImpl receives
-// (rawImage, Frame.cc:324), converted with COLOR_BGR2GRAY (binary_descriptor.cpp:490-493;
-// OpenCV 3.2 RGB2Gray<uchar> with the BGR coefficient order: (B*1868 + G*9617 + R*4899 +
-// 2^13) >> 14) as the tile is staged -- no gray plane is written or read.
-constexpr int LB_TW = 64, LB_TH = 16;
+// ---------------------------------------------------------------- maps
+// One kernel per 64x32 output tile: gray (CN = 3 / 4: the colour frame BinaryDescriptor::
+// detectImpl receives, rawImage of Frame.cc:324, converted with COLOR_BGR2GRAY,
+// binary_descriptor.cpp:490-493: OpenCV 3.2 RGB2Gray<uchar> with the BGR coefficient order
+// (B*1868 + G*9617 + R*4899 + 2^13) >> 14), the 8U fixed-point separable 5-tap Gaussian (taps
+// cvRound(k * 256), REFLECT_101, columns (s + 2^15) >> 16), Sobel 3x3 dx / dy (REFLECT_101), the
+// gradient code (thresholded |dx| + |dy| over 4, cvRound | Horizontal bit) and the walk's move
+// bytes (above), all staged in LDS with halos 4 / 2 / 1: the frame is read once and each map
+// written once. The gray halo is read at reflected coordinates; because the Gaussian is
+// symmetric, the blur evaluated 1-2 pixels outside the plane then equals the blur at the
+// reflected pixel, which is what the Sobel's own REFLECT_101 reads.
+constexpr int LF_TW = 64, LF_TH = 32;
+// one reflection: exact for the positions in-plane outputs read (at most 4 outside, len >= 8);
+// positions further out (a partial tile's unused tail) are only kept inside the plane
+__device__ __forceinline__ int refl1(int p, int len) {
+  return min(max(p < 0 ? -p : (p >= len ? 2 * len - 2 - p : p), 0), len - 1);
+}
+// the loops below walk a [rows][cols] region with a flat index t, t + 256, ...: (r, c) advanced
+// incrementally (no division per element)
+template <int COLS>
+struct Walk2 {
+  int r, c;
+  __device__ __forceinline__ explicit Walk2(int t) : r(t / COLS), c(t - (t / COLS) * COLS) {}
+  __device__ __forceinline__ void next() {
+    r += 256 / COLS;
+    c += 256 % COLS;
+    if (c >= COLS) {
+      c -= COLS;
+      r++;
+    }
+  }
+};
 template <int CN>
-__global__ __launch_bounds__(256) void k_line_blur(const uint8_t* __restrict__ img, int pitch, long long fstride,
-                                                   int w, int h, int k0, int k1, int k2,
-                                                   uint8_t* __restrict__ blur) {
-  __shared__ uint8_t in[LB_TH + 4][LB_TW + 4];
-  __shared__ int hs[LB_TH + 4][LB_TW];
-  const int f = blockIdx.z, x0 = blockIdx.x * LB_TW, y0 = blockIdx.y * LB_TH, t = threadIdx.x;
+__global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ img, int pitch, long long fstride,
+                                                   int w, int h, int MP, int k0, int k1, int k2, int vec,
+                                                   uint8_t* __restrict__ blur, int16_t* __restrict__ dxo,
+                                                   int16_t* __restrict__ dyo, uint16_t* __restrict__ code,
+                                                   uint8_t* __restrict__ moves, uint16_t* __restrict__ amask) {
+  constexpr int GW = LF_TW + 8, GH = LF_TH + 8;  // gray: halo 4 (blur 2 + Sobel 1 + moves 1)
+  constexpr int BW = LF_TW + 4, BH = LF_TH + 4;  // blur: halo 2
+  constexpr int CW = LF_TW + 2, CH = LF_TH + 2;  // code: halo 1
+  constexpr int RW = GW * CN, RD = RW / 4;       // a staged row: bytes, dwords
+  constexpr int NL = (GH * RD + 255) / 256;      // dword loads per thread
+  __shared__ __attribute__((aligned(16))) uint8_t raw[CN == 1 ? 16 : GH * RW];
+  __shared__ __attribute__((aligned(16))) uint8_t g[GH][GW];
+  __shared__ int hs[GH][BW];
+  __shared__ uint8_t bl[BH][BW];
+  __shared__ uint16_t cd[CH][CW];
+  __shared__ uint32_t am[LF_TW / 2];
+  const int f = blockIdx.z, x0 = blockIdx.x * LF_TW, y0 = blockIdx.y * LF_TH, t = threadIdx.x;
   const uint8_t* G = img + f * fstride;
-  for (int i = t; i < (LB_TH + 4) * (LB_TW + 4); i += 256) {
-    const int r = i / (LB_TW + 4), c = i - r * (LB_TW + 4);
-    const uint8_t* q = G + (long long)refl101(y0 - 2 + r, h) * pitch + (long long)refl101(x0 - 2 + c, w) * CN;
-    if (CN == 1)
-      in[r][c] = q[0];
-    else
-      in[r][c] = (uint8_t)((q[0] * 1868 + q[1] * 9617 + q[2] * 4899 + (1 << 13)) >> 14);
+  const long long fo = (long long)f * w * h;
+  if (t < LF_TW / 2) am[t] = 0u;
+  if (vec && x0 >= 4 && x0 + LF_TW + 4 <= w) {
+    // an inner tile: its rows (reflected at the top / bottom) staged with aligned 4-byte
+    // loads, all in flight before the first LDS store
+    uint32_t v[NL];
+    const uint8_t* base = G + (long long)(x0 - 4) * CN;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+      const int i = t + 256 * k, r = i / RD, c = i - r * RD;
+      v[k] = 0u;
+      if (i < GH * RD) v[k] = *(const uint32_t*)(base + (long long)refl1(y0 - 4 + r, h) * pitch + 4 * c);
+    }
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+      const int i = t + 256 * k, r = i / RD, c = i - r * RD;
+      if (i < GH * RD) {
+        if (CN == 1)
+          *(uint32_t*)&g[r][4 * c] = v[k];
+        else
+          *(uint32_t*)&raw[r * RW + 4 * c] = v[k];
+      }
+    }
+    if (CN != 1) {
+      __syncthreads();
+      Walk2<GW> q(t);
+      for (; q.r < GH; q.next()) {
+        const uint8_t* p = &raw[q.r * RW + q.c * CN];
+        g[q.r][q.c] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+      }
+    }
+  } else {
+    // a border tile: gray at reflected coordinates (BORDER_REFLECT_101 of the blur's input)
+    constexpr int NE = (GH * GW + 255) / 256;
+    uint8_t v[NE][CN];
+#pragma unroll
+    for (int k = 0; k < NE; k++) {
+      const int i = t + 256 * k, r = i / GW, c = i - r * GW;
+#pragma unroll
+      for (int j = 0; j < CN; j++) v[k][j] = 0;
+      if (i < GH * GW) {
+        const uint8_t* p = G + (long long)refl1(y0 - 4 + r, h) * pitch + (long long)refl1(x0 - 4 + c, w) * CN;
+#pragma unroll
+        for (int j = 0; j < CN; j++) v[k][j] = p[j];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NE; k++) {
+      const int i = t + 256 * k, r = i / GW, c = i - r * GW;
+      if (i < GH * GW)
+        g[r][c] = CN == 1 ? v[k][0] : (uint8_t)((v[k][0] * 1868 + v[k][1] * 9617 + v[k][2] * 4899 + (1 << 13)) >> 14);
+    }
   }
   __syncthreads();
-  for (int i = t; i < (LB_TH + 4) * LB_TW; i += 256) {
-    const int r = i / LB_TW, c = i - r * LB_TW;
-    hs[r][c] = k0 * ((int)in[r][c] + in[r][c + 4]) + k1 * ((int)in[r][c + 1] + in[r][c + 3]) + k2 * in[r][c + 2];
+  for (Walk2<BW> q(t); q.r < GH; q.next()) {
+    const uint8_t* p = &g[q.r][q.c];
+    hs[q.r][q.c] = k0 * ((int)p[0] + p[4]) + k1 * ((int)p[1] + p[3]) + k2 * p[2];
   }
   __syncthreads();
-  for (int i = t; i < LB_TH * LB_TW; i += 256) {
-    const int r = i / LB_TW, c = i - r * LB_TW;
-    const int x = x0 + c, y = y0 + r;
+  for (Walk2<BW> q(t); q.r < BH; q.next()) {  // blur at (x0 - 2 + c, y0 - 2 + r)
+    const int r = q.r, c = q.c;
+    const int sm = k0 * (hs[r][c] + hs[r + 4][c]) + k1 * (hs[r + 1][c] + hs[r + 3][c]) + k2 * hs[r + 2][c];
+    const uint8_t v = (uint8_t)min((sm + (1 << 15)) >> 16, 255);
+    bl[r][c] = v;
+    const int x = x0 - 2 + c, y = y0 - 2 + r;
+    if (r >= 2 && r < BH - 2 && c >= 2 && c < BW - 2 && x < w && y < h) blur[fo + (long long)y * w + x] = v;
+  }
+  __syncthreads();
+  for (Walk2<CW> q(t); q.r < CH; q.next()) {  // code at (x0 - 1 + c, y0 - 1 + r)
+    const int r = q.r, c = q.c;
+    const int a = bl[r][c], b = bl[r][c + 1], cc = bl[r][c + 2];
+    const int d = bl[r + 1][c], e = bl[r + 1][c + 2];
+    const int gg = bl[r + 2][c], hh = bl[r + 2][c + 1], k = bl[r + 2][c + 2];
+    const int gx = (cc - a) + 2 * (e - d) + (k - gg);
+    const int gy = (gg - a) + 2 * (hh - b) + (k - cc);
+    const int ax = abs(gx), ay = abs(gy), sm = ax + ay;
+    const int tz = sm > LN_GRAD_TH + 1 ? sm : 0;             // threshold(TOZERO, 81)
+    const int qv = __float2int_rn(fmul((float)tz, 0.25f));   // saturate_cast<short>(v * 0.25f)
+    const uint16_t cv = (uint16_t)(qv | (ax < ay ? LN_HORIZ : 0));
+    cd[r][c] = cv;
+    const int x = x0 - 1 + c, y = y0 - 1 + r;
+    if (r >= 1 && r < CH - 1 && c >= 1 && c < CW - 1 && x < w && y < h) {
+      const long long o = fo + (long long)y * w + x;
+      dxo[o] = (int16_t)gx;
+      dyo[o] = (int16_t)gy;
+      code[o] = cv;
+    }
+  }
+  __syncthreads();
+  // anchors (:1683-1693): the candidates (odd x <= w - 2, odd y <= h - 2) of the tile, as one
+  // 16-bit row mask per candidate column; k_line_anchors orders them
+  for (int i = t; i < (LF_TW / 2) * (LF_TH / 2); i += 256) {
+    const int cl = i & (LF_TW / 2 - 1), jb = i / (LF_TW / 2);
+    const int r = 2 + 2 * jb, c = 2 + 2 * cl;  // cd index of (x0 + 1 + 2 cl, y0 + 1 + 2 jb)
+    if (x0 + c - 1 <= w - 2 && y0 + r - 1 <= h - 2) {
+      const int cv = cd[r][c], gv = cv & 0x7fff;
+      const bool an = (cv & LN_HORIZ)
+                          ? (gv >= (cd[r - 1][c] & 0x7fff) + LN_ANCHOR_TH && gv >= (cd[r + 1][c] & 0x7fff) + LN_ANCHOR_TH)
+                          : (gv >= (cd[r][c - 1] & 0x7fff) + LN_ANCHOR_TH && gv >= (cd[r][c + 1] & 0x7fff) + LN_ANCHOR_TH);
+      if (an) atomicOr(&am[cl], 1u << jb);
+    }
+  }
+  for (Walk2<LF_TW> q(t); q.r < LF_TH; q.next()) {  // move bytes of the tile (see k_edge_draw)
+    const int r = q.r, c = q.c, x = x0 + c, y = y0 + r;
     if (x >= w || y >= h) continue;
-    const int s = k0 * (hs[r][c] + hs[r + 4][c]) + k1 * (hs[r + 1][c] + hs[r + 3][c]) + k2 * hs[r + 2][c];
-    blur[(long long)f * w * h + (long long)y * w + x] = (uint8_t)min((s + (1 << 15)) >> 16, 255);
+    const int cv = cd[r + 1][c + 1];
+    int m = 0;
+    if (cv & 0x7fff) {
+      // the walk compares gImg_ read as unsigned char (gValue1..3, :1643): the code's low byte;
+      // a neighbour outside the plane is never read (the border stops that direction)
+      auto gb = [&](int dx, int dy) { return (int)(uint8_t)cd[r + 1 + dy][c + 1 + dx]; };
+      m = LM_EDGE;
+      if (cv & LN_HORIZ) {
+        const int rt = (x == w - 1 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(1, -1), gb(1, 0), gb(1, 1));
+        const int lf = (x == 0 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(-1, -1), gb(-1, 0), gb(-1, 1));
+        m |= LM_HORIZ | rt << 2 | lf << 4;
+      } else {
+        const int dn = (x == 0 || x == w - 1 || y == h - 1) ? 3 : ln_pick(gb(1, 1), gb(0, 1), gb(-1, 1));
+        const int up = (x == 0 || x == w - 1 || y == 0) ? 3 : ln_pick(gb(1, -1), gb(0, -1), gb(-1, -1));
+        m |= dn << 2 | up << 4;
+      }
+    }
+    moves[(long long)f * MP * h + (long long)y * MP + x] = (uint8_t)m;
   }
-}
-
-// ---------------------------------------------------------------- gradient
-__global__ __launch_bounds__(256) void k_line_grad(const uint8_t* __restrict__ blur, int w, int h,
-                                                   int16_t* __restrict__ dxo, int16_t* __restrict__ dyo,
-                                                   uint16_t* __restrict__ code) {
-  const int f = blockIdx.y;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= w * h) return;
-  const int y = i / w, x = i - y * w;
-  const uint8_t* B = blur + (long long)f * w * h;
-  const int xm = refl101(x - 1, w), xp = refl101(x + 1, w), ym = refl101(y - 1, h), yp = refl101(y + 1, h);
-  const int a = B[ym * w + xm], b = B[ym * w + x], c = B[ym * w + xp];
-  const int d = B[y * w + xm], e = B[y * w + xp];
-  const int g = B[yp * w + xm], hh = B[yp * w + x], k = B[yp * w + xp];
-  const int gx = (c - a) + 2 * (e - d) + (k - g);
-  const int gy = (g - a) + 2 * (hh - b) + (k - c);
-  const long long o = (long long)f * w * h + i;
-  dxo[o] = (int16_t)gx;
-  dyo[o] = (int16_t)gy;
-  const int ax = abs(gx), ay = abs(gy), s = ax + ay;
-  const int tz = s > LN_GRAD_TH + 1 ? s : 0;                // threshold(TOZERO, 81)
-  const int q = __float2int_rn(fmul((float)tz, 0.25f));     // saturate_cast<short>(v * 0.25f)
-  code[o] = (uint16_t)(q | (ax < ay ? LN_HORIZ : 0));
+  __syncthreads();
+  if (t < LF_TW / 2)
+    amask[((long long)f * gridDim.y + blockIdx.y) * (gridDim.x * (LF_TW / 2)) + blockIdx.x * (LF_TW / 2) + t] =
+        (uint16_t)am[t];
 }
 
 // ---------------------------------------------------------------- anchors
-// anchor id k <-> (w = 1 + 2 * (k / nh), h = 1 + 2 * (k % nh)): the reference's scan order
-__device__ __forceinline__ bool is_anchor(const uint16_t* C, int W, int x, int y) {
-  const int i = y * W + x;
-  const int c = C[i], g = c & 0x7fff;
-  if (c & LN_HORIZ) return g >= (C[i - W] & 0x7fff) + LN_ANCHOR_TH && g >= (C[i + W] & 0x7fff) + LN_ANCHOR_TH;
-  return g >= (C[i - 1] & 0x7fff) + LN_ANCHOR_TH && g >= (C[i + 1] & 0x7fff) + LN_ANCHOR_TH;
-}
-// A thread per candidate column (x = 1 + 2 t, up to blockDim.x columns per pass): the anchors
-// of one column are consecutive in the reference's column-major order, so a block scan of
-// the per-column counts in thread order places every column; the column's rows are walked in
-// order, adjacent threads reading adjacent pixels (coalesced).
-__global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict__ code, int W, int H,
-                                                      uint32_t* __restrict__ anchors, int acap,
+// The reference's scan order is column-major (w outer, h inner, step 2, :1683-1693). k_line_maps
+// leaves one 16-bit row mask per (candidate column, 32-row band); here a thread per candidate
+// column (x = 1 + 2 k, blockDim.x columns per pass) counts its column, a block scan of the
+// counts in column order places every column, and the column's anchors are written in row order.
+__global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict__ amask, int W, int H, int nty,
+                                                      int ncp, uint32_t* __restrict__ anchors, int acap,
                                                       int* __restrict__ nanchor) {
   __shared__ int wsum[8], base;
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const uint16_t* C = code + (long long)f * W * H;
+  const uint16_t* AM = amask + (long long)f * nty * ncp;
   uint32_t* A = anchors + (long long)f * acap;
-  const int nw = (W - 2 + 1) / 2, nh = (H - 2 + 1) / 2;
+  const int nw = (W - 2 + 1) / 2;
   if (t == 0) base = 0;
   __syncthreads();
-  for (int x0 = 0; x0 < nw; x0 += blockDim.x) {
-    const int col = x0 + t, x = 1 + 2 * col;
+  for (int k0 = 0; k0 < nw; k0 += blockDim.x) {
+    const int col = k0 + t, x = 1 + 2 * col;
     int c = 0;
-    if (col < nw)
-      for (int j = 0; j < nh; j++) c += is_anchor(C, W, x, 1 + 2 * j) ? 1 : 0;
+    if (col < nw) {
+      int ty = 0;
+      for (; ty + 8 <= nty; ty += 8) {  // eight masks in flight
+        uint32_t m[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) m[u] = AM[(long long)(ty + u) * ncp + col];
+#pragma unroll
+        for (int u = 0; u < 8; u++) c += __popc(m[u]);
+      }
+      for (; ty < nty; ty++) c += __popc((uint32_t)AM[(long long)ty * ncp + col]);
+    }
     int v = c;  // inclusive scan over the block's columns
     for (int o = 1; o < 64; o <<= 1) {
       const int u = __shfl_up(v, o, 64);
@@ -145,13 +279,12 @@ __global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict
     int o = base + v - c;
     for (int w = 0; w < wave; w++) o += wsum[w];
     if (col < nw)
-      for (int j = 0; j < nh; j++) {
-        const int y = 1 + 2 * j;
-        if (is_anchor(C, W, x, y)) {
+      for (int ty = 0; ty < nty; ty++)
+        for (uint32_t m = AM[(long long)ty * ncp + col]; m; m &= m - 1) {
+          const int y = ty * LF_TH + 1 + 2 * __builtin_ctz(m);
           if (o < acap) A[o] = (uint32_t)x | ((uint32_t)y << 16);
           o++;
         }
-      }
     __syncthreads();
     if (t == blockDim.x - 1) {
       int tot = 0;
@@ -164,201 +297,171 @@ __global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict
 }
 
 // ---------------------------------------------------------------- edge drawing
-// EdgeDrawing's anchor loop (:1695-2327): the whole wave executes the walk with uniform
-// values (lane 0 writes), the edge map is a per-frame LDS bitmap
-struct WalkState {
-  uint32_t lastX, lastY;
+// The walk reads the move bytes through a 128 x 128 tile of them in LDS, reloaded (centred on
+// the step's pixel) when the pixel leaves it: one round of 16 aligned 16-byte loads per lane.
+// (No move byte is read outside the plane: the border steps stop the walk.)
+constexpr int LE_TW = 128, LE_TH = 128;
+struct MoveTile {
+  uint8_t* t;  // LDS [LE_TH][LE_TW]
+  int x0, y0;  // origin in the plane (x0 = -LE_TW: empty)
 };
-// one walk from (x, y); appends packed (y << 16 | x) to P[off..]; false on overflow
-// The walk reads the gradient code through a 64 x 64 tile of it cached in LDS, reloaded
-// (centred on the step's pixel, rows clamped to the plane) when the pixel's 3 x 3
-// neighbourhood leaves it: one round of coalesced loads per ~30 steps instead of one
-// global round trip per step.
-constexpr int LN_TS = 64;
-struct CodeTile {
-  uint16_t* t;  // LDS [LN_TS][LN_TS]
-  int x0, y0;   // origin in the plane (x0 = -LN_TS: empty)
-};
-__device__ __forceinline__ void tile_cover(const uint16_t* __restrict__ C, int W, int H, CodeTile& T, int x, int y) {
-  const int ax = max(x - 1, 0), bx = min(x + 1, W - 1), ay = max(y - 1, 0), by = min(y + 1, H - 1);
-  if (ax >= T.x0 && bx < T.x0 + LN_TS && ay >= T.y0 && by < T.y0 + LN_TS) return;  // uniform
-  T.x0 = min(max(x - LN_TS / 2, 0), max(W - LN_TS, 0));
-  T.y0 = min(max(y - LN_TS / 2, 0), max(H - LN_TS, 0));
-  const int lane = lane_id(), cx = min(T.x0 + lane, W - 1);
-  for (int r0 = 0; r0 < LN_TS; r0 += 16) {  // 16 row loads in flight per lane
-    uint16_t v[16];
+__device__ __forceinline__ void tile_load(const uint8_t* __restrict__ M, int MP, int H, MoveTile& T, int x, int y) {
+  T.x0 = min(max((x - LE_TW / 2) & ~15, 0), max(MP - LE_TW, 0));
+  T.y0 = min(max(y - LE_TH / 2, 0), max(H - LE_TH, 0));
+  const int lane = lane_id();
+  uint4 v[16];
 #pragma unroll
-    for (int r = 0; r < 16; r++) v[r] = C[min(T.y0 + r0 + r, H - 1) * W + cx];
+  for (int k = 0; k < 16; k++) {
+    const int id = lane + 64 * k, r = id >> 3, c = (id & 7) * 16;
+    v[k] = make_uint4(0u, 0u, 0u, 0u);
+    if (T.y0 + r < H && T.x0 + c < MP) v[k] = *(const uint4*)(M + (long long)(T.y0 + r) * MP + T.x0 + c);
+  }
 #pragma unroll
-    for (int r = 0; r < 16; r++) T.t[(r0 + r) * LN_TS + lane] = v[r];
+  for (int k = 0; k < 16; k++) {
+    const int id = lane + 64 * k, r = id >> 3, c = (id & 7) * 16;
+    *(uint4*)(T.t + r * LE_TW + c) = v[k];
   }
 }
-__device__ __forceinline__ int tile_at(const CodeTile& T, int x, int y) {  // inside the plane
-  return T.t[(y - T.y0) * LN_TS + (x - T.x0)];
-}
-__device__ bool walk(const uint16_t* __restrict__ C, int W, int H, uint32_t* bits, uint32_t x, uint32_t y, int lastDir,
-                     WalkState& st, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap, CodeTile& T) {
-  const int lane = threadIdx.x;
-  int idx = (int)(y * W + x);
-  // the pixel and its 8 neighbours from the tile (neighbour coordinates clamped to the plane:
-  // at a border the walk stops before using a neighbour)
-  int c;
-  uint8_t nUL, nU, nUR, nL, nR, nDL, nD, nDR;
-  auto load9 = [&](int, int xx, int yy) {
-    tile_cover(C, W, H, T, xx, yy);
-    const int xl = max(xx - 1, 0), xr = min(xx + 1, W - 1), yu = max(yy - 1, 0), yd = min(yy + 1, H - 1);
-    c = tile_at(T, xx, yy);
-    nUL = (uint8_t)tile_at(T, xl, yu);
-    nU = (uint8_t)tile_at(T, xx, yu);
-    nUR = (uint8_t)tile_at(T, xr, yu);
-    nL = (uint8_t)tile_at(T, xl, yy);
-    nR = (uint8_t)tile_at(T, xr, yy);
-    nDL = (uint8_t)tile_at(T, xl, yd);
-    nD = (uint8_t)tile_at(T, xx, yd);
-    nDR = (uint8_t)tile_at(T, xr, yd);
-  };
-  load9(idx, (int)x, (int)y);
+
+// one walk from (x, y) leaving in direction dir: its pixels appended (packed y << 16 | x) to
+// P[off..], off being the reference's running offF / offS and cap its edgePixelArraySize;
+// false on overflow. The whole wave runs the walk with uniform (scalar) values, lane 0 writes.
+// The direction rule (:1746-2000): a Horizontal pixel keeps a horizontal lastDir, else turns
+// RIGHT if x > lastX (the previous pixel's x), LEFT otherwise. A RIGHT step always has x >
+// lastX and a LEFT step never, so on a Horizontal pixel the walk goes RIGHT exactly when its
+// last step increased x -- and on a Vertical one DOWN exactly when the last step increased y.
+// The walk's state is those two bits (px, py), initialised from dir (an anchor's first step
+// leaves along dir: its own direction).
+__device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
+                                        MoveTile& T, int x, int y, int dir, uint32_t* __restrict__ P, uint32_t& off,
+                                        uint32_t cap) {
+  const bool l0 = lane_id() == 0;
+  // st bit 1: the last step increased x (px), bit 0: it increased y (py). (Scalar ints, not
+  // bools: the compiler keeps those as lane masks.)
+  int st = dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0);
+  if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) tile_load(M, MP, H, T, x, y);
+  int toff = (y - T.y0) * LE_TW + (x - T.x0);
   while (true) {
-    if ((c & 0x7fff) == 0 || ((bits[idx >> 5] >> (idx & 31)) & 1u)) break;
+    const int idx = y * W + x;
+    const int mw = __builtin_amdgcn_readfirstlane((int)T.t[toff]);
+    const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
+    const uint32_t bit = 1u << (idx & 31);
+    if (!(mw & LM_EDGE) || (bw & bit)) break;
     if (off >= cap) return false;
-    if (lane == 0) {
-      atomicOr(&bits[idx >> 5], 1u << (idx & 31));
-      P[off] = x | (y << 16);
+    if (l0) {
+      bits[idx >> 5] = bw | bit;  // the only writer of the frame's edge map
+      P[off] = (uint32_t)x | ((uint32_t)y << 16);
     }
     off++;
-    int should = 0;
-    if (c & LN_HORIZ) {
-      if (lastDir == LN_UP || lastDir == LN_DOWN) should = x > st.lastX ? LN_RIGHT : LN_LEFT;
-      st.lastX = x;
-      st.lastY = y;
-      if (lastDir == LN_RIGHT || should == LN_RIGHT) {
-        if (x == (uint32_t)W - 1 || y == 0 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = nUR, g2 = nR, g3 = nDR;
-        if (g1 >= g2 && g1 >= g3) {
-          x++;
-          y--;
-        } else if (g3 >= g2 && g3 >= g1) {
-          x++;
-          y++;
-        } else {
-          x++;
-        }
-        lastDir = LN_RIGHT;
-      } else if (lastDir == LN_LEFT || should == LN_LEFT) {
-        if (x == 0 || y == 0 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = nUL, g2 = nL, g3 = nDL;
-        if (g1 >= g2 && g1 >= g3) {
-          x--;
-          y--;
-        } else if (g3 >= g2 && g3 >= g1) {
-          x--;
-          y++;
-        } else {
-          x--;
-        }
-        lastDir = LN_LEFT;
-      }
-    } else {
-      if (lastDir == LN_RIGHT || lastDir == LN_LEFT) should = y > st.lastY ? LN_DOWN : LN_UP;
-      st.lastX = x;
-      st.lastY = y;
-      if (lastDir == LN_DOWN || should == LN_DOWN) {
-        if (x == 0 || x == (uint32_t)W - 1 || y == (uint32_t)H - 1) break;
-        const uint8_t g1 = nDR, g2 = nD, g3 = nDL;
-        if (g1 >= g2 && g1 >= g3) {
-          x++;
-          y++;
-        } else if (g3 >= g2 && g3 >= g1) {
-          x--;
-          y++;
-        } else {
-          y++;
-        }
-        lastDir = LN_DOWN;
-      } else if (lastDir == LN_UP || should == LN_UP) {
-        if (x == 0 || x == (uint32_t)W - 1 || y == 0) break;
-        const uint8_t g1 = nUR, g2 = nU, g3 = nUL;
-        if (g1 >= g2 && g1 >= g3) {
-          x++;
-          y--;
-        } else if (g3 >= g2 && g3 >= g1) {
-          x--;
-          y--;
-        } else {
-          y--;
-        }
-        lastDir = LN_UP;
-      }
+    const int hz = (mw >> 6) & 1;
+    const int fwd = (st >> hz) & 1;  // RIGHT (Horizontal: px) / DOWN (Vertical: py)
+    const int ch = (mw >> (4 - 2 * fwd)) & 3;
+    if (ch == 3) break;
+    const int along = 2 * fwd - 1, side = (ch >> 1) - (ch & 1);  // ch 1: the g1 side (-1), 2: g3 (+1)
+    const int dx = hz ? along : -side, dy = hz ? side : along;  // DOWN / UP: g1 is the x + 1 neighbour
+    x += dx;
+    y += dy;
+    st = (int)(((unsigned)(-dx) >> 31) << 1 | ((unsigned)(-dy) >> 31));
+    toff += dy * LE_TW + dx;
+    if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) {
+      tile_load(M, MP, H, T, x, y);
+      toff = (y - T.y0) * LE_TW + (x - T.x0);
     }
-    idx = (int)(y * W + x);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    load9(idx, (int)x, (int)y);
   }
   return true;
 }
 
-// per frame: anchors A[nanchor], parts scratch P1 / P2 [pcap], chains out Q[2 pcap] with
-// sid S[ecap + 1]; nedge[f] = kept chains, or -1 on overflow (the reference's -1 paths)
-__global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ code, int W, int H,
+// EdgeDrawing's anchor loop (:1695-2327), one wave per frame. Anchors are taken 64 at a time
+// (one per lane, with their move byte); the ones an earlier walk has marked are dropped by one
+// ballot after each walk, so an anchor costs no round trip of its own. Both parts of a chain
+// go to P1 / P2 at the reference's running offsets offF / offS (a short chain's pixels are
+// overwritten by the next walk, as there); the chains are assembled into Q once the frame is
+// done, by the whole wave: the first part reversed, then the second without its copy of the
+// anchor (chain e starts at fS[e] + sS[e] - e).
+__global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ moves, int W, int H, int MP,
                                                   const uint32_t* __restrict__ anchors, const int* __restrict__ nanchor,
                                                   int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2,
                                                   int pcap, uint32_t* __restrict__ chains, uint32_t* __restrict__ sid,
                                                   int ecap, int* __restrict__ nedge) {
-  extern __shared__ uint32_t bits[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
   const int f = blockIdx.x, lane = threadIdx.x;
-  const uint16_t* C = code + (long long)f * W * H;
-  const int nb = (W * H + 31) / 32;
-  CodeTile T{(uint16_t*)(bits + ((nb + 3) & ~3)), -LN_TS, -LN_TS};
+  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
+  uint32_t* bits = lds_ed;
+  uint32_t* fS = bits + nbp;  // the kept chains' offF / offS starts (the reference's fS / sS)
+  uint32_t* sS = fS + ep;
+  MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
   for (int i = lane; i < nb; i += 64) bits[i] = 0;
   __syncthreads();
+  const uint8_t* M = moves + (long long)f * MP * H;
   const uint32_t* A = anchors + (long long)f * acap;
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
   uint32_t* Q = chains + (long long)f * 2 * pcap;
   uint32_t* S = sid + (long long)f * (ecap + 1);
   const int na = nanchor[f];
-  WalkState st{0u, 0u};
-  uint32_t nq = 0;
-  int ne = 0;
-  bool fail = na > acap || na > pcap;  // anchorsSize > edgePixelArraySize
-  for (int a = 0; a < na && !fail; a++) {
-    const uint32_t ap = A[a], x = ap & 0xffffu, y = ap >> 16;
-    const int idx = (int)(y * W + x);
-    if ((bits[idx >> 5] >> (idx & 31)) & 1u) continue;
-    if (ne > ecap) {
-      fail = true;
-      break;
+  uint32_t b1 = 0, b2 = 0;  // offF / offS after the last kept chain
+  int ne = 0;               // offPS
+  bool fail = na > acap;    // anchorsSize > edgePixelArraySize (acap is that size)
+  for (int a0 = 0; a0 < na && !fail; a0 += 64) {
+    const int a = a0 + lane;
+    const uint32_t ap = a < na ? A[a] : 0u;
+    const int ax = (int)(ap & 0xffffu), ay = (int)(ap >> 16), aidx = ay * W + ax;
+    const int amw = a < na ? (int)M[(long long)ay * MP + ax] : 0;
+    uint64_t pend = ballot(a < na);
+    while (true) {
+      pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);  // edgeImg_[anchor] set: skipped
+      if (!pend) break;
+      const int k = __builtin_ctzll(pend);
+      pend &= pend - 1;
+      if (ne > ecap) {  // offPS > maxNumOfEdge
+        fail = true;
+        break;
+      }
+      const int x = __builtin_amdgcn_readlane(ax, k), y = __builtin_amdgcn_readlane(ay, k);
+      const bool horiz = (__builtin_amdgcn_readlane(amw, k) & LM_HORIZ) != 0;
+      uint32_t o1 = b1, o2 = b2;
+      if (!ed_walk(M, W, MP, H, bits, T, x, y, horiz ? LN_RIGHT : LN_DOWN, P1, o1, (uint32_t)pcap)) {
+        fail = true;
+        break;
+      }
+      const int idx = y * W + x;
+      if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));  // the second part walks the anchor again
+      if (!ed_walk(M, W, MP, H, bits, T, x, y, horiz ? LN_LEFT : LN_UP, P2, o2, (uint32_t)pcap)) {
+        fail = true;
+        break;
+      }
+      if ((int)((o1 - b1) + (o2 - b2)) < LN_MIN_LEN + 1) continue;  // short edge: dropped, its pixels stay marked
+      if (lane == 0) {
+        fS[ne] = b1;
+        sS[ne] = b2;
+      }
+      b1 = o1;
+      b2 = o2;
+      ne++;
     }
-    const bool horiz = (C[idx] & LN_HORIZ) != 0;
-    uint32_t o1 = 0, o2 = 0;
-    if (!walk(C, W, H, bits, x, y, horiz ? LN_RIGHT : LN_DOWN, st, P1, o1, (uint32_t)pcap, T)) {
-      fail = true;
-      break;
-    }
-    if (lane == 0) atomicAnd(&bits[idx >> 5], ~(1u << (idx & 31)));  // the second part walks the anchor again
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (!walk(C, W, H, bits, x, y, horiz ? LN_LEFT : LN_UP, st, P2, o2, (uint32_t)pcap, T)) {
-      fail = true;
-      break;
-    }
-    if ((int)(o1 + o2) < LN_MIN_LEN + 1) continue;  // short edge: dropped, its pixels stay marked
-    // chain: the first part reversed, then the second part without its copy of the anchor
-    __syncthreads();
-    if (nq + o1 + o2 > 2u * (uint32_t)pcap) {
-      fail = true;
-      break;
-    }
-    if (lane == 0) S[ne] = nq;
-    for (uint32_t i = lane; i < o1; i += 64) Q[nq + i] = P1[o1 - 1 - i];
-    for (uint32_t i = 1 + lane; i < o2; i += 64) Q[nq + o1 + i - 1] = P2[i];
-    nq += o1 + (o2 > 0 ? o2 - 1 : 0);
-    ne++;
-    __syncthreads();
+  }
+  if (ne > ecap) fail = true;
+  if (fail) {
+    if (lane == 0) nedge[f] = -1;
+    return;
   }
   if (lane == 0) {
-    if (!fail) S[ne] = nq;
-    nedge[f] = fail ? -1 : ne;
+    fS[ne] = b1;
+    sS[ne] = b2;
   }
+  __syncthreads();  // lane 0's P1 / P2 stores complete, fS / sS visible
+  for (int e = lane; e <= ne; e += 64) S[e] = fS[e] + sS[e] - (uint32_t)e;
+  int e = 0;
+  for (uint32_t t = lane; t < b1; t += 64) {  // part 1 of chain e, reversed
+    while (fS[e + 1] <= t) e++;
+    Q[fS[e] + sS[e] - (uint32_t)e + fS[e + 1] - 1 - t] = P1[t];
+  }
+  e = 0;
+  for (uint32_t t = lane; t < b2; t += 64) {  // part 2 without its first pixel (the anchor)
+    while (sS[e + 1] <= t) e++;
+    if (t > sS[e]) Q[fS[e + 1] + t - (uint32_t)e - 1] = P2[t];
+  }
+  if (lane == 0) nedge[f] = ne;
 }
 
 // ---------------------------------------------------------------- EDline
@@ -679,11 +782,14 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
 struct LineEngine {
   int dev = 0, W = 0, H = 0, B = 0;
   int acap = 0, pcap = 0, ecap = 0;
+  int MP = 0;  // the move bytes' row pitch (a multiple of 16)
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
   uint8_t* d_blur = nullptr;
   int16_t *d_dx = nullptr, *d_dy = nullptr;
   uint16_t* d_code = nullptr;
+  uint8_t* d_moves = nullptr;
+  uint16_t* d_amask = nullptr;  // [frame][row band][candidate column] anchor row masks
   uint32_t *d_anch = nullptr, *d_p1 = nullptr, *d_p2 = nullptr, *d_chain = nullptr, *d_sid = nullptr,
            *d_lscr = nullptr;
   int *d_nanch = nullptr, *d_nedge = nullptr;
@@ -692,7 +798,7 @@ struct LineEngine {
   int* d_nlines = nullptr;
   int* h_n = nullptr;  // pinned: the single-frame line count
   ~LineEngine() {
-    void* p[] = {d_blur, d_dx, d_dy, d_code, d_anch, d_p1, d_p2, d_chain, d_sid, d_lscr, d_nanch, d_nedge, d_img,
+    void* p[] = {d_blur, d_dx, d_dy, d_code, d_moves, d_amask, d_anch, d_p1, d_p2, d_chain, d_sid, d_lscr, d_nanch, d_nedge, d_img,
                  d_lines, d_nlines};
     for (void* q : p)
       if (q) (void)hipFree(q);
@@ -717,6 +823,11 @@ static void gauss5(int* k) {
   }
 }
 
+// k_edge_draw's dynamic LDS: the edge bitmap, the chains' fS / sS starts, the move tile
+static size_t edge_draw_lds(int W, int H, int ecap) {
+  return ((size_t)((((W * H + 31) / 32) + 3) & ~3) + 2 * (size_t)((ecap + 2 + 3) & ~3)) * 4 + (size_t)LE_TW * LE_TH;
+}
+
 }  // namespace eao
 
 using namespace eao;
@@ -734,10 +845,10 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
     set_error("no usable gfx950 device (the engine has no CPU fallback)");
     return EAO_E_NODEVICE;
   }
-  // the same dynamic LDS k_edge_draw is launched with: the edge bitmap (16-byte padded) +
-  // the gradient-code tile
-  if ((size_t)(((width * height + 31) / 32 + 3) & ~3) * 4 + sizeof(uint16_t) * LN_TS * LN_TS > 160 * 1024) {
-    set_error("eao_lines_create: the per-frame edge bitmap and code tile exceed the LDS");
+  // the same dynamic LDS k_edge_draw is launched with (edge bitmap, chain starts, move tile);
+  // EdgeDrawing's arrays: edgePixelArraySize = pixels / 5, maxNumOfEdge = that / 20
+  if (edge_draw_lds(width, height, width * height / 5 / 20) > 160 * 1024) {
+    set_error("eao_lines_create: the per-frame edge bitmap, chain starts and move tile exceed the LDS");
     return EAO_E_CAPACITY;
   }
   eao_lines* L = new eao_lines();
@@ -746,8 +857,8 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   e.W = width;
   e.H = height;
   e.B = max_batch;
-  // EdgeDrawing's arrays: edgePixelArraySize = pixels / 5, maxNumOfEdge = that / 20
   e.pcap = width * height / 5;
+  e.MP = (width + 15) & ~15;
   e.acap = e.pcap;
   e.ecap = e.pcap / 20;
   int k5[5];
@@ -763,6 +874,9 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&e.d_blur, px) != hipSuccess || hipMalloc(&e.d_dx, px * 2) != hipSuccess ||
       hipMalloc(&e.d_dy, px * 2) != hipSuccess || hipMalloc(&e.d_code, px * 2) != hipSuccess ||
+      hipMalloc(&e.d_moves, (size_t)e.MP * height * max_batch) != hipSuccess ||
+      hipMalloc(&e.d_amask, (size_t)((width + LF_TW - 1) / LF_TW) * (LF_TW / 2) * ((height + LF_TH - 1) / LF_TH) * 2 *
+                                max_batch) != hipSuccess ||
       hipMalloc(&e.d_anch, (size_t)e.acap * 4 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_p1, (size_t)e.pcap * 4 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_p2, (size_t)e.pcap * 4 * max_batch) != hipSuccess ||
@@ -801,20 +915,23 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = stream ? (hipStream_t)stream : e.stream;
   const int W = e.W, H = e.H;
-  const dim3 bg((W + LB_TW - 1) / LB_TW, (H + LB_TH - 1) / LB_TH, nframes);
+  const dim3 bg((W + LF_TW - 1) / LF_TW, (H + LF_TH - 1) / LF_TH, nframes);
   const long long fs = (long long)pitch * H;
+  // inner tiles stage their rows with aligned 4-byte loads when the layout allows it
+  const int vec = (pitch % 4 == 0 && fs % 4 == 0 && ((uintptr_t)d_img & 3) == 0) ? 1 : 0;
   if (channels == 1)
-    hipLaunchKernelGGL(k_line_blur<1>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
+    hipLaunchKernelGGL(k_line_maps<1>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.MP, e.k[0], e.k[1], e.k[2], vec,
+                       e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
   else if (channels == 3)
-    hipLaunchKernelGGL(k_line_blur<3>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
+    hipLaunchKernelGGL(k_line_maps<3>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.MP, e.k[0], e.k[1], e.k[2], vec,
+                       e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
   else
-    hipLaunchKernelGGL(k_line_blur<4>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.k[0], e.k[1], e.k[2], e.d_blur);
-  hipLaunchKernelGGL(k_line_grad, dim3((W * H + 255) / 256, nframes), dim3(256), 0, s, e.d_blur, W, H, e.d_dx,
-                     e.d_dy, e.d_code);
-  hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_code, W, H, e.d_anch, e.acap, e.d_nanch);
-  const size_t lds = (size_t)(((W * H + 31) / 32 + 3) & ~3) * 4 + sizeof(uint16_t) * LN_TS * LN_TS;
-  hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), lds, s, e.d_code, W, H, e.d_anch, e.d_nanch, e.acap,
-                     e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
+    hipLaunchKernelGGL(k_line_maps<4>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.MP, e.k[0], e.k[1], e.k[2], vec,
+                       e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
+  hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
+                     e.d_anch, e.acap, e.d_nanch);
+  hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W, H, e.MP,
+                     e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
   // (the parts scratch P1 is dead after k_edge_draw: it holds the per-chain line counts)
   hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
                      e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_p1, min_length, d_lines, d_counts,
