@@ -28,6 +28,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 #include "../../include/eao_accel.h"
@@ -375,30 +376,23 @@ __device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, in
 // (one per lane, with their move byte); the ones an earlier walk has marked are dropped by one
 // ballot after each walk, so an anchor costs no round trip of its own. Both parts of a chain
 // go to P1 / P2 at the reference's running offsets offF / offS (a short chain's pixels are
-// overwritten by the next walk, as there); the chains are assembled into Q once the frame is
-// done, by the whole wave: the first part reversed, then the second without its copy of the
-// anchor (chain e starts at fS[e] + sS[e] - e).
-__global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ moves, int W, int H, int MP,
-                                                  const uint32_t* __restrict__ anchors, const int* __restrict__ nanchor,
-                                                  int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2,
-                                                  int pcap, uint32_t* __restrict__ chains, uint32_t* __restrict__ sid,
-                                                  int ecap, int* __restrict__ nedge) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
-  const int f = blockIdx.x, lane = threadIdx.x;
-  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
-  uint32_t* bits = lds_ed;
-  uint32_t* fS = bits + nbp;  // the kept chains' offF / offS starts (the reference's fS / sS)
-  uint32_t* sS = fS + ep;
-  MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
+// overwritten by the next walk, as there); chain e is P1[fS[e], fS[e + 1]) reversed, then
+// P2[sS[e] + 1, sS[e + 1]) (the second part without its copy of the anchor), and it starts at
+// fS[e] + sS[e] - e in the assembled chain array Q. STREAM (k_edge_lines): each kept chain is
+// published to the workgroup's line waves as soon as it is complete (*pub = chains complete,
+// release); the walk's pixel stores are made visible to them first. Returns the number of
+// chains, or -1 where the reference returns -1.
+template <bool STREAM>
+__device__ int ed_walker(const uint8_t* __restrict__ M, int W, int H, int MP, const uint32_t* __restrict__ A, int na,
+                         int acap, uint32_t* __restrict__ P1, uint32_t* __restrict__ P2, int pcap, int ecap,
+                         uint32_t* bits, uint32_t* fS, uint32_t* sS, MoveTile& T, int* pub) {
+  const int lane = lane_id();
+  const int nb = (W * H + 31) / 32;
   for (int i = lane; i < nb; i += 64) bits[i] = 0;
-  __syncthreads();
-  const uint8_t* M = moves + (long long)f * MP * H;
-  const uint32_t* A = anchors + (long long)f * acap;
-  uint32_t* P1 = p1 + (long long)f * pcap;
-  uint32_t* P2 = p2 + (long long)f * pcap;
-  uint32_t* Q = chains + (long long)f * 2 * pcap;
-  uint32_t* S = sid + (long long)f * (ecap + 1);
-  const int na = nanchor[f];
+  if (lane == 0) {
+    fS[0] = 0;
+    sS[0] = 0;
+  }
   uint32_t b1 = 0, b2 = 0;  // offF / offS after the last kept chain
   int ne = 0;               // offPS
   bool fail = na > acap;    // anchorsSize > edgePixelArraySize (acap is that size)
@@ -431,26 +425,48 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ mo
         break;
       }
       if ((int)((o1 - b1) + (o2 - b2)) < LN_MIN_LEN + 1) continue;  // short edge: dropped, its pixels stay marked
-      if (lane == 0) {
-        fS[ne] = b1;
-        sS[ne] = b2;
-      }
       b1 = o1;
       b2 = o2;
       ne++;
+      if (ne <= ecap + 1 && lane == 0) {  // the end of chain ne - 1 = the start of the next
+        fS[ne] = b1;
+        sS[ne] = b2;
+      }
+      if (STREAM) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the chain's pixels and bounds first
+        if (lane == 0) __hip_atomic_store(pub, ne, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   }
   if (ne > ecap) fail = true;
-  if (fail) {
+  return fail ? -1 : ne;
+}
+
+__global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ moves, int W, int H, int MP,
+                                                  const uint32_t* __restrict__ anchors, const int* __restrict__ nanchor,
+                                                  int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2,
+                                                  int pcap, uint32_t* __restrict__ chains, uint32_t* __restrict__ sid,
+                                                  int ecap, int* __restrict__ nedge) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
+  uint32_t* bits = lds_ed;
+  uint32_t* fS = bits + nbp;  // the kept chains' offF / offS starts (the reference's fS / sS)
+  uint32_t* sS = fS + ep;
+  MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
+  uint32_t* P1 = p1 + (long long)f * pcap;
+  uint32_t* P2 = p2 + (long long)f * pcap;
+  uint32_t* Q = chains + (long long)f * 2 * pcap;
+  uint32_t* S = sid + (long long)f * (ecap + 1);
+  const int ne = ed_walker<false>(moves + (long long)f * MP * H, W, H, MP, anchors + (long long)f * acap, nanchor[f],
+                                  acap, P1, P2, pcap, ecap, bits, fS, sS, T, nullptr);
+  if (ne < 0) {
     if (lane == 0) nedge[f] = -1;
     return;
   }
-  if (lane == 0) {
-    fS[ne] = b1;
-    sS[ne] = b2;
-  }
   __syncthreads();  // lane 0's P1 / P2 stores complete, fS / sS visible
   for (int e = lane; e <= ne; e += 64) S[e] = fS[e] + sS[e] - (uint32_t)e;
+  const uint32_t b1 = fS[ne], b2 = sS[ne];
   int e = 0;
   for (uint32_t t = lane; t < b1; t += 64) {  // part 1 of chain e, reversed
     while (fS[e + 1] <= t) e++;
@@ -541,215 +557,195 @@ __device__ __forceinline__ void solve2(const float* ata, const float* atv, doubl
   le[1] = __dmul_rn(coef, __dsub_rn(__dmul_rn((double)ata[0], (double)atv[1]), __dmul_rn((double)ata[2], (double)atv[0])));
 }
 
-// one wave per frame: chains Q / S -> lines out [cap][6] (sx, sy, ex, ey, angle, length)
-__global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __restrict__ code,
-                                                          const int16_t* __restrict__ dxi,
-                                                          const int16_t* __restrict__ dyi, int W, int H,
-                                                          const uint32_t* __restrict__ chains,
-                                                          const uint32_t* __restrict__ sid,
-                                                          const int* __restrict__ nedge, int pcap, int ecap,
-                                                          uint32_t* __restrict__ lscratch,
-                                                          uint32_t* __restrict__ ccount, float min_length,
-                                                          float* __restrict__ out, int* __restrict__ nout, int cap) {
-  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint16_t* C = code + (long long)f * W * H;
-  const int16_t* DX = dxi + (long long)f * W * H;
-  const int16_t* DY = dyi + (long long)f * W * H;
-  const uint32_t* Q = chains + (long long)f * 2 * pcap;
-  const uint32_t* S = sid + (long long)f * (ecap + 1);
-  uint32_t* L = lscratch + (long long)f * 2 * pcap;
-  float* O = out + (long long)f * cap * 6;
-  int* CNT = (int*)(ccount + (long long)f * pcap);  // lines kept per chain
-  const int ne = nedge[f];
-  if (ne < 0) {  // the whole workgroup
-    if (threadIdx.x == 0) nout[f] = -1;
-    return;
-  }
-  const double logNT = 2.0 * (log10((double)W) + log10((double)H));
+// EDline on one chain (:2380-2906): Q[s0, end) -> the chain's kept lines as records of 6
+// words at L[s0 + 6 k] (L[s0, end) is the chain's own scratch), their count in CNT[e]; one wave
+__device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* __restrict__ Q, uint32_t* __restrict__ L,
+                               const uint16_t* __restrict__ C, const int16_t* __restrict__ DX,
+                               const int16_t* __restrict__ DY, int W, int H, double logNT, float min_length,
+                               int* __restrict__ CNT) {
+  const int lane = lane_id();
   auto horiz_at = [&](uint32_t p) { return (C[px_y(p) * W + px_x(p)] & LN_HORIZ) != 0; };
-  // chains are independent: wave w takes chains w, w + nw, ...; a chain's line pixels use its
-  // own stretch of the scratch [S[e], S[e + 1]), and its kept lines are parked at the start
-  // of that stretch (record k at 6 k: below the next line's pixels, see the store) until the
-  // block places every chain's lines in chain order
-  for (int e = wave; e < ne; e += nw) {
-    uint32_t s = S[e];
-    const uint32_t end = S[e + 1];
-    uint32_t offL = s;
-    int nl = 0;
-    double le2[2] = {0, 0};
-    float ata[4], atv[2];
+  uint32_t s = s0;
+  uint32_t offL = s;
+  int nl = 0;
+  double le2[2] = {0, 0};
+  float ata[4], atv[2];
+  while (end > s + LN_MIN_LEN) {
+    double fitErr = 0;
     while (end > s + LN_MIN_LEN) {
-      double fitErr = 0;
-      while (end > s + LN_MIN_LEN) {
-        const bool h0 = horiz_at(Q[s]);
-        fit_block(Q, s, s + LN_MIN_LEN, h0, ata, atv);
-        solve2(ata, atv, le2);
-        double c2 = 0;  // fit error in the reference's order: one lane, sequential
-        for (uint32_t i = s; i < s + LN_MIN_LEN; i++) {
-          const uint32_t p = Q[i];
-          const double u = (double)(h0 ? px_x(p) : px_y(p)), v = (double)(h0 ? px_y(p) : px_x(p));
-          const double c = __dsub_rn(__dsub_rn(v, __dmul_rn(u, le2[0])), le2[1]);
-          c2 = __dadd_rn(c2, __dmul_rn(c, c));
-        }
-        fitErr = sqrt(c2);
-        if (fitErr <= LN_FIT_ERR) break;
-        s += LN_SKIP;
+      const bool h0 = horiz_at(Q[s]);
+      fit_block(Q, s, s + LN_MIN_LEN, h0, ata, atv);
+      solve2(ata, atv, le2);
+      double c2 = 0;  // fit error in the reference's order: one lane, sequential
+      for (uint32_t i = s; i < s + LN_MIN_LEN; i++) {
+        const uint32_t p = Q[i];
+        const double u = (double)(h0 ? px_x(p) : px_y(p)), v = (double)(h0 ? px_y(p) : px_x(p));
+        const double c = __dsub_rn(__dsub_rn(v, __dmul_rn(u, le2[0])), le2[1]);
+        c2 = __dadd_rn(c2, __dmul_rn(c, c));
       }
-      if (fitErr > LN_FIT_ERR) break;
-      const uint32_t lineStart = offL;
-      const bool horiz = horiz_at(Q[s]);
-      double coef1 = 0;
-      bool extended = true, first = true;
-      int tryTimes = 0, outliers = 0;
-      uint32_t newOffS = 0;
-      while (extended) {
-        tryTimes++;
-        if (first) {
-          first = false;
-          for (int i = lane; i < LN_MIN_LEN; i += 64) L[offL + i] = Q[s + i];
-          offL += LN_MIN_LEN;
-          s += LN_MIN_LEN;
-        } else {
-          float ta[4], tv[2];
-          fit_block(L, newOffS, offL, horiz, ta, tv);
-          for (int q = 0; q < 4; q++) ata[q] = fadd(ata[q], ta[q]);
-          for (int q = 0; q < 2; q++) atv[q] = fadd(atv[q], tv[q]);
-          solve2(ata, atv, le2);
-        }
-        coef1 = 1 / sqrt(__dadd_rn(__dmul_rn(le2[0], le2[0]), 1.0));
-        outliers = 0;
-        newOffS = offL;
-        // the extension walk: sequential in the reference (it stops after four outliers
-        // in a row); evaluated 64 pixels at a time, the stop found by ballot
-        while (end > s) {
-          const uint32_t i = s + lane;
-          bool out_ = false;
-          if (i < end) {
-            const uint32_t p = Q[i];
-            const double xx = (double)px_x(p), yy = (double)px_y(p);
-            const double d = horiz ? fabs(__dadd_rn(__dsub_rn(__dmul_rn(le2[0], xx), yy), le2[1]))
-                                   : fabs(__dsub_rn(__dsub_rn(xx, __dmul_rn(le2[0], yy)), le2[1]));
-            out_ = __dmul_rn(d, coef1) > LN_FIT_ERR;
-            L[offL + lane] = p;
-          }
-          const uint64_t om = ballot(i < end && out_);
-          const int nvalid = (int)min<uint32_t>(64u, end - s);
-          // replay the sequential outlier counter over this block
-          int stop = -1, run = outliers;
-          for (int j = 0; j < nvalid; j++) {
-            if ((om >> j) & 1ull) {
-              if (++run > 3) {
-                stop = j;
-                break;
-              }
-            } else {
-              run = 0;
-            }
-          }
-          outliers = run;
-          if (stop >= 0) {
-            offL += (uint32_t)stop + 1;
-            s += (uint32_t)stop + 1;
-            break;
-          }
-          offL += (uint32_t)nvalid;
-          s += (uint32_t)nvalid;
-        }
-        offL -= (uint32_t)outliers;
-        s -= (uint32_t)outliers;
-        extended = offL - newOffS > 0 && tryTimes < LN_TRY;
-      }
-      double le[3];
-      if (horiz) {
-        le[0] = __dmul_rn(le2[0], coef1);
-        le[1] = -1 * coef1;
-        le[2] = __dmul_rn(le2[1], coef1);
+      fitErr = sqrt(c2);
+      if (fitErr <= LN_FIT_ERR) break;
+      s += LN_SKIP;
+    }
+    if (fitErr > LN_FIT_ERR) break;
+    const uint32_t lineStart = offL;
+    const bool horiz = horiz_at(Q[s]);
+    double coef1 = 0;
+    bool extended = true, first = true;
+    int tryTimes = 0, outliers = 0;
+    uint32_t newOffS = 0;
+    while (extended) {
+      tryTimes++;
+      if (first) {
+        first = false;
+        for (int i = lane; i < LN_MIN_LEN; i += 64) L[offL + i] = Q[s + i];
+        offL += LN_MIN_LEN;
+        s += LN_MIN_LEN;
       } else {
-        le[0] = 1 * coef1;
-        le[1] = __dmul_rn(-le2[0], coef1);
-        le[2] = __dmul_rn(-le2[1], coef1);
+        float ta[4], tv[2];
+        fit_block(L, newOffS, offL, horiz, ta, tv);
+        for (int q = 0; q < 4; q++) ata[q] = fadd(ata[q], ta[q]);
+        for (int q = 0; q < 2; q++) atv[q] = fadd(atv[q], tv[q]);
+        solve2(ata, atv, le2);
       }
-      // LineValidation_ (:2793-2874)
-      const int n = (int)(offL - lineStart);
-      int mgx = 0, mgy = 0;
+      coef1 = 1 / sqrt(__dadd_rn(__dmul_rn(le2[0], le2[0]), 1.0));
+      outliers = 0;
+      newOffS = offL;
+      // the extension walk: sequential in the reference (it stops after four outliers
+      // in a row); evaluated 64 pixels at a time, the stop found by ballot
+      while (end > s) {
+        const uint32_t i = s + lane;
+        bool out_ = false;
+        if (i < end) {
+          const uint32_t p = Q[i];
+          const double xx = (double)px_x(p), yy = (double)px_y(p);
+          const double d = horiz ? fabs(__dadd_rn(__dsub_rn(__dmul_rn(le2[0], xx), yy), le2[1]))
+                                 : fabs(__dsub_rn(__dsub_rn(xx, __dmul_rn(le2[0], yy)), le2[1]));
+          out_ = __dmul_rn(d, coef1) > LN_FIT_ERR;
+          L[offL + lane] = p;
+        }
+        const uint64_t om = ballot(i < end && out_);
+        const int nvalid = (int)min<uint32_t>(64u, end - s);
+        // replay the sequential outlier counter over this block
+        int stop = -1, run = outliers;
+        for (int j = 0; j < nvalid; j++) {
+          if ((om >> j) & 1ull) {
+            if (++run > 3) {
+              stop = j;
+              break;
+            }
+          } else {
+            run = 0;
+          }
+        }
+        outliers = run;
+        if (stop >= 0) {
+          offL += (uint32_t)stop + 1;
+          s += (uint32_t)stop + 1;
+          break;
+        }
+        offL += (uint32_t)nvalid;
+        s += (uint32_t)nvalid;
+      }
+      offL -= (uint32_t)outliers;
+      s -= (uint32_t)outliers;
+      extended = offL - newOffS > 0 && tryTimes < LN_TRY;
+    }
+    double le[3];
+    if (horiz) {
+      le[0] = __dmul_rn(le2[0], coef1);
+      le[1] = -1 * coef1;
+      le[2] = __dmul_rn(le2[1], coef1);
+    } else {
+      le[0] = 1 * coef1;
+      le[1] = __dmul_rn(-le2[0], coef1);
+      le[2] = __dmul_rn(-le2[1], coef1);
+    }
+    // LineValidation_ (:2793-2874)
+    const int n = (int)(offL - lineStart);
+    int mgx = 0, mgy = 0;
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t p = L[lineStart + i];
+      const int idx = px_y(p) * W + px_x(p);
+      mgx += DX[idx];
+      mgy += DY[idx];
+    }
+    mgx = wave_sum(mgx);
+    mgy = wave_sum(mgy);
+    const double dxl = fabs(le[1]), dyl = fabs(le[0]);
+    bool ok = !(mgx == 0 && mgy == 0);
+    float direction = 0.f;
+    if (ok) {
+      if (mgx > 0 && mgy >= 0) direction = (float)atan2(-dyl, dxl);
+      if (mgx <= 0 && mgy > 0) direction = (float)atan2(dyl, dxl);
+      if (mgx < 0 && mgy <= 0) direction = (float)atan2(dyl, -dxl);
+      if (mgx >= 0 && mgy < 0) direction = (float)atan2(-dyl, -dxl);
+      const double fd = (double)fabsf(direction);
+      if (fd < 0.15 || M_PI - fd < 0.15)
+        if (fabs(le[2]) < 10 || fabs(H - fabs(le[2])) < 10) ok = false;
+      if (fabs(fd - M_PI * 0.5) < 0.15)
+        if (fabs(le[2]) < 10 || fabs(W - fabs(le[2])) < 10) ok = false;
+    }
+    if (ok) {
+      int k = 0;
       for (int i = lane; i < n; i += 64) {
         const uint32_t p = L[lineStart + i];
         const int idx = px_y(p) * W + px_x(p);
-        mgx += DX[idx];
-        mgy += DY[idx];
+        const double pd = atan2(-(double)DX[idx], (double)DY[idx]);
+        const double dd = fabs((double)direction - pd);
+        if (fabs(2 * M_PI - dd) < 0.392699 || dd < 0.392699) k++;
       }
-      mgx = wave_sum(mgx);
-      mgy = wave_sum(mgy);
-      const double dxl = fabs(le[1]), dyl = fabs(le[0]);
-      bool ok = !(mgx == 0 && mgy == 0);
-      float direction = 0.f;
-      if (ok) {
-        if (mgx > 0 && mgy >= 0) direction = (float)atan2(-dyl, dxl);
-        if (mgx <= 0 && mgy > 0) direction = (float)atan2(dyl, dxl);
-        if (mgx < 0 && mgy <= 0) direction = (float)atan2(dyl, -dxl);
-        if (mgx >= 0 && mgy < 0) direction = (float)atan2(-dyl, -dxl);
-        const double fd = (double)fabsf(direction);
-        if (fd < 0.15 || M_PI - fd < 0.15)
-          if (fabs(le[2]) < 10 || fabs(H - fabs(le[2])) < 10) ok = false;
-        if (fabs(fd - M_PI * 0.5) < 0.15)
-          if (fabs(le[2]) < 10 || fabs(W - fabs(le[2])) < 10) ok = false;
-      }
-      if (ok) {
-        int k = 0;
-        for (int i = lane; i < n; i += 64) {
-          const uint32_t p = L[lineStart + i];
-          const int idx = px_y(p) * W + px_x(p);
-          const double pd = atan2(-(double)DX[idx], (double)DY[idx]);
-          const double dd = fabs((double)direction - pd);
-          if (fabs(2 * M_PI - dd) < 0.392699 || dd < 0.392699) k++;
-        }
-        k = wave_sum(k);
-        ok = ln_nfa(n, k, 0.125, logNT) > 0;
-      }
-      if (ok) {
-        const double a1 = __dmul_rn(le[1], le[1]), a2 = __dmul_rn(le[0], le[0]), a3 = __dmul_rn(le[0], le[1]),
-                     a4 = __dmul_rn(le[2], le[0]), a5 = __dmul_rn(le[2], le[1]);
-        const uint32_t p0 = L[lineStart], p1 = L[offL - 1];
-        float ep[4];
-        ep[0] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a1, (double)px_x(p0)), __dmul_rn(a3, (double)px_y(p0))), a4);
-        ep[1] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a2, (double)px_y(p0)), __dmul_rn(a3, (double)px_x(p0))), a5);
-        ep[2] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a1, (double)px_x(p1)), __dmul_rn(a3, (double)px_y(p1))), a4);
-        ep[3] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a2, (double)px_y(p1)), __dmul_rn(a3, (double)px_x(p1))), a5);
-        // OctaveKeyLines: length from the fitted endpoints, start / end by direction
-        const float dxa = fabsf(fsub(ep[0], ep[2])), dya = fabsf(fsub(ep[1], ep[3]));
-        // sqrt of the float sum, correctly rounded (through double: innocuous double rounding)
-        const float length = (float)sqrt((double)fadd(fmul(dxa, dxa), fmul(dya, dya)));
-        const float ddx = fsub(ep[2], ep[0]), ddy = fsub(ep[3], ep[1]);
-        const double d = (double)direction;
-        bool change = false;
-        if (d >= -0.75 * M_PI && d < -0.25 * M_PI && ddy > 0) change = true;
-        if (d >= -0.25 * M_PI && d < 0.25 * M_PI && ddx < 0) change = true;
-        if (d >= 0.25 * M_PI && d < 0.75 * M_PI && ddy < 0) change = true;
-        if (((d >= 0.75 * M_PI && d < M_PI) || (d >= -M_PI && d < -0.75 * M_PI)) && ddx > 0) change = true;
-        if (length > min_length) {
-          // record nl of this chain at L[S[e] + 6 nl]: every earlier kept line of the chain
-          // spans >= LN_MIN_LEN - 3 > 6 pixels, so the record lies below this line's start
-          // (or, for nl = 0, over this line's own pixels, read above)
-          if (lane < 6) {
-            const float v = lane == 0 ? (change ? ep[2] : ep[0])
-                          : lane == 1 ? (change ? ep[3] : ep[1])
-                          : lane == 2 ? (change ? ep[0] : ep[2])
-                          : lane == 3 ? (change ? ep[1] : ep[3])
-                          : lane == 4 ? direction : length;
-            L[S[e] + 6 * nl + lane] = __float_as_uint(v);
-          }
-          nl++;
-        }
-      } else {
-        offL = lineStart;
-      }
+      k = wave_sum(k);
+      ok = ln_nfa(n, k, 0.125, logNT) > 0;
     }
-    if (lane == 0) CNT[e] = nl;
+    if (ok) {
+      const double a1 = __dmul_rn(le[1], le[1]), a2 = __dmul_rn(le[0], le[0]), a3 = __dmul_rn(le[0], le[1]),
+                   a4 = __dmul_rn(le[2], le[0]), a5 = __dmul_rn(le[2], le[1]);
+      const uint32_t p0 = L[lineStart], p1 = L[offL - 1];
+      float ep[4];
+      ep[0] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a1, (double)px_x(p0)), __dmul_rn(a3, (double)px_y(p0))), a4);
+      ep[1] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a2, (double)px_y(p0)), __dmul_rn(a3, (double)px_x(p0))), a5);
+      ep[2] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a1, (double)px_x(p1)), __dmul_rn(a3, (double)px_y(p1))), a4);
+      ep[3] = (float)__dsub_rn(__dsub_rn(__dmul_rn(a2, (double)px_y(p1)), __dmul_rn(a3, (double)px_x(p1))), a5);
+      // OctaveKeyLines: length from the fitted endpoints, start / end by direction
+      const float dxa = fabsf(fsub(ep[0], ep[2])), dya = fabsf(fsub(ep[1], ep[3]));
+      // sqrt of the float sum, correctly rounded (through double: innocuous double rounding)
+      const float length = (float)sqrt((double)fadd(fmul(dxa, dxa), fmul(dya, dya)));
+      const float ddx = fsub(ep[2], ep[0]), ddy = fsub(ep[3], ep[1]);
+      const double d = (double)direction;
+      bool change = false;
+      if (d >= -0.75 * M_PI && d < -0.25 * M_PI && ddy > 0) change = true;
+      if (d >= -0.25 * M_PI && d < 0.25 * M_PI && ddx < 0) change = true;
+      if (d >= 0.25 * M_PI && d < 0.75 * M_PI && ddy < 0) change = true;
+      if (((d >= 0.75 * M_PI && d < M_PI) || (d >= -M_PI && d < -0.75 * M_PI)) && ddx > 0) change = true;
+      if (length > min_length) {
+        // record nl of this chain at L[S[e] + 6 nl]: every earlier kept line of the chain
+        // spans >= LN_MIN_LEN - 3 > 6 pixels, so the record lies below this line's start
+        // (or, for nl = 0, over this line's own pixels, read above)
+        if (lane < 6) {
+          const float v = lane == 0 ? (change ? ep[2] : ep[0])
+                        : lane == 1 ? (change ? ep[3] : ep[1])
+                        : lane == 2 ? (change ? ep[0] : ep[2])
+                        : lane == 3 ? (change ? ep[1] : ep[3])
+                        : lane == 4 ? direction : length;
+          L[s0 + 6 * nl + lane] = __float_as_uint(v);
+        }
+        nl++;
+      }
+    } else {
+      offL = lineStart;
+    }
   }
-  __syncthreads();
-  // the chains' lines in chain order: a block scan of the per-chain counts; a chain's thread
-  // copies its records (lines past cap are counted, not stored, as the reference's nl)
+  if (lane == 0) CNT[e] = nl;
+}
+
+// the chains' lines in chain order: a block scan of the per-chain counts; a chain's thread
+// copies its records (lines past cap are counted, not stored, as the reference's nl). The whole
+// workgroup; returns the line count.
+__device__ int ed_place_lines(int ne, const uint32_t* __restrict__ S, const uint32_t* __restrict__ L,
+                              const int* __restrict__ CNT, float* __restrict__ O, int cap) {
   __shared__ int wsum[16], carry;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (threadIdx.x == 0) carry = 0;
   __syncthreads();
   for (int c0 = 0; c0 < ne; c0 += blockDim.x) {
@@ -775,7 +771,110 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
     if (threadIdx.x == blockDim.x - 1) carry = base + v;
     __syncthreads();
   }
-  if (threadIdx.x == 0) nout[f] = carry;
+  return carry;
+}
+
+// one workgroup of LN_WAVES waves per frame: chains Q / S -> lines out [cap][6] (sx, sy, ex, ey,
+// angle, length); chains are independent: wave w takes chains w, w + nw, ...
+__global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __restrict__ code,
+                                                          const int16_t* __restrict__ dxi,
+                                                          const int16_t* __restrict__ dyi, int W, int H,
+                                                          const uint32_t* __restrict__ chains,
+                                                          const uint32_t* __restrict__ sid,
+                                                          const int* __restrict__ nedge, int pcap, int ecap,
+                                                          uint32_t* __restrict__ lscratch,
+                                                          uint32_t* __restrict__ ccount, float min_length,
+                                                          float* __restrict__ out, int* __restrict__ nout, int cap) {
+  const int f = blockIdx.x, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const long long fo = (long long)f * W * H;
+  const uint32_t* Q = chains + (long long)f * 2 * pcap;
+  const uint32_t* S = sid + (long long)f * (ecap + 1);
+  uint32_t* L = lscratch + (long long)f * 2 * pcap;
+  int* CNT = (int*)(ccount + (long long)f * (ecap + 1));  // lines kept per chain
+  const int ne = nedge[f];
+  if (ne < 0) {  // the whole workgroup
+    if (threadIdx.x == 0) nout[f] = -1;
+    return;
+  }
+  const double logNT = 2.0 * (log10((double)W) + log10((double)H));
+  for (int e = wave; e < ne; e += nw)
+    ed_chain_lines(e, S[e], S[e + 1], Q, L, code + fo, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
+  __syncthreads();
+  const int n = ed_place_lines(ne, S, L, CNT, out + (long long)f * cap * 6, cap);
+  if (threadIdx.x == 0) nout[f] = n;
+}
+
+// EdgeDrawing + EDline of a frame in one workgroup: wave 0 walks (ed_walker<true>) and publishes
+// each kept chain; the other LE_WAVES - 1 waves take the published chains in order (an LDS
+// ticket), assemble each into Q and run EDline on it while the walk goes on, so a frame costs
+// its walk plus the last chains' lines instead of the walk plus all of EDline. Four waves: EDline
+// needs ~250 VGPRs, so two workgroups per CU (the LDS allows two) hold 2 waves per SIMD, and all
+// 405 frames of a step run in one round over the 256 CUs (8 waves: one workgroup per CU, two
+// rounds, 9.9 ms against 6.5 ms per 405 frames; r04_ab_lines.txt).
+constexpr int LE_WAVES = 4;
+__global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
+    const uint8_t* __restrict__ moves, int W, int H, int MP, const uint32_t* __restrict__ anchors,
+    const int* __restrict__ nanchor, int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2, int pcap,
+    uint32_t* __restrict__ chains, uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
+    const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi, const int16_t* __restrict__ dyi,
+    uint32_t* __restrict__ lscratch, uint32_t* __restrict__ ccount, float min_length, float* __restrict__ out,
+    int* __restrict__ nout, int cap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
+  __shared__ int pub, ticket, state;  // chains published, next chain to take, 0 walking / 1 done / -1 failed
+  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
+  uint32_t* bits = lds_ed;
+  uint32_t* fS = bits + nbp;
+  uint32_t* sS = fS + ep;
+  const long long fo = (long long)f * W * H;
+  uint32_t* P1 = p1 + (long long)f * pcap;
+  uint32_t* P2 = p2 + (long long)f * pcap;
+  uint32_t* Q = chains + (long long)f * 2 * pcap;
+  uint32_t* S = sid + (long long)f * (ecap + 1);
+  uint32_t* L = lscratch + (long long)f * 2 * pcap;
+  int* CNT = (int*)(ccount + (long long)f * (ecap + 1));
+  if (threadIdx.x == 0) {
+    pub = 0;
+    ticket = 0;
+    state = 0;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
+    const int ne = ed_walker<true>(moves + (long long)f * MP * H, W, H, MP, anchors + (long long)f * acap, nanchor[f],
+                                   acap, P1, P2, pcap, ecap, bits, fS, sS, T, &pub);
+    if (lane == 0) {
+      nedge[f] = ne;
+      __hip_atomic_store(&state, ne < 0 ? -1 : 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+    const double logNT = 2.0 * (log10((double)W) + log10((double)H));
+    while (true) {
+      int e = 0;
+      if (lane == 0) e = atomicAdd(&ticket, 1);
+      e = __shfl(e, 0, 64);
+      int st = 0;
+      while (true) {  // chain e published, or the walk over
+        st = __hip_atomic_load(&state, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__hip_atomic_load(&pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > e || st != 0) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+      if (st < 0 || __hip_atomic_load(&pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= e) break;
+      const uint32_t f0 = fS[e], f1 = fS[e + 1], s0 = sS[e], s1 = sS[e + 1];
+      const uint32_t q0 = f0 + s0 - (uint32_t)e, q1 = f1 + s1 - (uint32_t)e - 1;
+      for (uint32_t i = lane; i < f1 - f0; i += 64) Q[q0 + i] = P1[f1 - 1 - i];
+      for (uint32_t i = lane + 1; i < s1 - s0; i += 64) Q[q0 + (f1 - f0) + i - 1] = P2[s0 + i];
+      if (lane == 0) S[e] = q0;
+      ed_chain_lines(e, q0, q1, Q, L, code + fo, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
+    }
+  }
+  __syncthreads();
+  if (state < 0) {
+    if (threadIdx.x == 0) nout[f] = -1;
+    return;
+  }
+  const int n = ed_place_lines(pub, S, L, CNT, out + (long long)f * cap * 6, cap);
+  if (threadIdx.x == 0) nout[f] = n;
 }
 
 // ================================================================ host
@@ -783,6 +882,7 @@ struct LineEngine {
   int dev = 0, W = 0, H = 0, B = 0;
   int acap = 0, pcap = 0, ecap = 0;
   int MP = 0;  // the move bytes' row pitch (a multiple of 16)
+  bool fused = true;  // k_edge_lines (EAO_LINES_FUSED=0: k_edge_draw, then k_edlines)
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
   uint8_t* d_blur = nullptr;
@@ -791,15 +891,15 @@ struct LineEngine {
   uint8_t* d_moves = nullptr;
   uint16_t* d_amask = nullptr;  // [frame][row band][candidate column] anchor row masks
   uint32_t *d_anch = nullptr, *d_p1 = nullptr, *d_p2 = nullptr, *d_chain = nullptr, *d_sid = nullptr,
-           *d_lscr = nullptr;
+           *d_lscr = nullptr, *d_ccnt = nullptr;
   int *d_nanch = nullptr, *d_nedge = nullptr;
   uint8_t* d_img = nullptr;  // [H][W * 4]: one host frame of up to 4 channels
   float* d_lines = nullptr;
   int* d_nlines = nullptr;
   int* h_n = nullptr;  // pinned: the single-frame line count
   ~LineEngine() {
-    void* p[] = {d_blur, d_dx, d_dy, d_code, d_moves, d_amask, d_anch, d_p1, d_p2, d_chain, d_sid, d_lscr, d_nanch, d_nedge, d_img,
-                 d_lines, d_nlines};
+    void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
+                 d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines};
     for (void* q : p)
       if (q) (void)hipFree(q);
     if (h_n) (void)hipHostFree(h_n);
@@ -859,6 +959,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   e.B = max_batch;
   e.pcap = width * height / 5;
   e.MP = (width + 15) & ~15;
+  if (const char* v = getenv("EAO_LINES_FUSED")) e.fused = v[0] != '0';
   e.acap = e.pcap;
   e.ecap = e.pcap / 20;
   int k5[5];
@@ -883,6 +984,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
       hipMalloc(&e.d_chain, (size_t)e.pcap * 8 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_lscr, (size_t)e.pcap * 8 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_sid, (size_t)(e.ecap + 1) * 4 * max_batch) != hipSuccess ||
+      hipMalloc(&e.d_ccnt, (size_t)(e.ecap + 1) * 4 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_nanch, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_nedge, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_img, (size_t)width * height * 4) != hipSuccess ||
@@ -930,12 +1032,17 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
                        e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
                      e.d_anch, e.acap, e.d_nanch);
-  hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W, H, e.MP,
-                     e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
-  // (the parts scratch P1 is dead after k_edge_draw: it holds the per-chain line counts)
-  hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
-                     e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_p1, min_length, d_lines, d_counts,
-                     cap);
+  if (e.fused) {
+    hipLaunchKernelGGL(k_edge_lines, dim3(nframes), dim3(64 * LE_WAVES), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W,
+                       H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap,
+                       e.d_nedge, e.d_code, e.d_dx, e.d_dy, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts, cap);
+  } else {
+    hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W, H, e.MP,
+                       e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
+    hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
+                       e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts,
+                       cap);
+  }
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
