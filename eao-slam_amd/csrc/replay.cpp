@@ -66,6 +66,13 @@ static hipError_t spin_event_plain(hipEvent_t e) {
     __builtin_ia32_pause();
   }
 }
+// look-ahead steps 1-2 run over kPrepChunk points per step, so a wait the look-ahead fills
+// notices its GPU result within one short step (EAO_PREP_CHUNK: A/B switch)
+static const int kPrepChunk = [] {
+  const char* v = getenv("EAO_PREP_CHUNK");
+  const int c = v ? atoi(v) : 0;
+  return c > 0 ? c : 128;
+}();
 static const bool g_sentinel = [] {
   const char* v = getenv("EAO_SENTINEL_WAIT");
   return !(v && v[0] == '0');
@@ -2481,10 +2488,12 @@ class ReplayEngine {
   }
   // fill a wait on `ev` with the next frame's steps 1-6 (until the event, or `ready()`)
   void idle_work(hipEvent_t ev) {
-    idle_work(ev, [] { return false; });
+    idle_work(ev, [] { return false; }, false);
   }
+  // (with a sentinel test the cheap ready() runs after every step and hipEventQuery, a runtime
+  // call, after every fourth)
   template <class Ready>
-  void idle_work(hipEvent_t ev, Ready&& ready) {
+  void idle_work(hipEvent_t ev, Ready&& ready, bool has_ready = true) {
     if (!prep.active) {
       if (!g_lookahead || !la_set || prep.ok || !ini) return;
       la_set = false;
@@ -2501,7 +2510,12 @@ class ReplayEngine {
       prof[53] += 1;
     }
     Tick tk(&prof[52]);
-    while (!prep.ok && !(g_sentinel && ready()) && hipEventQuery(ev) == hipErrorNotReady) prep.ok = prep_step(prep);
+    const unsigned qmask = (g_sentinel && has_ready) ? 3u : 0u;
+    for (unsigned it = 0; !prep.ok; it++) {
+      if (g_sentinel && has_ready && ready()) break;
+      if ((it & qmask) == 0 && hipEventQuery(ev) != hipErrorNotReady) break;
+      prep.ok = prep_step(prep);
+    }
   }
   void prep_begin(Prep& s, const FrameIn& in) {
     s.in = in;
@@ -2537,20 +2551,32 @@ class ReplayEngine {
           dets.push_back(std::move(f));
         }
         s.tr.resize(in.npts);
-        for (int i = 0; i < in.npts; i++) {
+        s.phase = 1;
+        s.k = 0;
+        prof[12] += now_us() - tA;
+        return false;
+      }
+      case 1: {  // the frame's map points, kPrepChunk per step
+        const int e = std::min(in.npts, (int)s.k + kPrepChunk);
+        for (int i = (int)s.k; i < e; i++) {
           MapPt* p = mappoint(in.ids[i]);
           for (int a = 0; a < 3; a++) p->pos[a] = in.pos[3 * i + a];
           p->proj_epoch = 0;
           p->bad = in.bad ? in.bad[i] != 0 : false;
           s.tr[i] = p;
         }
-        s.phase = 1;
+        s.k = (size_t)e;
+        if (e >= in.npts) {
+          s.phase = 2;
+          s.k = 0;
+        }
         prof[12] += now_us() - tA;
         return false;
       }
-      case 1: {  // STEP 2 AssociateObjAndPoints, Tracking.cc:2434-2468
+      case 2: {  // STEP 2 AssociateObjAndPoints, Tracking.cc:2434-2468 (in point order, kPrepChunk per step)
         const float* uv = in.uv;
-        for (int i = 0; i < in.npts; i++) {
+        const int e = std::min(in.npts, (int)s.k + kPrepChunk);
+        for (int i = (int)s.k; i < e; i++) {
           MapPt* p = s.tr[i];
           if (p->bad) continue;
           const int px = (int)lrintf(uv[2 * i]), py = (int)lrintf(uv[2 * i + 1]);
@@ -2562,23 +2588,24 @@ class ReplayEngine {
               for (int a = 0; a < 3; a++) f->sum[a] += p->pos[a];
             }
         }
-        s.phase = 2;
+        s.k = (size_t)e;
+        if (e >= in.npts) s.phase = 3;
         prof[12] += now_us() - tA;
         return false;
       }
-      case 2:
+      case 3:
         associate_lines(o2, &s == &prep ? &s.lines : nullptr, &s.took_lines);  // STEP 3, Tracking.cc:1286
-        s.phase = 3;
+        s.phase = 4;
         s.k = 0;
         prof[12] += now_us() - tA;
         return false;
-      case 3:  // STEP 4, one detection per step
+      case 4:  // STEP 4, one detection per step
         if (s.k < o2.size()) {
           Det* f = o2[s.k++];
           frame_mean(f);
           if (f->pts.size() >= 8) boxplot(f, P);
         }
-        if (s.k >= o2.size()) s.phase = 4;
+        if (s.k >= o2.size()) s.phase = 5;
         prof[13] += now_us() - tA;
         return false;
       default:
