@@ -202,10 +202,12 @@ def main():
                     help="extract+match single-thread CPU sample (60 frames; 3 at 1080p for config b)")
     ap.add_argument("--cpu-mt-frames", type=int, default=256, help="extract+match all-cores CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true", help="run association after extract+match")
+    ap.add_argument("--thread", action="store_true",
+                    help="A/B: replay the association on a second thread while the frame work is enqueued")
     ap.add_argument("--shard", action="store_true",
                     help="config c: the object-sharded exchange path also at world 1 (one-rank RCCL communicator)")
     ap.add_argument("--poll", action="store_true", help="A/B: poll the extraction stream while the association runs")
+    ap.add_argument("--line-batches", type=int, default=1, help="line detection in this many launches per step")
     args = ap.parse_args()
     if args.cpu_frames is None:
         args.cpu_frames = 3 if args.config == "b" else 60
@@ -302,8 +304,14 @@ def main():
         ea.color_to_gray_batch_device(d_color.data_ptr(), F, W, H, 3 * W, 3, True, d_frames.data_ptr(), W, gpu, sptr)
 
     def detect_lines():  # Frame ctor's detect_raw_lines + filter_lines of every frame (Frame.cc:324-335)
-        lines.detect_color_batch_device(d_color.data_ptr(), F, 3 * W, 3, 50.0, d_lines.data_ptr(), d_lcnt.data_ptr(),
-                                        LCAP, sptr)
+        # in --line-batches launches of consecutive frames (each frame's walk holds its CU's LDS
+        # for ~5 ms: fewer frames per launch leave CUs to the association's kernels)
+        nbat = max(1, min(args.line_batches, F))
+        for j in range(nbat):
+            f0, f1 = j * F // nbat, (j + 1) * F // nbat
+            lines.detect_color_batch_device(d_color.data_ptr() + f0 * H * W * 3, f1 - f0, 3 * W, 3, 50.0,
+                                            d_lines.data_ptr() + f0 * LCAP * 6 * 4, d_lcnt.data_ptr() + f0 * 4,
+                                            LCAP, sptr)
 
     def extract():
         orb.extract_batch_device(d_frames.data_ptr(), F, W, d_kps.data_ptr(), d_desc.data_ptr(), d_cnt.data_ptr(),
@@ -368,16 +376,19 @@ def main():
     def step(record):
         out = {}
         th = None
-        if args.no_overlap:
+        if not args.thread:
+            # the frame work is only enqueued (asynchronous launches on the extraction stream),
+            # so it runs on the GPU while this thread replays the association, the critical path
             front()
             associate(out)
         else:
+            # A/B: the association on a second Python thread (it waits for the GIL while the
+            # main thread enqueues the frame work: ~4 ms per step, r04_ab_front_enqueue.txt)
             th = threading.Thread(target=associate, args=(out,))
             th.start()
             front()
-        # the association thread is the critical path: the main thread makes no HIP call while it
-        # runs (it joins it first), then waits for the extraction stream only (a device-wide
-        # synchronize would also serialise against other streams)
+        # then wait for the extraction stream only (a device-wide synchronize would also
+        # serialise against other streams)
         ev_done.record(stream)
         if args.poll:
             while not ev_done.query():
