@@ -13,7 +13,9 @@ from tools import synth  # noqa: E402
 
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 405
 W, H, NF = (int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (640, 480, 1000)
-fr, _ = synth.frame_stream(min(F, 64) if W > 640 else F, w=W, h=H)
+# the EAO bench's frames have office-like straight structure (bench.py); STRUCT=0: the plain
+# procedural texture of Config B and the PMC extract
+fr, _ = synth.frame_stream(min(F, 64) if W > 640 else F, w=W, h=H, structure=os.environ.get("STRUCT", "1") != "0")
 fr = np.stack([fr[i % len(fr)] for i in range(F)])
 dev = torch.device("cuda", 0)
 orb = ea.Orb(NF, 1.2, 8, 20, 7, W, H, max_batch=F)
