@@ -671,14 +671,14 @@ def pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=True, reps=3, distinct=64)
 
 def valu_roof(kernel, frames, ms):
     """The dominant extraction kernel against the VALU issue roofline: lane-ops per launch
-    (committed SQ_INSTS_VALU pass, profiles/r02_pmc_sq.txt) over this run's launch time."""
+    (the committed SQ_INSTS_VALU pass, PMC_FILES["sq"]) over this run's launch time."""
     ops = pmc_valu(kernel, frames)
     if ops is None:
         return None
     ach = ops / (ms * 1e-3)
     return {"bound": "valu", "kernel": kernel, "achieved": ach / 1e12, "peak": PEAK_VALU_LANE_OPS / 1e12,
             "unit": "T lane-ops/s", "frac": ach / PEAK_VALU_LANE_OPS, "lane_ops_per_launch": ops,
-            "source": "rocprofv3 --pmc SQ_INSTS_VALU x 64 (profiles/r02_pmc_sq.txt), same 405-frame launch"}
+            "source": "rocprofv3 --pmc SQ_INSTS_VALU x 64 (profiles/%s), same 405-frame launch" % PMC_FILES["sq"]}
 
 
 def search_legs(ea, torch, matcher, cam, stream, F, cap, poses, kps, cnt, mpos, has, sc, d_kps, d_desc, d_cnt,
