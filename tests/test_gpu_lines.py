@@ -141,3 +141,71 @@ def test_lines_color_batch_device(frames):
     for t in range(F):
         o = orc.edlines_color(cf[t])
         assert hc[t] == len(o) and np.array_equal(ho[t, :hc[t]], o), t
+
+
+@pytest.mark.parametrize("w,h", [(130, 97), (33, 20), (200, 128), (641, 479)])
+def test_lines_odd_sizes(frames, w, h):
+    """Planes whose width is no multiple of 16 (the move bytes' padded pitch), heights that
+    leave partial 64x32 map tiles, planes narrower / shorter than the walk's 128x128 tile (its
+    loads clamped to the plane), and one past 640x480 (the last tile column partial)."""
+    rng = np.random.default_rng(w * 1000 + h)
+    L = ea.Lines(w, h)
+    tot = 0
+    for f in frames[:3]:
+        y0, x0 = int(rng.integers(0, 480 - min(h, 479))), int(rng.integers(0, 640 - min(w, 639)))
+        g = np.zeros((h, w), np.uint8)
+        src = f[y0:y0 + h, x0:x0 + w]
+        g[:src.shape[0], :src.shape[1]] = src
+        if g.shape[0] > src.shape[0] or g.shape[1] > src.shape[1]:  # 641x479: mirror the last column in
+            g[:, src.shape[1]:] = g[:, src.shape[1] - 1:src.shape[1]]
+        out = L.detect(g, min_length=0.0)
+        o = orc.edlines(g, min_length=0.0)
+        assert out.shape == o.shape and np.array_equal(out, o)
+        tot += len(o)
+    assert tot > 0 or w * h < 10000  # (a 33x20 crop holds no line of 50 px)
+
+
+def rings(period):
+    yy, xx = np.mgrid[0:480, 0:640]
+    return ((np.hypot(xx - 320, yy - 240) // (period / 2)) % 2 * 255).astype(np.uint8)
+
+
+def test_lines_dense_rings():
+    """Concentric rings of period 8: ~54k chain pixels and ~800 lines per frame, close to
+    EdgeDrawing's array capacity (pixels / 5): long walks, many chains, parity all the same."""
+    L = ea.Lines()
+    img = rings(8)
+    g, o = L.detect(img), orc.edlines(img)
+    assert len(o) > 500 and g.shape == o.shape and np.array_equal(g, o)
+
+
+def test_lines_edge_overflow_matches_reference():
+    """Rings of period 6 overflow EdgeDrawing's arrays (pixels / 5), where the reference returns
+    -1 (binary_descriptor.cpp EdgeDrawing) and detect_raw_lines yields no lines: the engine
+    reports the overflow for that frame (single frame: an error; in a batch: count -1) and the
+    frames beside it are unaffected."""
+    import ctypes
+    import torch
+    bad = rings(6)
+    out = np.zeros((16, 6), np.float32)
+    n = ctypes.c_int()
+    rc = orc.lib().orc_edlines(orc.P(bad), 640, 480, ctypes.c_float(50.0), orc.P(out), 16, ctypes.byref(n))
+    assert rc != 0  # the restatement overflows too
+    L = ea.Lines()
+    with pytest.raises(Exception):
+        L.detect(bad)
+    fr = synth.line_frames(2, seed=0xEA8)
+    batch = np.stack([fr[0], bad, fr[1]])
+    dev = torch.device("cuda", 0)
+    LB = ea.Lines(max_batch=3)
+    d = torch.from_numpy(np.ascontiguousarray(batch)).to(dev)
+    cap = 256
+    o = torch.zeros((3, cap, 6), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(3, dtype=torch.int32, device=dev)
+    LB.detect_batch_device(d.data_ptr(), 3, 640, 50.0, o.data_ptr(), cnt.data_ptr(), cap)
+    torch.cuda.synchronize()
+    ho, hc = o.cpu().numpy(), cnt.cpu().numpy()
+    assert hc[1] == -1
+    for t in (0, 2):
+        ref = orc.edlines(batch[t])
+        assert hc[t] == len(ref) and np.array_equal(ho[t, :hc[t]], ref), t
