@@ -1685,6 +1685,8 @@ class ReplayEngine {
     uint8_t* valid = h_in + o_val;
     std::memcpy(h_in + o_T, pz.T, sizeof(float) * 16);
     {
+      Tick tpk(&prof[54]);
+      prof[55] += (double)total;
       size_t o = 0;
       for (const std::vector<MapPt*>* v : srcs)
         for (MapPt* p : *v) {
