@@ -493,7 +493,7 @@ sums:
   }
 }
 
-__global__ __launch_bounds__(1024) void k_np_pairs(const float* __restrict__ fp, const uint8_t* __restrict__ fv,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_np_pairs(const float* __restrict__ fp, const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff, const int* __restrict__ flen,
                                                   const float* __restrict__ op, const uint8_t* __restrict__ ov,
                                                   const int* __restrict__ ooff, const int* __restrict__ olen,
@@ -598,7 +598,7 @@ __global__ __launch_bounds__(256) void k_rects(CamDev cam, const float* __restri
 // the frame start in one launch: workgroups [0, npairs) are NoParaDataAssociation pairs
 // (np_pair_body), the rest the projected rects of the recent objects (rects_body). Inputs
 // may be read straight from pinned host memory (no staging copy on the chain).
-__global__ __launch_bounds__(1024) void k_rects_np(int npairs, const float* __restrict__ fp,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_rects_np(int npairs, const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv, const int* __restrict__ foff,
                                                   const int* __restrict__ flen, const float* __restrict__ op,
                                                   const uint8_t* __restrict__ ov, const int* __restrict__ ooff,
@@ -763,7 +763,7 @@ __device__ __forceinline__ void if_sample(WaveRng& g, int n, int psi, uint16_t* 
 //
 // mt_init: per tree, the mt19937 state after seeding and the first twist
 // (the seeds are fixed per forest, so it is computed once on the host).
-__global__ __launch_bounds__(1024) void k_iforest_tree(const float* __restrict__ pts,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_iforest_tree(const float* __restrict__ pts,
                                                       const int* __restrict__ off,
                                                       const int* __restrict__ len,
                                                       const uint32_t* __restrict__ mt_init,
