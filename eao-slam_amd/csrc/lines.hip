@@ -336,7 +336,6 @@ __device__ __forceinline__ void tile_load(const uint8_t* __restrict__ M, int MP,
 __device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
                                         MoveTile& T, int x, int y, int dir, uint32_t* __restrict__ P, uint32_t& off,
                                         uint32_t cap) {
-  const bool l0 = lane_id() == 0;
   // st bit 1: the last step increased x (px), bit 0: it increased y (py). (Scalar ints, not
   // bools: the compiler keeps those as lane masks.)
   int st = dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0);
@@ -349,10 +348,10 @@ __device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, in
     const uint32_t bit = 1u << (idx & 31);
     if (!(mw & LM_EDGE) || (bw & bit)) break;
     if (off >= cap) return false;
-    if (l0) {
-      bits[idx >> 5] = bw | bit;  // the only writer of the frame's edge map
-      P[off] = (uint32_t)x | ((uint32_t)y << 16);
-    }
+    // every lane stores the same word to the same address (no per-step exec-mask switch;
+    // the wave is the only writer of the frame's edge map)
+    bits[idx >> 5] = bw | bit;
+    P[off] = (uint32_t)x | ((uint32_t)y << 16);
     off++;
     const int hz = (mw >> 6) & 1;
     const int fwd = (st >> hz) & 1;  // RIGHT (Horizontal: px) / DOWN (Vertical: py)
