@@ -92,6 +92,11 @@ struct Walk2 {
     }
   }
 };
+// RGB2Gray of one pixel: bg = b | g << 16
+__device__ __forceinline__ uint32_t gray_bg(uint32_t bg, uint32_t r, uint32_t wbg) {
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  return __builtin_amdgcn_udot2(__builtin_bit_cast(us2, bg), __builtin_bit_cast(us2, wbg), r * 4899u + (1u << 13), false) >> 14;
+}
 template <int CN>
 __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ img, int pitch, long long fstride,
                                                    int w, int h, int MP, int k0, int k1, int k2, int vec,
@@ -105,8 +110,8 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
   constexpr int NL = (GH * RD + 255) / 256;      // dword loads per thread
   __shared__ __attribute__((aligned(16))) uint8_t raw[CN == 1 ? 16 : GH * RW];
   __shared__ __attribute__((aligned(16))) uint8_t g[GH][GW];
-  __shared__ int hs[GH][BW];
-  __shared__ uint8_t bl[BH][BW];
+  __shared__ __attribute__((aligned(16))) uint16_t hs[GH][BW];
+  __shared__ __attribute__((aligned(16))) uint8_t bl[BH][BW];
   __shared__ uint16_t cd[CH][CW];
   __shared__ uint32_t am[LF_TW / 2];
   const int f = blockIdx.z, x0 = blockIdx.x * LF_TW, y0 = blockIdx.y * LF_TH, t = threadIdx.x;
@@ -134,7 +139,21 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
           *(uint32_t*)&raw[r * RW + 4 * c] = v[k];
       }
     }
-    if (CN != 1) {
+    if (CN == 3) {
+      // 4 pixels (3 dwords: b0 g0 r0 b1 | g1 r1 b2 g2 | r2 b3 g3 r3) per item: each pixel's
+      // (b, g) as a u16 pair through v_perm, one v_dot2 with (1868, 9617) on r * 4899 + 2^13
+      __syncthreads();
+      constexpr uint32_t WBG = 1868u | 9617u << 16;
+      for (Walk2<GW / 4> q(t); q.r < GH; q.next()) {
+        const uint32_t* p = (const uint32_t*)&raw[q.r * RW + 12 * q.c];
+        const uint32_t d0 = p[0], d1 = p[1], d2 = p[2];
+        const uint32_t g0 = gray_bg(__builtin_amdgcn_perm(d0, d0, 0x0c010c00u), (d0 >> 16) & 0xffu, WBG);
+        const uint32_t g1 = gray_bg(__builtin_amdgcn_perm(d0, d1, 0x0c000c07u), (d1 >> 8) & 0xffu, WBG);
+        const uint32_t g2 = gray_bg(__builtin_amdgcn_perm(d1, d1, 0x0c030c02u), d2 & 0xffu, WBG);
+        const uint32_t g3 = gray_bg(__builtin_amdgcn_perm(d2, d2, 0x0c020c01u), d2 >> 24, WBG);
+        *(uint32_t*)&g[q.r][4 * q.c] = g0 | g1 << 8 | g2 << 16 | g3 << 24;
+      }
+    } else if (CN == 4) {
       __syncthreads();
       Walk2<GW> q(t);
       for (; q.r < GH; q.next()) {
@@ -165,18 +184,43 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
     }
   }
   __syncthreads();
-  for (Walk2<BW> q(t); q.r < GH; q.next()) {
-    const uint8_t* p = &g[q.r][q.c];
-    hs[q.r][q.c] = k0 * ((int)p[0] + p[4]) + k1 * ((int)p[1] + p[3]) + k2 * p[2];
+  // horizontal taps, 4 outputs per item from the row's bytes c .. c + 7 (two dwords): output k
+  // is v_dot4(bytes k .. k + 3, (k0, k1, k2, k1)) + k0 * byte k + 4 (the taps are < 256 and
+  // sum to 257: a sum is <= 65535 and fits 16 bits)
+  {
+    const uint32_t tp = (uint32_t)k0 | (uint32_t)k1 << 8 | (uint32_t)k2 << 16 | (uint32_t)k1 << 24;
+    for (Walk2<BW / 4> q(t); q.r < GH; q.next()) {
+      const uint32_t d0 = *(const uint32_t*)&g[q.r][4 * q.c], d1 = *(const uint32_t*)&g[q.r][4 * q.c + 4];
+      const uint32_t o0 = __builtin_amdgcn_udot4(d0, tp, (d1 & 0xffu) * k0, false);
+      const uint32_t o1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), tp, ((d1 >> 8) & 0xffu) * k0, false);
+      const uint32_t o2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), tp, ((d1 >> 16) & 0xffu) * k0, false);
+      const uint32_t o3 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), tp, (d1 >> 24) * k0, false);
+      *(uint2*)&hs[q.r][4 * q.c] = make_uint2(o0 | o1 << 16, o2 | o3 << 16);
+    }
   }
   __syncthreads();
-  for (Walk2<BW> q(t); q.r < BH; q.next()) {  // blur at (x0 - 2 + c, y0 - 2 + r)
-    const int r = q.r, c = q.c;
-    const int sm = k0 * (hs[r][c] + hs[r + 4][c]) + k1 * (hs[r + 1][c] + hs[r + 3][c]) + k2 * hs[r + 2][c];
-    const uint8_t v = (uint8_t)min((sm + (1 << 15)) >> 16, 255);
-    bl[r][c] = v;
-    const int x = x0 - 2 + c, y = y0 - 2 + r;
-    if (r >= 2 && r < BH - 2 && c >= 2 && c < BW - 2 && x < w && y < h) blur[fo + (long long)y * w + x] = v;
+  for (Walk2<BW / 4> q(t); q.r < BH; q.next()) {  // blur at (x0 - 2 + c, y0 - 2 + r), 4 per item
+    const int r = q.r, c4 = 4 * q.c;
+    uint2 a[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) a[i] = *(const uint2*)&hs[r + i][c4];
+    uint32_t pk = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int sh = 16 * (k & 1);
+      auto H = [&](int i) { return (int)(((k < 2 ? a[i].x : a[i].y) >> sh) & 0xffffu); };
+      const int sm = k0 * (H(0) + H(4)) + k1 * (H(1) + H(3)) + k2 * H(2);
+      pk |= (uint32_t)min((sm + (1 << 15)) >> 16, 255) << (8 * k);
+    }
+    *(uint32_t*)&bl[r][c4] = pk;
+    const int y = y0 - 2 + r;
+    if (r >= 2 && r < BH - 2 && y < h) {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int c = c4 + k, x = x0 - 2 + c;
+        if (c >= 2 && c < BW - 2 && x < w) blur[fo + (long long)y * w + x] = (uint8_t)(pk >> (8 * k));
+      }
+    }
   }
   __syncthreads();
   for (Walk2<CW> q(t); q.r < CH; q.next()) {  // code at (x0 - 1 + c, y0 - 1 + r)
@@ -906,7 +950,8 @@ struct LineEngine {
   }
 };
 
-// getGaussianKernel(5, 1, CV_32F) -> the 8U fixed-point taps (cvRound(k * 256))
+// getGaussianKernel(5, 1, CV_32F) -> the 8U fixed-point taps (cvRound(k * 256)): 14, 63, 103, 63, 14 --
+// each < 256 and summing to 257 (<= 257), which k_line_maps' byte dot products and 16-bit row sums rely on
 static void gauss5(int* k) {
   float cf[5];
   double sum = 0;

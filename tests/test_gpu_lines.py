@@ -179,6 +179,20 @@ def test_lines_dense_rings():
     assert len(o) > 500 and g.shape == o.shape and np.array_equal(g, o)
 
 
+def test_maps_saturated_rings():
+    """Maps on 0 / 255 rings: the Gaussian taps sum to 257, so a white area's blur sum rounds to
+    257 before the clamp to 255 (the packed 4-pixel blur must clamp each byte)."""
+    L = ea.Lines()
+    for period in (8, 12):
+        img = rings(period)
+        L.detect(img)
+        blur, dx, dy, code = L.debug_maps()
+        ob, odx, ody, og, odr = orc.line_maps(img)
+        assert np.array_equal(blur, ob) and (ob == 255).any()
+        assert np.array_equal(dx, odx) and np.array_equal(dy, ody)
+        assert np.array_equal((code & 0x7fff).astype(np.int16), og)
+
+
 def test_lines_edge_overflow_matches_reference():
     """Rings of period 6 overflow EdgeDrawing's arrays (pixels / 5), where the reference returns
     -1 (binary_descriptor.cpp EdgeDrawing) and detect_raw_lines yields no lines: the engine

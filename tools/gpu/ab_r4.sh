@@ -191,5 +191,15 @@ linecu() {
   EAO_LINES_CU_QUARTERS=2 timeout -k 10 300 python -u -m pytest tests/test_gpu_lines.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r4cu_tests.log 2>&1
 }
 
+
+# ldelay: marginal cost of forest-batch launch time on the association chain (knob EAO_LAUNCH_DELAY_US: a busy wait after each batch launch in kick(), removed after the measurement): replay probe pass 2 at 0 / 13 / 26 us of extra host time per batch launch, alternating.
+ldelay() {
+  for r in 1 2 3; do
+    for d in 0 13 26; do
+      EAO_LAUNCH_DELAY_US=$d timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" | cut -c1-60 | sed "s/^/delay=$d /" || exit 1
+    done
+  done > gpurun_out/r4_ldelay.log 2>&1
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 <experiment>"; exit 2; }
 "$1"
