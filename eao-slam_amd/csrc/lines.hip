@@ -47,15 +47,25 @@ constexpr double LN_FIT_ERR = 1.6;
 // its direction (dirImg_), and, for each of the two directions a walk can take through it, which
 // of the three forward neighbours has the largest gImg_ byte (the reference's if-chain, ties
 // included) or that the image border ends the walk there. k_line_maps evaluates this once per
-// pixel into a byte, so a step of the sequential walk is two LDS reads (the
-// byte through a tile cache, the edge-map bit) and a few scalar operations:
-//   bit 7: gImg_ > 0   bit 6: Horizontal
-//   bits 2-3: the step when walking RIGHT (Horizontal) / DOWN (Vertical)
-//   bits 4-5: the step when walking LEFT (Horizontal) / UP (Vertical)
-//   step: 0 straight, 1 the g1 diagonal, 2 the g3 diagonal, 3 at the border: stop after the pixel
-// (a Horizontal pixel is only ever left RIGHT or LEFT, a Vertical one DOWN or UP). Rows have
-// the pitch MP (a multiple of 16) so the tile loads are aligned 16-byte loads.
-constexpr int LM_EDGE = 0x80, LM_HORIZ = 0x40;
+// pixel into a 16-bit move word, so a step of the sequential walk is two LDS reads (the
+// word through a tile cache, the edge-map bit) and a few scalar operations. The walk's state is
+// two bits st = (the last step increased x) << 1 | (it increased y) (ed_walk); nibble st of the
+// word is the step the walk takes from the pixel in state st, as (dx + 1) | (dy + 1) << 2:
+// a Horizontal pixel is left RIGHT when st's x bit is set, else LEFT; a Vertical one DOWN when
+// st's y bit is set, else UP; of the three forward neighbours the one with the largest gImg_
+// byte (the reference's if-chain, ties included). At the image border the step is (0, 0):
+// stop after the pixel (the walk finds its own pixel marked next). A non-edge pixel (gImg_ == 0)
+// has the word 0 (an edge pixel's forward nibbles are never 0). Rows have the pitch MP (a
+// multiple of 16) so the tile loads are aligned 16-byte loads.
+constexpr int LM_STOP = 5;  // (0, 0)
+// the nibble of a step: forward (fwd: RIGHT / DOWN) or back, ch the reference's choice
+// (0 straight, 1 the g1 diagonal, 2 the g3 diagonal, 3 the border)
+__device__ __forceinline__ int lm_nibble(bool hz, int fwd, int ch) {
+  if (ch == 3) return LM_STOP;
+  const int along = 2 * fwd - 1, side = (ch >> 1) - (ch & 1);  // ch 1: the g1 side (-1), 2: g3 (+1)
+  const int dx = hz ? along : -side, dy = hz ? side : along;  // DOWN / UP: g1 is the x + 1 neighbour
+  return (dx + 1) | (dy + 1) << 2;
+}
 __device__ __forceinline__ int ln_pick(int g1, int g2, int g3) {
   return (g1 >= g2 && g1 >= g3) ? 1 : ((g3 >= g2 && g3 >= g1) ? 2 : 0);
 }
@@ -102,7 +112,7 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
                                                    int w, int h, int MP, int k0, int k1, int k2, int vec,
                                                    uint8_t* __restrict__ blur, int16_t* __restrict__ dxo,
                                                    int16_t* __restrict__ dyo, uint16_t* __restrict__ code,
-                                                   uint8_t* __restrict__ moves, uint16_t* __restrict__ amask) {
+                                                   uint16_t* __restrict__ moves, uint16_t* __restrict__ amask) {
   constexpr int GW = LF_TW + 8, GH = LF_TH + 8;  // gray: halo 4 (blur 2 + Sobel 1 + moves 1)
   constexpr int BW = LF_TW + 4, BH = LF_TH + 4;  // blur: halo 2
   constexpr int CW = LF_TW + 2, CH = LF_TH + 2;  // code: halo 1
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
       if (an) atomicOr(&am[cl], 1u << jb);
     }
   }
-  for (Walk2<LF_TW> q(t); q.r < LF_TH; q.next()) {  // move bytes of the tile (see k_edge_draw)
+  for (Walk2<LF_TW> q(t); q.r < LF_TH; q.next()) {  // move words of the tile (see lm_nibble)
     const int r = q.r, c = q.c, x = x0 + c, y = y0 + r;
     if (x >= w || y >= h) continue;
     const int cv = cd[r + 1][c + 1];
@@ -266,18 +276,19 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
       // the walk compares gImg_ read as unsigned char (gValue1..3, :1643): the code's low byte;
       // a neighbour outside the plane is never read (the border stops that direction)
       auto gb = [&](int dx, int dy) { return (int)(uint8_t)cd[r + 1 + dy][c + 1 + dx]; };
-      m = LM_EDGE;
-      if (cv & LN_HORIZ) {
+      if (cv & LN_HORIZ) {  // st 0, 1: LEFT; st 2, 3: RIGHT
         const int rt = (x == w - 1 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(1, -1), gb(1, 0), gb(1, 1));
         const int lf = (x == 0 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(-1, -1), gb(-1, 0), gb(-1, 1));
-        m |= LM_HORIZ | rt << 2 | lf << 4;
-      } else {
+        const int nl = lm_nibble(true, 0, lf), nr = lm_nibble(true, 1, rt);
+        m = nl | nl << 4 | nr << 8 | nr << 12;
+      } else {  // st 0, 2: UP; st 1, 3: DOWN
         const int dn = (x == 0 || x == w - 1 || y == h - 1) ? 3 : ln_pick(gb(1, 1), gb(0, 1), gb(-1, 1));
         const int up = (x == 0 || x == w - 1 || y == 0) ? 3 : ln_pick(gb(1, -1), gb(0, -1), gb(-1, -1));
-        m |= dn << 2 | up << 4;
+        const int nu = lm_nibble(false, 0, up), nd = lm_nibble(false, 1, dn);
+        m = nu | nd << 4 | nu << 8 | nd << 12;
       }
     }
-    moves[(long long)f * MP * h + (long long)y * MP + x] = (uint8_t)m;
+    moves[(long long)f * MP * h + (long long)y * MP + x] = (uint16_t)m;
   }
   __syncthreads();
   if (t < LF_TW / 2)
@@ -342,28 +353,28 @@ __global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict
 }
 
 // ---------------------------------------------------------------- edge drawing
-// The walk reads the move bytes through a 128 x 128 tile of them in LDS, reloaded (centred on
-// the step's pixel) when the pixel leaves it: one round of 16 aligned 16-byte loads per lane.
-// (No move byte is read outside the plane: the border steps stop the walk.)
-constexpr int LE_TW = 128, LE_TH = 128;
+// The walk reads the move words through a 128 x 64 tile of them in LDS (16 KB), reloaded
+// (centred on the step's pixel) when the pixel leaves it: one round of 16 aligned 16-byte loads
+// per lane. (No move word is read outside the plane: the border steps stop the walk.)
+constexpr int LE_TW = 128, LE_TH = 64;
 struct MoveTile {
-  uint8_t* t;  // LDS [LE_TH][LE_TW]
-  int x0, y0;  // origin in the plane (x0 = -LE_TW: empty)
+  uint16_t* t;  // LDS [LE_TH][LE_TW]
+  int x0, y0;   // origin in the plane (x0 = -LE_TW: empty)
 };
-__device__ __forceinline__ void tile_load(const uint8_t* __restrict__ M, int MP, int H, MoveTile& T, int x, int y) {
-  T.x0 = min(max((x - LE_TW / 2) & ~15, 0), max(MP - LE_TW, 0));
+__device__ __forceinline__ void tile_load(const uint16_t* __restrict__ M, int MP, int H, MoveTile& T, int x, int y) {
+  T.x0 = min(max((x - LE_TW / 2) & ~7, 0), max(MP - LE_TW, 0));
   T.y0 = min(max(y - LE_TH / 2, 0), max(H - LE_TH, 0));
   const int lane = lane_id();
   uint4 v[16];
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int id = lane + 64 * k, r = id >> 3, c = (id & 7) * 16;
+    const int id = lane + 64 * k, r = id >> 4, c = (id & 15) * 8;
     v[k] = make_uint4(0u, 0u, 0u, 0u);
     if (T.y0 + r < H && T.x0 + c < MP) v[k] = *(const uint4*)(M + (long long)(T.y0 + r) * MP + T.x0 + c);
   }
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    const int id = lane + 64 * k, r = id >> 3, c = (id & 7) * 16;
+    const int id = lane + 64 * k, r = id >> 4, c = (id & 15) * 8;
     *(uint4*)(T.t + r * LE_TW + c) = v[k];
   }
 }
@@ -377,39 +388,40 @@ __device__ __forceinline__ void tile_load(const uint8_t* __restrict__ M, int MP,
 // last step increased x -- and on a Vertical one DOWN exactly when the last step increased y.
 // The walk's state is those two bits (px, py), initialised from dir (an anchor's first step
 // leaves along dir: its own direction).
-__device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
+__device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
                                         MoveTile& T, int x, int y, int dir, uint32_t* __restrict__ P, uint32_t& off,
                                         uint32_t cap) {
-  // st bit 1: the last step increased x (px), bit 0: it increased y (py). (Scalar ints, not
-  // bools: the compiler keeps those as lane masks.)
+  // st bit 1: the last step increased x (px), bit 0: it increased y (py) (see lm_nibble)
   int st = dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0);
   if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) tile_load(M, MP, H, T, x, y);
-  int toff = (y - T.y0) * LE_TW + (x - T.x0);
+  // the pixel as its packed record, its edge-map index, its tile offset and tile coordinates,
+  // all advanced by the step
+  int pk = x | y << 16, idx = y * W + x, tx = x - T.x0, ty = y - T.y0, toff = ty * LE_TW + tx;
   while (true) {
-    const int idx = y * W + x;
     const int mw = __builtin_amdgcn_readfirstlane((int)T.t[toff]);
     const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
     const uint32_t bit = 1u << (idx & 31);
-    if (!(mw & LM_EDGE) || (bw & bit)) break;
+    if (mw == 0 || (bw & bit)) break;
     if (off >= cap) return false;
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
-    P[off] = (uint32_t)x | ((uint32_t)y << 16);
+    P[off] = (uint32_t)pk;
     off++;
-    const int hz = (mw >> 6) & 1;
-    const int fwd = (st >> hz) & 1;  // RIGHT (Horizontal: px) / DOWN (Vertical: py)
-    const int ch = (mw >> (4 - 2 * fwd)) & 3;
-    if (ch == 3) break;
-    const int along = 2 * fwd - 1, side = (ch >> 1) - (ch & 1);  // ch 1: the g1 side (-1), 2: g3 (+1)
-    const int dx = hz ? along : -side, dy = hz ? side : along;  // DOWN / UP: g1 is the x + 1 neighbour
-    x += dx;
-    y += dy;
-    st = (int)(((unsigned)(-dx) >> 31) << 1 | ((unsigned)(-dy) >> 31));
-    toff += dy * LE_TW + dx;
-    if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) {
-      tile_load(M, MP, H, T, x, y);
-      toff = (y - T.y0) * LE_TW + (x - T.x0);
+    const int nib = (mw >> (4 * st)) & 15;
+    const int dx = (nib & 3) - 1, dy = (nib >> 2) - 1;  // (0, 0) at the border: the pixel is marked
+    st = (nib & 2) | (nib >> 3);
+    pk += dx + dy * 65536;
+    idx += dx + dy * W;
+    tx += dx;
+    ty += dy;
+    toff += dx + dy * LE_TW;
+    if ((unsigned)tx >= (unsigned)LE_TW || (unsigned)ty >= (unsigned)LE_TH) {
+      const int xx = pk & 0xffff, yy = pk >> 16;
+      tile_load(M, MP, H, T, xx, yy);
+      tx = xx - T.x0;
+      ty = yy - T.y0;
+      toff = ty * LE_TW + tx;
     }
   }
   return true;
@@ -426,7 +438,8 @@ __device__ __forceinline__ bool ed_walk(const uint8_t* __restrict__ M, int W, in
 // release); the walk's pixel stores are made visible to them first. Returns the number of
 // chains, or -1 where the reference returns -1.
 template <bool STREAM>
-__device__ int ed_walker(const uint8_t* __restrict__ M, int W, int H, int MP, const uint32_t* __restrict__ A, int na,
+__device__ int ed_walker(const uint16_t* __restrict__ M, const uint16_t* __restrict__ C, int W, int H, int MP,
+                         const uint32_t* __restrict__ A, int na,
                          int acap, uint32_t* __restrict__ P1, uint32_t* __restrict__ P2, int pcap, int ecap,
                          uint32_t* bits, uint32_t* fS, uint32_t* sS, MoveTile& T, int* pub) {
   const int lane = lane_id();
@@ -443,7 +456,7 @@ __device__ int ed_walker(const uint8_t* __restrict__ M, int W, int H, int MP, co
     const int a = a0 + lane;
     const uint32_t ap = a < na ? A[a] : 0u;
     const int ax = (int)(ap & 0xffffu), ay = (int)(ap >> 16), aidx = ay * W + ax;
-    const int amw = a < na ? (int)M[(long long)ay * MP + ax] : 0;
+    const int acv = a < na ? (int)C[(long long)ay * W + ax] : 0;  // the anchor's code (its direction)
     uint64_t pend = ballot(a < na);
     while (true) {
       pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);  // edgeImg_[anchor] set: skipped
@@ -455,7 +468,7 @@ __device__ int ed_walker(const uint8_t* __restrict__ M, int W, int H, int MP, co
         break;
       }
       const int x = __builtin_amdgcn_readlane(ax, k), y = __builtin_amdgcn_readlane(ay, k);
-      const bool horiz = (__builtin_amdgcn_readlane(amw, k) & LM_HORIZ) != 0;
+      const bool horiz = (__builtin_amdgcn_readlane(acv, k) & LN_HORIZ) != 0;
       uint32_t o1 = b1, o2 = b2;
       if (!ed_walk(M, W, MP, H, bits, T, x, y, horiz ? LN_RIGHT : LN_DOWN, P1, o1, (uint32_t)pcap)) {
         fail = true;
@@ -485,7 +498,8 @@ __device__ int ed_walker(const uint8_t* __restrict__ M, int W, int H, int MP, co
   return fail ? -1 : ne;
 }
 
-__global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ moves, int W, int H, int MP,
+__global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ moves, const uint16_t* __restrict__ code,
+                                                  int W, int H, int MP,
                                                   const uint32_t* __restrict__ anchors, const int* __restrict__ nanchor,
                                                   int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2,
                                                   int pcap, uint32_t* __restrict__ chains, uint32_t* __restrict__ sid,
@@ -496,12 +510,12 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint8_t* __restrict__ mo
   uint32_t* bits = lds_ed;
   uint32_t* fS = bits + nbp;  // the kept chains' offF / offS starts (the reference's fS / sS)
   uint32_t* sS = fS + ep;
-  MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
+  MoveTile T{(uint16_t*)(sS + ep), -LE_TW, -LE_TH};
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
   uint32_t* Q = chains + (long long)f * 2 * pcap;
   uint32_t* S = sid + (long long)f * (ecap + 1);
-  const int ne = ed_walker<false>(moves + (long long)f * MP * H, W, H, MP, anchors + (long long)f * acap, nanchor[f],
+  const int ne = ed_walker<false>(moves + (long long)f * MP * H, code + (long long)f * W * H, W, H, MP, anchors + (long long)f * acap, nanchor[f],
                                   acap, P1, P2, pcap, ecap, bits, fS, sS, T, nullptr);
   if (ne < 0) {
     if (lane == 0) nedge[f] = -1;
@@ -856,7 +870,7 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
 // rounds, 9.9 ms against 6.5 ms per 405 frames; r04_ab_lines.txt).
 constexpr int LE_WAVES = 4;
 __global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
-    const uint8_t* __restrict__ moves, int W, int H, int MP, const uint32_t* __restrict__ anchors,
+    const uint16_t* __restrict__ moves, int W, int H, int MP, const uint32_t* __restrict__ anchors,
     const int* __restrict__ nanchor, int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2, int pcap,
     uint32_t* __restrict__ chains, uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
     const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi, const int16_t* __restrict__ dyi,
@@ -883,8 +897,8 @@ __global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
   }
   __syncthreads();
   if (wave == 0) {
-    MoveTile T{(uint8_t*)(sS + ep), -LE_TW, -LE_TH};
-    const int ne = ed_walker<true>(moves + (long long)f * MP * H, W, H, MP, anchors + (long long)f * acap, nanchor[f],
+    MoveTile T{(uint16_t*)(sS + ep), -LE_TW, -LE_TH};
+    const int ne = ed_walker<true>(moves + (long long)f * MP * H, code + fo, W, H, MP, anchors + (long long)f * acap, nanchor[f],
                                    acap, P1, P2, pcap, ecap, bits, fS, sS, T, &pub);
     if (lane == 0) {
       nedge[f] = ne;
@@ -931,7 +945,7 @@ struct LineEngine {
   uint8_t* d_blur = nullptr;
   int16_t *d_dx = nullptr, *d_dy = nullptr;
   uint16_t* d_code = nullptr;
-  uint8_t* d_moves = nullptr;
+  uint16_t* d_moves = nullptr;
   uint16_t* d_amask = nullptr;  // [frame][row band][candidate column] anchor row masks
   uint32_t *d_anch = nullptr, *d_p1 = nullptr, *d_p2 = nullptr, *d_chain = nullptr, *d_sid = nullptr,
            *d_lscr = nullptr, *d_ccnt = nullptr;
@@ -969,7 +983,7 @@ static void gauss5(int* k) {
 
 // k_edge_draw's dynamic LDS: the edge bitmap, the chains' fS / sS starts, the move tile
 static size_t edge_draw_lds(int W, int H, int ecap) {
-  return ((size_t)((((W * H + 31) / 32) + 3) & ~3) + 2 * (size_t)((ecap + 2 + 3) & ~3)) * 4 + (size_t)LE_TW * LE_TH;
+  return ((size_t)((((W * H + 31) / 32) + 3) & ~3) + 2 * (size_t)((ecap + 2 + 3) & ~3)) * 4 + sizeof(uint16_t) * LE_TW * LE_TH;
 }
 
 }  // namespace eao
@@ -1019,7 +1033,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc(&e.d_blur, px) != hipSuccess || hipMalloc(&e.d_dx, px * 2) != hipSuccess ||
       hipMalloc(&e.d_dy, px * 2) != hipSuccess || hipMalloc(&e.d_code, px * 2) != hipSuccess ||
-      hipMalloc(&e.d_moves, (size_t)e.MP * height * max_batch) != hipSuccess ||
+      hipMalloc(&e.d_moves, sizeof(uint16_t) * e.MP * height * max_batch) != hipSuccess ||
       hipMalloc(&e.d_amask, (size_t)((width + LF_TW - 1) / LF_TW) * (LF_TW / 2) * ((height + LF_TH - 1) / LF_TH) * 2 *
                                 max_batch) != hipSuccess ||
       hipMalloc(&e.d_anch, (size_t)e.acap * 4 * max_batch) != hipSuccess ||
@@ -1081,7 +1095,7 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
                        H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap,
                        e.d_nedge, e.d_code, e.d_dx, e.d_dy, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts, cap);
   } else {
-    hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W, H, e.MP,
+    hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, e.d_code, W, H, e.MP,
                        e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
     hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
                        e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts,
