@@ -397,12 +397,16 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   // the pixel as its packed record, its edge-map index, its tile offset and tile coordinates,
   // all advanced by the step
   int pk = x | y << 16, idx = y * W + x, tx = x - T.x0, ty = y - T.y0, toff = ty * LE_TW + tx;
+  // one loop exit (separate exits for the stop and the overflow cost the compiler's exit
+  // bookkeeping on every step): the walk ends at a marked or non-edge pixel (stop != 0), or
+  // with the pixel arrays full (an overflow: the reference returns -1)
+  uint32_t stop;
   while (true) {
     const int mw = __builtin_amdgcn_readfirstlane((int)T.t[toff]);
     const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
     const uint32_t bit = 1u << (idx & 31);
-    if (mw == 0 || (bw & bit)) break;
-    if (off >= cap) return false;
+    stop = (bw & bit) | ((uint32_t)(mw - 1) >> 31);  // marked, or not an edge pixel (mw == 0)
+    if (stop | (uint32_t)((int)(cap - off - 1) >> 31)) break;  // or off >= cap (cap < 2^31), as integers
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
@@ -416,7 +420,8 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
     tx += dx;
     ty += dy;
     toff += dx + dy * LE_TW;
-    if ((unsigned)tx >= (unsigned)LE_TW || (unsigned)ty >= (unsigned)LE_TH) {
+    static_assert(LE_TW == 2 * LE_TH && (LE_TW & (LE_TW - 1)) == 0, "one mask test for both tile bounds");
+    if ((tx | ty * 2) & ~(LE_TW - 1)) {  // left the tile (a negative coordinate sets the high bits)
       const int xx = pk & 0xffff, yy = pk >> 16;
       tile_load(M, MP, H, T, xx, yy);
       tx = xx - T.x0;
@@ -424,7 +429,7 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
       toff = ty * LE_TW + tx;
     }
   }
-  return true;
+  return stop != 0;
 }
 
 // EdgeDrawing's anchor loop (:1695-2327), one wave per frame. Anchors are taken 64 at a time
