@@ -394,15 +394,24 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   // st bit 1: the last step increased x (px), bit 0: it increased y (py) (see lm_nibble)
   int st = dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0);
   if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) tile_load(M, MP, H, T, x, y);
-  // the pixel as its packed record, its edge-map index, its tile offset and tile coordinates,
-  // all advanced by the step
-  int pk = x | y << 16, idx = y * W + x, tx = x - T.x0, ty = y - T.y0, toff = ty * LE_TW + tx;
+  // the pixel as its packed record (x | y << 16), its edge-map index, its tile offset (bytes)
+  // and its tile coordinates packed like the record, all advanced by the step. The step's
+  // increments of each, and the next state's nibble shift, are read from per-nibble tables in
+  // lane k of a VGPR (v_readlane with the nibble as the lane): four reads instead of a decode.
+  const int lane = lane_id(), ndx = (lane & 3) - 1, ndy = ((lane >> 2) & 3) - 1;
+  const int t_pk = ndx + ndy * 65536, t_idx = ndx + ndy * W, t_off = 2 * (ndx + ndy * LE_TW);
+  const int t_sh = 4 * ((lane & 2) | ((lane >> 3) & 1));
+  int pk = x | y << 16, idx = y * W + x, tp = (x - T.x0) | (y - T.y0) << 16;
+  int toff = 2 * ((y - T.y0) * LE_TW + (x - T.x0)), sh = 4 * st;
+  static_assert(LE_TW == 128 && LE_TH == 64, "the tile test mask");
+  constexpr int kOut = (int)0xFFC0FF80u;  // tp outside [0, 128) x [0, 64) (a negative coordinate sets the high bits)
   // one loop exit (separate exits for the stop and the overflow cost the compiler's exit
   // bookkeeping on every step): the walk ends at a marked or non-edge pixel (stop != 0), or
   // with the pixel arrays full (an overflow: the reference returns -1)
   uint32_t stop;
+  uint32_t* Pw = P + off;  // the next pixel record
   while (true) {
-    const int mw = __builtin_amdgcn_readfirstlane((int)T.t[toff]);
+    const int mw = __builtin_amdgcn_readfirstlane((int)*(const uint16_t*)((const uint8_t*)T.t + toff));
     const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
     const uint32_t bit = 1u << (idx & 31);
     stop = (bw & bit) | ((uint32_t)(mw - 1) >> 31);  // marked, or not an edge pixel (mw == 0)
@@ -410,23 +419,20 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
-    P[off] = (uint32_t)pk;
+    *Pw++ = (uint32_t)pk;
     off++;
-    const int nib = (mw >> (4 * st)) & 15;
-    const int dx = (nib & 3) - 1, dy = (nib >> 2) - 1;  // (0, 0) at the border: the pixel is marked
-    st = (nib & 2) | (nib >> 3);
-    pk += dx + dy * 65536;
-    idx += dx + dy * W;
-    tx += dx;
-    ty += dy;
-    toff += dx + dy * LE_TW;
-    static_assert(LE_TW == 2 * LE_TH && (LE_TW & (LE_TW - 1)) == 0, "one mask test for both tile bounds");
-    if ((tx | ty * 2) & ~(LE_TW - 1)) {  // left the tile (a negative coordinate sets the high bits)
+    const int nib = (mw >> sh) & 15;  // (0, 0) at the border: the pixel is marked, the walk stops next
+    const int dpk = __builtin_amdgcn_readlane(t_pk, nib);
+    pk += dpk;
+    tp += dpk;
+    idx += __builtin_amdgcn_readlane(t_idx, nib);
+    toff += __builtin_amdgcn_readlane(t_off, nib);
+    sh = __builtin_amdgcn_readlane(t_sh, nib);
+    if (tp & kOut) {  // left the tile
       const int xx = pk & 0xffff, yy = pk >> 16;
       tile_load(M, MP, H, T, xx, yy);
-      tx = xx - T.x0;
-      ty = yy - T.y0;
-      toff = ty * LE_TW + tx;
+      tp = (xx - T.x0) | (yy - T.y0) << 16;
+      toff = 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
     }
   }
   return stop != 0;
