@@ -53,10 +53,12 @@ constexpr double LN_FIT_ERR = 1.6;
 // word is the step the walk takes from the pixel in state st, as (dx + 1) | (dy + 1) << 2:
 // a Horizontal pixel is left RIGHT when st's x bit is set, else LEFT; a Vertical one DOWN when
 // st's y bit is set, else UP; of the three forward neighbours the one with the largest gImg_
-// byte (the reference's if-chain, ties included). At the image border the step is (0, 0):
-// stop after the pixel (the walk finds its own pixel marked next). A non-edge pixel (gImg_ == 0)
-// has the word 0 (an edge pixel's forward nibbles are never 0). Rows have the pitch MP (a
-// multiple of 16) so the tile loads are aligned 16-byte loads.
+// byte (the reference's if-chain, ties included). At the image border, and where the step would
+// land on a non-edge pixel (gImg_ == 0, where the reference's walk ends without taking it), the
+// step is (0, 0): stop after the pixel (the walk finds its own pixel marked next). So a walk,
+// which starts at an anchor (an edge pixel), only ever reads edge pixels' words; a non-edge
+// pixel's word is 0. Rows have the pitch MP (a multiple of 16) so the tile loads are aligned
+// 16-byte loads.
 constexpr int LM_STOP = 5;  // (0, 0)
 // the nibble of a step: forward (fwd: RIGHT / DOWN) or back, ch the reference's choice
 // (0 straight, 1 the g1 diagonal, 2 the g3 diagonal, 3 the border)
@@ -276,15 +278,22 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
       // the walk compares gImg_ read as unsigned char (gValue1..3, :1643): the code's low byte;
       // a neighbour outside the plane is never read (the border stops that direction)
       auto gb = [&](int dx, int dy) { return (int)(uint8_t)cd[r + 1 + dy][c + 1 + dx]; };
+      // a step onto a non-edge pixel ends the walk there (the pixel is not taken): that step is
+      // stored as the border's (0, 0), so the walk never reads a non-edge pixel's word
+      auto to_edge = [&](int nb) {
+        if (nb == LM_STOP) return nb;
+        const int dx = (nb & 3) - 1, dy = (nb >> 2) - 1;
+        return (cd[r + 1 + dy][c + 1 + dx] & 0x7fff) ? nb : LM_STOP;
+      };
       if (cv & LN_HORIZ) {  // st 0, 1: LEFT; st 2, 3: RIGHT
         const int rt = (x == w - 1 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(1, -1), gb(1, 0), gb(1, 1));
         const int lf = (x == 0 || y == 0 || y == h - 1) ? 3 : ln_pick(gb(-1, -1), gb(-1, 0), gb(-1, 1));
-        const int nl = lm_nibble(true, 0, lf), nr = lm_nibble(true, 1, rt);
+        const int nl = to_edge(lm_nibble(true, 0, lf)), nr = to_edge(lm_nibble(true, 1, rt));
         m = nl | nl << 4 | nr << 8 | nr << 12;
       } else {  // st 0, 2: UP; st 1, 3: DOWN
         const int dn = (x == 0 || x == w - 1 || y == h - 1) ? 3 : ln_pick(gb(1, 1), gb(0, 1), gb(-1, 1));
         const int up = (x == 0 || x == w - 1 || y == 0) ? 3 : ln_pick(gb(1, -1), gb(0, -1), gb(-1, -1));
-        const int nu = lm_nibble(false, 0, up), nd = lm_nibble(false, 1, dn);
+        const int nu = to_edge(lm_nibble(false, 0, up)), nd = to_edge(lm_nibble(false, 1, dn));
         m = nu | nd << 4 | nu << 8 | nd << 12;
       }
     }
@@ -402,7 +411,8 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   const int t_pk = ndx + ndy * 65536, t_idx = ndx + ndy * W, t_off = 2 * (ndx + ndy * LE_TW);
   const int t_sh = 4 * ((lane & 2) | ((lane >> 3) & 1));
   int pk = x | y << 16, idx = y * W + x, tp = (x - T.x0) | (y - T.y0) << 16;
-  int toff = 2 * ((y - T.y0) * LE_TW + (x - T.x0)), sh = 4 * st;
+  const uint8_t* tw = (const uint8_t*)T.t + 2 * ((y - T.y0) * LE_TW + (x - T.x0));  // the pixel's word in the tile
+  int sh = 4 * st;
   static_assert(LE_TW == 128 && LE_TH == 64, "the tile test mask");
   constexpr int kOut = (int)0xFFC0FF80u;  // tp outside [0, 128) x [0, 64) (a negative coordinate sets the high bits)
   // one loop exit (separate exits for the stop and the overflow cost the compiler's exit
@@ -411,10 +421,10 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   uint32_t stop;
   uint32_t* Pw = P + off;  // the next pixel record
   while (true) {
-    const int mw = __builtin_amdgcn_readfirstlane((int)*(const uint16_t*)((const uint8_t*)T.t + toff));
+    const int mw = __builtin_amdgcn_readfirstlane((int)*(const uint16_t*)tw);
     const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
     const uint32_t bit = 1u << (idx & 31);
-    stop = (bw & bit) | ((uint32_t)(mw - 1) >> 31);  // marked, or not an edge pixel (mw == 0)
+    stop = bw & bit;  // marked (a walk reaches only edge pixels: a step onto a non-edge one is stored as (0, 0))
     if (stop | (uint32_t)((int)(cap - off - 1) >> 31)) break;  // or off >= cap (cap < 2^31), as integers
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
@@ -426,13 +436,13 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
     pk += dpk;
     tp += dpk;
     idx += __builtin_amdgcn_readlane(t_idx, nib);
-    toff += __builtin_amdgcn_readlane(t_off, nib);
+    tw += __builtin_amdgcn_readlane(t_off, nib);
     sh = __builtin_amdgcn_readlane(t_sh, nib);
     if (tp & kOut) {  // left the tile
       const int xx = pk & 0xffff, yy = pk >> 16;
       tile_load(M, MP, H, T, xx, yy);
       tp = (xx - T.x0) | (yy - T.y0) << 16;
-      toff = 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
+      tw = (const uint8_t*)T.t + 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
     }
   }
   return stop != 0;
