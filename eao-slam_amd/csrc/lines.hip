@@ -418,19 +418,20 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   // one loop exit (separate exits for the stop and the overflow cost the compiler's exit
   // bookkeeping on every step): the walk ends at a marked or non-edge pixel (stop != 0), or
   // with the pixel arrays full (an overflow: the reference returns -1)
-  uint32_t stop;
   uint32_t* Pw = P + off;  // the next pixel record
+  int rem = (int)(cap - off) - 1;  // records left after this one (< 0: the arrays are full)
   while (true) {
     const int mw = __builtin_amdgcn_readfirstlane((int)*(const uint16_t*)tw);
     const uint32_t bw = (uint32_t)__builtin_amdgcn_readfirstlane((int)bits[idx >> 5]);
     const uint32_t bit = 1u << (idx & 31);
-    stop = bw & bit;  // marked (a walk reaches only edge pixels: a step onto a non-edge one is stored as (0, 0))
-    if (stop | (uint32_t)((int)(cap - off - 1) >> 31)) break;  // or off >= cap (cap < 2^31), as integers
+    // marked (a walk reaches only edge pixels: a step onto a non-edge one is stored as (0, 0)),
+    // or off >= cap (cap < 2^31)
+    if ((bw & bit) | ((uint32_t)rem >> 31)) break;
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
     *Pw++ = (uint32_t)pk;
-    off++;
+    rem--;
     const int nib = (mw >> sh) & 15;  // (0, 0) at the border: the pixel is marked, the walk stops next
     const int dpk = __builtin_amdgcn_readlane(t_pk, nib);
     pk += dpk;
@@ -445,7 +446,10 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
       tw = (const uint8_t*)T.t + 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
     }
   }
-  return stop != 0;
+  // stopped at a marked pixel (true), or the arrays are full there (an overflow)
+  const bool stop = (bits[idx >> 5] >> (idx & 31)) & 1u;
+  off = cap - 1 - (uint32_t)rem;
+  return stop;
 }
 
 // EdgeDrawing's anchor loop (:1695-2327), one wave per frame. Anchors are taken 64 at a time
