@@ -429,8 +429,8 @@ def main():
                            d_cnt, d_has, d_mpos, match_ms)
     hl = d_lcnt.cpu().numpy()
     lines_leg = {"in_step": True, "frames": F, "ms_per_step": lines_ms, "frames_per_s": F / (lines_ms * 1e-3),
-                 "mean_lines": float(hl.mean()), "kernels": "k_line_blur<3> (COLOR_BGR2GRAY fused) + k_line_grad + "
-                 "k_line_anchors + k_edge_draw + k_edlines",
+                 "mean_lines": float(hl.mean()), "kernels": "k_line_maps<3> (COLOR_BGR2GRAY, blur, Sobel, code, move words, "
+                 "anchor masks) + k_line_anchors + k_edge_lines (EdgeDrawing walk + EDline)",
                  "input": "the step's 3-channel colour frames (rawImage of the EAO Frame ctor, Frame.cc:324)"}
     pose = pose_leg(ea, torch, stream, F, cap, gpu, with_cpu=rank == 0 and not args.no_cpu_baseline)
     bow = bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt,
