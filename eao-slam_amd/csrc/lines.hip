@@ -426,7 +426,7 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
     const uint32_t bit = 1u << (idx & 31);
     // marked (a walk reaches only edge pixels: a step onto a non-edge one is stored as (0, 0)),
     // or off >= cap (cap < 2^31)
-    if ((bw & bit) | ((uint32_t)rem >> 31)) break;
+    if (__builtin_expect(((bw & bit) | ((uint32_t)rem >> 31)) != 0, 0)) break;
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
@@ -439,7 +439,7 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
     idx += __builtin_amdgcn_readlane(t_idx, nib);
     tw += __builtin_amdgcn_readlane(t_off, nib);
     sh = __builtin_amdgcn_readlane(t_sh, nib);
-    if (tp & kOut) {  // left the tile
+    if (__builtin_expect((tp & kOut) != 0, 0)) {  // left the tile
       const int xx = pk & 0xffff, yy = pk >> 16;
       tile_load(M, MP, H, T, xx, yy);
       tp = (xx - T.x0) | (yy - T.y0) << 16;

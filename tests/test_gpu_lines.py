@@ -125,6 +125,23 @@ def test_lines_color_exact(frames):
     assert tot > 50
 
 
+def test_lines_color_independent_channels(frames):
+    """B, G and R drawn independently (the colour frames above have G == R): the packed gray
+    conversion must take every byte from its own channel, 3- and 4-channel alike."""
+    rng = np.random.default_rng(0xC01)
+    L = ea.Lines()
+    for f in frames[:2]:
+        c = np.ascontiguousarray(np.stack([f, rng.integers(0, 256, f.shape, dtype=np.uint8),
+                                           (255 - f) // 2 + rng.integers(0, 64, f.shape, dtype=np.uint8)], 2))
+        g = L.detect_color(c)
+        blur, _, _, _ = L.debug_maps()
+        gray = orc.color_to_gray(c, rgb=False)
+        assert np.array_equal(blur, orc.line_maps(gray)[0])
+        assert np.array_equal(g, orc.edlines(gray))
+        c4 = np.ascontiguousarray(np.concatenate([c, rng.integers(0, 256, f.shape + (1,), dtype=np.uint8)], 2))
+        assert np.array_equal(L.detect_color(c4), g)
+
+
 def test_lines_color_batch_device(frames):
     import torch
     cf = color_frames(frames)
