@@ -201,5 +201,19 @@ ldelay() {
   done > gpurun_out/r4_ldelay.log 2>&1
 }
 
+# fastd16: FAST ring pairs loaded straight into packed halves (ds_read_u8_d16 / _hi, inline asm) against the base build (byte reads + v_lshl_or): ORB parity, then stage timings alternating (structured / plain 640x480, plain 1080p).
+fastd16() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_golden.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4d_tests.log 2>&1 &&
+  for r in 1 2; do
+    for lib in eao-slam_amd/lib/ab/base/libeao_accel.so eao-slam_amd/lib/libeao_accel.so; do
+      n=$(basename $(dirname $lib))
+      EAO_ACCEL_LIB=$lib timeout -k 10 200 python -u tools/micro/orb_stages.py > gpurun_out/r4d_s.log 2>&1 &&
+      EAO_ACCEL_LIB=$lib STRUCT=0 timeout -k 10 200 python -u tools/micro/orb_stages.py > gpurun_out/r4d_p.log 2>&1 &&
+      EAO_ACCEL_LIB=$lib STRUCT=0 timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 > gpurun_out/r4d_b.log 2>&1 &&
+      echo "$n struct640: $(tail -1 gpurun_out/r4d_s.log) | plain640: $(tail -1 gpurun_out/r4d_p.log | sed 's/.*fast/fast/;s/ distribute.*//') | plain1080: $(tail -1 gpurun_out/r4d_b.log | sed 's/.*fast/fast/;s/ distribute.*//')" || exit 1
+    done
+  done > gpurun_out/r4d_summary.txt 2>&1
+}
+
 [ $# -eq 1 ] && declare -F "$1" > /dev/null || { echo "usage: $0 <experiment>"; exit 2; }
 "$1"
