@@ -8,12 +8,12 @@
 // Pipeline per batch of HBM-resident gray frames:
 //   k_line_maps     64x32 output tiles through LDS: (COLOR_BGR2GRAY,) the 8U fixed-point
 //                   separable 5-tap Gaussian, Sobel 3x3 dx, dy, code = thresholded |dx| + |dy|
-//                   over 4 (cvRound) | Horizontal bit, and the walk's move bytes
+//                   over 4 (cvRound) | Horizontal bit, and the walk's 16-bit move words
 //   k_line_anchors  one workgroup per frame, a thread per candidate column (the candidates tested
 //                   in k_line_maps, one row mask per column and band): the anchors in the
 //                   reference's column-major scan order (w outer, h inner, step 2) from a
 //                   block scan of the per-column counts
-//   k_edge_draw     one wave per frame: the anchor walks over the move bytes (edge map as an
+//   k_edge_draw     one wave per frame: the anchor walks over the move words (edge map as an
 //                   LDS bitmap), the kept chains assembled by the whole wave
 //   k_edlines       8 waves per frame, a wave per chain (chains are independent): least-
 //                   squares fits and normal-equation sums as wave reductions (integer data,
@@ -42,7 +42,7 @@ constexpr int LN_GRAD_TH = 80, LN_ANCHOR_TH = 8, LN_MIN_LEN = 15, LN_TRY = 6, LN
 constexpr int LN_WAVES = 8;  // k_edlines: waves per frame (chains are independent)
 constexpr double LN_FIT_ERR = 1.6;
 
-// ---------------------------------------------------------------- move bytes
+// ---------------------------------------------------------------- move words
 // A walk step (:1746-2000) depends on the pixel only: whether it is an edge pixel (gImg_ > 0),
 // its direction (dirImg_), and, for each of the two directions a walk can take through it, which
 // of the three forward neighbours has the largest gImg_ byte (the reference's if-chain, ties
@@ -453,7 +453,7 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
 }
 
 // EdgeDrawing's anchor loop (:1695-2327), one wave per frame. Anchors are taken 64 at a time
-// (one per lane, with their move byte); the ones an earlier walk has marked are dropped by one
+// (one per lane, with their code word (direction)); the ones an earlier walk has marked are dropped by one
 // ballot after each walk, so an anchor costs no round trip of its own. Both parts of a chain
 // go to P1 / P2 at the reference's running offsets offF / offS (a short chain's pixels are
 // overwritten by the next walk, as there); chain e is P1[fS[e], fS[e + 1]) reversed, then
@@ -963,7 +963,7 @@ __global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
 struct LineEngine {
   int dev = 0, W = 0, H = 0, B = 0;
   int acap = 0, pcap = 0, ecap = 0;
-  int MP = 0;  // the move bytes' row pitch (a multiple of 16)
+  int MP = 0;  // the move words' row pitch in pixels (a multiple of 16)
   bool fused = true;  // k_edge_lines (EAO_LINES_FUSED=0: k_edge_draw, then k_edlines)
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
