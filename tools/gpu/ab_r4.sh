@@ -201,7 +201,7 @@ ldelay() {
   done > gpurun_out/r4_ldelay.log 2>&1
 }
 
-# fastd16: FAST ring pairs loaded straight into packed halves (ds_read_u8_d16 / _hi, inline asm) against the base build (byte reads + v_lshl_or): ORB parity, then stage timings alternating (structured / plain 640x480, plain 1080p).
+# fastd16: FAST kernel variant (the working tree build) against the base build (lib/ab/base): ORB parity, then stage timings alternating (structured / plain 640x480, plain 1080p). Used for the d16 ring gather (rejected) and the three-pair trip.
 fastd16() {
   timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_golden.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4d_tests.log 2>&1 &&
   for r in 1 2; do
