@@ -522,7 +522,8 @@ class ReplayEngine {
   int kept_pos = -1;              // the detection being associated
   bool cur_np_done = false;       // ... and whether its NP step has read the cache
   // wall-clock profile (us): frame, local mapping, iForest flushes, NP, rects
-  double prof[56] = {0};
+  double prof[60] = {0};
+  double frame_t0 = 0;  // now_us() at the current frame's begin (prof[58])
   int phase = 0;
   // development trace (EAO_REPLAY_TRACE=<file>): host events on the steady clock (ns, the
   // clock rocprofv3's kernel timestamps use), written at destruction -- tools/replay_timeline.py
@@ -1753,6 +1754,10 @@ class ReplayEngine {
     if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(gpu0_ev, ls));
     tr(2, lk, (int)wait_slots.size(), npairs);
+    if (phase == 0) {  // the frame start's launch: time since the frame began
+      prof[58] += now_us() - frame_t0;
+      prof[59] += 1;
+    }
     if (rn_dev) return EAO_OK;
     {
       Tick tw(&prof[41]);
@@ -1879,7 +1884,10 @@ class ReplayEngine {
   int frame_start_gpu(const std::vector<Obj*>& list, const std::vector<std::pair<Det*, Obj*>>& pairs,
                       const std::vector<int>& di, const std::vector<int>& oi) {
     if (list.empty() && pairs.empty()) return EAO_OK;
-    if (int rc = kick()) return rc;  // pending forests overlap this launch
+    {
+      Tick tfk(&prof[57]);
+      if (int rc = kick()) return rc;  // pending forests overlap this launch
+    }
     auto complete_pending = [&]() -> int {
       // forests left pending by the previous frame: their objects' points are read now
       Tick tk(&prof[17]);
@@ -2672,6 +2680,7 @@ class ReplayEngine {
             const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
     Tick tk(&prof[0]);
     tr(1, (int)fid);
+    frame_t0 = now_us();
     phase = 4;
     prof[8] += 1;
     cur = fid;
@@ -2685,6 +2694,7 @@ class ReplayEngine {
     over.assign(objs.size(), 0);
     if (prep.active && (prep.in.fid != fid || prep.in.nb != nb)) discard_lookahead();  // not the stream's next
     if (prep.active) {  // steps 1-6 (partly) ran ahead, while the previous frame waited on the GPU
+      Tick tpf(&prof[56]);
       while (!prep.ok) prep.ok = prep_step(prep);
       o2.swap(prep.o2);
       kept.swap(prep.kept);
@@ -3316,8 +3326,8 @@ int eao_replay_profile(eao_replay* r, double* out12) {
 int eao_replay_profile_n(eao_replay* r, double* out, int n) {
   if (!r || !out || n < 0) return EAO_E_ARG;
   EAO_REPLAY_LOCK(r);
-  std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 56));
-  return std::min(n, 56);
+  std::memcpy(out, r->r.prof, sizeof(double) * std::min(n, 60));
+  return std::min(n, 60);
 }
 
 }  // extern "C"

@@ -400,7 +400,7 @@ int eao_debug_iforest_stamps(uint64_t* out32);
    [2]/[3] iForest launches / time, [4]/[5] NP launches / time,
    [6]/[7] rect launches / time, [8] frames, [12..15] frame sections. */
 int eao_replay_profile(eao_replay* r, double* out24);
-/* The same wall-clock profile, up to n (<= 56) slots; returns the number copied. */
+/* The same wall-clock profile, up to n (<= 60) slots; returns the number copied. */
 int eao_replay_profile_n(eao_replay* r, double* out, int n);
 
 /* ---- frame input stage (src/Tracking.cc:340-554) ---- */

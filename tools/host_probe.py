@@ -25,8 +25,8 @@ keys = [28, 32, 33, 34, 35, 36, 25, 26, 29, 37, 38, 13, 12]
 for rep in range(3):
     g = T._HostReplay(H, flag)
     g._with(ea.Replay.run, g, packed)
-    pr = np.zeros(56)
-    H.eao_replay_profile_n(g.h, ea.P(pr), 56)
+    pr = np.zeros(60)
+    H.eao_replay_profile_n(g.h, ea.P(pr), 60)
     nf = len(frames)
     print("pass %d: " % rep + "  ".join("%s=%.1f%s" % (NAMES[k], pr[k] / (1 if NAMES[k][0] == "#" else nf),
                                                       "" if NAMES[k][0] == "#" else "us/f") for k in keys), flush=True)

@@ -30,8 +30,8 @@ for rep in range(3):
     t0 = time.perf_counter()
     rp.run(packed)
     dt = time.perf_counter() - t0
-    pr = np.zeros(56)
-    ea.lib().eao_replay_profile_n(rp.h, ea.P(pr), 56)
+    pr = np.zeros(60)
+    ea.lib().eao_replay_profile_n(rp.h, ea.P(pr), 60)
     nf = len(frames)
     print("pass %d: wall %.1f ms (%.0f us/frame)" % (rep, dt * 1e3, dt * 1e6 / nf))
     print("   " + "  ".join("%s=%.0f%s" % (NAMES[k], pr[k] / (1 if NAMES[k][0] == "#" else nf),
