@@ -489,6 +489,8 @@ sums:
       if (r.w[a] > r.r1 && r.w[a] < r.r2) add++;
     }
     r.verdict = add == 3 ? 1 : 2;
+    // the pair's only output store, after every read of its inputs (which may be pinned host
+    // memory): the host's early-exit wait relies on it (replay.cpp spin_ready, rules 1-3)
     out[p] = r;
   }
 }
@@ -579,6 +581,7 @@ __device__ __forceinline__ void rects_body(const int c, const CamDev& cam, const
     if (ymn < 0) ymn = 0;
     if (xmx > cam.maxX) xmx = cam.maxX;
     if (ymx > cam.maxY) ymx = cam.maxY;
+    // the rect's output stores come after all of the workgroup's input reads (spin_ready's rules)
     rect[4 * c] = (int)xmn;
     rect[4 * c + 1] = (int)ymn;
     rect[4 * c + 2] = (int)fsub(xmx, xmn);
@@ -1285,6 +1288,8 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
   } else if (sc > thb) {
     sc = thb;
   }
+  // each score stored once, final (the host's early-exit wait reads pinned `scores`; replay.cpp
+  // spin_ready, rules 1-3); the batch's pinned inputs were copied to the device by k_stage before
   scores[g] = sc;
   if (scores2) scores2[g] = sc;
 }

@@ -528,14 +528,16 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ m
                                                   const uint32_t* __restrict__ anchors, const int* __restrict__ nanchor,
                                                   int acap, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2,
                                                   int pcap, uint32_t* __restrict__ chains, uint32_t* __restrict__ sid,
-                                                  int ecap, int* __restrict__ nedge) {
+                                                  int ecap, int* __restrict__ nedge, uint32_t* __restrict__ gstarts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
   const int f = blockIdx.x, lane = threadIdx.x;
   const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
   uint32_t* bits = lds_ed;
-  uint32_t* fS = bits + nbp;  // the kept chains' offF / offS starts (the reference's fS / sS)
+  // the kept chains' offF / offS starts (the reference's fS / sS): in LDS after the bitmap, or in
+  // global memory (gstarts, frames whose bitmap + starts exceed the LDS; edge_draw_lds)
+  uint32_t* fS = gstarts ? gstarts + (long long)f * 2 * ep : bits + nbp;
   uint32_t* sS = fS + ep;
-  MoveTile T{(uint16_t*)(sS + ep), -LE_TW, -LE_TH};
+  MoveTile T{(uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep)), -LE_TW, -LE_TH};
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
   uint32_t* Q = chains + (long long)f * 2 * pcap;
@@ -900,14 +902,17 @@ __global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
     uint32_t* __restrict__ chains, uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
     const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi, const int16_t* __restrict__ dyi,
     uint32_t* __restrict__ lscratch, uint32_t* __restrict__ ccount, float min_length, float* __restrict__ out,
-    int* __restrict__ nout, int cap) {
+    int* __restrict__ nout, int cap, uint32_t* __restrict__ gstarts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
   __shared__ int pub, ticket, state;  // chains published, next chain to take, 0 walking / 1 done / -1 failed
   const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
   uint32_t* bits = lds_ed;
-  uint32_t* fS = bits + nbp;
+  // chain starts in LDS, or in global memory (gstarts) for large frames (k_edge_draw); the line
+  // waves read them after the walker's release on pub, like the chain pixels P1 / P2
+  uint32_t* fS = gstarts ? gstarts + (long long)f * 2 * ep : bits + nbp;
   uint32_t* sS = fS + ep;
+  uint16_t* tile = (uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep));
   const long long fo = (long long)f * W * H;
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
@@ -922,7 +927,7 @@ __global__ __launch_bounds__(64 * LE_WAVES) void k_edge_lines(
   }
   __syncthreads();
   if (wave == 0) {
-    MoveTile T{(uint16_t*)(sS + ep), -LE_TW, -LE_TH};
+    MoveTile T{tile, -LE_TW, -LE_TH};
     const int ne = ed_walker<true>(moves + (long long)f * MP * H, code + fo, W, H, MP, anchors + (long long)f * acap, nanchor[f],
                                    acap, P1, P2, pcap, ecap, bits, fS, sS, T, &pub);
     if (lane == 0) {
@@ -965,6 +970,8 @@ struct LineEngine {
   int acap = 0, pcap = 0, ecap = 0;
   int MP = 0;  // the move words' row pitch in pixels (a multiple of 16)
   bool fused = true;  // k_edge_lines (EAO_LINES_FUSED=0: k_edge_draw, then k_edlines)
+  bool gstarts = false;  // the chains' fS / sS starts in global memory (d_starts), not LDS
+  uint32_t* d_starts = nullptr;
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
   uint8_t* d_blur = nullptr;
@@ -981,7 +988,7 @@ struct LineEngine {
   int* h_n = nullptr;  // pinned: the single-frame line count
   ~LineEngine() {
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
-                 d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines};
+                 d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts};
     for (void* q : p)
       if (q) (void)hipFree(q);
     if (h_n) (void)hipHostFree(h_n);
@@ -1006,10 +1013,13 @@ static void gauss5(int* k) {
   }
 }
 
-// k_edge_draw's dynamic LDS: the edge bitmap, the chains' fS / sS starts, the move tile
-static size_t edge_draw_lds(int W, int H, int ecap) {
-  return ((size_t)((((W * H + 31) / 32) + 3) & ~3) + 2 * (size_t)((ecap + 2 + 3) & ~3)) * 4 + sizeof(uint16_t) * LE_TW * LE_TH;
+// k_edge_draw's dynamic LDS: the edge bitmap, the chains' fS / sS starts (unless they are kept in
+// global memory: gstarts), the move tile
+static size_t edge_draw_lds(int W, int H, int ecap, bool gstarts) {
+  return ((size_t)((((W * H + 31) / 32) + 3) & ~3) + (gstarts ? 0 : 2 * (size_t)((ecap + 2 + 3) & ~3))) * 4 +
+         sizeof(uint16_t) * LE_TW * LE_TH;
 }
+constexpr size_t kLdsMax = 160 * 1024;
 
 }  // namespace eao
 
@@ -1029,9 +1039,10 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
     return EAO_E_NODEVICE;
   }
   // the same dynamic LDS k_edge_draw is launched with (edge bitmap, chain starts, move tile);
-  // EdgeDrawing's arrays: edgePixelArraySize = pixels / 5, maxNumOfEdge = that / 20
-  if (edge_draw_lds(width, height, width * height / 5 / 20) > 160 * 1024) {
-    set_error("eao_lines_create: the per-frame edge bitmap, chain starts and move tile exceed the LDS");
+  // EdgeDrawing's arrays: edgePixelArraySize = pixels / 5, maxNumOfEdge = that / 20. Frames whose
+  // chain starts do not fit beside the bitmap keep the starts in global memory (up to ~1.18 M px)
+  if (edge_draw_lds(width, height, width * height / 5 / 20, true) > kLdsMax) {
+    set_error("eao_lines_create: the per-frame edge bitmap and move tile exceed the LDS");
     return EAO_E_CAPACITY;
   }
   eao_lines* L = new eao_lines();
@@ -1045,6 +1056,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   if (const char* v = getenv("EAO_LINES_FUSED")) e.fused = v[0] != '0';
   e.acap = e.pcap;
   e.ecap = e.pcap / 20;
+  e.gstarts = edge_draw_lds(width, height, e.ecap, false) > kLdsMax;
   int k5[5];
   gauss5(k5);
   e.k[0] = k5[0];
@@ -1068,6 +1080,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
       hipMalloc(&e.d_lscr, (size_t)e.pcap * 8 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_sid, (size_t)(e.ecap + 1) * 4 * max_batch) != hipSuccess ||
       hipMalloc(&e.d_ccnt, (size_t)(e.ecap + 1) * 4 * max_batch) != hipSuccess ||
+      (e.gstarts && hipMalloc(&e.d_starts, (size_t)2 * ((e.ecap + 2 + 3) & ~3) * 4 * max_batch) != hipSuccess) ||
       hipMalloc(&e.d_nanch, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_nedge, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_img, (size_t)width * height * 4) != hipSuccess ||
@@ -1116,12 +1129,14 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
                      e.d_anch, e.acap, e.d_nanch);
   if (e.fused) {
-    hipLaunchKernelGGL(k_edge_lines, dim3(nframes), dim3(64 * LE_WAVES), edge_draw_lds(W, H, e.ecap), s, e.d_moves, W,
-                       H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap,
-                       e.d_nedge, e.d_code, e.d_dx, e.d_dy, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts, cap);
+    hipLaunchKernelGGL(k_edge_lines, dim3(nframes), dim3(64 * LE_WAVES), edge_draw_lds(W, H, e.ecap, e.gstarts), s,
+                       e.d_moves, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid,
+                       e.ecap, e.d_nedge, e.d_code, e.d_dx, e.d_dy, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts,
+                       cap, e.d_starts);
   } else {
-    hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap), s, e.d_moves, e.d_code, W, H, e.MP,
-                       e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge);
+    hipLaunchKernelGGL(k_edge_draw, dim3(nframes), dim3(64), edge_draw_lds(W, H, e.ecap, e.gstarts), s, e.d_moves,
+                       e.d_code, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid,
+                       e.ecap, e.d_nedge, e.d_starts);
     hipLaunchKernelGGL(k_edlines, dim3(nframes), dim3(64 * LN_WAVES), 0, s, e.d_code, e.d_dx, e.d_dy, W, H,
                        e.d_chain, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts,
                        cap);

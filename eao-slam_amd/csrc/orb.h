@@ -57,6 +57,11 @@ class OrbEngine {
   std::vector<CellDev> cells;
   std::vector<int> resize_xofs, resize_yrows;
   std::vector<short> resize_ia, resize_ib;
+  struct ResizePlan {          // k_resize_lds launch of a level >= 1
+    int tr, block, tiles;
+    size_t lds;
+  };
+  std::vector<ResizePlan> resize_plan;
   std::vector<int2> slot_map;
   long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;
   std::vector<BandDev> bands;

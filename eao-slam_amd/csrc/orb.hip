@@ -80,6 +80,112 @@ __global__ __launch_bounds__(256) void k_resize_tile(const uint8_t* __restrict__
   }
 }
 
+// LDS-staged resize (the production path): one workgroup per (tile of tr output rows, frame).
+//   1. the tile's source rows [ys0, ys1] are staged in LDS with 16-byte loads (row stride sw16 =
+//      the source width rounded up to 16), all of them in flight;
+//   2. a work item = (group of 4 output columns, segment of RESIZE_RS rows): the item keeps its
+//      4 columns' x offsets and coefficients in registers, walks its rows keeping the last two
+//      source rows' horizontal sums (a source row is summed once per item, not per output row),
+//      taps are LDS byte reads, and the 4 outputs go out as one dword store (level planes are
+//      64-byte pitched, so the store is aligned; columns past dw repeat the last column's
+//      coefficients into the plane's pitch padding, which nothing reads).
+// Items are numbered column-group-fastest, so a wave's stores cover 256 contiguous bytes.
+// Arithmetic identical to k_resize_tile (OpenCV INTER_LINEAR 8U, ORBextractor.cc:1120).
+constexpr int RESIZE_RS = 4;
+template <bool VEC>
+__global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__ src, int spitch, long long sstride,
+                                                     uint8_t* __restrict__ dst, int dpitch, long long dstride,
+                                                     int sw, int dw, int dh, int tr,
+                                                     const int* __restrict__ xofs, const short* __restrict__ ialpha,
+                                                     int xmax, const int* __restrict__ yrows,
+                                                     const short* __restrict__ ibeta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int dy0 = blockIdx.x * tr, f = blockIdx.y;
+  const int dy1 = min(dy0 + tr, dh);
+  const int ys0 = yrows[2 * dy0], ys1 = yrows[2 * (dy1 - 1) + 1];
+  const int nrows = ys1 - ys0 + 1;
+  const int sw16 = (sw + 15) & ~15;
+  const uint8_t* sf = src + f * sstride + (long long)ys0 * spitch;
+  const int tid = threadIdx.x, nb = blockDim.x;
+  if (VEC) {
+    const int cpr = sw16 >> 4, nc = nrows * cpr;
+    int c = tid;
+    for (; c + 3 * nb < nc; c += 4 * nb) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int cc = c + u * nb, r = cc / cpr, k = cc - r * cpr;
+        v[u] = *(const uint4*)(sf + (long long)r * spitch + 16 * k);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) ((uint4*)smem)[c + u * nb] = v[u];
+    }
+    for (; c < nc; c += nb) {
+      const int r = c / cpr, k = c - r * cpr;
+      ((uint4*)smem)[c] = *(const uint4*)(sf + (long long)r * spitch + 16 * k);
+    }
+  } else {
+    for (int c = tid; c < nrows * sw16; c += nb) {
+      const int r = c / sw16, k = c - r * sw16;
+      smem[c] = k < sw ? sf[(long long)r * spitch + k] : 0;
+    }
+  }
+  __syncthreads();
+  const int G = (dw + 3) >> 2;
+  const int nseg = (dy1 - dy0 + RESIZE_RS - 1) / RESIZE_RS;
+  uint8_t* df = dst + f * dstride;
+  for (int it = tid; it < G * nseg; it += nb) {
+    const int seg = it / G, g = it - seg * G;
+    int sx[4], a0[4], a1[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int dx = min(4 * g + u, dw - 1);
+      sx[u] = xofs[dx];
+      const bool two = dx < xmax;
+      a0[u] = two ? ialpha[2 * dx] : 2048;
+      a1[u] = two ? ialpha[2 * dx + 1] : 0;
+    }
+    auto hsum = [&](int r, int (&h)[4]) {
+      const uint8_t* row = smem + (r - ys0) * sw16;
+#pragma unroll
+      for (int u = 0; u < 4; u++) h[u] = row[sx[u]] * a0[u] + row[sx[u] + 1] * a1[u];  // a1 = 0 past xmax
+    };
+    int ra = -1, rb = -1, ha[4], hb[4];
+    const int e0 = dy0 + seg * RESIZE_RS, e1 = min(e0 + RESIZE_RS, dy1);
+    for (int dy = e0; dy < e1; dy++) {
+      const int r0 = yrows[2 * dy], r1 = yrows[2 * dy + 1];
+      const int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
+      int d0[4], d1[4];
+      if (r0 == rb) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) d0[u] = hb[u];
+      } else if (r0 == ra) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) d0[u] = ha[u];
+      } else {
+        hsum(r0, d0);
+      }
+      if (r1 == rb) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) d1[u] = hb[u];
+      } else {
+        hsum(r1, d1);
+      }
+      uint32_t w = 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int v = (d0[u] * b0 + d1[u] * b1 + (1 << 21)) >> 22;
+        w |= (uint32_t)min(max(v, 0), 255) << (8 * u);
+        ha[u] = d0[u];
+        hb[u] = d1[u];
+      }
+      ra = r0;
+      rb = r1;
+      *(uint32_t*)(df + (long long)dy * dpitch + 4 * g) = w;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- FAST
 // FAST corner strength of a pixel (cv::FAST-9/16 + cornerScore<16>, ORBextractor.cc:809-815):
 // with A = min over the 16 arcs of 9 ring pixels of the arc's max and B = max over the arcs
@@ -1158,6 +1264,29 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
     }
   }
   pyr_bytes = (long long)((poff + 255) & ~255LL);
+  // k_resize_lds tiles: RESIZE_RS-row segments of 4-column groups, up to 4 segments per tile while
+  // a tile's items fit one 1024-thread workgroup; LDS = the tile's source rows (+16 B: a tap past
+  // the last row's end is read with coefficient 0)
+  resize_plan.assign(nl, ResizePlan{});
+  for (int l = 1; l < nl; l++) {
+    const LevelDev& L = levels[l];
+    const int G = (L.w + 3) / 4;
+    const int segs = std::max(1, std::min(4, 1024 / G));
+    ResizePlan& R = resize_plan[l];
+    R.tr = RESIZE_RS * segs;
+    R.tiles = (L.h + R.tr - 1) / R.tr;
+    R.block = std::min(1024, (G * segs + 63) / 64 * 64);
+    int rows = 0;
+    for (int t = 0; t < R.tiles; t++) {
+      const int d0 = t * R.tr, d1 = std::min(d0 + R.tr, L.h);
+      rows = std::max(rows, resize_yrows[2 * (L.tab_y + d1 - 1) + 1] - resize_yrows[2 * (L.tab_y + d0)] + 1);
+    }
+    R.lds = (size_t)rows * ((levels[l - 1].w + 15) & ~15) + 16;
+    if (R.lds > 64 * 1024) {
+      set_error("eao_orb_create: image too wide for the pyramid kernel's LDS tile");
+      return EAO_E_ARG;
+    }
+  }
   {
     // FAST bands: the cells of a level row share their ROI rows
     bands.clear();
@@ -1255,13 +1384,26 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
   const long long fstride = (long long)pitch * p.height;
   const int nl = p.nlevels;
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[0], s));
-  // pyramid
+  // pyramid: k_resize_lds (EAO_RESIZE=0: the round-4 k_resize_tile, A/B switch)
+  static const int resize_lds = [] {
+    const char* v = getenv("EAO_RESIZE");
+    return v && v[0] == '0' ? 0 : 1;
+  }();
   for (int l = 1; l < nl; l++) {
     const LevelDev& L = levels[l];
     const LevelDev& S = levels[l - 1];
     const uint8_t* src = l == 1 ? d_frames : d_pyr + S.plane_off;
     const int spitch = l == 1 ? pitch : S.pitch;
     const long long sstride = l == 1 ? fstride : pyr_bytes;
+    if (resize_lds) {
+      const ResizePlan& R = resize_plan[l];
+      const bool vec = l > 1 || ((uintptr_t)d_frames % 16 == 0 && pitch % 16 == 0);
+      auto kr = vec ? k_resize_lds<true> : k_resize_lds<false>;
+      hipLaunchKernelGGL(kr, dim3(R.tiles, nframes), dim3(R.block), R.lds, s, src, spitch, sstride,
+                         d_pyr + L.plane_off, L.pitch, pyr_bytes, S.w, L.w, L.h, R.tr, d_xofs + L.tab_x,
+                         d_ia + 2 * L.tab_x, L.xmax, d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
+      continue;
+    }
     dim3 g(1, (L.h + RESIZE_TR - 1) / RESIZE_TR, nframes);
     hipLaunchKernelGGL(k_resize_tile, g, dim3(256), 0, s, src, spitch, sstride, d_pyr + L.plane_off,
                        L.pitch, pyr_bytes, L.w, L.h, d_xofs + L.tab_x, d_ia + 2 * L.tab_x, L.xmax,

@@ -73,6 +73,12 @@ static const int kPrepChunk = [] {
   const int c = v ? atoi(v) : 0;
   return c > 0 ? c : 128;
 }();
+// test switch: EAO_LOOKAHEAD_EAGER=1 runs a wait's look-ahead to completion whatever the wait's
+// state (the CPU harness's kernels finish at launch, so its waits would otherwise never fill)
+static const bool g_la_eager = [] {
+  const char* v = getenv("EAO_LOOKAHEAD_EAGER");
+  return v && v[0] == '1';
+}();
 static const bool g_sentinel = [] {
   const char* v = getenv("EAO_SENTINEL_WAIT");
   return !(v && v[0] == '0');
@@ -91,7 +97,17 @@ static void fill64(void* p, size_t words) {
   uint64_t* q = (uint64_t*)p;
   for (size_t i = 0; i < words; i++) q[i] = kSent64;
 }
-// wait for `ready()` (sentinels overwritten) or the event, whichever comes first
+// wait for `ready()` (sentinels overwritten) or the event, whichever comes first.
+// Returning on the outputs alone is safe because the kernels that write these pinned outputs
+// (k_rects_np / k_np_pairs via np_pair_body and rects_body, k_iforest_sum) keep three rules:
+//   1. every output word the host waits for is stored exactly once, with its final value;
+//   2. a workgroup's output stores follow all of its reads of the pinned inputs (and k_stage,
+//      which copies a forest batch's pinned inputs to the device, precedes the tree kernel in
+//      stream order), so a buffer is free for refilling once every output has landed;
+//   3. no output word can equal its fill pattern (kSent32 / kSent64 are NaN payloads the
+//      hardware never produces; kSent8 is no flag value).
+// A fault after the outputs have landed is reported when the launch's event is queried before
+// its buffers are reused (rects_np_launch, kick).
 template <class Ready>
 static hipError_t spin_ready(hipEvent_t e, Ready&& ready) {
   if (!g_sentinel || !g_spin_wait) return g_spin_wait ? spin_event_plain(e) : hipEventSynchronize(e);
@@ -502,6 +518,17 @@ class ReplayEngine {
     }
     return u.get();
   }
+  void mp_erase(int id) {  // forget a map point (a discarded look-ahead's own creation)
+    if (id >= 0 && id < (1 << 24)) {
+      const size_t b = (size_t)id / kMpBlock, k = (size_t)id % kMpBlock;
+      if (b < mp_blocks.size() && mp_live[b] && mp_live[b][k]) {
+        mp_live[b][k] = 0;
+        mp_blocks[b][k] = MapPt();
+      }
+      return;
+    }
+    mps.erase(id);
+  }
   std::vector<std::unique_ptr<Det>> dets;
   bool ini = false;
   long ini_frame = 0;
@@ -789,15 +816,13 @@ class ReplayEngine {
   }
 
   // Tracking::AssociateObjAndLines (Tracking.cc:2472-2527) for the detections whose
-  // lines SampleObjYaw can read (yaw-sampled classes); the frame's staged line set
-  // `taken`: the consumed line set is kept there (a discarded look-ahead puts it back)
-  void associate_lines(const std::vector<Det*>& o2, std::vector<float>* taken = nullptr, bool* took = nullptr) {
+  // lines SampleObjYaw can read (yaw-sampled classes); the frame's staged line set.
+  // `took` (the look-ahead): set when a staged set was consumed -- a discarded look-ahead steps
+  // staged_next back over it, so the staged sets are not cleared while the look-ahead holds one
+  void associate_lines(const std::vector<Det*>& o2, bool* took = nullptr) {
     const std::vector<float>* fl = staged_next < staged_lines.size() ? &staged_lines[staged_next] : nullptr;
     if (fl) staged_next++;
-    if (fl && taken) {
-      *taken = *fl;
-      *took = true;
-    }
+    if (fl && took) *took = true;
     std::vector<double> all, in, ang;
     if (fl && yaw_on()) {
       all.assign(fl->begin(), fl->end());
@@ -825,6 +850,10 @@ class ReplayEngine {
         }
       }
     }
+    if (!took) release_staged_lines();
+  }
+  // all staged sets consumed (and none held by a look-ahead): drop them
+  void release_staged_lines() {
     if (staged_next == staged_lines.size() && !staged_lines.empty()) {
       staged_lines.clear();
       staged_next = 0;
@@ -1278,6 +1307,10 @@ class ReplayEngine {
         EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, c));
         b.cap_out = c;
       }
+      if (b.ev) {  // the slot's previous launch (completed on its outputs): a late fault surfaces here
+        const hipError_t e = hipEventQuery(b.ev);
+        if (e != hipSuccess && e != hipErrorNotReady) EAO_HIP_CHECK(e);
+      }
       if (g_sentinel && !sharded()) {  // scores and speculative stats pre-filled (spin_ready)
         fill64(b.h_out, (size_t)np);
         fill32(b.h_out + b.sp_out, (size_t)ns * (sizeof(eao_np_stats) / 4));
@@ -1671,6 +1704,13 @@ class ReplayEngine {
     const size_t o_osp = al16(o_val + total), o_oth = o_osp + sizeof(double*) * (size_t)(nb + npairs);
     const size_t in_bytes = chained ? o_oth + sizeof(float) * (size_t)(nb + npairs) : o_val + total;
     const size_t o_r = sizeof(eao_np_stats) * (size_t)npairs, o_ok = o_r + sizeof(int) * 4 * (size_t)nb;
+    // the previous frame start's wait may have ended on its outputs before its event: the event
+    // is queried once before its pinned buffers are refilled, so a fault of that launch is
+    // reported here (its outputs were complete: see spin_ready for the kernels' rules)
+    if (gpu0_ev) {
+      const hipError_t e = hipEventQuery(gpu0_ev);
+      if (e != hipSuccess && e != hipErrorNotReady) EAO_HIP_CHECK(e);
+    }
     int rc = stage(in_bytes, o_ok + nb);
     if (rc) return rc;
     // outputs: pinned host memory (read after the spin), or -- sharded, device-form
@@ -2481,19 +2521,22 @@ class ReplayEngine {
     size_t k = 0;
     std::vector<MapPt*> tr;
     std::vector<Det*> o2, kept;
-    bool took_lines = false;  // step 3 consumed a staged line set (kept in `lines`)
-    std::vector<float> lines;
+    bool took_lines = false;  // step 3 consumed a staged line set (staged_next moved past it)
+    std::vector<int> created;  // map-point ids step 1 created (look-ahead only: erased on discard)
   } prep, prep_now;
   // drop a look-ahead that will not be consumed (a failed stream call, or a frame call that
   // does not continue the stream): its detections stay unreferenced, a line set it consumed
   // goes back to the front of the staged sets, and the frame runs in order when it comes
+  // (the map points it created go too: a caller that resumes with another frame must not find
+  // them among the known points, e.g. in eao_replay_update_points)
   void discard_lookahead() {
-    if (prep.active && prep.took_lines) {
-      staged_lines.insert(staged_lines.begin() + (ptrdiff_t)staged_next, std::move(prep.lines));
-    }
+    if (prep.active && prep.took_lines && staged_next > 0) staged_next--;  // the set is still staged
+    if (prep.active)
+      for (int id : prep.created) mp_erase(id);
     prep.active = prep.ok = prep.took_lines = false;
     prep.o2.clear();
     prep.kept.clear();
+    prep.created.clear();
     la_set = false;
   }
   // fill a wait on `ev` with the next frame's steps 1-6 (until the event, or `ready()`)
@@ -2522,6 +2565,10 @@ class ReplayEngine {
     Tick tk(&prof[52]);
     const unsigned qmask = (g_sentinel && has_ready) ? 3u : 0u;
     for (unsigned it = 0; !prep.ok; it++) {
+      if (g_la_eager) {
+        prep.ok = prep_step(prep);
+        continue;
+      }
       if (g_sentinel && has_ready && ready()) break;
       if ((it & qmask) == 0 && hipEventQuery(ev) != hipErrorNotReady) break;
       prep.ok = prep_step(prep);
@@ -2536,6 +2583,7 @@ class ReplayEngine {
     s.took_lines = false;
     s.o2.clear();
     s.kept.clear();
+    s.created.clear();
   }
 
   // STEPS 1-6 of TrackWithMotionModel's object section for one frame's inputs (pose s.P),
@@ -2568,7 +2616,9 @@ class ReplayEngine {
       }
       case 1: {  // the frame's map points, kPrepChunk per step
         const int e = std::min(in.npts, (int)s.k + kPrepChunk);
+        const bool ahead = &s == &prep;
         for (int i = (int)s.k; i < e; i++) {
+          if (ahead && !mp_lookup(in.ids[i])) s.created.push_back(in.ids[i]);
           MapPt* p = mappoint(in.ids[i]);
           for (int a = 0; a < 3; a++) p->pos[a] = in.pos[3 * i + a];
           p->proj_epoch = 0;
@@ -2604,7 +2654,7 @@ class ReplayEngine {
         return false;
       }
       case 3:
-        associate_lines(o2, &s == &prep ? &s.lines : nullptr, &s.took_lines);  // STEP 3, Tracking.cc:1286
+        associate_lines(o2, &s == &prep ? &s.took_lines : nullptr);  // STEP 3, Tracking.cc:1286
         s.phase = 4;
         s.k = 0;
         prof[12] += now_us() - tA;
@@ -2699,6 +2749,9 @@ class ReplayEngine {
       o2.swap(prep.o2);
       kept.swap(prep.kept);
       prep.ok = prep.active = false;
+      if (prep.took_lines) release_staged_lines();  // its line set is consumed for good
+      prep.took_lines = false;
+      prep.created.clear();
     } else {
       bool pend = false;  // forests still pending from the previous frame read positions / flags
       for (auto& up : objs) pend |= up->pending != 0;
@@ -3239,7 +3292,8 @@ static int replay_stream(eao_replay* r, int n_frames, const int32_t* frame_ids, 
   for (int t = 0; t < n_frames; t++) {
     // the next frame's inputs, for the look-ahead of steps 1-6 (not across a point record)
     E.la_set = false;
-    if (t + 1 < n_frames && !(n_upd && n_upd[t])) {
+    // (only for well-formed counts: a malformed next frame is refused by its own call)
+    if (t + 1 < n_frames && !(n_upd && n_upd[t]) && n_boxes[t + 1] >= 0 && n_pts[t + 1] >= 0) {
       ReplayEngine::FrameIn& in = E.la;
       in.fid = (unsigned long)frame_ids[t + 1];
       in.T = Tcw + 16 * (size_t)(t + 1);
@@ -3316,10 +3370,10 @@ int eao_replay_local_mapping(eao_replay* r) {
   return r->r.local_mapping();
 }
 
-int eao_replay_profile(eao_replay* r, double* out12) {
-  if (!r || !out12) return EAO_E_ARG;
+int eao_replay_profile(eao_replay* r, double* out24) {
+  if (!r || !out24) return EAO_E_ARG;
   EAO_REPLAY_LOCK(r);
-  std::memcpy(out12, r->r.prof, sizeof(double) * 24);
+  std::memcpy(out24, r->r.prof, sizeof(double) * 24);
   return EAO_OK;
 }
 

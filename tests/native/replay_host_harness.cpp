@@ -22,12 +22,22 @@ CamDev make_cam(const eao_camera& c) {
   d.invW = 64.0f / d.maxX; d.invH = 48.0f / d.maxY;
   return d;
 }
+static bool g_in_rects_np = false;  // EAO_HARNESS_DUMP: tags the frame-start pairs
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
                           eao_np_stats* out, hipStream_t, int, const double* const* os_ptr, const float* oth) {
   static FILE* dump = std::getenv("EAO_HARNESS_DUMP") ? std::fopen(std::getenv("EAO_HARNESS_DUMP"), "w") : nullptr;
   for (int p = 0; p < npairs; p++) {
-    if (dump) std::fprintf(dump, "np %d %d %d\n", npairs, flen[p], olen[p]);
+    if (dump) {  // kind (fs: frame start, np: speculative / relaunch), pairs, m, n, valid m, kept valid n, kept n
+      int mv = 0, nv = 0, nk = 0;
+      for (int i = 0; i < flen[p]; i++) mv += fv[foff[p] + i] != 0;
+      for (int i = 0; i < olen[p]; i++) {
+        const bool k = !(os_ptr && os_ptr[p] && os_ptr[p][i] > (double)oth[p]);
+        nk += k;
+        nv += k && ov[ooff[p] + i];
+      }
+      std::fprintf(dump, "%s %d %d %d %d %d %d\n", g_in_rects_np ? "fs" : "np", npairs, flen[p], olen[p], mv, nv, nk);
+    }
     std::vector<float> pts;
     std::vector<uint8_t> val;
     const double* os = os_ptr ? os_ptr[p] : nullptr;
@@ -46,6 +56,13 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
                                uint32_t seed, const uint32_t* sample, double* scores, hipStream_t, int, int,
                                int, double*, double* scores2) {
+  // fault injection (tests): EAO_HARNESS_FAIL_IFOREST=N fails the N-th forest launch (1-based)
+  static int calls = 0;
+  static const int fail_at = std::getenv("EAO_HARNESS_FAIL_IFOREST") ? std::atoi(std::getenv("EAO_HARNESS_FAIL_IFOREST")) : 0;
+  if (++calls == fail_at) {
+    set_error("harness: injected forest launch failure");
+    return EAO_E_HIP;
+  }
   static FILE* dump = std::getenv("EAO_HARNESS_DUMP") ? std::fopen((std::string(std::getenv("EAO_HARNESS_DUMP")) + ".if").c_str(), "w") : nullptr;
   for (int c = 0; c < nclouds; c++) {
     if (dump) std::fprintf(dump, "if %d %d\n", nclouds, len[c]);
@@ -75,7 +92,10 @@ int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const 
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen, eao_np_stats* out,
                           hipStream_t s, int max_olen, const double* const* os_ptr, const float* oth) {
   rects(cam, T, nclouds, rpts, roff, rlen, rect, ok, s, ros, rth);
-  return np_batch(npairs, fp, fv, foff, flen, op, ov, ooff, olen, out, s, max_olen, os_ptr, oth);
+  g_in_rects_np = true;
+  const int rc = np_batch(npairs, fp, fv, foff, flen, op, ov, ooff, olen, out, s, max_olen, os_ptr, oth);
+  g_in_rects_np = false;
+  return rc;
 }
 bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }
 int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t) {

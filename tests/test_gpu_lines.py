@@ -182,9 +182,39 @@ def test_lines_odd_sizes(frames, w, h):
     assert tot > 0 or w * h < 10000  # (a 33x20 crop holds no line of 50 px)
 
 
-def rings(period):
-    yy, xx = np.mgrid[0:480, 0:640]
-    return ((np.hypot(xx - 320, yy - 240) // (period / 2)) % 2 * 255).astype(np.uint8)
+def rings(period, w=640, h=480):
+    yy, xx = np.mgrid[0:h, 0:w]
+    return ((np.hypot(xx - w // 2, yy - h // 2) // (period / 2)) % 2 * 255).astype(np.uint8)
+
+
+def test_lines_1280x720_chain_starts_in_global():
+    """1280x720: the edge bitmap (115 KB) and the move tile fill the LDS, so the chains' fS / sS
+    starts live in global memory (edge_draw_lds). Office frames and dense rings (thousands of
+    chains) through the single-frame and the batched entry points, bit-exact; frames past the
+    bitmap's LDS capacity (~1.18 M px) are refused at create."""
+    import torch
+    w, h = 1280, 720
+    fr = synth.line_frames(2, w=w, h=h, seed=0xEA9)
+    imgs = [fr[0], fr[1], rings(8, w, h)]
+    L = ea.Lines(w, h)
+    outs = []
+    for img in imgs:
+        g, o = L.detect(img), orc.edlines(img)
+        assert len(o) > 0 and g.shape == o.shape and np.array_equal(g, o)
+        outs.append(o)
+    LB = ea.Lines(w, h, max_batch=3)
+    dev = torch.device("cuda", 0)
+    d = torch.from_numpy(np.ascontiguousarray(np.stack(imgs))).to(dev)
+    cap = 4096
+    o = torch.zeros((3, cap, 6), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(3, dtype=torch.int32, device=dev)
+    LB.detect_batch_device(d.data_ptr(), 3, w, 50.0, o.data_ptr(), cnt.data_ptr(), cap)
+    torch.cuda.synchronize()
+    ho, hc = o.cpu().numpy(), cnt.cpu().numpy()
+    for t in range(3):
+        assert hc[t] == len(outs[t]) and np.array_equal(ho[t, :hc[t]], outs[t]), t
+    with pytest.raises(Exception):
+        ea.Lines(1920, 1080)
 
 
 def test_lines_dense_rings():

@@ -34,6 +34,19 @@ def test_pyramid_exact(frames):
         assert np.array_equal(a, b), "level %d differs at %d px" % (l, int((a != b).sum()))
 
 
+@pytest.mark.parametrize("w,h", [(641, 481), (1000, 700), (1280, 720), (1920, 1080), (3840, 2160)])
+def test_pyramid_exact_sizes(w, h):
+    # k_resize_lds: unaligned rows (odd widths: byte staging of level 0), a partial last column
+    # group / row tile, wide levels with one 4-row segment per 1024-thread tile (4K)
+    img = np.random.default_rng(w + h).integers(0, 256, (h, w), dtype=np.uint8)
+    orb = ea.Orb(width=w, height=h, nfeatures=2000)
+    g = orb.pyramid(img)
+    o = orc.pyramid(img)
+    for l, (a, b) in enumerate(zip(g, o)):
+        assert a.shape == b.shape
+        assert np.array_equal(a, b), "%dx%d level %d differs at %d px" % (w, h, l, int((a != b).sum()))
+
+
 def test_scale_tables_and_quotas():
     orb = ea.Orb()
     p = orc.orb_params()

@@ -138,12 +138,14 @@ def test_other_flags_short_stream(flag):
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-@pytest.mark.parametrize("name", ["replay_fr3_demo_eao", "replay_fr3_full"])
+@pytest.mark.parametrize("name", ["replay_fr3_demo_eao", "replay_fr3_full", "replay_config_c_200"])
 def test_independent_restatement_over_whole_streams(name):
     """The pure-Python restatement's outputs over the WHOLE streams (all 405 EAO frames, all 2582
-    Full frames; tools/make_assoc_py_golden.py, minutes of pure Python, hence fixtures) equal the
-    C++ oracle's fixtures that the engine's GPU tests compare against (tests/test_gpu_fr3.py):
-    every detection's outcome and object id, the object records and their point sets."""
+    Full frames, and the 200 Config C frames at the config's scale -- 64 objects x 2000 points, NP
+    subsampling at n > 3m, forests over clouds of >= 1500 points; tools/make_assoc_py_golden.py,
+    minutes of pure Python, hence fixtures) equal the C++ oracle's fixtures that the engine's GPU
+    tests compare against (tests/test_gpu_fr3.py, tests/test_gpu_shard.py): every detection's
+    outcome and object id, the object records (statistics within 1e-5) and their point sets."""
     c = np.load(os.path.join(GOLDEN, name + ".npz"))
     p = np.load(os.path.join(GOLDEN, name + "_py.npz"))
     assert int(c["digest"]) == int(p["digest"]) and c["flag"] == p["flag"]
@@ -152,6 +154,8 @@ def test_independent_restatement_over_whole_streams(name):
     assert np.array_equal(c["obj_ints"], p["obj_ints"])
     assert np.allclose(c["obj_floats"], p["obj_floats"], rtol=1e-5, atol=1e-5, equal_nan=True)
     assert np.array_equal(c["obj_pts_len"], p["obj_pts_len"]) and np.array_equal(c["obj_pts_crc"], p["obj_pts_crc"])
+    if name == "replay_config_c_200":  # the config's scale is reached: clouds of >= 1500 points
+        assert int(p["obj_pts_len"].max()) >= 1500
 
 
 def test_cpp_oracle_reproduces_demo_fixture():

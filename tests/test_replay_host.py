@@ -240,3 +240,56 @@ def test_host_outputs_complete_without_events(harness):
         _compare(g, o)
     finally:
         harness.harness_set_events_never(0)
+
+
+def _resume_after_failure(env):
+    """Run the fr3 stream through eao_replay_run with the K-th forest launch failing (harness fault
+    injection), then resume frame by frame with frames that do not continue the failed stream; in a
+    fresh process (the switches are read at load). Returns the resumed frames' rows, the held map
+    points and the object records."""
+    import json
+    import subprocess
+    code = r'''
+import ctypes, json, os, subprocess, sys
+sys.path[:0] = sys.argv[1].split(os.pathsep)
+import numpy as np
+import eao_accel as ea
+import test_replay_host as T
+from tools import synth
+subprocess.check_call(["make", "-s", "-C", T.NATIVE])
+H = ctypes.CDLL(os.path.join(T.NATIVE, "_build", "libreplay_host.so"))
+H.harness_assoc_create.restype = ctypes.c_void_p
+frames = synth.assoc_stream_fr3_real()[:60]
+g = T._HostReplay(H, "EAO")
+try:
+    g._with(ea.Replay.run, g, ea.Replay.pack(frames[:40]))
+    failed = False
+except Exception:
+    failed = True
+rows = [g.step(41 + i, f).tolist() for i, f in enumerate(frames[45:60])]  # not the stream's next frames
+gi, gf, gp = g.objects()
+print(json.dumps(dict(failed=failed, rows=rows, held=g._with(g.held_points).tolist(), ints=gi.tolist(),
+                      floats=np.nan_to_num(gf).tolist(), pts=[p.tolist() for p in gp])))
+'''
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    path = os.pathsep.join([here, root, os.path.join(root, "oracle"), os.path.join(root, "eao-slam_amd", "python")])
+    out = subprocess.run([sys.executable, "-c", code, path], env=dict(os.environ, **env), capture_output=True,
+                         text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_host_resume_after_failed_stream_with_other_frames(harness):
+    """ADVICE r4: a stream call that fails after its wait ran the next frame's look-ahead discards
+    that look-ahead -- the map points its step 1 created are erased and the staged line set its
+    step 3 consumed is staged again -- so a caller resuming with other frames gets what a replay
+    whose look-ahead never ran gets (EAO_LOOKAHEAD_EAGER=1 runs every wait's look-ahead to the end on
+    the harness, whose kernels finish at launch; EAO_HARNESS_FAIL_IFOREST fails the 40th forest
+    launch, inside the 40-frame stream)."""
+    a = _resume_after_failure({"EAO_LOOKAHEAD_EAGER": "1", "EAO_HARNESS_FAIL_IFOREST": "40"})
+    b = _resume_after_failure({"EAO_LOOKAHEAD_EAGER": "0", "EAO_HARNESS_FAIL_IFOREST": "40"})
+    assert a["failed"] and b["failed"]
+    assert a["rows"] == b["rows"]
+    assert a["held"] == b["held"] and a["ints"] == b["ints"] and a["pts"] == b["pts"]
+    assert np.allclose(a["floats"], b["floats"], rtol=1e-6, atol=1e-6)

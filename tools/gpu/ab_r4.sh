@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 
-# forest_fast: Round-4 kernel changes: forest (mask path, rank conversion, scalar RNG state) and the FAST whole-row ring gather (EAO_FAST_ROWS=1): parity first, then same-box A/B timings. (EAO_FAST_ROWS and the forest variants: tools/patches/r4_forest_unvalidated.patch; removed since)
+# forest_fast: Round-4 kernel changes: forest (mask path, rank conversion, scalar RNG state) and the FAST whole-row ring gather (EAO_FAST_ROWS=1): parity first, then same-box A/B timings. (EAO_FAST_ROWS and the forest variants: tools/patches/r4_forest_mask_rank_rejected.patch; removed since)
 forest_fast() {
   timeout -k 10 300 python -u -m pytest tests/test_gpu_assoc.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r4_ab_assoc.log 2>&1 &&
   EAO_FAST_ROWS=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_orb.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r4_ab_orb_rows.log 2>&1 &&

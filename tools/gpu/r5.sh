@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-5 GPU runs, one function each: bash tools/gpu/r5.sh <name> [args]
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+
+# base: state of the tree on this box: EAO bench, replay probe, extraction stages
+base() {
+  timeout -k 10 500 python -u bench.py > gpurun_out/r5_base_bench.log 2>&1 &&
+  timeout -k 10 200 python -u tools/replay_probe.py > gpurun_out/r5_base_probe.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/orb_stages.py > gpurun_out/r5_base_orb.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 >> gpurun_out/r5_base_orb.log 2>&1
+}
+
+# pyr: LDS-staged pyramid (k_resize_lds) against k_resize_tile (EAO_RESIZE=0): parity, stage A/B, traffic
+pyr() {
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_lines.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_pyr_tests.log 2>&1 &&
+  for r in 1 2; do
+    EAO_RESIZE=0 timeout -k 10 200 python -u tools/micro/orb_stages.py | sed "s/^/tile /" &&
+    timeout -k 10 200 python -u tools/micro/orb_stages.py | sed "s/^/lds  /" &&
+    EAO_RESIZE=0 timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 | sed "s/^/tile /" &&
+    timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 | sed "s/^/lds  /" || exit 1
+  done > gpurun_out/r5_pyr_stages.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_pyr_kt -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_pyr_kt.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r5_pyr_pmc_fetch -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_pyr_pmc_fetch.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r5_pyr_pmc_write -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_pyr_pmc_write.log 2>&1
+}
+
+# lsingle: single-frame line detection latency, fused and two-kernel (walk / EDline split in the trace)
+lsingle() {
+  timeout -k 10 200 python -u tools/micro/lines_single.py 64 --check > gpurun_out/r5_lsingle.log 2>&1 &&
+  EAO_LINES_FUSED=0 timeout -k 10 200 python -u tools/micro/lines_single.py 64 >> gpurun_out/r5_lsingle.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_lsingle_kt -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_lsingle_kt.log 2>&1 &&
+  EAO_LINES_FUSED=0 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_lsingle_kt2 -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_lsingle_kt2.log 2>&1
+}
+
+"$@"

@@ -2,8 +2,9 @@
 Object.cc / Tracking.cc / LocalMapping.cc / isolation_forest.h, not from assoc_ref.cpp) run over
 the WHOLE fr3 streams the GPU parity fixtures cover:
 
-    python tools/make_assoc_py_golden.py [demo|full]  ->  tests/golden/replay_fr3_demo_eao_py.npz
-                                                          tests/golden/replay_fr3_full_py.npz
+    python tools/make_assoc_py_golden.py [demo|full|configc]  ->  tests/golden/replay_fr3_demo_eao_py.npz
+                                                                  tests/golden/replay_fr3_full_py.npz
+                                                                  tests/golden/replay_config_c_200_py.npz
 
 Same record as tools/make_fr3_golden.py (every detection's row, final object records, point-set
 CRCs, input digest). tests/test_oracle_assoc_py.py then requires these to equal the C++ oracle's
@@ -23,14 +24,25 @@ from make_fr3_golden import point_crcs, stream_digest  # noqa: E402
 from tools import synth  # noqa: E402
 
 STREAMS = {"demo": ("replay_fr3_demo_eao_py.npz", None, None, "EAO"),
-           "full": ("replay_fr3_full_py.npz", 0, 2582, "Full")}
+           "full": ("replay_fr3_full_py.npz", 0, 2582, "Full"),
+           # BASELINE configs[3] at its scale (64 objects x 2000 points): the 200 frames of
+           # tools/make_config_c_golden.py -- NP subsampling at n > 3m (Object.cc:780-789) and
+           # forests over clouds of >= 1500 points (Object.cc:1202-1309)
+           "configc": ("replay_config_c_200_py.npz", None, None, "EAO")}
+
+
+def stream(key):
+    if key == "configc":
+        return synth.assoc_stream_config_c(1000)[:200]
+    _, start, n, _ = STREAMS[key]
+    return synth.assoc_stream_fr3_real(start, n)
 
 
 def main():
     which = sys.argv[1:] or list(STREAMS)
     for key in which:
-        name, start, n, flag = STREAMS[key]
-        fr = synth.assoc_stream_fr3_real(start, n)
+        name, _, _, flag = STREAMS[key]
+        fr = stream(key)
         t0 = time.time()
         p = ap.Replay(flag)
         outs = []
