@@ -174,8 +174,12 @@ __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__
       uint32_t w = 0;
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        const int v = (d0[u] * b0 + d1[u] * b1 + (1 << 21)) >> 22;
-        w |= (uint32_t)min(max(v, 0), 255) << (8 * u);
+        // no saturation: 0 <= v <= 255 already (taps >= 0, a0 + a1 <= 2049, b0 + b1 <= 2049:
+        // v <= (255 * 2049^2 + 2^21) >> 22 = 255), and the clamp made the compiler pack two
+        // bytes with v_ashr_pk_u8_i32, whose result's upper half is not zero on gfx950: the
+        // v_lshl_or of bytes 2 / 3 then OR'ed stale bits into them (round-5 miscompile)
+        const uint32_t v = (uint32_t)(d0[u] * b0 + d1[u] * b1 + (1 << 21)) >> 22;
+        w |= v << (8 * u);
         ha[u] = d0[u];
         hb[u] = d1[u];
       }
