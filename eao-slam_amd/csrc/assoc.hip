@@ -13,6 +13,7 @@
 //   k_iforest_sum  one thread per point: path lengths summed in tree order,
 //                  score 2^(-E[h]/c(psi)) (isolation_forest.h:499-530)
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstring>
 
 #include <algorithm>
@@ -159,6 +160,9 @@ __device__ void block_sort3_fast(float* S0, float* S1, float* S2, int P) {
 // latency chain (global reads, the sort's barrier phases, the searches) is what
 // costs, so a pair gets a whole CU's worth of waves
 constexpr int NPT = 1024;
+// pairs with m * nvalid up to this take the direct counts (np_pair_body); host-set at engine init
+// (EAO_NP_DIRECT=<max>, 0: always the sort / rank paths)
+__device__ int g_np_direct_max = 131072;
 // LDS behind the sort arrays for the rank path (launches with P >= 2048 only): 3 Pm frame
 // values and 3 (Pm + 1) counters, four copies at Pm = 256 (15.4 KB), one at Pm = 512
 constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * 4 * 3 * 257 + 64;
@@ -177,6 +181,10 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   extern __shared__ __attribute__((aligned(16))) float dsm[];
   __shared__ int red[9 * 16];
   __shared__ int wpos[4];
+  // direct-count path (np_direct): the frame points (NaN for an invalid one) and the per-point
+  // packed counts #{object values < x} | #{<= x} << 16 per axis
+  __shared__ float s_fp[3][NPT];
+  __shared__ int s_cnt[3][NPT];
   const int t = threadIdx.x;
   const float* F = fp + 3 * (long long)foff[p];
   const uint8_t* FV = fv + foff[p];
@@ -207,6 +215,11 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   if (t < 9) red[t] = 0;
   if (t == 9) red[9 * 16 - 1] = 0;
   if (t < 4) wpos[t] = 0;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {  // (read after the compaction's barrier, by the direct path only)
+    s_fp[a][t] = fv0 ? f0[a] : __int_as_float(0x7fc00000);
+    s_cnt[a][t] = 0;
+  }
   __syncthreads();
   float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
   // one pass over the object: the valid kept points compacted into the sort arrays
@@ -276,9 +289,9 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   const bool sub = nvalid > 3 * m;
   const int step = sub ? nt / (3 * m) : 1;  // step counts invalid points too (Q3)
   const int nsamp = sub ? (nvalid + step - 1) / step : nvalid;
+  int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int Pm = 256;
   while (Pm < m) Pm <<= 1;
-  int c9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   // rank path (the frame side is the smaller): the sample counts of a frame value x need
   // only r<(x) = #{object values < x} and r<=(x): #{samples < x} = ceil(r< / step)
   // (sorted[k step] < x iff k step < r<). The m frame values are sorted instead of the
@@ -293,6 +306,62 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   bool rank = !wpos[3] && P >= 2048 && Pmax >= 2048 && Pm < P && Pm <= 512;
   float* D[3] = {dsm + 3 * Pmax, dsm + 3 * Pmax + Pm, dsm + 3 * Pmax + 2 * Pm};
   int* H = (int*)(dsm + 3 * Pmax + 3 * Pm);  // [NH][3][Pm + 1]
+  // Direct counts (small pairs, no sort and one barrier): the sample counts of a frame value x
+  // need only lt = #{object values < x} and le = #{<= x} (the rank path's identity: sample k is
+  // sorted[k step], so #{samples < x} = ceil(lt / step), also for step = 1), counted by brute
+  // force against the compacted object values in LDS. Thread t takes frame-point slot t % npg and
+  // the t / npg-th of nsplit contiguous 4-aligned chunks of the values (a wave shares one chunk:
+  // broadcast ds_read_b128); chunks' counts meet in s_cnt by LDS atomics. NaN object values take
+  // the sort path (their order under std::sort is what the samples follow); a NaN frame value
+  // counts on no axis it is NaN in, an invalid frame point (NaN in s_fp) on none.
+  if (!wpos[3] && mt <= NPT && (long long)m * nvalid <= (long long)g_np_direct_max) {
+    const int npg = (mt + 63) & ~63, nsplit = NPT / npg;
+    const int slot = t % npg, split = t / npg;
+    const int nq = nvalid >> 2;  // whole quads; the < 4 tail values go to split 0
+    if (split < nsplit && slot < mt) {
+      float x[3];
+      int lt[3] = {0, 0, 0}, le[3] = {0, 0, 0};
+#pragma unroll
+      for (int a = 0; a < 3; a++) x[a] = s_fp[a][slot];
+      const int q0 = split * nq / nsplit, q1 = (split + 1) * nq / nsplit;
+      for (int q = q0; q < q1; q++) {
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+          const float4 v = ((const float4*)S[a])[q];
+          lt[a] += (v.x < x[a]) + (v.y < x[a]) + (v.z < x[a]) + (v.w < x[a]);
+          le[a] += (v.x <= x[a]) + (v.y <= x[a]) + (v.z <= x[a]) + (v.w <= x[a]);
+        }
+      }
+      if (split == 0)
+        for (int j = 4 * nq; j < nvalid; j++)
+#pragma unroll
+          for (int a = 0; a < 3; a++) {
+            const float v = S[a][j];
+            lt[a] += v < x[a];
+            le[a] += v <= x[a];
+          }
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        if (nsplit > 1)
+          atomicAdd(&s_cnt[a][slot], lt[a] | (le[a] << 16));
+        else
+          s_cnt[a][slot] = lt[a] | (le[a] << 16);
+      }
+    }
+    __syncthreads();
+    if (t < mt) {
+#pragma unroll
+      for (int a = 0; a < 3; a++) {
+        if (s_fp[a][t] != s_fp[a][t]) continue;  // NaN (or an invalid point): no count
+        const int v = s_cnt[a][t];
+        const int lo = ((v & 0xffff) + step - 1) / step, hi = ((v >> 16) + step - 1) / step;
+        c9[3 * a] += lo;
+        c9[3 * a + 2] += hi - lo;
+        c9[3 * a + 1] += nsamp - hi;
+      }
+    }
+    goto sums;
+  }
   if (rank) {
     __syncthreads();  // every thread has read wpos
     if (t == 0) wpos[3] = 0;
@@ -766,7 +835,8 @@ __device__ __forceinline__ void if_sample(WaveRng& g, int n, int psi, uint16_t* 
 //
 // mt_init: per tree, the mt19937 state after seeding and the first twist
 // (the seeds are fixed per forest, so it is computed once on the host).
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_iforest_tree(const float* __restrict__ pts,
+template <int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_iforest_tree(const float* __restrict__ pts,
                                                       const int* __restrict__ off,
                                                       const int* __restrict__ len,
                                                       const uint32_t* __restrict__ mt_init,
@@ -808,7 +878,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const bool tab = valid && n <= tab_n && psi == n / 2 && tab_D[(size_t)n * gridDim.x + tr] >= 0;  // uniform
   // the score walk (after the build) is done by the waves that neither build nor sort: they load
   // their points now, so the loads' latency hides behind the sample gather and the build
-  constexpr int SW0 = IF_HELPERS + 1, SWT = 1024 - 64 * SW0;  // first scoring wave, scoring threads
+  // (NT = 64: samples of <= 64 items -- the whole tree one rank-space / register subtree -- built
+  // and scored by the one wave, no helpers)
+  constexpr int SW0 = NT == 1024 ? IF_HELPERS + 1 : 0, SWT = NT - 64 * SW0;  // first scoring wave, scoring threads
   const int st = tid - 64 * SW0;
   float sx[4][3];
 #pragma unroll
@@ -1111,7 +1183,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       __hip_atomic_store(&s_stop, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (lane == 0 && blockIdx.x == 0 && blockIdx.y == 0) g_if_stamp[10] = nn;
-  } else if (wave <= IF_HELPERS) {
+  } else if (NT > 64 && wave <= IF_HELPERS) {
     // helper: take posted subtree jobs in order, sort their items into the job's slot
     while (true) {
       int j = -1;
@@ -1343,6 +1415,10 @@ int AssocEngine::init(int device, int mp) {
   EAO_HIP_CHECK(hipMalloc(&d_mtinit, sizeof(uint32_t) * 624 * max_trees));
   EAO_HIP_CHECK(hipMalloc(&d_scores, sizeof(double) * (size_t)mp));
   EAO_HIP_CHECK(hipMalloc(&d_contrib, sizeof(double) * (size_t)mp * max_trees));
+  if (const char* v = std::getenv("EAO_NP_DIRECT")) {  // A/B: the NP direct-count threshold (m * n)
+    const int mx = std::atoi(v);
+    EAO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_np_direct_max), &mx, sizeof(int)));
+  }
   pow_x0[0] = pow_threshold((double)0.6f);
   pow_x0[1] = pow_threshold((double)0.65f);
   {  // CalculateC (isolation_forest.h:97-118) of every leaf / sample size, host libm like the reference
@@ -1501,12 +1577,19 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     if (int rc = iforest_table(seed, trees, s)) return rc;
   }
   // helper job slots: as many as the LDS left by the tree allows (up to IF_JSLOTS)
-  int jslots = IF_JSLOTS;
+  // samples of <= 64 items (clouds of < 130 points): one wave per (tree, cloud) builds the tree (one
+  // rank-space or register subtree) and scores the cloud; EAO_IF_SMALL=0 keeps the 16-wave form
+  static const bool small_ok = [] {
+    const char* v = std::getenv("EAO_IF_SMALL");
+    return !(v && v[0] == '0');
+  }();
+  const bool small = small_ok && maxS <= 64;
+  int jslots = small ? 0 : IF_JSLOTS;
   while (jslots > 0 && IfLds(maxN, maxS, jslots).total > lds_limit) jslots--;
   const IfLds L(maxN, maxS, jslots);
-  hipLaunchKernelGGL(k_iforest_tree, dim3(trees, nclouds), dim3(1024), L.total, s, pts, off, len,
-                     d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n, d_tab_ids, d_tab_off,
-                     d_tab_D, d_tab_states, jslots);
+  hipLaunchKernelGGL(small ? k_iforest_tree<64> : k_iforest_tree<1024>, dim3(trees, nclouds), dim3(small ? 64 : 1024),
+                     L.total, s, pts, off, len, d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n,
+                     d_tab_ids, d_tab_off, d_tab_D, d_tab_states, jslots);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,

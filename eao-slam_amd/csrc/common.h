@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <cstdio>
+#include <cstring>
 #include <string>
 
 namespace eao {
@@ -60,5 +61,43 @@ __device__ __forceinline__ int wave_min_int(int v) {
   for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
   return v;
 }
+
+// Staging of the C ABI's host-buffer (single-call) entry points: a pinned host image and its
+// device mirror. Inputs are packed 16-byte aligned into the pinned image and go over in one
+// DMA copy (a pageable source would be bounced through a driver buffer, copy by copy); outputs
+// come back into pinned memory. Returns EAO status codes (the including file defines them).
+struct HostStage {
+  unsigned char* h = nullptr;
+  unsigned char* d = nullptr;
+  size_t cap = 0, used = 0;
+  static size_t al(size_t x) { return (x + 15) & ~(size_t)15; }
+  hipError_t reserve(size_t bytes) {
+    used = 0;
+    if (bytes <= cap) return hipSuccess;
+    release();
+    const size_t c = al(bytes + bytes / 4 + 4096);
+    hipError_t e = hipHostMalloc((void**)&h, c, 0);
+    if (e == hipSuccess) e = hipMalloc((void**)&d, c);
+    if (e == hipSuccess) cap = c;
+    return e;
+  }
+  // the next 16-aligned slot of `bytes`, filled from src when given: its offset
+  size_t put(const void* src, size_t bytes) {
+    const size_t at = used;
+    if (src && bytes) std::memcpy(h + at, src, bytes);
+    used = al(at + bytes);
+    return at;
+  }
+  template <class T>
+  T* dev(size_t off) const { return (T*)(d + off); }
+  hipError_t upload(hipStream_t s) const { return used ? hipMemcpyAsync(d, h, used, hipMemcpyHostToDevice, s) : hipSuccess; }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    if (d) (void)hipFree(d);
+    h = d = nullptr;
+    cap = used = 0;
+  }
+  ~HostStage() { release(); }
+};
 
 }  // namespace eao

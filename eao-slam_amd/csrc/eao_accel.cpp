@@ -95,21 +95,29 @@ int eao_orb_extract(eao_orb* h, const uint8_t* gray, int w, int hh, int stride, 
     return EAO_E_ARG;
   }
   EAO_HIP_CHECK(hipSetDevice(e.dev));
-  EAO_HIP_CHECK(hipMemcpy2DAsync(e.d_img, w, gray, stride, w, hh, hipMemcpyHostToDevice, e.stream));
+  // the image through pinned staging (one DMA copy), the outputs back in one copy
+  EAO_HIP_CHECK(e.stage_in.reserve((size_t)w * hh));
+  if (stride == w) {
+    e.stage_in.put(gray, (size_t)w * hh);
+  } else {
+    const size_t o = e.stage_in.put(nullptr, (size_t)w * hh);
+    for (int y = 0; y < hh; y++) std::memcpy(e.stage_in.h + o + (size_t)y * w, gray + (size_t)y * stride, w);
+  }
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)w * hh, hipMemcpyHostToDevice, e.stream));
   int rc = e.run(e.d_img, 1, w, e.d_out_kps, e.d_out_desc, e.d_out_cnt, e.cap, e.stream);
   if (rc) return rc;
-  int n = 0;
-  // the stream's work is complete before the count is read (no async copy into a stack variable)
+  EAO_HIP_CHECK(e.stage_out.reserve(e.out_bytes));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_out_blk, e.out_bytes, hipMemcpyDeviceToHost, e.stream));
   EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
-  EAO_HIP_CHECK(hipMemcpy(&n, e.d_out_cnt, sizeof(int), hipMemcpyDeviceToHost));
+  const int n = *(const int*)e.stage_out.h;
   *n_out = n;
   if (n > cap) {
     set_error("eao_orb_extract: output capacity too small");
     return EAO_E_CAPACITY;
   }
   if (n > 0) {
-    if (kps) EAO_HIP_CHECK(hipMemcpy(kps, e.d_out_kps, (size_t)n * sizeof(eao_keypoint), hipMemcpyDeviceToHost));
-    if (desc) EAO_HIP_CHECK(hipMemcpy(desc, e.d_out_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
+    if (kps) std::memcpy(kps, e.stage_out.h + e.out_kps_off, (size_t)n * sizeof(eao_keypoint));
+    if (desc) std::memcpy(desc, e.stage_out.h + e.out_desc_off, (size_t)n * 32);
   }
   return EAO_OK;
 }

@@ -986,6 +986,7 @@ struct LineEngine {
   float* d_lines = nullptr;
   int* d_nlines = nullptr;
   int* h_n = nullptr;  // pinned: the single-frame line count
+  HostStage stage_in, stage_out;  // single-frame staging: the pinned image in, count + lines back
   ~LineEngine() {
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
                  d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts};
@@ -1158,10 +1159,22 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = e.stream;
   const int row = e.W * channels;
-  EAO_HIP_CHECK(hipMemcpy2DAsync(e.d_img, row, img, pitch, row, e.H, hipMemcpyHostToDevice, s));
+  // the frame through pinned staging (one DMA copy); the count and every line slot back into
+  // pinned memory behind the kernels, one synchronisation
+  EAO_HIP_CHECK(e.stage_in.reserve((size_t)row * e.H));
+  if (pitch == row) {
+    e.stage_in.put(img, (size_t)row * e.H);
+  } else {
+    const size_t o = e.stage_in.put(nullptr, (size_t)row * e.H);
+    for (int y = 0; y < e.H; y++) std::memcpy(e.stage_in.h + o + (size_t)y * row, img + (size_t)y * pitch, row);
+  }
+  EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)row * e.H, hipMemcpyHostToDevice, s));
   int rc = eao_lines_detect_color_batch_device(L, e.d_img, 1, row, channels, min_length, e.d_lines, e.d_nlines, 4096, s);
   if (rc) return rc;
+  const size_t lb = sizeof(float) * 6 * (size_t)std::min(std::max(cap, 0), 4096);
+  EAO_HIP_CHECK(e.stage_out.reserve(lb));
   EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, 4, hipMemcpyDeviceToHost, s));
+  if (lb) EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_lines, lb, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
   const int n = *e.h_n;
   if (n < 0) {
@@ -1170,7 +1183,7 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
   }
   *n_out = n;
   const int k = n < cap ? n : cap;
-  if (k > 0) EAO_HIP_CHECK(hipMemcpy(lines, e.d_lines, sizeof(float) * 6 * k, hipMemcpyDeviceToHost));
+  if (k > 0) std::memcpy(lines, e.stage_out.h, sizeof(float) * 6 * k);
   return n > cap ? EAO_E_CAPACITY : EAO_OK;
 }
 

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/eao_accel.h"
+#include "common.h"
 #include "orb.h"
 
 namespace eao {
@@ -46,6 +47,7 @@ class MatchEngine {
   unsigned long long* d_ckeys = nullptr;
   signed char* d_cbins = nullptr;
   int* d_ccnt = nullptr;
+  HostStage stage, res;  // single-call inputs (pinned image + device mirror) / results (pinned)
 
   int init(int device, int max_kps, int max_batch);
   ~MatchEngine();

@@ -1211,31 +1211,44 @@ int eao_match_motion(eao_matcher* m, const eao_camera* cam, const float* Tcw, fl
   }
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = e.stream;
-  const int counts[2] = {n_last, n_cur};
+  // slot stride C (the kernels take it as cap): the two frames' inputs packed into the pinned
+  // staging image, one copy over; the current frame's matches and the counts come back in one
+  const int C = (std::max(std::max(n_last, n_cur), 1) + 63) & ~63;
+  const int counts[4] = {n_last, n_cur, 0, 0};
   float T2[32];
   for (int k = 0; k < 16; k++) T2[k] = T2[16 + k] = Tcw[k];
-  // slot 0 = last, slot 1 = current; cap = K
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps, last_kps, sizeof(eao_keypoint) * n_last, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_kps + K, cur_kps, sizeof(eao_keypoint) * n_cur, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_desc + (size_t)K * 32, cur_desc, (size_t)n_cur * 32, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_u8, last_has_mp, n_last, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_f, last_mp_pos, sizeof(float) * 3 * n_last, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_mdesc, last_mp_desc, (size_t)n_last * 32, hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_i32, counts, sizeof(counts), hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_T, T2, sizeof(T2), hipMemcpyHostToDevice, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_scales, scale_factors, sizeof(float) * nlevels, hipMemcpyHostToDevice, s));
+  HostStage& st = e.stage;
+  const size_t kb = sizeof(eao_keypoint);
+  EAO_HIP_CHECK(st.reserve(HostStage::al(2 * C * kb) + 2 * (size_t)C * 32 + C + 12 * (size_t)C + 32 * (size_t)C + 512));
+  const size_t o_kps = st.put(nullptr, 2 * C * kb);
+  std::memcpy(st.h + o_kps, last_kps, kb * n_last);
+  std::memcpy(st.h + o_kps + kb * C, cur_kps, kb * n_cur);
+  const size_t o_desc = st.put(nullptr, 2 * (size_t)C * 32);  // slot 0 unused by the motion search
+  std::memcpy(st.h + o_desc + (size_t)C * 32, cur_desc, (size_t)n_cur * 32);
+  const size_t o_has = st.put(last_has_mp, n_last);
+  const size_t o_pos = st.put(last_mp_pos, sizeof(float) * 3 * n_last);
+  const size_t o_md = st.put(last_mp_desc, (size_t)n_last * 32);
+  const size_t o_cnt = st.put(counts, sizeof(counts));
+  const size_t o_T = st.put(T2, sizeof(T2));
+  const size_t o_sc = st.put(scale_factors, sizeof(float) * nlevels);
+  EAO_HIP_CHECK(st.upload(s));
   const CamDev cd = make_cam(*cam);
-  int rc = e.build_grid(cd, e.d_kps, e.d_i32, 0, K, 2, s);
+  const eao_keypoint_dev* dk = st.dev<const eao_keypoint_dev>(o_kps);
+  const int* dc = st.dev<const int>(o_cnt);
+  int rc = e.build_grid(cd, dk, dc, 0, C, 2, s);
   if (rc) return rc;
-  rc = e.motion(cd, e.d_T, th, check_ori, e.d_kps, e.d_desc, e.d_i32, K, e.d_u8, e.d_f, e.d_mdesc, e.d_scales,
-                2, e.d_out, e.d_out + 2 * K, s);
+  rc = e.motion(cd, st.dev<const float>(o_T), th, check_ori, dk, st.dev<const uint8_t>(o_desc), dc, C,
+                st.dev<const uint8_t>(o_has), st.dev<const float>(o_pos), st.dev<const uint8_t>(o_md),
+                st.dev<const float>(o_sc), 2, e.d_out, e.d_out + 2 * C, s);
   if (rc) return rc;
   EAO_HIP_CHECK(hipGetLastError());
-  int nm[2] = {0, 0};
-  EAO_HIP_CHECK(hipMemcpyAsync(cur_match, e.d_out + K, sizeof(int) * n_cur, hipMemcpyDeviceToHost, s));
-  EAO_HIP_CHECK(hipMemcpyAsync(nm, e.d_out + 2 * K, sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+  // [C matches of slot 1][nm[0], nm[1]]
+  EAO_HIP_CHECK(e.res.reserve(sizeof(int) * (C + 2)));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.res.h, e.d_out + C, sizeof(int) * (C + 2), hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
-  return nm[1];
+  const int* r = (const int*)e.res.h;
+  std::memcpy(cur_match, r, sizeof(int) * n_cur);
+  return r[C + 1];
 }
 
 int eao_match_motion_batch_device(eao_matcher* m, const eao_camera* cam, int nframes, int cap,

@@ -1,5 +1,6 @@
 // orb.h -- ORB extraction engine (host side of orb.hip).
 #pragma once
+#include "common.h"
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -86,6 +87,9 @@ class OrbEngine {
   eao_keypoint_dev* d_out_kps = nullptr;
   uint8_t* d_out_desc = nullptr;
   int* d_out_cnt = nullptr;
+  uint8_t* d_out_blk = nullptr;  // the three single-image outputs above, one allocation
+  size_t out_kps_off = 0, out_desc_off = 0, out_bytes = 0;
+  HostStage stage_in, stage_out;  // single-image staging (pinned image in, outputs back)
 
   int plan(const eao_orb_params& prm, int device);
   int init(const eao_orb_params& prm, int device);

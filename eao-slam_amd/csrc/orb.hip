@@ -84,29 +84,76 @@ __global__ __launch_bounds__(256) void k_resize_tile(const uint8_t* __restrict__
 //   1. the tile's source rows [ys0, ys1] are staged in LDS with 16-byte loads (row stride sw16 =
 //      the source width rounded up to 16), all of them in flight;
 //   2. a work item = (group of 4 output columns, segment of RESIZE_RS rows): the item keeps its
-//      4 columns' x offsets and coefficients in registers, walks its rows keeping the last two
-//      source rows' horizontal sums (a source row is summed once per item, not per output row),
-//      taps are LDS byte reads, and the 4 outputs go out as one dword store (level planes are
-//      64-byte pitched, so the store is aligned; columns past dw repeat the last column's
-//      coefficients into the plane's pitch padding, which nothing reads).
+//      4 columns' x offsets and coefficients and its rows' source rows and coefficients in
+//      registers, walks its rows keeping the last two source rows' horizontal sums (a source row
+//      is summed once per item, not per output row), taps are LDS byte reads, and the 4 outputs go
+//      out as one dword store (level planes are 64-byte pitched, so the store is aligned; columns
+//      past dw repeat the last column's coefficients into the plane's pitch padding, which nothing
+//      reads).
+// Latency: the kernel is a chain of memory round trips per workgroup, so every load is issued up
+// front -- ys0 / ys1 are recomputed from scale_y (the host's float expression, bit-identical) instead
+// of read from the row table, and the first item's table entries are loaded together with the
+// staging loads, before the barrier.
 // Items are numbered column-group-fastest, so a wave's stores cover 256 contiguous bytes.
 // Arithmetic identical to k_resize_tile (OpenCV INTER_LINEAR 8U, ORBextractor.cc:1120).
 constexpr int RESIZE_RS = 4;
+__device__ __forceinline__ int resize_src_row(int dy, double scale_y, int sh, int k) {
+  const float fy = (float)((dy + 0.5) * scale_y - 0.5);  // OrbEngine::plan's resize_yrows
+  return min(max((int)floorf(fy) + k, 0), sh - 1);
+}
+// an item's table entries, packed: x offsets; coefficient pairs a0 | a1 << 16 (a1 = 0 past xmax)
+// and b0 | b1 << 16 (all in [0, 2048]); source rows r0 | r1 << 16
+struct ResizeItem {
+  int sx[4], a[4], r[RESIZE_RS], b[RESIZE_RS];
+};
+__device__ __forceinline__ void resize_item_load(ResizeItem& I, int g, int e0, int e1, int dw, int xmax,
+                                                 const int* __restrict__ xofs, const short* __restrict__ ialpha,
+                                                 const int* __restrict__ yrows, const short* __restrict__ ibeta) {
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int dx = min(4 * g + u, dw - 1);
+    I.sx[u] = xofs[dx];
+    const int pa = *(const int*)(ialpha + 2 * dx);  // the (a0, a1) pair: 4-byte aligned
+    I.a[u] = dx < xmax ? pa : 2048;
+  }
+#pragma unroll
+  for (int k = 0; k < RESIZE_RS; k++) {
+    const int dy = min(e0 + k, e1 - 1);
+    const int2 yr = *(const int2*)(yrows + 2 * dy);
+    I.r[k] = yr.x | (yr.y << 16);
+    I.b[k] = *(const int*)(ibeta + 2 * dy);
+  }
+}
 template <bool VEC>
 __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__ src, int spitch, long long sstride,
                                                      uint8_t* __restrict__ dst, int dpitch, long long dstride,
-                                                     int sw, int dw, int dh, int tr,
+                                                     int sw, int sh, int dw, int dh, int tr, double scale_y,
                                                      const int* __restrict__ xofs, const short* __restrict__ ialpha,
                                                      int xmax, const int* __restrict__ yrows,
                                                      const short* __restrict__ ibeta) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int dy0 = blockIdx.x * tr, f = blockIdx.y;
   const int dy1 = min(dy0 + tr, dh);
-  const int ys0 = yrows[2 * dy0], ys1 = yrows[2 * (dy1 - 1) + 1];
+  const int ys0 = resize_src_row(dy0, scale_y, sh, 0), ys1 = resize_src_row(dy1 - 1, scale_y, sh, 1);
   const int nrows = ys1 - ys0 + 1;
   const int sw16 = (sw + 15) & ~15;
   const uint8_t* sf = src + f * sstride + (long long)ys0 * spitch;
   const int tid = threadIdx.x, nb = blockDim.x;
+  const int G = (dw + 3) >> 2;
+  const int nseg = (dy1 - dy0 + RESIZE_RS - 1) / RESIZE_RS;
+  const int nit = G * nseg;
+  ResizeItem I;
+  auto seg_rows = [&](int it, int& g, int& e0, int& e1) {
+    const int seg = it / G;
+    g = it - seg * G;
+    e0 = dy0 + seg * RESIZE_RS;
+    e1 = min(e0 + RESIZE_RS, dy1);
+  };
+  int g = 0, e0 = 0, e1 = 0;
+  if (tid < nit) {  // the first item's tables: in flight with the staging loads
+    seg_rows(tid, g, e0, e1);
+    resize_item_load(I, g, e0, e1, dw, xmax, xofs, ialpha, yrows, ibeta);
+  }
   if (VEC) {
     const int cpr = sw16 >> 4, nc = nrows * cpr;
     int c = tid;
@@ -120,9 +167,16 @@ __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__
 #pragma unroll
       for (int u = 0; u < 4; u++) ((uint4*)smem)[c + u * nb] = v[u];
     }
-    for (; c < nc; c += nb) {
-      const int r = c / cpr, k = c - r * cpr;
-      ((uint4*)smem)[c] = *(const uint4*)(sf + (long long)r * spitch + 16 * k);
+    if (c < nc) {  // the rest: at most three loads per thread, all in flight
+      uint4 v[3];
+#pragma unroll
+      for (int u = 0; u < 3; u++) {
+        const int cc = c + u * nb, r = cc / cpr, k = cc - r * cpr;
+        v[u] = *(const uint4*)(sf + (long long)(cc < nc ? r : 0) * spitch + 16 * (cc < nc ? k : 0));
+      }
+#pragma unroll
+      for (int u = 0; u < 3; u++)
+        if (c + u * nb < nc) ((uint4*)smem)[c + u * nb] = v[u];
     }
   } else {
     for (int c = tid; c < nrows * sw16; c += nb) {
@@ -131,30 +185,23 @@ __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__
     }
   }
   __syncthreads();
-  const int G = (dw + 3) >> 2;
-  const int nseg = (dy1 - dy0 + RESIZE_RS - 1) / RESIZE_RS;
   uint8_t* df = dst + f * dstride;
-  for (int it = tid; it < G * nseg; it += nb) {
-    const int seg = it / G, g = it - seg * G;
-    int sx[4], a0[4], a1[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int dx = min(4 * g + u, dw - 1);
-      sx[u] = xofs[dx];
-      const bool two = dx < xmax;
-      a0[u] = two ? ialpha[2 * dx] : 2048;
-      a1[u] = two ? ialpha[2 * dx + 1] : 0;
+  for (int it = tid; it < nit; it += nb) {
+    if (it != tid) {
+      seg_rows(it, g, e0, e1);
+      resize_item_load(I, g, e0, e1, dw, xmax, xofs, ialpha, yrows, ibeta);
     }
     auto hsum = [&](int r, int (&h)[4]) {
       const uint8_t* row = smem + (r - ys0) * sw16;
 #pragma unroll
-      for (int u = 0; u < 4; u++) h[u] = row[sx[u]] * a0[u] + row[sx[u] + 1] * a1[u];  // a1 = 0 past xmax
+      for (int u = 0; u < 4; u++) h[u] = row[I.sx[u]] * (I.a[u] & 0xffff) + row[I.sx[u] + 1] * (I.a[u] >> 16);
     };
     int ra = -1, rb = -1, ha[4], hb[4];
-    const int e0 = dy0 + seg * RESIZE_RS, e1 = min(e0 + RESIZE_RS, dy1);
-    for (int dy = e0; dy < e1; dy++) {
-      const int r0 = yrows[2 * dy], r1 = yrows[2 * dy + 1];
-      const int b0 = ibeta[2 * dy], b1 = ibeta[2 * dy + 1];
+#pragma unroll
+    for (int k = 0; k < RESIZE_RS; k++) {
+      const int dy = e0 + k;
+      if (dy >= e1) break;
+      const int r0 = I.r[k] & 0xffff, r1 = I.r[k] >> 16;
       int d0[4], d1[4];
       if (r0 == rb) {
 #pragma unroll
@@ -178,7 +225,7 @@ __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__
         // v <= (255 * 2049^2 + 2^21) >> 22 = 255), and the clamp made the compiler pack two
         // bytes with v_ashr_pk_u8_i32, whose result's upper half is not zero on gfx950: the
         // v_lshl_or of bytes 2 / 3 then OR'ed stale bits into them (round-5 miscompile)
-        const uint32_t v = (uint32_t)(d0[u] * b0 + d1[u] * b1 + (1 << 21)) >> 22;
+        const uint32_t v = (uint32_t)(d0[u] * (I.b[k] & 0xffff) + d1[u] * (I.b[k] >> 16) + (1 << 21)) >> 22;
         w |= v << (8 * u);
         ha[u] = d0[u];
         hb[u] = d1[u];
@@ -1361,16 +1408,20 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
   EAO_HIP_CHECK(hipMalloc(&d_sel_cnt, p.nlevels * sizeof(int) * B));
   // single-image staging
   EAO_HIP_CHECK(hipMalloc(&d_img, (size_t)p.width * p.height));
-  EAO_HIP_CHECK(hipMalloc(&d_out_kps, (size_t)cap * sizeof(eao_keypoint_dev)));
-  EAO_HIP_CHECK(hipMalloc(&d_out_desc, (size_t)cap * 32));
-  EAO_HIP_CHECK(hipMalloc(&d_out_cnt, sizeof(int)));
+  // single-image outputs in one block [count | keypoints | descriptors]: one copy back
+  out_kps_off = 16;
+  out_desc_off = (out_kps_off + (size_t)cap * sizeof(eao_keypoint_dev) + 15) & ~(size_t)15;
+  out_bytes = out_desc_off + (size_t)cap * 32;
+  EAO_HIP_CHECK(hipMalloc(&d_out_blk, out_bytes));
+  d_out_cnt = (int*)d_out_blk;
+  d_out_kps = (eao_keypoint_dev*)(d_out_blk + out_kps_off);
+  d_out_desc = d_out_blk + out_desc_off;
   return EAO_OK;
 }
 
 OrbEngine::~OrbEngine() {
   void* ptrs[] = {d_levels, d_cells, d_xofs, d_ia, d_yrows, d_ib, d_umax, d_gk, d_slot_map,
-                  d_bands, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_kps,
-                  d_out_desc, d_out_cnt};
+                  d_bands, d_pyr, d_cand, d_qbuf, d_cell_cnt, d_sel, d_sel_cnt, d_img, d_out_blk};
   for (void* q : ptrs)
     if (q) (void)hipFree(q);
   if (stream) (void)hipStreamDestroy(stream);
@@ -1404,8 +1455,9 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
       const bool vec = l > 1 || ((uintptr_t)d_frames % 16 == 0 && pitch % 16 == 0);
       auto kr = vec ? k_resize_lds<true> : k_resize_lds<false>;
       hipLaunchKernelGGL(kr, dim3(R.tiles, nframes), dim3(R.block), R.lds, s, src, spitch, sstride,
-                         d_pyr + L.plane_off, L.pitch, pyr_bytes, S.w, L.w, L.h, R.tr, d_xofs + L.tab_x,
-                         d_ia + 2 * L.tab_x, L.xmax, d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
+                         d_pyr + L.plane_off, L.pitch, pyr_bytes, S.w, S.h, L.w, L.h, R.tr,
+                         1. / ((double)L.h / S.h), d_xofs + L.tab_x, d_ia + 2 * L.tab_x, L.xmax,
+                         d_yrows + 2 * L.tab_y, d_ib + 2 * L.tab_y);
       continue;
     }
     dim3 g(1, (L.h + RESIZE_TR - 1) / RESIZE_TR, nframes);

@@ -30,13 +30,28 @@ namespace {
     }                                                                             \
   } while (0)
 
+// The gathered records' way back to the host: one workgroup behind the all-gather on its stream
+// copies them into pinned host memory and then publishes the call's sequence number in a flag
+// word after them (every thread's stores drained system-wide before the barrier; the flag stored
+// last), so the host waits on that word instead of a DMA copy plus an event.
+__global__ __launch_bounds__(256) void k_recv_out(const unsigned char* __restrict__ d, unsigned char* h, size_t n,
+                                                  unsigned* flag, unsigned seq) {
+  const size_t n16 = n / 16;
+  for (size_t i = threadIdx.x; i < n16; i += blockDim.x) ((uint4*)h)[i] = ((const uint4*)d)[i];
+  for (size_t i = 16 * n16 + threadIdx.x; i < n; i += blockDim.x) h[i] = d[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct RcclExchanger : Exchanger {
   int dev = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;  // the gathered records' copy-back
+  hipEvent_t done = nullptr;  // the gathered records' copy-back (its errors)
   unsigned char *h_recv = nullptr, *d_recv = nullptr;
-  size_t cap = 0;  // bytes per rank
+  size_t cap = 0;    // bytes per rank
+  unsigned seq = 0;  // k_recv_out's flag value of the latest call
 
   ~RcclExchanger() override {
     if (stream) (void)hipStreamSynchronize(stream);
@@ -66,8 +81,9 @@ struct RcclExchanger : Exchanger {
     if (d_recv) (void)hipFree(d_recv);
     h_recv = d_recv = nullptr;
     cap = 0;
-    EAO_HIP_CHECK(hipHostMalloc((void**)&h_recv, c * world, 0));
+    EAO_HIP_CHECK(hipHostMalloc((void**)&h_recv, c * world + 64, 0));  // + the flag word
     EAO_HIP_CHECK(hipMalloc((void**)&d_recv, c * world));
+    *(volatile unsigned*)(h_recv + c * world) = seq;
     cap = c;
     return EAO_OK;
   }
@@ -81,15 +97,24 @@ struct RcclExchanger : Exchanger {
     if (int rc = grow(bytes)) return rc;
     if (ready) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready, 0));
     EAO_NCCL_CHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
-    EAO_HIP_CHECK(hipMemcpyAsync(h_recv, d_recv, bytes * world, hipMemcpyDeviceToHost, stream));
-    // the replay thread spins on the copy's event, as on its own launches: a blocking
-    // synchronisation may park the thread and pay a wake-up per exchange
+    unsigned* flag = (unsigned*)(h_recv + cap * world);
+    const unsigned want = ++seq;
+    hipLaunchKernelGGL(k_recv_out, dim3(1), dim3(256), 0, stream, d_recv, h_recv, bytes * world, flag, want);
+    EAO_HIP_CHECK(hipGetLastError());
     if (!done) EAO_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(done, stream));
-    for (;;) {
-      const hipError_t r = hipEventQuery(done);
-      if (r == hipSuccess) break;
-      if (r != hipErrorNotReady) EAO_HIP_CHECK(r);
+    // the replay thread spins (a blocking synchronisation may park it and pay a wake-up per
+    // exchange) on the flag; the event reports a failed launch (queried every 64 spins)
+    for (unsigned k = 1;; k++) {
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want) break;
+      if ((k & 63) == 0) {
+        const hipError_t r = hipEventQuery(done);
+        if (r != hipSuccess && r != hipErrorNotReady) EAO_HIP_CHECK(r);
+        if (r == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != want) {
+          set_error("rccl exchanger: copy-back completed without its flag");
+          return EAO_E_HIP;
+        }
+      }
       __builtin_ia32_pause();
     }
     *out = h_recv;

@@ -50,6 +50,48 @@ def test_np_pairs():
             assert np.allclose([g["r1"], g["r2"]], [o["r1"], o["r2"]], rtol=1e-5, atol=1e-5)
 
 
+def test_np_pairs_direct_counts():
+    """Pairs with m * n up to the direct-count threshold (131072) are counted by brute force
+    against the compacted object values (no sort): with and without the n > 3m subsampling, ties
+    (quantised clouds, frame values equal to object values), +-inf coordinates, invalid points on
+    both sides, a NaN frame value (no count on its axis), a NaN object value (the sort path), tail
+    quads (n % 4 != 0), one wave of frame points (m <= 64: 16 chunks) and up to 1024 (one chunk),
+    and pairs just past the threshold (the sort path) in the same launch."""
+    rng = np.random.default_rng(0xD1C7)
+    cases = [(20, 20), (21, 61), (22, 63), (40, 121), (64, 2047), (65, 2016), (88, 195), (100, 1300),
+             (128, 1024), (300, 437), (500, 262), (1000, 131), (1024, 128), (60, 2000), (120, 1093),
+             (128, 1025), (400, 330), (30, 3000), (70, 1800)]
+    fs, os_, exp = [], [], []
+    for k, (m, n) in enumerate(cases):
+        q = 0.01 if k % 3 == 0 else None
+        f = _cloud(rng, m, [1, 2, 3], 0.1, quant=q)
+        o = _cloud(rng, n, [1, 2, 3] if k % 2 else [1.03, 2, 3.04], 0.1, quant=q)
+        fv = (rng.random(m) > 0.1).astype(np.uint8)
+        ov = (rng.random(n) > 0.1).astype(np.uint8)
+        if k == 4:
+            f[:12] = o[:12]
+        if k == 5:
+            o[:3, 0], o[3:6, 2], f[:2, 1] = np.inf, -np.inf, np.inf
+        if k == 6:
+            f[5, 1] = np.nan
+        if k == 7:
+            o[11, 2] = np.nan
+        if k == 8:
+            fv[:] = 1
+            ov[:] = 1
+        fs.append((f, fv))
+        os_.append((o, ov))
+        exp.append(orc.np_test(f, fv, o, ov))
+    got = ea.Assoc().np_batch(fs, os_)
+    for k, (g, o) in enumerate(zip(got, exp)):
+        info = (k, cases[k], {x: g[x] for x in ("verdict", "m", "n", "cnt_gt", "cnt_lt", "cnt_eq")},
+                {x: o[x] for x in ("verdict", "m", "n", "cnt_gt", "cnt_lt", "cnt_eq")})
+        assert g["verdict"] == o["verdict"] and g["m"] == o["m"] and g["n"] == o["n"], info
+        assert np.array_equal(g["cnt_gt"], o["cnt_gt"]) and np.array_equal(g["cnt_lt"], o["cnt_lt"]), info
+        assert np.array_equal(g["cnt_eq"], o["cnt_eq"]), info
+        assert np.allclose(g["w"], o["w"], rtol=1e-5, atol=1e-5), info
+
+
 def test_np_pairs_rank_path():
     """Large objects against small detections take the rank path of k_np_pairs (the m
     frame values sorted, the object streamed through binary searches): the counts must
@@ -131,6 +173,36 @@ def test_iforest_mask_path_boundaries():
             o = orc.iforest(c)
             assert np.allclose(g, o, rtol=1e-5, atol=1e-9, equal_nan=True), len(c)
             assert np.array_equal(g > 0.6, o > 0.6), len(c)
+
+
+def test_iforest_one_wave_small_batches():
+    """Batches whose samples all have <= 64 items run the one-wave forest kernel (k_iforest_tree<64>:
+    build and score by the same wave): sizes around the register / rank-space subtree boundary
+    (sample 7 / 8) and the 64-item limit (n = 128, 129), ties, duplicated and repeated points, the
+    sample from the table and drawn in the kernel (sample n / 3), batched and alone."""
+    rng = np.random.default_rng(0x51A11)
+    clouds = []
+    for n in (2, 3, 5, 14, 15, 16, 17, 18, 31, 63, 64, 65, 100, 127, 128, 129):
+        c = _cloud(rng, n, [0, 0, 2], 0.05)
+        c[: max(1, n // 10)] += rng.uniform(-0.5, 0.5, (max(1, n // 10), 3)).astype(np.float32)
+        clouds.append(c)
+    lat = np.round(_cloud(rng, 120, [0, 0, 2], 0.05) * 40) / 40  # many equal keys
+    clouds.append(lat.astype(np.float32))
+    dup = _cloud(rng, 90, [0, 0, 2], 0.05)
+    dup[30:] = dup[:60]
+    clouds.append(dup)
+    clouds.append(np.tile(np.float32([[0.1, -0.2, 2.0]]), (50, 1)))  # one point repeated
+    a = ea.Assoc(max_points=40000)
+    for batch in (clouds, [[c] for c in clouds]):
+        got = a.iforest(batch) if isinstance(batch[0], np.ndarray) else [a.iforest(b)[0] for b in batch]
+        for c, g in zip(clouds, got):
+            o = orc.iforest(c)
+            assert np.allclose(g, o, rtol=1e-5, atol=1e-9, equal_nan=True), len(c)
+            assert np.array_equal(g > 0.6, o > 0.6), len(c)
+    samples = [max(1, len(c) // 3) for c in clouds]
+    for c, m, g in zip(clouds, samples, a.iforest(clouds, samples=samples)):
+        o = orc.iforest(c, sample=m)
+        assert np.allclose(g, o, rtol=1e-5, atol=1e-9, equal_nan=True), (len(c), m)
 
 
 def test_iforest_sample_table_and_drawn_paths():

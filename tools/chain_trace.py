@@ -6,6 +6,7 @@ streams since the previous frame start, and summarises per frame: busy time of t
 association kernels, the forest chains (k_stage -> k_iforest_tree -> k_iforest_sum
 [-> k_np_pairs]) with their launch gaps, and the frame period."""
 import collections
+import re
 import sqlite3
 import sys
 
@@ -13,7 +14,7 @@ import numpy as np
 
 c = sqlite3.connect(sys.argv[1])
 rows = c.execute("select name, start, end, stream_id, grid_x, grid_y from kernels order by start").fetchall()
-K = [(n.split('(')[0].replace("eao::", ""), s, e, st, gx, gy) for n, s, e, st, gx, gy in rows]
+K = [(re.sub(r"<.*$", "", n.split('(')[0].replace("eao::", "").replace("void ", "")), s, e, st, gx, gy) for n, s, e, st, gx, gy in rows]
 ASSOC = {"k_stage", "k_iforest_tree", "k_iforest_sum", "k_np_pairs", "k_rects_np", "k_pack_masks", "k_rects"}
 A = [k for k in K if k[0] in ASSOC]
 fs = [i for i, k in enumerate(A) if k[0] == "k_rects_np"]

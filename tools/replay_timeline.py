@@ -6,6 +6,7 @@ Host events: 1 frame begin, 2 frame-start launch, 3 frame-start done, 4 associat
 5 forest batch launch (slot, clouds, max n), 6/7 forest wait begin/end (slot, phase),
 8/9 local mapping begin/end. The last replay pass in the file is analysed."""
 import collections
+import re
 import sqlite3
 import sys
 
@@ -53,7 +54,7 @@ if len(sys.argv) < 3:
     sys.exit(0)
 c = sqlite3.connect(sys.argv[2])
 rows = c.execute("select name, start, end, stream_id from kernels order by start").fetchall()
-K = [(n.split('(')[0].replace("eao::", ""), s / 1e3, e / 1e3, st) for n, s, e, st in rows]
+K = [(re.sub(r"<.*$", "", n.split('(')[0].replace("eao::", "").replace("void ", "")), s / 1e3, e / 1e3, st) for n, s, e, st in rows]
 K = [k for k in K if t[0] - 1000 <= k[1] <= t[-1] + 1000]
 rn = [k for k in K if k[0] == "k_rects_np"]
 fs = np.nonzero(E == 2)[0]
@@ -85,8 +86,24 @@ if len(st) == len(fl):
     dur = np.array([k[2] - k[1] for k in tr_])
     print("forest batches %d: stage start - launch event med %.1f | tree med %.1f mean %.1f p90 %.1f us"
           % (len(st), np.median(a), np.median(dur), dur.mean(), np.percentile(dur, 90)))
+    # the batch's chain on its stream: k_stage -> k_iforest_tree -> k_iforest_sum (+ speculative NP)
+    by_stream = collections.defaultdict(list)
+    for k in K:
+        by_stream[k[3]].append(k)
+    parts = []
+    for s0 in st:
+        q = by_stream[s0[3]]
+        i = q.index(s0)
+        if i + 2 < len(q) and q[i + 1][0] == "k_iforest_tree" and q[i + 2][0] == "k_iforest_sum":
+            t1, t2 = q[i + 1], q[i + 2]
+            parts.append((s0[2] - s0[1], t1[1] - s0[2], t1[2] - t1[1], t2[1] - t1[2], t2[2] - t2[1], t2[2] - s0[1]))
+    if parts:
+        P = np.array(parts)
+        print("forest chain (med / mean us): stage %.1f / %.1f | gap %.1f / %.1f | tree %.1f / %.1f | gap %.1f / %.1f"
+              " | sum %.1f / %.1f | stage start -> sum end %.1f / %.1f"
+              % tuple(v for c in range(6) for v in (np.median(P[:, c]), P[:, c].mean())))
     mx = ev["c"][fl]
-    for lo, hi in ((0, 200), (200, 400), (400, 800), (800, 1600), (1600, 99999)):
+    for lo, hi in ((0, 130), (130, 200), (200, 400), (400, 800), (800, 1600), (1600, 99999)):
         m = (mx >= lo) & (mx < hi)
         if m.any():
             print("   max n in [%4d, %5d): %4d batches, tree med %.1f us" % (lo, hi, m.sum(), np.median(dur[m])))
