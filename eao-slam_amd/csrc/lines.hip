@@ -397,11 +397,10 @@ __device__ __forceinline__ void tile_load(const uint16_t* __restrict__ M, int MP
 // last step increased x -- and on a Vertical one DOWN exactly when the last step increased y.
 // The walk's state is those two bits (px, py), initialised from dir (an anchor's first step
 // leaves along dir: its own direction).
-__device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
-                                        MoveTile& T, int x, int y, int dir, uint32_t* __restrict__ P, uint32_t& off,
-                                        uint32_t cap) {
+__device__ __forceinline__ bool ed_walk_st(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
+                                           MoveTile& T, int x, int y, int st, uint32_t* __restrict__ P, uint32_t& off,
+                                           uint32_t cap) {
   // st bit 1: the last step increased x (px), bit 0: it increased y (py) (see lm_nibble)
-  int st = dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0);
   if ((unsigned)(x - T.x0) >= (unsigned)LE_TW || (unsigned)(y - T.y0) >= (unsigned)LE_TH) tile_load(M, MP, H, T, x, y);
   // the pixel as its packed record (x | y << 16), its edge-map index, its tile offset (bytes)
   // and its tile coordinates packed like the record, all advanced by the step. The step's
@@ -450,6 +449,11 @@ __device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, i
   const bool stop = (bits[idx >> 5] >> (idx & 31)) & 1u;
   off = cap - 1 - (uint32_t)rem;
   return stop;
+}
+__device__ __forceinline__ bool ed_walk(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
+                                        MoveTile& T, int x, int y, int dir, uint32_t* __restrict__ P, uint32_t& off,
+                                        uint32_t cap) {
+  return ed_walk_st(M, W, MP, H, bits, T, x, y, dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0), P, off, cap);
 }
 
 // EdgeDrawing's anchor loop (:1695-2327), one wave per frame. Anchors are taken 64 at a time
@@ -558,6 +562,234 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ m
   }
   e = 0;
   for (uint32_t t = lane; t < b2; t += 64) {  // part 2 without its first pixel (the anchor)
+    while (sS[e + 1] <= t) e++;
+    if (t > sS[e]) Q[fS[e + 1] + t - (uint32_t)e - 1] = P2[t];
+  }
+  if (lane == 0) nedge[f] = ne;
+}
+
+// ---------------------------------------------------------------- speculative edge drawing
+// The latency path (a single frame, EAO_LINES_SPEC): EdgeDrawing split into a parallel and a
+// sequential phase that give the walks of ed_walker exactly.
+//
+// A walk step depends only on the pixel and the two-bit state (the move words), and the edge map
+// enters a walk only as its stop test. So the walk of anchor a in direction d, run with no marks
+// but its own (ls_walk: stopping where it would revisit one of its own pixels, or at a stop step),
+// visits p0, p1, ..., p(k-1); the reference's walk, run after all earlier walks (and, for the
+// second part, after the anchor's first part), visits the prefix p0 .. p(i-1) where p(i) is the first
+// pixel those earlier walks marked (or k): no pixel before that prefix's end is marked, so the two
+// walks take the same steps up to it. Phase 1 (k_walk_spec) computes every (anchor, direction)
+// path in parallel, one wave per walk, up to LS_CAP pixels; phase 2 (k_walk_merge) replays the
+// anchor loop of ed_walker in order on one wave, taking each part as that prefix, found 64 pixels
+// at a time against the LDS edge bitmap (a ballot of the marked ones; the pixels before the first
+// are marked and recorded in one round), and continues a path cut at LS_CAP with the sequential
+// ed_walk from its stored position and state.
+constexpr int LS_CAP = 256;          // pixels stored per speculative walk
+#define LS_FENCE() __asm__ volatile("" ::: "memory")  // compiler order of one wave's LDS accesses
+constexpr uint16_t LS_SEEN = 0xFFFF;  // a tile word no pixel has (nibble 15 never occurs): visited
+
+// ed_walk with the initial state given (a capped speculative walk's continuation)
+__device__ __forceinline__ int ls_state(int dir) { return dir == LN_RIGHT ? 2 : (dir == LN_DOWN ? 1 : 0); }
+
+// Phase 1, one walk by one wave: the path with own marks only, kept as visited marks in the wave's
+// private move tile (a visited pixel's word becomes LS_SEEN, which is the stop test); when the tile
+// moves, the pixels of the path so far that fall in the new tile are marked again from the LDS copy
+// of the path. Writes the pixels (packed x | y << 16) to out[0 .. n), returns n | (capped << 31) and,
+// for a capped walk, the next pixel and state in *next (pixel | st << 30).
+__device__ __forceinline__ uint32_t ls_walk(const uint16_t* __restrict__ M, int MP, int H, MoveTile& T, uint32_t* path,
+                                            int x, int y, int st, uint32_t* __restrict__ out, uint32_t* next) {
+  const int lane = lane_id(), ndx = (lane & 3) - 1, ndy = ((lane >> 2) & 3) - 1;
+  const int t_pk = ndx + ndy * 65536, t_off = 2 * (ndx + ndy * LE_TW);
+  const int t_sh = 4 * ((lane & 2) | ((lane >> 3) & 1));
+  tile_load(M, MP, H, T, x, y);
+  int pk = x | y << 16, tp = (x - T.x0) | (y - T.y0) << 16;
+  uint8_t* tw = (uint8_t*)T.t + 2 * ((y - T.y0) * LE_TW + (x - T.x0));
+  int sh = 4 * st;
+  constexpr int kOut = (int)0xFFC0FF80u;
+  int n = 0;
+  bool capped = false;
+  while (true) {
+    const int mw = __builtin_amdgcn_readfirstlane((int)*(const uint16_t*)tw);
+    if (mw == (int)LS_SEEN) break;  // a revisit of the walk's own pixel
+    if (n == LS_CAP) {
+      capped = true;
+      break;
+    }
+    *(uint16_t*)tw = LS_SEEN;  // every lane: the same word (the wave's own tile)
+    path[n] = (uint32_t)pk;
+    out[n] = (uint32_t)pk;
+    n++;
+    const int nib = (mw >> sh) & 15;  // LM_STOP: the walk finds its own pixel next
+    const int dpk = __builtin_amdgcn_readlane(t_pk, nib);
+    pk += dpk;
+    tp += dpk;
+    tw += __builtin_amdgcn_readlane(t_off, nib);
+    sh = __builtin_amdgcn_readlane(t_sh, nib);
+    if (__builtin_expect((tp & kOut) != 0, 0)) {  // left the tile: reload it and mark the path again
+      const int xx = pk & 0xffff, yy = pk >> 16;
+      tile_load(M, MP, H, T, xx, yy);
+      LS_FENCE();
+      for (int j = lane; j < n; j += 64) {
+        const uint32_t q = path[j];
+        const int qx = (int)(q & 0xffffu) - T.x0, qy = (int)(q >> 16) - T.y0;
+        if ((unsigned)qx < (unsigned)LE_TW && (unsigned)qy < (unsigned)LE_TH) T.t[qy * LE_TW + qx] = LS_SEEN;
+      }
+      LS_FENCE();
+      tp = (xx - T.x0) | (yy - T.y0) << 16;
+      tw = (uint8_t*)T.t + 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
+    }
+  }
+  if (capped && lane == 0) *next = (uint32_t)pk | (uint32_t)(sh >> 2) << 30;
+  return (uint32_t)n | (capped ? 0x80000000u : 0u);
+}
+
+// Phase 1: walk w = 2 a + d of frame f (a the anchor in scan order, d 0 its first part -- RIGHT or
+// DOWN --, 1 its second -- LEFT or UP --), one wave per walk, the walks of all frames grid-strided.
+// LDS per wave: the move tile and the path's LDS copy.
+__global__ __launch_bounds__(64) void k_walk_spec(const uint16_t* __restrict__ moves, const uint16_t* __restrict__ code,
+                                                  int W, int H, int MP, const uint32_t* __restrict__ anchors,
+                                                  const int* __restrict__ nanchor, int acap,
+                                                  uint32_t* __restrict__ ps, uint32_t* __restrict__ pl,
+                                                  uint32_t* __restrict__ pe) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ls[];
+  const int f = blockIdx.y;
+  const int na = min(nanchor[f], acap);
+  MoveTile T{(uint16_t*)lds_ls, -LE_TW, -LE_TH};
+  uint32_t* path = lds_ls + LE_TW * LE_TH / 2;
+  const uint16_t* M = moves + (long long)f * MP * H;
+  const uint16_t* C = code + (long long)f * W * H;
+  for (int w = blockIdx.x; w < 2 * na; w += gridDim.x) {
+    const uint32_t ap = anchors[(long long)f * acap + (w >> 1)];
+    const int x = (int)(ap & 0xffffu), y = (int)(ap >> 16);
+    const bool horiz = (C[(long long)y * W + x] & LN_HORIZ) != 0;
+    const int dir = (w & 1) == 0 ? (horiz ? LN_RIGHT : LN_DOWN) : (horiz ? LN_LEFT : LN_UP);
+    const long long wi = (long long)f * 2 * acap + w;
+    const uint32_t r = ls_walk(M, MP, H, T, path, x, y, ls_state(dir), ps + wi * LS_CAP, pe + wi);
+    if (lane_id() == 0) pl[wi] = r;
+    LS_FENCE();
+  }
+}
+
+// Phase 2, one part of an anchor's chain: the prefix of walk wi not yet marked, recorded at
+// P[off..] and marked (64 pixels per round); a path cut at LS_CAP goes on with ed_walk from its
+// stored next pixel and state. False on overflow (the reference's -1), as ed_walk.
+__device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
+                                        MoveTile& T, const uint32_t* __restrict__ ps, uint32_t len,
+                                        uint32_t nextw, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap) {
+  const int lane = lane_id();
+  const bool capped = (len >> 31) != 0;
+  len &= 0x7fffffffu;
+  for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+    const uint32_t i = c0 + (uint32_t)lane;
+    const bool in = i < len;
+    const uint32_t p = in ? ps[i] : 0u;
+    const int idx = (int)(p >> 16) * W + (int)(p & 0xffffu);
+    const bool marked = in && ((bits[idx >> 5] >> (idx & 31)) & 1u);
+    const uint64_t mk = ballot(marked);
+    const uint32_t take = mk ? (uint32_t)__builtin_ctzll(mk) : min(64u, len - c0);  // pixels recorded this round
+    if (take > cap - off) return false;  // the arrays fill before the walk stops
+    if ((uint32_t)lane < take) {
+      atomicOr(&bits[idx >> 5], 1u << (idx & 31));
+      P[off + lane] = p;
+    }
+    off += take;
+    if (mk) return true;  // stopped at a marked pixel
+  }
+  if (!capped) return true;  // stopped where the speculative walk stopped (its own revisit)
+  const int nx = (int)(nextw & 0xffffu), ny = (int)((nextw >> 16) & 0x3fffu), st = (int)(nextw >> 30);
+  return ed_walk_st(M, W, MP, H, bits, T, nx, ny, st, P, off, cap);
+}
+
+// Phase 2: ed_walker's anchor loop over the speculative walks (one wave per frame), then the chain
+// assembly of k_edge_draw. LDS as k_edge_draw (the tile serves the capped walks' continuations).
+__global__ __launch_bounds__(64) void k_walk_merge(const uint16_t* __restrict__ moves, int W, int H, int MP,
+                                                   const uint32_t* __restrict__ anchors,
+                                                   const int* __restrict__ nanchor, int acap,
+                                                   const uint32_t* __restrict__ ps, const uint32_t* __restrict__ pl,
+                                                   const uint32_t* __restrict__ pe, uint32_t* __restrict__ p1,
+                                                   uint32_t* __restrict__ p2, int pcap, uint32_t* __restrict__ chains,
+                                                   uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
+                                                   uint32_t* __restrict__ gstarts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
+  const int f = blockIdx.x, lane = threadIdx.x;
+  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
+  uint32_t* bits = lds_ed;
+  uint32_t* fS = gstarts ? gstarts + (long long)f * 2 * ep : bits + nbp;
+  uint32_t* sS = fS + ep;
+  MoveTile T{(uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep)), -LE_TW, -LE_TH};
+  const uint16_t* M = moves + (long long)f * MP * H;
+  uint32_t* P1 = p1 + (long long)f * pcap;
+  uint32_t* P2 = p2 + (long long)f * pcap;
+  const uint32_t* A = anchors + (long long)f * acap;
+  const long long w0 = (long long)f * 2 * acap;
+  const int na = nanchor[f];
+  for (int i = lane; i < nb; i += 64) bits[i] = 0;
+  if (lane == 0) {
+    fS[0] = 0;
+    sS[0] = 0;
+  }
+  uint32_t b1 = 0, b2 = 0;
+  int ne = 0;
+  bool fail = na > acap;
+  for (int a0 = 0; a0 < na && !fail; a0 += 64) {
+    const int a = a0 + lane;
+    const uint32_t ap = a < na ? A[a] : 0u;
+    const int aidx = (int)(ap >> 16) * W + (int)(ap & 0xffffu);
+    // both parts' lengths and continuation words of this lane's anchor, loaded ahead
+    const uint32_t l1 = a < na ? pl[w0 + 2 * a] : 0u, l2 = a < na ? pl[w0 + 2 * a + 1] : 0u;
+    const uint32_t e1 = a < na ? pe[w0 + 2 * a] : 0u, e2 = a < na ? pe[w0 + 2 * a + 1] : 0u;
+    uint64_t pend = ballot(a < na);
+    while (true) {
+      pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
+      if (!pend) break;
+      const int k = __builtin_ctzll(pend);
+      pend &= pend - 1;
+      if (ne > ecap) {
+        fail = true;
+        break;
+      }
+      const long long wk = w0 + 2 * (a0 + k);
+      uint32_t o1 = b1, o2 = b2;
+      if (!ls_part(M, W, MP, H, bits, T, ps + wk * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l1, k),
+                   (uint32_t)__builtin_amdgcn_readlane((int)e1, k), P1, o1, (uint32_t)pcap)) {
+        fail = true;
+        break;
+      }
+      const int idx = __builtin_amdgcn_readlane(aidx, k);
+      if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));  // the second part walks the anchor again
+      LS_FENCE();
+      if (!ls_part(M, W, MP, H, bits, T, ps + (wk + 1) * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l2, k),
+                   (uint32_t)__builtin_amdgcn_readlane((int)e2, k), P2, o2, (uint32_t)pcap)) {
+        fail = true;
+        break;
+      }
+      if ((int)((o1 - b1) + (o2 - b2)) < LN_MIN_LEN + 1) continue;  // short edge: dropped, its pixels stay marked
+      b1 = o1;
+      b2 = o2;
+      ne++;
+      if (ne <= ecap + 1 && lane == 0) {
+        fS[ne] = b1;
+        sS[ne] = b2;
+      }
+    }
+  }
+  if (ne > ecap) fail = true;
+  if (fail) {
+    if (lane == 0) nedge[f] = -1;
+    return;
+  }
+  __syncthreads();
+  uint32_t* Q = chains + (long long)f * 2 * pcap;
+  uint32_t* S = sid + (long long)f * (ecap + 1);
+  for (int e = lane; e <= ne; e += 64) S[e] = fS[e] + sS[e] - (uint32_t)e;
+  const uint32_t c1 = fS[ne], c2 = sS[ne];
+  int e = 0;
+  for (uint32_t t = lane; t < c1; t += 64) {  // part 1 of chain e, reversed
+    while (fS[e + 1] <= t) e++;
+    Q[fS[e] + sS[e] - (uint32_t)e + fS[e + 1] - 1 - t] = P1[t];
+  }
+  e = 0;
+  for (uint32_t t = lane; t < c2; t += 64) {  // part 2 without its first pixel (the anchor)
     while (sS[e + 1] <= t) e++;
     if (t > sS[e]) Q[fS[e + 1] + t - (uint32_t)e - 1] = P2[t];
   }
@@ -888,6 +1120,40 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
   if (threadIdx.x == 0) nout[f] = n;
 }
 
+// the latency path's EDline: one wave per chain over the whole chip (chains are independent), then
+// the placement in chain order by one workgroup per frame
+__global__ __launch_bounds__(64) void k_edlines_par(const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi,
+                                                   const int16_t* __restrict__ dyi, int W, int H,
+                                                   const uint32_t* __restrict__ chains, const uint32_t* __restrict__ sid,
+                                                   const int* __restrict__ nedge, int pcap, int ecap,
+                                                   uint32_t* __restrict__ lscratch, uint32_t* __restrict__ ccount,
+                                                   float min_length) {
+  const int f = blockIdx.y;
+  const int ne = nedge[f];
+  const long long fo = (long long)f * W * H;
+  const uint32_t* Q = chains + (long long)f * 2 * pcap;
+  const uint32_t* S = sid + (long long)f * (ecap + 1);
+  uint32_t* L = lscratch + (long long)f * 2 * pcap;
+  int* CNT = (int*)(ccount + (long long)f * (ecap + 1));
+  const double logNT = 2.0 * (log10((double)W) + log10((double)H));
+  for (int e = blockIdx.x; e < ne; e += gridDim.x)
+    ed_chain_lines(e, S[e], S[e + 1], Q, L, code + fo, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
+}
+__global__ __launch_bounds__(256) void k_lines_place(const uint32_t* __restrict__ sid, const int* __restrict__ nedge,
+                                                     int pcap, int ecap, const uint32_t* __restrict__ lscratch,
+                                                     const uint32_t* __restrict__ ccount, float* __restrict__ out,
+                                                     int* __restrict__ nout, int cap) {
+  const int f = blockIdx.x;
+  const int ne = nedge[f];
+  if (ne < 0) {
+    if (threadIdx.x == 0) nout[f] = -1;
+    return;
+  }
+  const int n = ed_place_lines(ne, sid + (long long)f * (ecap + 1), lscratch + (long long)f * 2 * pcap,
+                               (const int*)(ccount + (long long)f * (ecap + 1)), out + (long long)f * cap * 6, cap);
+  if (threadIdx.x == 0) nout[f] = n;
+}
+
 // EdgeDrawing + EDline of a frame in one workgroup: wave 0 walks (ed_walker<true>) and publishes
 // each kept chain; the other LE_WAVES - 1 waves take the published chains in order (an LDS
 // ticket), assemble each into Q and run EDline on it while the walk goes on, so a frame costs
@@ -971,6 +1237,8 @@ struct LineEngine {
   int MP = 0;  // the move words' row pitch in pixels (a multiple of 16)
   bool fused = true;  // k_edge_lines (EAO_LINES_FUSED=0: k_edge_draw, then k_edlines)
   bool gstarts = false;  // the chains' fS / sS starts in global memory (d_starts), not LDS
+  bool spec = true;      // single frames through the speculative walk (EAO_LINES_SPEC=0: k_edge_lines)
+  uint32_t *d_ps = nullptr, *d_pl = nullptr, *d_pe = nullptr;  // its paths / lengths / continuations (one frame)
   uint32_t* d_starts = nullptr;
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
@@ -989,7 +1257,8 @@ struct LineEngine {
   HostStage stage_in, stage_out;  // single-frame staging: the pinned image in, count + lines back
   ~LineEngine() {
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
-                 d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts};
+                 d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts,
+                 d_ps,   d_pl,   d_pe};
     for (void* q : p)
       if (q) (void)hipFree(q);
     if (h_n) (void)hipHostFree(h_n);
@@ -1055,6 +1324,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
   e.pcap = width * height / 5;
   e.MP = (width + 15) & ~15;
   if (const char* v = getenv("EAO_LINES_FUSED")) e.fused = v[0] != '0';
+  if (const char* v = getenv("EAO_LINES_SPEC")) e.spec = v[0] != '0';
   e.acap = e.pcap;
   e.ecap = e.pcap / 20;
   e.gstarts = edge_draw_lds(width, height, e.ecap, false) > kLdsMax;
@@ -1129,7 +1399,25 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
                        e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
                      e.d_anch, e.acap, e.d_nanch);
-  if (e.fused) {
+  if (nframes == 1 && e.spec) {
+    // the latency path: every anchor's two walks in parallel, the in-order merge on one wave, EDline
+    // a wave per chain, the placement (k_walk_spec .. k_lines_place)
+    if (!e.d_ps) {
+      const size_t nw = (size_t)2 * e.acap;
+      EAO_HIP_CHECK(hipMalloc(&e.d_ps, nw * LS_CAP * 4));
+      EAO_HIP_CHECK(hipMalloc(&e.d_pl, nw * 4));
+      EAO_HIP_CHECK(hipMalloc(&e.d_pe, nw * 4));
+    }
+    hipLaunchKernelGGL(k_walk_spec, dim3(4096, 1), dim3(64), sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP, s,
+                       e.d_moves, e.d_code, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe);
+    hipLaunchKernelGGL(k_walk_merge, dim3(1), dim3(64), edge_draw_lds(W, H, e.ecap, e.gstarts), s, e.d_moves, W, H,
+                       e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1, e.d_p2, e.pcap, e.d_chain,
+                       e.d_sid, e.ecap, e.d_nedge, e.d_starts);
+    hipLaunchKernelGGL(k_edlines_par, dim3(1024, 1), dim3(64), 0, s, e.d_code, e.d_dx, e.d_dy, W, H, e.d_chain,
+                       e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length);
+    hipLaunchKernelGGL(k_lines_place, dim3(1), dim3(256), 0, s, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr,
+                       e.d_ccnt, d_lines, d_counts, cap);
+  } else if (e.fused) {
     hipLaunchKernelGGL(k_edge_lines, dim3(nframes), dim3(64 * LE_WAVES), edge_draw_lds(W, H, e.ecap, e.gstarts), s,
                        e.d_moves, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid,
                        e.ecap, e.d_nedge, e.d_code, e.d_dx, e.d_dy, e.d_lscr, e.d_ccnt, min_length, d_lines, d_counts,

@@ -54,9 +54,11 @@ def test_np_pairs_direct_counts():
     """Pairs with m * n up to the direct-count threshold (131072) are counted by brute force
     against the compacted object values (no sort): with and without the n > 3m subsampling, ties
     (quantised clouds, frame values equal to object values), +-inf coordinates, invalid points on
-    both sides, a NaN frame value (no count on its axis), a NaN object value (the sort path), tail
-    quads (n % 4 != 0), one wave of frame points (m <= 64: 16 chunks) and up to 1024 (one chunk),
-    and pairs just past the threshold (the sort path) in the same launch."""
+    both sides, a NaN frame value (no count on its axis), tail quads (n % 4 != 0), one wave of
+    frame points (m <= 64: 16 chunks) and up to 1024 (one chunk), and pairs just past the
+    threshold (the sort path) in the same launch. (A NaN object value sends a pair to the sort
+    path, whose order of NaN need not match std::sort's: map-point positions are finite, and that
+    case is not pinned.)"""
     rng = np.random.default_rng(0xD1C7)
     cases = [(20, 20), (21, 61), (22, 63), (40, 121), (64, 2047), (65, 2016), (88, 195), (100, 1300),
              (128, 1024), (300, 437), (500, 262), (1000, 131), (1024, 128), (60, 2000), (120, 1093),
@@ -74,8 +76,6 @@ def test_np_pairs_direct_counts():
             o[:3, 0], o[3:6, 2], f[:2, 1] = np.inf, -np.inf, np.inf
         if k == 6:
             f[5, 1] = np.nan
-        if k == 7:
-            o[11, 2] = np.nan
         if k == 8:
             fv[:] = 1
             ov[:] = 1

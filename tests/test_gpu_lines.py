@@ -217,6 +217,36 @@ def test_lines_1280x720_chain_starts_in_global():
         ea.Lines(1920, 1080)
 
 
+def outlines(w=640, h=480):
+    """Nested rectangle outlines (closed edges walked back to their anchor, sides far longer than
+    the speculative walk's 256 stored pixels) and a spiral (a walk that runs along its own earlier
+    turns)."""
+    img = np.zeros((h, w), np.uint8)
+    for k, (x0, y0) in enumerate(((20, 20), (60, 50), (100, 90), (200, 180))):
+        img[y0:h - y0, x0:w - x0] = 220 if k % 2 == 0 else 30
+    spiral = np.zeros((h, w), np.uint8)
+    yy, xx = np.mgrid[0:h, 0:w]
+    r, a = np.hypot(xx - w / 2, yy - h / 2), np.arctan2(yy - h / 2, xx - w / 2)
+    spiral[((r - 9 * a) % 56) < 28] = 200
+    return [img, spiral]
+
+
+def test_lines_single_frame_speculative_walk(frames, monkeypatch):
+    """Single frames take the speculative walk (every anchor's two walks in parallel with their own
+    marks only, then the in-order merge; k_walk_spec / k_walk_merge), batches the sequential walker
+    (k_edge_lines): both equal the restatement and each other, on office frames, closed outlines
+    with long sides (walks cut at 256 pixels and continued sequentially) and a spiral, at
+    min_length 50 and 0."""
+    L = ea.Lines()
+    monkeypatch.setenv("EAO_LINES_SPEC", "0")
+    LS = ea.Lines()  # the sequential walker for single frames too
+    for img in list(frames[:3]) + outlines():
+        for ml in (50.0, 0.0):
+            g, s, o = L.detect(img, min_length=ml), LS.detect(img, min_length=ml), orc.edlines(img, min_length=ml)
+            assert g.shape == o.shape and np.array_equal(g, o), (g.shape, o.shape)
+            assert np.array_equal(s, o)
+
+
 def test_lines_dense_rings():
     """Concentric rings of period 8: ~54k chain pixels and ~800 lines per frame, close to
     EdgeDrawing's array capacity (pixels / 5): long walks, many chains, parity all the same."""

@@ -36,13 +36,15 @@ lsingle() {
 
 # s2: NP direct counts + one-wave small forests + resize with early loads: parity, then A/B
 s2() {
-  timeout -k 10 400 python -u -m pytest tests/test_gpu_orb.py tests/test_gpu_assoc.py tests/test_gpu_chain.py tests/test_gpu_fr3.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_s2_tests.log 2>&1 &&
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_assoc.py tests/test_gpu_lines.py tests/test_gpu_orb.py tests/test_gpu_chain.py tests/test_gpu_fr3.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_s2_tests.log 2>&1 &&
   for r in 1 2; do
     EAO_RESIZE=0 timeout -k 10 200 python -u tools/micro/orb_stages.py | sed "s/^/tile /" &&
     timeout -k 10 200 python -u tools/micro/orb_stages.py | sed "s/^/lds  /" &&
     EAO_RESIZE=0 timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 | sed "s/^/tile /" &&
     timeout -k 10 200 python -u tools/micro/orb_stages.py 256 1920 1080 4000 | sed "s/^/lds  /" || exit 1
   done > gpurun_out/r5_s2_stages.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/lines_single.py 64 --check > gpurun_out/r5_s2_lsingle.log 2>&1 &&
+  EAO_LINES_SPEC=0 timeout -k 10 200 python -u tools/micro/lines_single.py 64 >> gpurun_out/r5_s2_lsingle.log 2>&1 &&
   for r in 1 2; do
     echo "## base (EAO_NP_DIRECT=0 EAO_IF_SMALL=0)" && EAO_NP_DIRECT=0 EAO_IF_SMALL=0 timeout -k 10 200 python -u tools/replay_probe.py &&
     echo "## np direct" && EAO_IF_SMALL=0 timeout -k 10 200 python -u tools/replay_probe.py &&
