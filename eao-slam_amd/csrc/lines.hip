@@ -670,130 +670,203 @@ __global__ __launch_bounds__(64) void k_walk_spec(const uint16_t* __restrict__ m
   }
 }
 
+// Phase 2's pixel records go through an LDS ring to a second wave that stores them to P1 / P2: the
+// merging wave then issues no global stores, so waiting for its look-ahead loads never waits for
+// store completions too (the vector-memory counter retires loads and stores in one order).
+constexpr int LS_RING = 2048;  // records: (part << 31 | index into P1 / P2, pixel)
+struct LsRing {
+  uint2* r;
+  int *wpos, *rpos;
+};
+
 // Phase 2, one part of an anchor's chain: the prefix of walk wi not yet marked, recorded at
-// P[off..] and marked (64 pixels per round); a path cut at LS_CAP goes on with ed_walk from its
-// stored next pixel and state. False on overflow (the reference's -1), as ed_walk.
+// P[off..] (part: P1 / P2) and marked, 64 pixels per round; a path cut at LS_CAP goes on with
+// ed_walk from its stored next pixel and state (whose stores go straight to P). False on overflow
+// (the reference's -1), as ed_walk. p is the lane's pixel of the first round, loaded ahead by the
+// caller; each round loads the next one's before it tests its own.
 __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
-                                        MoveTile& T, const uint32_t* __restrict__ ps, uint32_t len,
-                                        uint32_t nextw, uint32_t* __restrict__ P, uint32_t& off, uint32_t cap) {
+                                        MoveTile& T, const uint32_t* __restrict__ ps, uint32_t len, uint32_t nextw,
+                                        uint32_t p, uint32_t* __restrict__ P, uint32_t part, uint32_t& off, uint32_t cap,
+                                        LsRing& R, int& w) {
   const int lane = lane_id();
   const bool capped = (len >> 31) != 0;
   len &= 0x7fffffffu;
   for (uint32_t c0 = 0; c0 < len; c0 += 64) {
     const uint32_t i = c0 + (uint32_t)lane;
     const bool in = i < len;
-    const uint32_t p = in ? ps[i] : 0u;
+    const uint32_t pn = i + 64 < len ? ps[i + 64] : 0u;  // the next round's pixel, in flight
     const int idx = (int)(p >> 16) * W + (int)(p & 0xffffu);
     const bool marked = in && ((bits[idx >> 5] >> (idx & 31)) & 1u);
     const uint64_t mk = ballot(marked);
     const uint32_t take = mk ? (uint32_t)__builtin_ctzll(mk) : min(64u, len - c0);  // pixels recorded this round
     if (take > cap - off) return false;  // the arrays fill before the walk stops
+    while (w + 64 - __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > LS_RING)
+      __builtin_amdgcn_s_sleep(1);  // the ring is full: the writer is behind
     if ((uint32_t)lane < take) {
       atomicOr(&bits[idx >> 5], 1u << (idx & 31));
-      P[off + lane] = p;
+      R.r[(w + lane) & (LS_RING - 1)] = make_uint2(part << 31 | (off + lane), p);
     }
+    w += (int)take;
+    if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     off += take;
     if (mk) return true;  // stopped at a marked pixel
+    p = pn;
   }
   if (!capped) return true;  // stopped where the speculative walk stopped (its own revisit)
   const int nx = (int)(nextw & 0xffffu), ny = (int)((nextw >> 16) & 0x3fffu), st = (int)(nextw >> 30);
   return ed_walk_st(M, W, MP, H, bits, T, nx, ny, st, P, off, cap);
 }
 
-// Phase 2: ed_walker's anchor loop over the speculative walks (one wave per frame), then the chain
-// assembly of k_edge_draw. LDS as k_edge_draw (the tile serves the capped walks' continuations).
-__global__ __launch_bounds__(64) void k_walk_merge(const uint16_t* __restrict__ moves, int W, int H, int MP,
-                                                   const uint32_t* __restrict__ anchors,
-                                                   const int* __restrict__ nanchor, int acap,
-                                                   const uint32_t* __restrict__ ps, const uint32_t* __restrict__ pl,
-                                                   const uint32_t* __restrict__ pe, uint32_t* __restrict__ p1,
-                                                   uint32_t* __restrict__ p2, int pcap, uint32_t* __restrict__ chains,
-                                                   uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
-                                                   uint32_t* __restrict__ gstarts) {
+// Phase 2: ed_walker's anchor loop over the speculative walks (wave 0), the records stored by wave 1
+// from the ring, then the chain assembly of k_edge_draw by both. LDS as k_edge_draw (the tile serves
+// the capped walks' continuations) plus the ring. The first round of both parts of the next pending
+// anchor is loaded while the current one is merged (used when that anchor is still the next one
+// after the current walk's marks).
+__global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__ moves, int W, int H, int MP,
+                                                    const uint32_t* __restrict__ anchors,
+                                                    const int* __restrict__ nanchor, int acap,
+                                                    const uint32_t* __restrict__ ps, const uint32_t* __restrict__ pl,
+                                                    const uint32_t* __restrict__ pe, uint32_t* __restrict__ p1,
+                                                    uint32_t* __restrict__ p2, int pcap, uint32_t* __restrict__ chains,
+                                                    uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
+                                                    uint32_t* __restrict__ gstarts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
-  const int f = blockIdx.x, lane = threadIdx.x;
+  __shared__ int s_w, s_r, s_done, s_ne;
+  const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
   uint32_t* bits = lds_ed;
   uint32_t* fS = gstarts ? gstarts + (long long)f * 2 * ep : bits + nbp;
   uint32_t* sS = fS + ep;
-  MoveTile T{(uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep)), -LE_TW, -LE_TH};
-  const uint16_t* M = moves + (long long)f * MP * H;
+  uint16_t* tile = (uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep));
+  LsRing R{(uint2*)(tile + LE_TW * LE_TH), &s_w, &s_r};
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
-  const uint32_t* A = anchors + (long long)f * acap;
-  const long long w0 = (long long)f * 2 * acap;
-  const int na = nanchor[f];
-  for (int i = lane; i < nb; i += 64) bits[i] = 0;
-  if (lane == 0) {
-    fS[0] = 0;
-    sS[0] = 0;
-  }
-  uint32_t b1 = 0, b2 = 0;
-  int ne = 0;
-  bool fail = na > acap;
-  for (int a0 = 0; a0 < na && !fail; a0 += 64) {
-    const int a = a0 + lane;
-    const uint32_t ap = a < na ? A[a] : 0u;
-    const int aidx = (int)(ap >> 16) * W + (int)(ap & 0xffffu);
-    // both parts' lengths and continuation words of this lane's anchor, loaded ahead
-    const uint32_t l1 = a < na ? pl[w0 + 2 * a] : 0u, l2 = a < na ? pl[w0 + 2 * a + 1] : 0u;
-    const uint32_t e1 = a < na ? pe[w0 + 2 * a] : 0u, e2 = a < na ? pe[w0 + 2 * a + 1] : 0u;
-    uint64_t pend = ballot(a < na);
+  if (threadIdx.x == 0) s_w = s_r = s_done = 0;
+  __syncthreads();
+  if (wave == 0) {
+    MoveTile T{tile, -LE_TW, -LE_TH};
+    const uint16_t* M = moves + (long long)f * MP * H;
+    const uint32_t* A = anchors + (long long)f * acap;
+    const long long w0 = (long long)f * 2 * acap;
+    const int na = nanchor[f];
+    for (int i = lane; i < nb; i += 64) bits[i] = 0;
+    if (lane == 0) {
+      fS[0] = 0;
+      sS[0] = 0;
+    }
+    uint32_t b1 = 0, b2 = 0;
+    int ne = 0, w = 0;
+    bool fail = na > acap;
+    for (int a0 = 0; a0 < na && !fail; a0 += 64) {
+      const int a = a0 + lane;
+      const uint32_t ap = a < na ? A[a] : 0u;
+      const int aidx = (int)(ap >> 16) * W + (int)(ap & 0xffffu);
+      // both parts' lengths and continuation words of this lane's anchor, loaded ahead
+      const uint32_t l1 = a < na ? pl[w0 + 2 * a] : 0u, l2 = a < na ? pl[w0 + 2 * a + 1] : 0u;
+      const uint32_t e1 = a < na ? pe[w0 + 2 * a] : 0u, e2 = a < na ? pe[w0 + 2 * a + 1] : 0u;
+      // lane's pixel of the first round of both parts of walk pair k (anchor a0 + k)
+      auto first = [&](int k, uint32_t& q1, uint32_t& q2) {
+        const long long wk = w0 + 2 * (a0 + k);
+        const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k) & 0x7fffffffu;
+        const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k) & 0x7fffffffu;
+        q1 = (uint32_t)lane < n1 ? ps[wk * LS_CAP + lane] : 0u;
+        q2 = (uint32_t)lane < n2 ? ps[(wk + 1) * LS_CAP + lane] : 0u;
+      };
+      uint64_t pend = ballot(a < na) & ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
+      int k = pend ? __builtin_ctzll(pend) : -1;
+      uint32_t c1 = 0, c2 = 0;
+      if (k >= 0) first(k, c1, c2);
+      while (k >= 0) {
+        pend &= pend - 1;
+        const int kn = pend ? __builtin_ctzll(pend) : -1;  // the next pending anchor as things stand
+        uint32_t n1 = 0, n2 = 0;
+        if (kn >= 0) first(kn, n1, n2);
+        if (ne > ecap) {  // offPS > maxNumOfEdge
+          fail = true;
+          break;
+        }
+        const long long wk = w0 + 2 * (a0 + k);
+        uint32_t o1 = b1, o2 = b2;
+        if (!ls_part(M, W, MP, H, bits, T, ps + wk * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l1, k),
+                     (uint32_t)__builtin_amdgcn_readlane((int)e1, k), c1, P1, 0u, o1, (uint32_t)pcap, R, w)) {
+          fail = true;
+          break;
+        }
+        const int idx = __builtin_amdgcn_readlane(aidx, k);
+        if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));  // the second part walks the anchor again
+        LS_FENCE();
+        if (!ls_part(M, W, MP, H, bits, T, ps + (wk + 1) * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l2, k),
+                     (uint32_t)__builtin_amdgcn_readlane((int)e2, k), c2, P2, 1u, o2, (uint32_t)pcap, R, w)) {
+          fail = true;
+          break;
+        }
+        if ((int)((o1 - b1) + (o2 - b2)) >= LN_MIN_LEN + 1) {  // else a short edge: dropped, its pixels stay marked
+          b1 = o1;
+          b2 = o2;
+          ne++;
+          if (ne <= ecap + 1 && lane == 0) {
+            fS[ne] = b1;
+            sS[ne] = b2;
+          }
+        }
+        pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);  // anchors this walk marked: skipped
+        k = pend ? __builtin_ctzll(pend) : -1;
+        if (k >= 0 && k == kn) {
+          c1 = n1;
+          c2 = n2;
+        } else if (k >= 0) {
+          first(k, c1, c2);
+        }
+      }
+    }
+    if (ne > ecap) fail = true;
+    if (lane == 0) {
+      s_ne = fail ? -1 : ne;
+      __hip_atomic_store(&s_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  } else {
+    // the writer: ring records to P1 / P2 until the merge is done and the ring drained
+    int r = 0;
     while (true) {
-      pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
-      if (!pend) break;
-      const int k = __builtin_ctzll(pend);
-      pend &= pend - 1;
-      if (ne > ecap) {
-        fail = true;
+      const int d = __hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int w = __hip_atomic_load(&s_w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (r < w) {
+        for (int i = r + lane; i < w; i += 64) {
+          const uint2 e = R.r[i & (LS_RING - 1)];
+          ((e.x >> 31) ? P2 : P1)[e.x & 0x7fffffffu] = e.y;
+        }
+        r = w;
+        LS_FENCE();
+        if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (d) {
         break;
-      }
-      const long long wk = w0 + 2 * (a0 + k);
-      uint32_t o1 = b1, o2 = b2;
-      if (!ls_part(M, W, MP, H, bits, T, ps + wk * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l1, k),
-                   (uint32_t)__builtin_amdgcn_readlane((int)e1, k), P1, o1, (uint32_t)pcap)) {
-        fail = true;
-        break;
-      }
-      const int idx = __builtin_amdgcn_readlane(aidx, k);
-      if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));  // the second part walks the anchor again
-      LS_FENCE();
-      if (!ls_part(M, W, MP, H, bits, T, ps + (wk + 1) * LS_CAP, (uint32_t)__builtin_amdgcn_readlane((int)l2, k),
-                   (uint32_t)__builtin_amdgcn_readlane((int)e2, k), P2, o2, (uint32_t)pcap)) {
-        fail = true;
-        break;
-      }
-      if ((int)((o1 - b1) + (o2 - b2)) < LN_MIN_LEN + 1) continue;  // short edge: dropped, its pixels stay marked
-      b1 = o1;
-      b2 = o2;
-      ne++;
-      if (ne <= ecap + 1 && lane == 0) {
-        fS[ne] = b1;
-        sS[ne] = b2;
+      } else {
+        __builtin_amdgcn_s_sleep(2);
       }
     }
   }
-  if (ne > ecap) fail = true;
-  if (fail) {
-    if (lane == 0) nedge[f] = -1;
+  __syncthreads();  // the records in P1 / P2 (both waves' stores), fS / sS visible
+  const int ne = s_ne;
+  if (ne < 0) {
+    if (threadIdx.x == 0) nedge[f] = -1;
     return;
   }
-  __syncthreads();
+  const int t0 = threadIdx.x, nt = blockDim.x;
   uint32_t* Q = chains + (long long)f * 2 * pcap;
   uint32_t* S = sid + (long long)f * (ecap + 1);
-  for (int e = lane; e <= ne; e += 64) S[e] = fS[e] + sS[e] - (uint32_t)e;
+  for (int e = t0; e <= ne; e += nt) S[e] = fS[e] + sS[e] - (uint32_t)e;
   const uint32_t c1 = fS[ne], c2 = sS[ne];
   int e = 0;
-  for (uint32_t t = lane; t < c1; t += 64) {  // part 1 of chain e, reversed
+  for (uint32_t t = t0; t < c1; t += nt) {  // part 1 of chain e, reversed
     while (fS[e + 1] <= t) e++;
     Q[fS[e] + sS[e] - (uint32_t)e + fS[e + 1] - 1 - t] = P1[t];
   }
   e = 0;
-  for (uint32_t t = lane; t < c2; t += 64) {  // part 2 without its first pixel (the anchor)
+  for (uint32_t t = t0; t < c2; t += nt) {  // part 2 without its first pixel (the anchor)
     while (sS[e + 1] <= t) e++;
     if (t > sS[e]) Q[fS[e + 1] + t - (uint32_t)e - 1] = P2[t];
   }
-  if (lane == 0) nedge[f] = ne;
+  if (threadIdx.x == 0) nedge[f] = ne;
 }
 
 // ---------------------------------------------------------------- EDline
@@ -1399,7 +1472,7 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
                        e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
                      e.d_anch, e.acap, e.d_nanch);
-  if (nframes == 1 && e.spec) {
+  if (nframes == 1 && e.spec && edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING <= kLdsMax - 64) {
     // the latency path: every anchor's two walks in parallel, the in-order merge on one wave, EDline
     // a wave per chain, the placement (k_walk_spec .. k_lines_place)
     if (!e.d_ps) {
@@ -1410,7 +1483,8 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
     }
     hipLaunchKernelGGL(k_walk_spec, dim3(4096, 1), dim3(64), sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP, s,
                        e.d_moves, e.d_code, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe);
-    hipLaunchKernelGGL(k_walk_merge, dim3(1), dim3(64), edge_draw_lds(W, H, e.ecap, e.gstarts), s, e.d_moves, W, H,
+    hipLaunchKernelGGL(k_walk_merge, dim3(1), dim3(128), edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING, s,
+                       e.d_moves, W, H,
                        e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1, e.d_p2, e.pcap, e.d_chain,
                        e.d_sid, e.ecap, e.d_nedge, e.d_starts);
     hipLaunchKernelGGL(k_edlines_par, dim3(1024, 1), dim3(64), 0, s, e.d_code, e.d_dx, e.d_dy, W, H, e.d_chain,

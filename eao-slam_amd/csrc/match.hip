@@ -302,6 +302,119 @@ __global__ __launch_bounds__(256) void k_motion_cand(
   }
 }
 
+// k_motion_cand with one wave per query (the latency form, few pairs: a single-call search has
+// ~1000 queries, 4 workgroups of the thread-per-query form): the lanes share the query's window
+// cells, each keeps its MK smallest keys, and the wave merges them by MK wave minima (keys are
+// unique: the index is in them). Same outputs as k_motion_cand.
+__global__ __launch_bounds__(256) void k_motion_cand_wave(
+    CamDev cam, const float* __restrict__ Tcw, float th, const eao_keypoint_dev* __restrict__ kps,
+    const uint8_t* __restrict__ desc, const int* __restrict__ counts, int cap,
+    const uint8_t* __restrict__ has_mp, const float* __restrict__ mp_pos, const uint8_t* __restrict__ mp_desc,
+    const float* __restrict__ scales, const int* __restrict__ gstart, const int* __restrict__ gitems,
+    unsigned long long* __restrict__ ckeys, signed char* __restrict__ cbins, int* __restrict__ ccnt) {
+  const int p = blockIdx.y, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ls = p, cs = p + 1;
+  if (i >= counts[ls]) return;  // the whole wave
+  const eao_keypoint_dev* LK = kps + (long long)ls * cap;
+  const eao_keypoint_dev* CK = kps + (long long)cs * cap;
+  const uint8_t* CD = desc + (long long)cs * cap * 32;
+  const int* GS = gstart + (long long)cs * (GRID_CELLS + 1);
+  const int* GI = gitems + (long long)cs * cap;
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
+  const long long qi = (long long)p * cap + i;
+  const MotionGeom g = motion_geom(cam, T, th, LK, has_mp + (long long)ls * cap, mp_pos + (long long)ls * cap * 3,
+                                   scales, i);
+  int n = 0;
+  unsigned long long best[MK];
+#pragma unroll
+  for (int k = 0; k < MK; k++) best[k] = KEY_NONE;
+  if (g.ok) {
+    const Window w = window_cells(cam, g.u, g.v, g.r);
+    if (!w.empty) {
+      const int minL = g.oct - 1, maxL = g.oct + 1;
+      const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+      const uint4* pd = (const uint4*)(mp_desc + ((long long)ls * cap + i) * 32);
+      const uint4 d0 = pd[0], d1 = pd[1];
+      for (int ck = lane; ck < ncell; ck += 64) {
+        const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+        for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+          const int i2 = GI[q];
+          const eao_keypoint_dev& kp = CK[i2];
+          if (kp.octave < minL || kp.octave > maxL) continue;
+          if (!(fabsf(fsub(kp.x, g.u)) < g.r && fabsf(fsub(kp.y, g.v)) < g.r)) continue;
+          const uint4* pc = (const uint4*)(CD + 32 * (long long)i2);
+          const uint4 c0 = pc[0], c1 = pc[1];
+          const int dist = __popc(d0.x ^ c0.x) + __popc(d0.y ^ c0.y) + __popc(d0.z ^ c0.z) + __popc(d0.w ^ c0.w) +
+                           __popc(d1.x ^ c1.x) + __popc(d1.y ^ c1.y) + __popc(d1.z ^ c1.z) + __popc(d1.w ^ c1.w);
+          if (dist > TH_HIGH) continue;
+          n++;
+          unsigned long long key = make_key(dist, ck, i2);
+#pragma unroll
+          for (int k = 0; k < MK; k++) {  // sorted insertion, smallest first
+            const unsigned long long lo = key < best[k] ? key : best[k];
+            key = key < best[k] ? best[k] : key;
+            best[k] = lo;
+          }
+        }
+      }
+    }
+  }
+  n = wave_sum(n);
+  const int nk = min(n, MK);
+  for (int k = 0; k < nk; k++) {  // the wave's k-th smallest: its holder pops it
+    const unsigned long long m = wave_min_u64(best[0]);
+    if (best[0] == m) {
+#pragma unroll
+      for (int j = 0; j < MK - 1; j++) best[j] = best[j + 1];
+      best[MK - 1] = KEY_NONE;
+    }
+    if (lane == 0) {
+      ckeys[qi * MK + k] = m;
+      cbins[qi * MK + k] = (signed char)rot_bin(LK[i].angle, CK[key_idx(m)].angle);
+    }
+  }
+  if (lane == 0) ccnt[qi] = n;
+}
+
+// the full window scan of query i against the untaken current keypoints (its stored candidates are
+// all taken and it has more): the whole wave, the smallest (distance, window order, index) key
+__device__ __forceinline__ void motion_rescan(const CamDev& cam, const float* __restrict__ Tcw, float th,
+                                              const eao_keypoint_dev* LK, const eao_keypoint_dev* CK,
+                                              const uint8_t* CD, const int* GS, const int* GI,
+                                              const uint8_t* __restrict__ has_mp, const float* __restrict__ mp_pos,
+                                              const uint8_t* __restrict__ mp_desc, const float* __restrict__ scales,
+                                              const int* match, int ls, int cs, int cap, int i, int& i2, int& bin) {
+  const int lane = threadIdx.x & 63;
+  float T[16];
+  for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
+  const MotionGeom g = motion_geom(cam, T, th, LK, has_mp + (long long)ls * cap, mp_pos + (long long)ls * cap * 3,
+                                   scales, i);
+  const Window w = window_cells(cam, g.u, g.v, g.r);
+  const int minL = g.oct - 1, maxL = g.oct + 1;
+  const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
+  const uint8_t* d = mp_desc + ((long long)ls * cap + i) * 32;
+  unsigned long long best = KEY_NONE;
+  for (int ck = lane; ck < ncell; ck += 64) {
+    const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
+    for (int q = GS[cell]; q < GS[cell + 1]; q++) {
+      const int c2 = GI[q];
+      const eao_keypoint_dev& kp = CK[c2];
+      if (kp.octave < minL || kp.octave > maxL) continue;
+      if (!(fabsf(fsub(kp.x, g.u)) < g.r && fabsf(fsub(kp.y, g.v)) < g.r)) continue;
+      if (match[c2] >= 0) continue;
+      const unsigned long long k2 = make_key(hamming256(d, CD + 32 * (long long)c2), ck, c2);
+      best = k2 < best ? k2 : best;
+    }
+  }
+  best = wave_min_u64(best);
+  if (best != KEY_NONE && key_dist(best) <= TH_HIGH) {
+    i2 = key_idx(best);
+    bin = rot_bin(LK[i].angle, CK[i2].angle);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_motion_resolve(
     CamDev cam, const float* __restrict__ Tcw, float th, int check_ori, const eao_keypoint_dev* __restrict__ kps,
     const uint8_t* __restrict__ desc, const int* __restrict__ counts, int cap, const uint8_t* __restrict__ has_mp,
@@ -315,6 +428,7 @@ __global__ __launch_bounds__(64) void k_motion_resolve(
   __shared__ unsigned long long kb[64 * MK];
   __shared__ signed char bb[64 * MK];
   __shared__ int nb[64];
+  __shared__ int claim[MAXK];  // the lowest lane proposing a current keypoint in a round (64: none)
   const int p = blockIdx.x, lane = threadIdx.x;
   const int ls = p, cs = p + 1;
   const int n_last = counts[ls], n_cur = counts[cs];
@@ -326,6 +440,7 @@ __global__ __launch_bounds__(64) void k_motion_resolve(
   for (int i = lane; i < n_cur; i += 64) {
     match[i] = -1;
     bins[i] = -1;
+    claim[i] = 64;
   }
   int nmatches = 0;
   for (int base = 0; base < n_last; base += 64) {
@@ -342,57 +457,56 @@ __global__ __launch_bounds__(64) void k_motion_resolve(
       }
     }
     __syncthreads();
-    for (int j = 0; j < nq; j++) {
-      const int n = __builtin_amdgcn_readlane(myn, j);
-      if (n == 0) continue;
-      const int nk = min(n, MK);
-      const unsigned long long key = lane < nk ? kb[j * MK + lane] : KEY_NONE;
-      const bool free_ = lane < nk && match[key_idx(key)] < 0;
-      const uint64_t fm = ballot(free_);
-      int i2 = -1, bin = -1;
-      if (fm) {
-        const int c = __builtin_ctzll(fm);
-        i2 = __builtin_amdgcn_readlane(key_idx(key), c);
-        bin = bb[j * MK + c];
-      } else if (n > MK) {
-        // every stored candidate is taken: the full window scan (as the reference)
-        const int i = base + j;
-        float T[16];
-        for (int k = 0; k < 16; k++) T[k] = Tcw[cs * 16 + k];
-        const MotionGeom g = motion_geom(cam, T, th, LK, has_mp + (long long)ls * cap,
-                                         mp_pos + (long long)ls * cap * 3, scales, i);
-        const Window w = window_cells(cam, g.u, g.v, g.r);
-        const int minL = g.oct - 1, maxL = g.oct + 1;
-        const int ncy = w.y1 - w.y0 + 1, ncell = (w.x1 - w.x0 + 1) * ncy;
-        const uint8_t* d = mp_desc + ((long long)ls * cap + i) * 32;
-        unsigned long long best = KEY_NONE;
-        for (int ck = lane; ck < ncell; ck += 64) {
-          const int cell = (w.x0 + ck / ncy) * GRID_ROWS + w.y0 + ck % ncy;
-          for (int q = GS[cell]; q < GS[cell + 1]; q++) {
-            const int c2 = GI[q];
-            const eao_keypoint_dev& kp = CK[c2];
-            if (kp.octave < minL || kp.octave > maxL) continue;
-            if (!(fabsf(fsub(kp.x, g.u)) < g.r && fabsf(fsub(kp.y, g.v)) < g.r)) continue;
-            if (match[c2] >= 0) continue;
-            const unsigned long long k2 = make_key(hamming256(d, CD + 32 * (long long)c2), ck, c2);
-            best = k2 < best ? k2 : best;
-          }
-        }
-        best = wave_min_u64(best);
-        if (best != KEY_NONE && key_dist(best) <= TH_HIGH) {
-          i2 = key_idx(best);
-          bin = rot_bin(LK[i].angle, CK[i2].angle);
-        }
+    // The block's queries in rounds (the first-wins order kept): every undone lane proposes its
+    // first stored candidate not yet taken; the lanes commit up to the first one whose proposal an
+    // earlier undone lane of the round also makes (claims by LDS atomicMin: that lane re-proposes
+    // next round, after its predecessors are in) or that needs the window rescan (run right after
+    // the commit, by the whole wave). A committed lane's proposal is the sequential walk's choice:
+    // its skipped candidates were taken before the round, and no earlier lane of the round takes it.
+    const int nk = min(myn, MK);
+    int pos = 0;
+    bool done = lane >= nq || myn == 0;
+    while (true) {
+      if (!ballot(!done)) break;
+      int c = -1;
+      bool resc = false;
+      if (!done) {
+        while (pos < nk && match[key_idx(kb[lane * MK + pos])] >= 0) pos++;
+        if (pos < nk)
+          c = key_idx(kb[lane * MK + pos]);
+        else
+          resc = myn > MK;  // every stored candidate taken and more exist: the rescan
       }
-      if (i2 >= 0) {
-        if (lane == 0) {
-          match[i2] = base + j;
-          bins[i2] = (signed char)bin;
+      if (c >= 0) atomicMin(&claim[c], lane);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      const bool conflict = c >= 0 && claim[c] != lane;
+      const uint64_t stop = ballot(!done && (conflict || resc));
+      const int f = stop ? __builtin_ctzll(stop) : 64;
+      if (c >= 0 && !conflict) claim[c] = 64;  // the claim's owner resets it (after every lane read it)
+      const bool commit = !done && lane < f;
+      if (commit && c >= 0) {
+        match[c] = base + lane;
+        bins[c] = bb[lane * MK + pos];
+      }
+      nmatches += popc64(ballot(commit && c >= 0));
+      done = done || commit;
+      if (f < 64 && __builtin_amdgcn_readlane((int)resc, f)) {
+        __syncthreads();  // the commits visible to every lane of the rescan
+        int i2 = -1, bin = -1;
+        motion_rescan(cam, Tcw, th, LK, CK, CD, GS, GI, has_mp, mp_pos, mp_desc, scales, match, ls, cs, cap,
+                      base + f, i2, bin);
+        if (i2 >= 0) {
+          if (lane == 0) {
+            match[i2] = base + f;
+            bins[i2] = (signed char)bin;
+          }
+          nmatches++;
         }
-        nmatches++;
+        if (lane == f) done = true;
       }
       __syncthreads();
     }
+    __syncthreads();
   }
   if (check_ori) {
     for (int b = lane; b < HISTO_LENGTH; b += 64) hist[b] = 0;
@@ -1127,8 +1241,12 @@ int MatchEngine::motion(const CamDev& cd, const float* d_T, float th, int check_
     set_error("motion search: scratch too small");
     return EAO_E_CAPACITY;
   }
-  hipLaunchKernelGGL(k_motion_cand, dim3((cap + 255) / 256, np), dim3(256), 0, s, cd, d_T, th, d_kps, d_desc,
-                     d_counts, cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt);
+  if (np <= 4)  // latency form: a wave per query (a single call's ~1000 queries fill the chip)
+    hipLaunchKernelGGL(k_motion_cand_wave, dim3((cap + 3) / 4, np), dim3(256), 0, s, cd, d_T, th, d_kps, d_desc,
+                       d_counts, cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt);
+  else
+    hipLaunchKernelGGL(k_motion_cand, dim3((cap + 255) / 256, np), dim3(256), 0, s, cd, d_T, th, d_kps, d_desc,
+                       d_counts, cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt);
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_motion_resolve, dim3(np), dim3(64), 0, s, cd, d_T, th, check_ori, d_kps, d_desc, d_counts,
                      cap, d_has, d_pos, d_mdesc_, d_sc, d_gstart, d_gitems, d_ckeys, d_cbins, d_ccnt, d_match, d_nm);

@@ -53,4 +53,32 @@ s2() {
   timeout -k 10 300 python -u bench.py > gpurun_out/r5_s2_bench.log 2>&1
 }
 
+# s3: association timeline on this build, single-call extract / motion split, pyramid traffic
+s3() {
+  bash tools/gpu/timeline.sh &&
+  timeout -k 10 200 python -u tools/micro/dropin_single.py 64 > gpurun_out/r5_s3_dropin.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s3_dropin_kt -o run -- python3 tools/micro/dropin_single.py 32 > gpurun_out/r5_s3_dropin_kt.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s3_lsingle_kt -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_s3_lsingle_kt.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/r5_s3_pmc_fetch -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_s3_pmc_fetch.log 2>&1 &&
+  timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/r5_s3_pmc_write -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_s3_pmc_write.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s3_orb_kt -o run -- python3 tools/pmc_extract.py > gpurun_out/r5_s3_orb_kt.log 2>&1
+}
+
+# s4: merge look-ahead loads, motion search in rounds + wave-per-query candidates: parity, single-call split, bench
+s4() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_match.py tests/test_gpu_lines.py tests/test_gpu_chain.py tests/test_gpu_fr3.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_s4_tests.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/dropin_single.py 64 > gpurun_out/r5_s4_single.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/lines_single.py 64 --check >> gpurun_out/r5_s4_single.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s4_dropin_kt -o run -- python3 tools/micro/dropin_single.py 32 > gpurun_out/r5_s4_dropin_kt.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s4_lsingle_kt -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_s4_lsingle_kt.log 2>&1 &&
+  timeout -k 10 300 python -u bench.py > gpurun_out/r5_s4_bench.log 2>&1
+}
+
+# s5: merge with the writer wave: line parity, single-frame time and split
+s5() {
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_lines.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_s5_tests.log 2>&1 &&
+  timeout -k 10 200 python -u tools/micro/lines_single.py 64 --check > gpurun_out/r5_s5_single.log 2>&1 &&
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s5_lsingle_kt -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_s5_lsingle_kt.log 2>&1
+}
+
 "$@"
