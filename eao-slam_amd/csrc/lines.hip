@@ -948,12 +948,13 @@ __device__ __forceinline__ void solve2(const float* ata, const float* atv, doubl
 
 // EDline on one chain (:2380-2906): Q[s0, end) -> the chain's kept lines as records of 6
 // words at L[s0 + 6 k] (L[s0, end) is the chain's own scratch), their count in CNT[e]; one wave
-__device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* __restrict__ Q, uint32_t* __restrict__ L,
-                               const uint16_t* __restrict__ C, const int16_t* __restrict__ DX,
-                               const int16_t* __restrict__ DY, int W, int H, double logNT, float min_length,
-                               int* __restrict__ CNT) {
+// HZ (optional): the chain's Horizontal flags by position, for a chain staged with them (k_edlines_par)
+__device__ int ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* __restrict__ Q, uint32_t* __restrict__ L,
+                              const uint16_t* __restrict__ C, const int16_t* __restrict__ DX,
+                              const int16_t* __restrict__ DY, int W, int H, double logNT, float min_length,
+                              int* __restrict__ CNT, const uint8_t* __restrict__ HZ = nullptr) {
   const int lane = lane_id();
-  auto horiz_at = [&](uint32_t p) { return (C[px_y(p) * W + px_x(p)] & LN_HORIZ) != 0; };
+  auto horiz_at = [&](uint32_t i) { return HZ ? HZ[i] != 0 : (C[px_y(Q[i]) * W + px_x(Q[i])] & LN_HORIZ) != 0; };
   uint32_t s = s0;
   uint32_t offL = s;
   int nl = 0;
@@ -962,7 +963,7 @@ __device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t*
   while (end > s + LN_MIN_LEN) {
     double fitErr = 0;
     while (end > s + LN_MIN_LEN) {
-      const bool h0 = horiz_at(Q[s]);
+      const bool h0 = horiz_at(s);
       fit_block(Q, s, s + LN_MIN_LEN, h0, ata, atv);
       solve2(ata, atv, le2);
       double c2 = 0;  // fit error in the reference's order: one lane, sequential
@@ -978,7 +979,7 @@ __device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t*
     }
     if (fitErr > LN_FIT_ERR) break;
     const uint32_t lineStart = offL;
-    const bool horiz = horiz_at(Q[s]);
+    const bool horiz = horiz_at(s);
     double coef1 = 0;
     bool extended = true, first = true;
     int tryTimes = 0, outliers = 0;
@@ -1126,6 +1127,7 @@ __device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t*
     }
   }
   if (lane == 0) CNT[e] = nl;
+  return nl;
 }
 
 // the chains' lines in chain order: a block scan of the per-chain counts; a chain's thread
@@ -1194,23 +1196,44 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
 }
 
 // the latency path's EDline: one wave per chain over the whole chip (chains are independent), then
-// the placement in chain order by one workgroup per frame
+// the placement in chain order by one workgroup per frame. A chain of <= LN_LQ pixels is staged in
+// LDS with its Horizontal flags (the fit loop's many passes over it then read LDS, not global
+// memory), its scratch too; its line records are copied out to L afterwards.
+constexpr int LN_LQ = 3072;
 __global__ __launch_bounds__(64) void k_edlines_par(const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi,
                                                    const int16_t* __restrict__ dyi, int W, int H,
                                                    const uint32_t* __restrict__ chains, const uint32_t* __restrict__ sid,
                                                    const int* __restrict__ nedge, int pcap, int ecap,
                                                    uint32_t* __restrict__ lscratch, uint32_t* __restrict__ ccount,
                                                    float min_length) {
-  const int f = blockIdx.y;
+  __shared__ uint32_t qs[LN_LQ], ls[LN_LQ];
+  __shared__ uint8_t hz[LN_LQ];
+  const int f = blockIdx.y, lane = threadIdx.x;
   const int ne = nedge[f];
   const long long fo = (long long)f * W * H;
   const uint32_t* Q = chains + (long long)f * 2 * pcap;
   const uint32_t* S = sid + (long long)f * (ecap + 1);
   uint32_t* L = lscratch + (long long)f * 2 * pcap;
   int* CNT = (int*)(ccount + (long long)f * (ecap + 1));
+  const uint16_t* C = code + fo;
   const double logNT = 2.0 * (log10((double)W) + log10((double)H));
-  for (int e = blockIdx.x; e < ne; e += gridDim.x)
-    ed_chain_lines(e, S[e], S[e + 1], Q, L, code + fo, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
+  for (int e = blockIdx.x; e < ne; e += gridDim.x) {
+    const uint32_t s0 = S[e], s1 = S[e + 1], n = s1 - s0;
+    if (n > (uint32_t)LN_LQ) {
+      ed_chain_lines(e, s0, s1, Q, L, C, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
+      continue;
+    }
+    for (uint32_t i = lane; i < n; i += 64) {
+      const uint32_t p = Q[s0 + i];
+      qs[i] = p;
+      hz[i] = (C[px_y(p) * W + px_x(p)] & LN_HORIZ) != 0;
+    }
+    __syncthreads();
+    const int nl = ed_chain_lines(e, 0, n, qs, ls, C, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT, hz);
+    __syncthreads();
+    for (int i = lane; i < 6 * nl; i += 64) L[s0 + i] = ls[i];
+    __syncthreads();
+  }
 }
 __global__ __launch_bounds__(256) void k_lines_place(const uint32_t* __restrict__ sid, const int* __restrict__ nedge,
                                                      int pcap, int ecap, const uint32_t* __restrict__ lscratch,
