@@ -677,6 +677,7 @@ constexpr int LS_RING = 2048;  // records: (part << 31 | index into P1 / P2, pix
 struct LsRing {
   uint2* r;
   int *wpos, *rpos;
+  int rseen;  // the writer's position as last read (re-read only when the ring may be full)
 };
 
 // Phase 2, one part of an anchor's chain: the prefix of walk wi not yet marked, recorded at
@@ -700,8 +701,10 @@ __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, i
     const uint64_t mk = ballot(marked);
     const uint32_t take = mk ? (uint32_t)__builtin_ctzll(mk) : min(64u, len - c0);  // pixels recorded this round
     if (take > cap - off) return false;  // the arrays fill before the walk stops
-    while (w + 64 - __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) > LS_RING)
-      __builtin_amdgcn_s_sleep(1);  // the ring is full: the writer is behind
+    while (w + 64 - R.rseen > LS_RING) {  // the ring may be full: look where the writer is
+      R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (w + 64 - R.rseen > LS_RING) __builtin_amdgcn_s_sleep(1);
+    }
     if ((uint32_t)lane < take) {
       atomicOr(&bits[idx >> 5], 1u << (idx & 31));
       R.r[(w + lane) & (LS_RING - 1)] = make_uint2(part << 31 | (off + lane), p);
@@ -738,7 +741,7 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
   uint32_t* fS = gstarts ? gstarts + (long long)f * 2 * ep : bits + nbp;
   uint32_t* sS = fS + ep;
   uint16_t* tile = (uint16_t*)(bits + nbp + (gstarts ? 0 : 2 * ep));
-  LsRing R{(uint2*)(tile + LE_TW * LE_TH), &s_w, &s_r};
+  LsRing R{(uint2*)(tile + LE_TW * LE_TH), &s_w, &s_r, 0};
   uint32_t* P1 = p1 + (long long)f * pcap;
   uint32_t* P2 = p2 + (long long)f * pcap;
   if (threadIdx.x == 0) s_w = s_r = s_done = 0;

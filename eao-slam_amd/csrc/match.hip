@@ -1331,7 +1331,8 @@ int eao_match_motion(eao_matcher* m, const eao_camera* cam, const float* Tcw, fl
   hipStream_t s = e.stream;
   // slot stride C (the kernels take it as cap): the two frames' inputs packed into the pinned
   // staging image, one copy over; the current frame's matches and the counts come back in one
-  const int C = (std::max(std::max(n_last, n_cur), 1) + 63) & ~63;
+  // (C <= max_kps: the grid items, candidate keys and results are sized [2][max_kps])
+  const int C = std::min((std::max(std::max(n_last, n_cur), 1) + 63) & ~63, K);
   const int counts[4] = {n_last, n_cur, 0, 0};
   float T2[32];
   for (int k = 0; k < 16; k++) T2[k] = T2[16 + k] = Tcw[k];

@@ -39,6 +39,21 @@ def test_motion_exact(frames, th, ori):
     assert no > 50  # the synthetic stream is trackable
 
 
+def test_motion_single_call_full_capacity(frames):
+    """A single call packs both frames with a slot stride of their keypoint count rounded up to 64,
+    clamped to the matcher's max_kps: a matcher whose max_kps is no multiple of 64, called with
+    frames that fill it (the round-up alone would overrun the [2][max_kps] candidate, grid and
+    result buffers) and with frames of different sizes, matches the oracle."""
+    k0, d0, k1, d1, has, pos, T = _scene(frames, 0, 1)
+    n = min(len(k0), len(k1))
+    cap = n - 3 if (n - 3) % 64 else n - 4  # no multiple of 64
+    for a, b in ((cap, cap), (cap, cap - 100), (cap - 200, cap)):
+        m = ea.Matcher(max_kps=cap, max_batch=2)
+        ng, mg = m.motion(ea.camera(), T, 15, 1, k0[:a], has[:a], pos[:a], d0[:a], k1[:b], d1[:b], SC)
+        no, mo = orc.match_motion(orc.cam(), T, 15, 1, k0[:a], has[:a], pos[:a], d0[:a], k1[:b], d1[:b], SC)
+        assert ng == no and np.array_equal(mg, mo), (a, b)
+
+
 def test_motion_perturbed_descriptors(frames):
     # flip bits so distances tie and exceed TH_HIGH: exercises first-wins ties
     k0, d0, k1, d1, has, pos, T = _scene(frames, 0, 2, seed=3)
