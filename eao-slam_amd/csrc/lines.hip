@@ -29,6 +29,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../../include/eao_accel.h"
@@ -584,6 +585,8 @@ __global__ __launch_bounds__(64) void k_edge_draw(const uint16_t* __restrict__ m
 // at a time against the LDS edge bitmap (a ballot of the marked ones; the pixels before the first
 // are marked and recorded in one round), and continues a path cut at LS_CAP with the sequential
 // ed_walk from its stored position and state.
+__device__ __forceinline__ uint32_t px_x(uint32_t p) { return p & 0xffffu; }
+__device__ __forceinline__ uint32_t px_y(uint32_t p) { return p >> 16; }
 constexpr int LS_CAP = 256;          // pixels stored per speculative walk
 #define LS_FENCE() __asm__ volatile("" ::: "memory")  // compiler order of one wave's LDS accesses
 constexpr uint16_t LS_SEEN = 0xFFFF;  // a tile word no pixel has (nibble 15 never occurs): visited
@@ -732,7 +735,7 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
                                                     const uint32_t* __restrict__ pe, uint32_t* __restrict__ p1,
                                                     uint32_t* __restrict__ p2, int pcap, uint32_t* __restrict__ chains,
                                                     uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
-                                                    uint32_t* __restrict__ gstarts) {
+                                                    uint32_t* __restrict__ gstarts, int* __restrict__ diag) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_ed[];
   __shared__ int s_w, s_r, s_done, s_ne;
   const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -836,7 +839,10 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
       if (r < w) {
         for (int i = r + lane; i < w; i += 64) {
           const uint2 e = R.r[i & (LS_RING - 1)];
-          ((e.x >> 31) ? P2 : P1)[e.x & 0x7fffffffu] = e.y;
+          if (diag && ((e.x & 0x7fffffffu) >= (uint32_t)pcap || px_x(e.y) >= (uint32_t)W || px_y(e.y) >= (uint32_t)H))
+            atomicOr(diag, 1);  // a record out of range (checking mode: not stored)
+          else
+            ((e.x >> 31) ? P2 : P1)[e.x & 0x7fffffffu] = e.y;
         }
         r = w;
         LS_FENCE();
@@ -859,6 +865,11 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
   uint32_t* S = sid + (long long)f * (ecap + 1);
   for (int e = t0; e <= ne; e += nt) S[e] = fS[e] + sS[e] - (uint32_t)e;
   const uint32_t c1 = fS[ne], c2 = sS[ne];
+  if (diag && threadIdx.x == 0) {  // checking mode: the chain starts in order and in range
+    bool bad = c1 > (uint32_t)pcap || c2 > (uint32_t)pcap;
+    for (int k = 0; k < ne && !bad; k++) bad = fS[k] > fS[k + 1] || sS[k] >= sS[k + 1];
+    if (bad) atomicOr(diag, 2);
+  }
   int e = 0;
   for (uint32_t t = t0; t < c1; t += nt) {  // part 1 of chain e, reversed
     while (fS[e + 1] <= t) e++;
@@ -917,8 +928,6 @@ __device__ double ln_nfa(int n, int k, double p, double logNT) {  // descriptor.
   return -log10(bin_tail) - logNT;
 }
 
-__device__ __forceinline__ uint32_t px_x(uint32_t p) { return p & 0xffffu; }
-__device__ __forceinline__ uint32_t px_y(uint32_t p) { return p >> 16; }
 
 // sums over pixels [s, e) of u = x (horiz) or y, v = the other: sum u^2, sum u, count,
 // sum u v, sum v -- integers, exact in double whatever the order; rounded to float once
@@ -951,13 +960,12 @@ __device__ __forceinline__ void solve2(const float* ata, const float* atv, doubl
 
 // EDline on one chain (:2380-2906): Q[s0, end) -> the chain's kept lines as records of 6
 // words at L[s0 + 6 k] (L[s0, end) is the chain's own scratch), their count in CNT[e]; one wave
-// HZ (optional): the chain's Horizontal flags by position, for a chain staged with them (k_edlines_par)
-__device__ int ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* __restrict__ Q, uint32_t* __restrict__ L,
-                              const uint16_t* __restrict__ C, const int16_t* __restrict__ DX,
-                              const int16_t* __restrict__ DY, int W, int H, double logNT, float min_length,
-                              int* __restrict__ CNT, const uint8_t* __restrict__ HZ = nullptr) {
+__device__ void ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* __restrict__ Q, uint32_t* __restrict__ L,
+                               const uint16_t* __restrict__ C, const int16_t* __restrict__ DX,
+                               const int16_t* __restrict__ DY, int W, int H, double logNT, float min_length,
+                               int* __restrict__ CNT) {
   const int lane = lane_id();
-  auto horiz_at = [&](uint32_t i) { return HZ ? HZ[i] != 0 : (C[px_y(Q[i]) * W + px_x(Q[i])] & LN_HORIZ) != 0; };
+  auto horiz_at = [&](uint32_t i) { return (C[px_y(Q[i]) * W + px_x(Q[i])] & LN_HORIZ) != 0; };
   uint32_t s = s0;
   uint32_t offL = s;
   int nl = 0;
@@ -1130,7 +1138,6 @@ __device__ int ed_chain_lines(int e, uint32_t s0, uint32_t end, const uint32_t* 
     }
   }
   if (lane == 0) CNT[e] = nl;
-  return nl;
 }
 
 // the chains' lines in chain order: a block scan of the per-chain counts; a chain's thread
@@ -1199,18 +1206,14 @@ __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __res
 }
 
 // the latency path's EDline: one wave per chain over the whole chip (chains are independent), then
-// the placement in chain order by one workgroup per frame. A chain of <= LN_LQ pixels is staged in
-// LDS with its Horizontal flags (the fit loop's many passes over it then read LDS, not global
-// memory), its scratch too; its line records are copied out to L afterwards.
-constexpr int LN_LQ = 3072;
+// the placement in chain order by one workgroup per frame. (Staging chains of <= 3072 pixels in LDS
+// gained nothing, 136 -> 139 us, and the build that did faulted intermittently: DESIGN.md section 9.)
 __global__ __launch_bounds__(64) void k_edlines_par(const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi,
                                                    const int16_t* __restrict__ dyi, int W, int H,
                                                    const uint32_t* __restrict__ chains, const uint32_t* __restrict__ sid,
                                                    const int* __restrict__ nedge, int pcap, int ecap,
                                                    uint32_t* __restrict__ lscratch, uint32_t* __restrict__ ccount,
-                                                   float min_length) {
-  __shared__ uint32_t qs[LN_LQ], ls[LN_LQ];
-  __shared__ uint8_t hz[LN_LQ];
+                                                   float min_length, int* __restrict__ diag) {
   const int f = blockIdx.y, lane = threadIdx.x;
   const int ne = nedge[f];
   const long long fo = (long long)f * W * H;
@@ -1218,24 +1221,22 @@ __global__ __launch_bounds__(64) void k_edlines_par(const uint16_t* __restrict__
   const uint32_t* S = sid + (long long)f * (ecap + 1);
   uint32_t* L = lscratch + (long long)f * 2 * pcap;
   int* CNT = (int*)(ccount + (long long)f * (ecap + 1));
-  const uint16_t* C = code + fo;
   const double logNT = 2.0 * (log10((double)W) + log10((double)H));
   for (int e = blockIdx.x; e < ne; e += gridDim.x) {
-    const uint32_t s0 = S[e], s1 = S[e + 1], n = s1 - s0;
-    if (n > (uint32_t)LN_LQ) {
-      ed_chain_lines(e, s0, s1, Q, L, C, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
-      continue;
+    const uint32_t s0 = S[e], s1 = S[e + 1];
+    if (diag) {  // checking mode: the chain in range, its pixels in the image (else skipped)
+      bool bad = s1 < s0 || s1 > 2u * (uint32_t)pcap;
+      for (uint32_t i = s0 + lane; i < s1 && !bad; i += 64) {
+        const uint32_t p = Q[i];
+        if (px_x(p) >= (uint32_t)W || px_y(p) >= (uint32_t)H) atomicOr(diag, 16);
+      }
+      if (bad) atomicOr(diag, 8);
+      if (bad || __hip_atomic_load(diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 24) {
+        if (lane == 0) CNT[e] = 0;
+        continue;
+      }
     }
-    for (uint32_t i = lane; i < n; i += 64) {
-      const uint32_t p = Q[s0 + i];
-      qs[i] = p;
-      hz[i] = (C[px_y(p) * W + px_x(p)] & LN_HORIZ) != 0;
-    }
-    __syncthreads();
-    const int nl = ed_chain_lines(e, 0, n, qs, ls, C, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT, hz);
-    __syncthreads();
-    for (int i = lane; i < 6 * nl; i += 64) L[s0 + i] = ls[i];
-    __syncthreads();
+    ed_chain_lines(e, s0, s1, Q, L, code + fo, dxi + fo, dyi + fo, W, H, logNT, min_length, CNT);
   }
 }
 __global__ __launch_bounds__(256) void k_lines_place(const uint32_t* __restrict__ sid, const int* __restrict__ nedge,
@@ -1352,7 +1353,7 @@ struct LineEngine {
   uint8_t* d_img = nullptr;  // [H][W * 4]: one host frame of up to 4 channels
   float* d_lines = nullptr;
   int* d_nlines = nullptr;
-  int* h_n = nullptr;  // pinned: the single-frame line count
+  int* h_n = nullptr;  // pinned: the single-frame line count (and, checking, the diagnostic word)
   HostStage stage_in, stage_out;  // single-frame staging: the pinned image in, count + lines back
   ~LineEngine() {
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
@@ -1396,6 +1397,11 @@ using namespace eao;
 struct eao_lines {
   LineEngine e;
 };
+
+static bool lines_check() {
+  static const bool on = [] { const char* v = getenv("EAO_LINES_CHECK"); return v && v[0] == '1'; }();
+  return on;
+}
 
 extern "C" {
 
@@ -1454,8 +1460,8 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
       hipMalloc(&e.d_nanch, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_nedge, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_img, (size_t)width * height * 4) != hipSuccess ||
-      hipMalloc(&e.d_lines, sizeof(float) * 6 * 4096) != hipSuccess || hipMalloc(&e.d_nlines, 4) != hipSuccess ||
-      hipHostMalloc((void**)&e.h_n, sizeof(int), 0) != hipSuccess) {
+      hipMalloc(&e.d_lines, sizeof(float) * 6 * 4096) != hipSuccess || hipMalloc(&e.d_nlines, 8) != hipSuccess ||
+      hipHostMalloc((void**)&e.h_n, 2 * sizeof(int), 0) != hipSuccess) {
     set_error("eao_lines_create: device allocation failed");
     return fail(EAO_E_HIP);
   }
@@ -1507,16 +1513,35 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
       EAO_HIP_CHECK(hipMalloc(&e.d_pl, nw * 4));
       EAO_HIP_CHECK(hipMalloc(&e.d_pe, nw * 4));
     }
+    // development switches: EAO_LINES_DEBUG_SYNC=1 checks every kernel of this path on its own;
+    // EAO_LINES_CHECK=1 range-checks the
+    // merge's records and the chains (a diagnostic word beside the count, eao_lines_detect_color)
+    static const bool dbg = [] { const char* v = getenv("EAO_LINES_DEBUG_SYNC"); return v && v[0] == '1'; }();
+    int* diag = lines_check() && d_counts == e.d_nlines ? e.d_nlines + 1 : nullptr;
+    if (diag) EAO_HIP_CHECK(hipMemsetAsync(diag, 0, 4, s));
+    auto dsync = [&](const char* k) -> int {
+      if (!dbg) return EAO_OK;
+      const hipError_t r = hipStreamSynchronize(s);
+      if (r != hipSuccess) {
+        set_error(std::string(k) + ": " + hipGetErrorString(r));
+        return EAO_E_HIP;
+      }
+      return EAO_OK;
+    };
     hipLaunchKernelGGL(k_walk_spec, dim3(4096, 1), dim3(64), sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP, s,
                        e.d_moves, e.d_code, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe);
+    if (int rc = dsync("k_walk_spec")) return rc;
     hipLaunchKernelGGL(k_walk_merge, dim3(1), dim3(128), edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING, s,
                        e.d_moves, W, H,
                        e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1, e.d_p2, e.pcap, e.d_chain,
-                       e.d_sid, e.ecap, e.d_nedge, e.d_starts);
+                       e.d_sid, e.ecap, e.d_nedge, e.d_starts, diag);
+    if (int rc = dsync("k_walk_merge")) return rc;
     hipLaunchKernelGGL(k_edlines_par, dim3(1024, 1), dim3(64), 0, s, e.d_code, e.d_dx, e.d_dy, W, H, e.d_chain,
-                       e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length);
+                       e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr, e.d_ccnt, min_length, diag);
+    if (int rc = dsync("k_edlines_par")) return rc;
     hipLaunchKernelGGL(k_lines_place, dim3(1), dim3(256), 0, s, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr,
                        e.d_ccnt, d_lines, d_counts, cap);
+    if (int rc = dsync("k_lines_place")) return rc;
   } else if (e.fused) {
     hipLaunchKernelGGL(k_edge_lines, dim3(nframes), dim3(64 * LE_WAVES), edge_draw_lds(W, H, e.ecap, e.gstarts), s,
                        e.d_moves, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_p1, e.d_p2, e.pcap, e.d_chain, e.d_sid,
@@ -1561,10 +1586,15 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
   if (rc) return rc;
   const size_t lb = sizeof(float) * 6 * (size_t)std::min(std::max(cap, 0), 4096);
   EAO_HIP_CHECK(e.stage_out.reserve(lb));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, 4, hipMemcpyDeviceToHost, s));
+  EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, lines_check() ? 8 : 4, hipMemcpyDeviceToHost, s));
   if (lb) EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_lines, lb, hipMemcpyDeviceToHost, s));
   EAO_HIP_CHECK(hipStreamSynchronize(s));
   const int n = *e.h_n;
+  if (lines_check() && e.h_n[1]) {
+    set_error("eao_lines_detect: checking mode found out-of-range records or chains (diag 0x" +
+              std::to_string(e.h_n[1]) + ": 1 merge record, 2 chain starts, 8 chain span, 16 chain pixel)");
+    return EAO_E_HIP;
+  }
   if (n < 0) {
     set_error("eao_lines_detect: edge arrays overflowed (the reference's EdgeDrawing -1)");
     return EAO_E_CAPACITY;
