@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "../../include/eao_accel.h"
+#include "hsa_lane.h"
 #include "match.h"
 
 namespace eao {
@@ -57,16 +58,17 @@ class AssocEngine {
 
   int init(int device, int max_points);
   ~AssocEngine();
-  // device-level entry points (inputs already on device, stream s)
+  // device-level entry points (inputs already on device, launched on lane s: a HIP stream or an
+  // HSA queue, hsa_lane.h)
   int np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                const int* d_flen, const float* d_op, const uint8_t* d_ov, const int* d_ooff,
-               const int* d_olen, eao_np_stats* d_out, hipStream_t s, int max_olen,
+               const int* d_olen, eao_np_stats* d_out, const Lane& s, int max_olen,
                // per pair: the device scores of the object's pending forest (null: none) and its
                // erase threshold -- the erasure is applied on the fly
                const double* const* d_os_ptr = nullptr, const float* d_oth = nullptr);
   int iforest_batch(int nclouds, const float* d_pts, const int* d_off, const int* d_len,
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
-                    hipStream_t s, int max_len, int max_sample, int npts_total,
+                    const Lane& s, int max_len, int max_sample, int npts_total,
                     double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
                     double* scores2 = nullptr);  // optional second copy of the scores
   // sharded forests (shard.h, device form): per launched cloud c the outlier bit mask
@@ -76,7 +78,7 @@ class AssocEngine {
   int pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores, unsigned char* d_dst,
                  hipStream_t s);
   // host (pinned) to device copy as a kernel on stream s (16-byte aligned buffers)
-  int stage_in(void* d_dst, const void* h_src, size_t bytes, hipStream_t s);
+  int stage_in(void* d_dst, const void* h_src, size_t bytes, const Lane& s);
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples
   bool iforest_fits(int max_len, int max_sample) const;
   // the frame start's projected rects and NP pairs in one launch (k_rects_np); the inputs
@@ -84,7 +86,7 @@ class AssocEngine {
   int rects_np(const CamDev& cam, const float* T, int nclouds, const float* rpts, const int* roff, const int* rlen,
                int* rect, uint8_t* ok, const double* const* ros, const float* rth, int npairs, const float* fp,
                const uint8_t* fv, const int* foff, const int* flen, const float* op, const uint8_t* ov,
-               const int* ooff, const int* olen, eao_np_stats* out, hipStream_t s, int max_olen,
+               const int* ooff, const int* olen, eao_np_stats* out, const Lane& s, int max_olen,
                const double* const* os_ptr, const float* oth);
   int rects(const CamDev& cam, const float* d_T, int nclouds, const float* d_pts, const int* d_off,
             const int* d_len, int* d_rect, uint8_t* d_ok, hipStream_t s,

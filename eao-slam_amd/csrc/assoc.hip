@@ -1453,12 +1453,17 @@ int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const 
                           const int* rlen, int* rect, uint8_t* ok, const double* const* ros, const float* rth,
                           int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen, eao_np_stats* out,
-                          hipStream_t s, int max_olen, const double* const* os_ptr, const float* oth) {
+                          const Lane& s, int max_olen, const double* const* os_ptr, const float* oth) {
   if (npairs + nclouds <= 0) return EAO_OK;
   int P = 256;
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
   const size_t lds = sizeof(float) * 3 * P + (P >= 2048 ? NP_LDS_EXTRA : 64);
-  hipLaunchKernelGGL(k_rects_np, dim3(npairs + nclouds), dim3(NPT), lds, s, npairs, fp, fv, foff, flen, op, ov, ooff,
+  if (s.hsa()) {
+    static const int kid = hsa_kernel_id("eao::k_rects_np(");
+    return hsa_launch(s.q, kid, dim3(npairs + nclouds), dim3(NPT), (uint32_t)lds, npairs, fp, fv, foff, flen, op, ov,
+                      ooff, olen, P, os_ptr, oth, out, cam, T, rpts, roff, rlen, rect, ok, ros, rth);
+  }
+  hipLaunchKernelGGL(k_rects_np, dim3(npairs + nclouds), dim3(NPT), lds, s.s, npairs, fp, fv, foff, flen, op, ov, ooff,
                      olen, P, os_ptr, oth, out, cam, T, rpts, roff, rlen, rect, ok, ros, rth);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
@@ -1467,13 +1472,18 @@ int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const 
 int AssocEngine::np_batch(int npairs, const float* d_fp, const uint8_t* d_fv, const int* d_foff,
                           const int* d_flen, const float* d_op, const uint8_t* d_ov,
                           const int* d_ooff, const int* d_olen, eao_np_stats* d_out,
-                          hipStream_t s, int max_olen, const double* const* d_os_ptr, const float* d_oth) {
+                          const Lane& s, int max_olen, const double* const* d_os_ptr, const float* d_oth) {
   if (npairs <= 0) return EAO_OK;
   int P = 256;  // k_np_pairs sorts whole 256-element runs
   while (P < std::min(max_olen, NP_MAXN)) P <<= 1;
   // the object's sort arrays, then the rank path's frame values and counters (NP_LDS_EXTRA)
   const size_t lds = sizeof(float) * 3 * P + (P >= 2048 ? NP_LDS_EXTRA : 64);
-  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), lds, s, d_fp, d_fv, d_foff,
+  if (s.hsa()) {
+    static const int kid = hsa_kernel_id("eao::k_np_pairs(");
+    return hsa_launch(s.q, kid, dim3(npairs), dim3(NPT), (uint32_t)lds, d_fp, d_fv, d_foff, d_flen, d_op, d_ov,
+                      d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
+  }
+  hipLaunchKernelGGL(k_np_pairs, dim3(npairs), dim3(NPT), lds, s.s, d_fp, d_fv, d_foff,
                      d_flen, d_op, d_ov, d_ooff, d_olen, P, d_os_ptr, d_oth, d_out);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
@@ -1561,7 +1571,7 @@ int AssocEngine::iforest_table(uint32_t seed, uint32_t trees, hipStream_t s) {
 
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len,
                                uint32_t trees, uint32_t seed, const uint32_t* d_sample,
-                               double* scores, hipStream_t s, int maxN, int maxS, int npts_total,
+                               double* scores, const Lane& s, int maxN, int maxS, int npts_total,
                                double* contrib, double* scores2) {
   if (!contrib) contrib = d_contrib;
   if (nclouds <= 0) return EAO_OK;
@@ -1573,8 +1583,8 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
     set_error("iforest: cloud exceeds the LDS-resident tree capacity");
     return EAO_E_CAPACITY;
   }
-  if (seed != cached_seed || trees != cached_trees || !tab_n) {
-    if (int rc = iforest_table(seed, trees, s)) return rc;
+  if (seed != cached_seed || trees != cached_trees || !tab_n) {  // synchronous, on the engine's stream
+    if (int rc = iforest_table(seed, trees, s.hsa() ? stream : s.s)) return rc;
   }
   // helper job slots: as many as the LDS left by the tree allows (up to IF_JSLOTS)
   // samples of <= 64 items (clouds of < 130 points): one wave per (tree, cloud) builds the tree (one
@@ -1587,11 +1597,24 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
   int jslots = small ? 0 : IF_JSLOTS;
   while (jslots > 0 && IfLds(maxN, maxS, jslots).total > lds_limit) jslots--;
   const IfLds L(maxN, maxS, jslots);
+  if (s.hsa()) {
+    static const int k64 = hsa_kernel_id("void eao::k_iforest_tree<64>("),
+                     k1024 = hsa_kernel_id("void eao::k_iforest_tree<1024>("),
+                     ksum = hsa_kernel_id("eao::k_iforest_sum(");
+    if (int rc = hsa_launch(s.q, small ? k64 : k1024, dim3(trees, nclouds), dim3(small ? 64 : 1024), (uint32_t)L.total,
+                            pts, off, len, (const uint32_t*)d_mtinit, d_sample, maxN, maxS, npts_total,
+                            (const double*)d_ctab, contrib, tab_n, (const uint16_t*)d_tab_ids,
+                            (const long long*)d_tab_off, (const int*)d_tab_D, (const uint32_t*)d_tab_states, jslots))
+      return rc;
+    return hsa_launch(s.q, ksum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0u, off, len, d_sample,
+                      (const double*)d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2, pow_x0[0],
+                      pow_x0[1]);
+  }
   hipLaunchKernelGGL(small ? k_iforest_tree<64> : k_iforest_tree<1024>, dim3(trees, nclouds), dim3(small ? 64 : 1024),
-                     L.total, s, pts, off, len, d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n,
+                     L.total, s.s, pts, off, len, d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n,
                      d_tab_ids, d_tab_off, d_tab_D, d_tab_states, jslots);
   EAO_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s, off, len,
+  hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s.s, off, len,
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,
                      pow_x0[0], pow_x0[1]);
   EAO_HIP_CHECK(hipGetLastError());
@@ -1636,14 +1659,19 @@ int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const
   return EAO_OK;
 }
 
-int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t s) {
+int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, const Lane& s) {
   if (!bytes) return EAO_OK;
   if (((uintptr_t)dst | (uintptr_t)src) & 15) {
     set_error("stage_in: buffers must be 16-byte aligned");
     return EAO_E_ARG;
   }
   const size_t blocks = std::min<size_t>(512, (bytes / 16 + 255) / 256 + 1);
-  hipLaunchKernelGGL(k_stage, dim3((unsigned)blocks), dim3(256), 0, s, (const unsigned char*)src, (unsigned char*)dst,
+  if (s.hsa()) {
+    static const int kid = hsa_kernel_id("eao::k_stage(");
+    return hsa_launch(s.q, kid, dim3((unsigned)blocks), dim3(256), 0u, (const unsigned char*)src, (unsigned char*)dst,
+                      bytes);
+  }
+  hipLaunchKernelGGL(k_stage, dim3((unsigned)blocks), dim3(256), 0, s.s, (const unsigned char*)src, (unsigned char*)dst,
                      bytes);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;

@@ -59,9 +59,9 @@ static const bool g_lookahead = [] {
 // has been overwritten -- or until the launch's event completes, whichever comes first: the
 // data lands a few microseconds before the command processor's end-of-kernel signal.
 // EAO_SENTINEL_WAIT=0 waits on the events only (A/B switch).
-static hipError_t spin_event_plain(hipEvent_t e) {
+static hipError_t spin_event_plain(const eao::Done& e) {
   for (;;) {
-    const hipError_t r = hipEventQuery(e);
+    const hipError_t r = eao::done_query(e);
     if (r != hipErrorNotReady) return r;
     __builtin_ia32_pause();
   }
@@ -108,20 +108,22 @@ static void fill64(void* p, size_t words) {
 //      hardware never produces; kSent8 is no flag value).
 // A fault after the outputs have landed is reported when the launch's event is queried before
 // its buffers are reused (rects_np_launch, kick).
+// (the wait's completion marker is a HIP event or an HSA signal, hsa_lane.h; a blocking wait
+// applies to events only)
 template <class Ready>
-static hipError_t spin_ready(hipEvent_t e, Ready&& ready) {
-  if (!g_sentinel || !g_spin_wait) return g_spin_wait ? spin_event_plain(e) : hipEventSynchronize(e);
+static hipError_t spin_ready(const eao::Done& e, Ready&& ready) {
+  if (!g_sentinel || !g_spin_wait) return g_spin_wait || !e.e ? spin_event_plain(e) : hipEventSynchronize(e.e);
   for (;;) {
     if (ready()) return hipSuccess;
-    const hipError_t r = hipEventQuery(e);
+    const hipError_t r = eao::done_query(e);
     if (r != hipErrorNotReady) return r;
     __builtin_ia32_pause();
   }
 }
-static hipError_t spin_event(hipEvent_t e) {
-  if (!g_spin_wait) return hipEventSynchronize(e);
+static hipError_t spin_event(const eao::Done& e) {
+  if (!g_spin_wait && e.e) return hipEventSynchronize(e.e);
   for (;;) {
-    const hipError_t r = hipEventQuery(e);
+    const hipError_t r = eao::done_query(e);
     if (r != hipErrorNotReady) return r;
     __builtin_ia32_pause();
   }
@@ -598,7 +600,7 @@ class ReplayEngine {
     std::vector<unsigned char> xres;
     std::vector<size_t> mask_off;
     std::vector<eao_np_stats> spst;
-    hipEvent_t ev = nullptr;
+    Done done;  // the batch's launches complete (its lane's last packet / event)
     unsigned char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
     double* contrib = nullptr;  // [50][max_points]
@@ -611,7 +613,10 @@ class ReplayEngine {
     size_t cap_x = 0;
   };
   std::vector<IfBatch> ifb;
-  hipStream_t if_stream[kIfStreams] = {};
+  // the forest lanes, and the frame start's own lane (HSA form; the HIP form launches the
+  // frame start on the engine's stream): HSA queues unless sharded or EAO_HSA_LANES=0
+  Lane if_stream[kIfStreams];
+  Lane fs_lane;
   // the batch whose launch is the last work queued on each forest stream (-1: other work
   // or none): a launch that waits on that batch alone can queue behind it on its stream
   int if_tail[kIfStreams] = {-1, -1, -1, -1};
@@ -646,9 +651,13 @@ class ReplayEngine {
   }
   // device form: this rank's `bytes` at d_send (ready behind `ev`) gathered on the GPU;
   // *recv = the [sworld][bytes] records in pinned host memory
-  int exchange_device(const void* d_send, hipEvent_t ev, size_t bytes, const unsigned char** recv) {
+  int exchange_device(const void* d_send, const Done& ev, size_t bytes, const unsigned char** recv) {
     const double t0 = now_us();
-    int rc = ex->allgather_device(d_send, ev, bytes, recv);
+    if (!ev.e) {  // sharded replays launch on HIP lanes (if_init)
+      set_error("replay: the device-form exchange needs HIP lanes");
+      return EAO_E_STATE;
+    }
+    int rc = ex->allgather_device(d_send, ev.e, bytes, recv);
     xstat[0] += 1;
     xstat[1] += (double)bytes;
     xstat[2] += now_us() - t0;
@@ -657,11 +666,11 @@ class ReplayEngine {
 
   // forest slots, streams and staging outlive the replay: the next replay on
   // the same engine adopts them (allocation is not per replay)
-  hipEvent_t gpu0_ev = nullptr;  // frame-start launch completion (spin-waited)
-  bool rn_dev = false;           // rects_np_launch writes its outputs to d_out (device-form exchange)
+  Done gpu0;            // frame-start launch completion (spin-waited)
+  bool rn_dev = false;  // rects_np_launch writes its outputs to d_out (device-form exchange)
   struct Pool {
     std::vector<IfBatch> ifb;
-    hipStream_t if_stream[kIfStreams] = {};
+    Lane if_stream[kIfStreams], fs_lane;
     unsigned char *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
   };
@@ -670,6 +679,7 @@ class ReplayEngine {
     ReplayEngine tmp;  // its destructor releases the resources
     tmp.ifb.swap(p->ifb);
     for (int k = 0; k < kIfStreams; k++) tmp.if_stream[k] = p->if_stream[k];
+    tmp.fs_lane = p->fs_lane;
     tmp.h_in = p->h_in;
     tmp.d_in = p->d_in;
     tmp.h_out = p->h_out;
@@ -688,6 +698,7 @@ class ReplayEngine {
       b.launched = false;
     }
     for (int k = 0; k < kIfStreams; k++) if_stream[k] = p->if_stream[k];
+    fs_lane = p->fs_lane;
     h_in = p->h_in;
     d_in = p->d_in;
     h_out = p->h_out;
@@ -697,21 +708,23 @@ class ReplayEngine {
     delete p;
   }
   ~ReplayEngine() {
-    for (hipStream_t st : if_stream)
-      if (st) (void)hipStreamSynchronize(st);
+    for (const Lane& st : if_stream) (void)lane_sync(st);
+    (void)lane_sync(fs_lane);
     if (trace_path && !trace.empty())
       if (FILE* f = std::fopen(trace_path, "ab")) {
         std::fwrite(trace.data(), sizeof(TraceEv), trace.size(), f);
         std::fclose(f);
       }
-    if (gpu0_ev) (void)hipEventDestroy(gpu0_ev);
+    done_close(gpu0);
     if (A && !A->replay_pool && !ifb.empty()) {
       Pool* p = new Pool();
       p->ifb.swap(ifb);
       for (int k = 0; k < kIfStreams; k++) {
         p->if_stream[k] = if_stream[k];
-        if_stream[k] = nullptr;
+        if_stream[k] = Lane();
       }
+      p->fs_lane = fs_lane;
+      fs_lane = Lane();
       p->h_in = h_in;
       p->d_in = d_in;
       p->h_out = h_out;
@@ -723,7 +736,7 @@ class ReplayEngine {
       A->replay_pool_free = &ReplayEngine::free_pool;
     }
     for (IfBatch& sl : ifb) {
-      if (sl.ev) (void)hipEventDestroy(sl.ev);
+      done_close(sl.done);
       if (sl.h_in) (void)hipHostFree(sl.h_in);
       if (sl.h_out) (void)hipHostFree(sl.h_out);
       if (sl.d_in) (void)hipFree(sl.d_in);
@@ -731,8 +744,8 @@ class ReplayEngine {
       if (sl.d_x) (void)hipFree(sl.d_x);
       if (sl.contrib) (void)hipFree(sl.contrib);
     }
-    for (hipStream_t st : if_stream)
-      if (st) (void)hipStreamDestroy(st);
+    for (Lane& st : if_stream) lane_close(st);
+    lane_close(fs_lane);
     if (h_in) (void)hipHostFree(h_in);
     if (h_out) (void)hipHostFree(h_out);
     if (d_in) (void)hipFree(d_in);
@@ -1102,16 +1115,28 @@ class ReplayEngine {
   // order, Q8, then ComputeMeanAndStandard for pending 2)
   int if_init() {
     ifb.resize(kIfBatches);
-    // the association is the latency-bound chain of the step: its launches get the
-    // highest stream priority so extraction work queued on other streams cannot delay them
-    int lo_pri = 0, hi_pri = 0;
-    EAO_HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
-    for (int k = 0; k < kIfStreams; k++)
-      EAO_HIP_CHECK(hipStreamCreateWithPriority(&if_stream[k], hipStreamNonBlocking, hi_pri));
-    for (IfBatch& b : ifb) {
-      EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
-      EAO_HIP_CHECK(hipMalloc((void**)&b.contrib, sizeof(double) * 50 * (size_t)A->max_points));
+    for (IfBatch& b : ifb)
+      if (!b.contrib) EAO_HIP_CHECK(hipMalloc((void**)&b.contrib, sizeof(double) * 50 * (size_t)A->max_points));
+    return lanes_init();
+  }
+  // the association is the latency-bound chain of the step: its launches go to lanes of the
+  // highest priority (extraction work queued elsewhere cannot delay them), HSA queues fed with
+  // AQL packets directly (hsa_lane.h) unless the replay is sharded (RCCL waits on HIP events)
+  // or EAO_HSA_LANES=0. Lanes adopted from a previous replay of the other kind are replaced.
+  bool lanes_hsa = false;
+  int lanes_init() {
+    const bool want = !sharded() && hsa_lanes_available(A->dev);
+    if (if_stream[0].s || if_stream[0].q) {
+      if (if_stream[0].hsa() == want) return EAO_OK;
+      for (Lane& l : if_stream) lane_close(l);
+      lane_close(fs_lane);
+      for (IfBatch& b : ifb) done_close(b.done);
+      done_close(gpu0);
     }
+    if (int rc = lanes_open(if_stream, kIfStreams, want, A->dev)) return rc;
+    if (want)
+      if (int rc = lanes_open(&fs_lane, 1, true, A->dev)) return rc;
+    lanes_hsa = want;
     return EAO_OK;
   }
   int resolve_trivial(Obj* o) {  // pending objects the forest does not apply to
@@ -1261,11 +1286,10 @@ class ReplayEngine {
           b.cap_x = c;
         }
         if (xdev() && !b.launched) {  // nothing owned: an empty record, ready behind b.ev
-          hipStream_t st = if_stream[k % kIfStreams];
+          const Lane& st = if_stream[k % kIfStreams];
           if_tail[k % kIfStreams] = -1;
-          if (!b.ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&b.ev, hipEventDisableTiming));
-          EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st));
-          EAO_HIP_CHECK(hipEventRecord(b.ev, st));
+          EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st.s));
+          if (int rc = lane_record(st, b.done)) return rc;
         }
       }
       if (!b.launched) continue;
@@ -1307,8 +1331,8 @@ class ReplayEngine {
         EAO_HIP_CHECK(hipMalloc((void**)&b.d_out, c));
         b.cap_out = c;
       }
-      if (b.ev) {  // the slot's previous launch (completed on its outputs): a late fault surfaces here
-        const hipError_t e = hipEventQuery(b.ev);
+      if (b.done.e || b.done.sig) {  // the slot's previous launch (completed on its outputs): a late fault surfaces here
+        const hipError_t e = done_query(b.done);
         if (e != hipSuccess && e != hipErrorNotReady) EAO_HIP_CHECK(e);
       }
       if (g_sentinel && !sharded()) {  // scores and speculative stats pre-filled (spin_ready)
@@ -1366,7 +1390,7 @@ class ReplayEngine {
           w += (o->pts.size() + 7) / 8;
         }
       }
-      hipStream_t st = if_stream[k % kIfStreams];
+      const Lane& st = if_stream[k % kIfStreams];
       b.seq = ++if_seq;
       if_tail[k % kIfStreams] = k;
       prof[2] += 1;
@@ -1394,10 +1418,10 @@ class ReplayEngine {
       }
       if (xdev()) {
         const int* dpk = (const int*)(b.d_in + o_pk);
-        rc = A->pack_masks(nl, dpk, (const float*)(b.d_in + o_pkth), (const double*)b.d_out, b.d_x, st);
+        rc = A->pack_masks(nl, dpk, (const float*)(b.d_in + o_pkth), (const double*)b.d_out, b.d_x, st.s);
         if (rc) return rc;
       }
-      EAO_HIP_CHECK(hipEventRecord(b.ev, st));
+      if (int rc1 = lane_record(st, b.done)) return rc1;
       tr(5, k, nl, maxN);
     }
     return EAO_OK;
@@ -1412,9 +1436,9 @@ class ReplayEngine {
     const unsigned char* recv = nullptr;
     if (xdev()) {
       // the owner's kernels wrote the record into b.d_x; gathered on the GPU behind b.ev
-      if (int rc = exchange_device(b.d_x, b.ev, bytes, &recv)) return rc;
+      if (int rc = exchange_device(b.d_x, b.done, bytes, &recv)) return rc;
     } else {
-      if (b.launched) EAO_HIP_CHECK(spin_event(b.ev));
+      if (b.launched) EAO_HIP_CHECK(spin_event(b.done));
       xsend.assign(bytes, 0);
       size_t w = 0;
       for (int c : b.lc) {
@@ -1488,11 +1512,11 @@ class ReplayEngine {
         return true;
       };
       if (sharded()) {  // outputs come from the exchange; no sentinels there
-        idle_work(b.ev);
-        EAO_HIP_CHECK(spin_event(b.ev));
+        idle_work(b.done);
+        EAO_HIP_CHECK(spin_event(b.done));
       } else {
-        idle_work(b.ev, ready);
-        EAO_HIP_CHECK(spin_ready(b.ev, ready));
+        idle_work(b.done, ready);
+        EAO_HIP_CHECK(spin_ready(b.done, ready));
         std::atomic_thread_fence(std::memory_order_acquire);
       }
       tr(7, o->slot, phase);
@@ -1707,8 +1731,8 @@ class ReplayEngine {
     // the previous frame start's wait may have ended on its outputs before its event: the event
     // is queried once before its pinned buffers are refilled, so a fault of that launch is
     // reported here (its outputs were complete: see spin_ready for the kernels' rules)
-    if (gpu0_ev) {
-      const hipError_t e = hipEventQuery(gpu0_ev);
+    if (gpu0.e || gpu0.sig) {
+      const hipError_t e = done_query(gpu0);
       if (e != hipSuccess && e != hipErrorNotReady) EAO_HIP_CHECK(e);
     }
     int rc = stage(in_bytes, o_ok + nb);
@@ -1768,7 +1792,8 @@ class ReplayEngine {
     // stream's last work (in-queue order: no cross-queue event wait on the chain, which
     // costs 10-25 us between the forest's end and this launch's start); the others, if
     // any, through event waits
-    hipStream_t ls = A->stream;
+    if (int rc0 = lanes_init()) return rc0;
+    Lane ls = lanes_hsa ? fs_lane : Lane(A->stream);
     int lk = -1;
     for (int k : wait_slots)
       if (if_tail[k % kIfStreams] == k && (lk < 0 || ifb[k].seq > ifb[lk].seq)) lk = k;
@@ -1777,7 +1802,8 @@ class ReplayEngine {
       if_tail[lk % kIfStreams] = -1;
     }
     for (int k : wait_slots)
-      if (k != lk) EAO_HIP_CHECK(hipStreamWaitEvent(ls, ifb[k].ev, 0));
+      if (k != lk)
+        if (int rc0 = lane_wait(ls, ifb[k].done)) return rc0;
     // one launch reads the packed inputs in place from pinned host memory (no staging
     // kernel on the chain) and writes the results straight back into pinned host memory
     const unsigned char* din = h_in;
@@ -1791,8 +1817,7 @@ class ReplayEngine {
                      dosp, doth, npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
                      (eao_np_stats*)ob, ls, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
-    if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
-    EAO_HIP_CHECK(hipEventRecord(gpu0_ev, ls));
+    if (int rc0 = lane_record(ls, gpu0)) return rc0;
     tr(2, lk, (int)wait_slots.size(), npairs);
     if (phase == 0) {  // the frame start's launch: time since the frame began
       prof[58] += now_us() - frame_t0;
@@ -1818,8 +1843,8 @@ class ReplayEngine {
         }
         return true;
       };
-      idle_work(gpu0_ev, ready);  // the next frame's steps 1-6, while the GPU is busy
-      EAO_HIP_CHECK(spin_ready(gpu0_ev, ready));
+      idle_work(gpu0, ready);  // the next frame's steps 1-6, while the GPU is busy
+      EAO_HIP_CHECK(spin_ready(gpu0, ready));
       std::atomic_thread_fence(std::memory_order_acquire);
     }
     tr(3);
@@ -1867,18 +1892,17 @@ class ReplayEngine {
       if (int rc = stage(0, bytes)) return rc;
       int rc;
       if (L.empty() && P.empty()) {  // nothing owned: an empty record
-        if (!gpu0_ev) EAO_HIP_CHECK(hipEventCreateWithFlags(&gpu0_ev, hipEventDisableTiming));
         EAO_HIP_CHECK(hipMemsetAsync(d_out, 0, bytes, A->stream));
-        EAO_HIP_CHECK(hipEventRecord(gpu0_ev, A->stream));
+        if (int rc0 = lane_record(Lane(A->stream), gpu0)) return rc0;
       } else {
         rn_dev = true;
         rc = rects_np_launch(L, P, R, S);
         rn_dev = false;
         if (rc) return rc;
       }
-      idle_work(gpu0_ev);  // the next frame's steps 1-6, while the GPU is busy
+      idle_work(gpu0);  // the next frame's steps 1-6, while the GPU is busy
       const unsigned char* recv = nullptr;
-      if ((rc = exchange_device(d_out, gpu0_ev, bytes, &recv))) return rc;
+      if ((rc = exchange_device(d_out, gpu0, bytes, &recv))) return rc;
       std::vector<int> il(sworld, 0), ip(sworld, 0);
       rects.assign(5 * list.size(), 0);
       stats.resize(pairs.size());
@@ -2540,13 +2564,13 @@ class ReplayEngine {
     la_set = false;
   }
   // fill a wait on `ev` with the next frame's steps 1-6 (until the event, or `ready()`)
-  void idle_work(hipEvent_t ev) {
+  void idle_work(const Done& ev) {
     idle_work(ev, [] { return false; }, false);
   }
   // (with a sentinel test the cheap ready() runs after every step and hipEventQuery, a runtime
   // call, after every fourth)
   template <class Ready>
-  void idle_work(hipEvent_t ev, Ready&& ready, bool has_ready = true) {
+  void idle_work(const Done& ev, Ready&& ready, bool has_ready = true) {
     if (!prep.active) {
       if (!g_lookahead || !la_set || prep.ok || !ini) return;
       la_set = false;
@@ -2570,7 +2594,7 @@ class ReplayEngine {
         continue;
       }
       if (g_sentinel && has_ready && ready()) break;
-      if ((it & qmask) == 0 && hipEventQuery(ev) != hipErrorNotReady) break;
+      if ((it & qmask) == 0 && done_query(ev) != hipErrorNotReady) break;
       prep.ok = prep_step(prep);
     }
   }

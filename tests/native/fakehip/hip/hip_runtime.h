@@ -33,6 +33,10 @@ inline float __fdiv_rn(float a, float b) { return a / b; }
 #include <algorithm>
 using std::max; using std::min;
 struct dim3_ { unsigned x, y, z; };
+struct dim3 {
+  unsigned x, y, z;
+  dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
 static struct { unsigned x; } threadIdx;
 template <typename T> T __shfl_xor(T v, int, int) { return v; }
 inline unsigned long long __ballot(bool p) { return p; }

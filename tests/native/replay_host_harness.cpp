@@ -25,7 +25,7 @@ CamDev make_cam(const eao_camera& c) {
 static bool g_in_rects_np = false;  // EAO_HARNESS_DUMP: tags the frame-start pairs
 int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen,
-                          eao_np_stats* out, hipStream_t, int, const double* const* os_ptr, const float* oth) {
+                          eao_np_stats* out, const Lane&, int, const double* const* os_ptr, const float* oth) {
   static FILE* dump = std::getenv("EAO_HARNESS_DUMP") ? std::fopen(std::getenv("EAO_HARNESS_DUMP"), "w") : nullptr;
   for (int p = 0; p < npairs; p++) {
     if (dump) {  // kind (fs: frame start, np: speculative / relaunch), pairs, m, n, valid m, kept valid n, kept n
@@ -54,7 +54,7 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
   return 0;
 }
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
-                               uint32_t seed, const uint32_t* sample, double* scores, hipStream_t, int, int,
+                               uint32_t seed, const uint32_t* sample, double* scores, const Lane&, int, int,
                                int, double*, double* scores2) {
   // fault injection (tests): EAO_HARNESS_FAIL_IFOREST=N fails the N-th forest launch (1-based)
   static int calls = 0;
@@ -90,15 +90,15 @@ int AssocEngine::rects_np(const CamDev& cam, const float* T, int nclouds, const 
                           const int* rlen, int* rect, uint8_t* ok, const double* const* ros, const float* rth,
                           int npairs, const float* fp, const uint8_t* fv, const int* foff, const int* flen,
                           const float* op, const uint8_t* ov, const int* ooff, const int* olen, eao_np_stats* out,
-                          hipStream_t s, int max_olen, const double* const* os_ptr, const float* oth) {
-  rects(cam, T, nclouds, rpts, roff, rlen, rect, ok, s, ros, rth);
+                          const Lane& s, int max_olen, const double* const* os_ptr, const float* oth) {
+  rects(cam, T, nclouds, rpts, roff, rlen, rect, ok, s.s, ros, rth);
   g_in_rects_np = true;
   const int rc = np_batch(npairs, fp, fv, foff, flen, op, ov, ooff, olen, out, s, max_olen, os_ptr, oth);
   g_in_rects_np = false;
   return rc;
 }
 bool AssocEngine::iforest_fits(int max_len, int) const { return max_len <= IF_MAXN; }
-int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, hipStream_t) {
+int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, const Lane&) {
   std::memcpy(dst, src, bytes);  // host "device" memory
   return EAO_OK;
 }
@@ -163,3 +163,21 @@ extern "C" void harness_set_device_exchange(eao_allgather_fn fn, void* ctx) {
   eao::g_dev_ctx = ctx;
 }
 extern "C" void harness_set_events_never(int v) { fake_events_never() = v; }
+
+// launch lanes (hsa_lane.h): HIP-stream lanes only; completion markers follow the fake events
+namespace eao {
+bool hsa_lanes_available(int) { return false; }
+int lanes_open(Lane* l, int n, bool, int) {
+  for (int i = 0; i < n; i++) l[i] = Lane((hipStream_t)1);
+  return 0;
+}
+void lane_close(Lane& l) { l = Lane(); }
+int lane_sync(const Lane&) { return 0; }
+void done_close(Done& d) { d = Done(); }
+int lane_record(const Lane&, Done& d) {
+  d.e = (hipEvent_t)1;
+  return 0;
+}
+int lane_wait(const Lane&, const Done&) { return 0; }
+hipError_t done_query(const Done& d) { return d.e ? hipEventQuery(d.e) : hipSuccess; }
+}  // namespace eao

@@ -81,4 +81,30 @@ s5() {
   timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r5_s5_lsingle_kt -o run -- python3 tools/micro/lines_single.py 32 > gpurun_out/r5_s5_lsingle_kt.log 2>&1
 }
 
+# hsa: association launches through HSA lanes (AQL packets) against HIP streams (EAO_HSA_LANES=0)
+hsa() {
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_assoc.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_hsa_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## hip streams" && EAO_HSA_LANES=0 timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hsa lanes" && timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_hsa_probe.log 2>&1 &&
+  timeout -k 10 300 python -u bench.py > gpurun_out/r5_hsa_bench.log 2>&1
+}
+
+# hsa2: HSA lane variants (acquire scope, kernargs in device memory) against HIP streams
+hsa2() {
+  for r in 1 2; do
+    echo "## hsa acq agent, host kernargs" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hip streams" && EAO_HSA_LANES=0 timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hsa acq system" && EAO_HSA_ACQ=system timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_hsa2_probe.log 2>&1
+}
+# hsa3: kernel arguments in device memory (BAR writes, HDP flush, read-back) against the kernarg pool
+hsa3() {
+  for r in 1 2; do
+    echo "## hsa host kernargs" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hsa dev kernargs" && EAO_HSA_KARG=dev timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_hsa3_probe.log 2>&1
+}
+
 "$@"
