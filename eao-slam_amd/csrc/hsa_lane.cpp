@@ -60,11 +60,12 @@ void queue_error(hsa_status_t s, hsa_queue_t*, void*) {
 }
 
 // A/B switches (measurements): EAO_HSA_ACQ = agent (default) | system, the acquire fence of every
-// dispatch (at least agent scope: it also invalidates the scalar cache, where a kernel would
-// otherwise read the previous dispatch's kernel arguments from a reused kernarg slot -- a
-// measured GPU memory fault with no acquire fence); EAO_HSA_KARG = host (default, the CPU's
-// kernarg pool) | dev (device memory written through the BAR, HDP flush + read-back before the
-// doorbell)
+// dispatch (at least agent scope: without an acquire fence a kernel can read stale lines of
+// reused buffers -- kernarg slots, the batch staging -- from the CUs' caches, a measured GPU
+// memory fault); EAO_HSA_KARG = dev (default: device memory written through the BAR, one HDP
+// flush + read-back before each doorbell) | host (the CPU's kernarg pool: every wave then loads its
+// arguments over PCIe, and the forest's tree kernel takes 10-20 us longer,
+// profiles/r05_ab_hsa_kernargs_probe.txt)
 const int g_acq = [] {
   const char* v = std::getenv("EAO_HSA_ACQ");
   if (v && v[0] == 's') return (int)HSA_FENCE_SCOPE_SYSTEM;
@@ -72,7 +73,7 @@ const int g_acq = [] {
 }();
 const bool g_dev_karg = [] {
   const char* v = std::getenv("EAO_HSA_KARG");
-  return v && v[0] == 'd';
+  return !(v && v[0] == 'h');
 }();
 
 struct DevRt {
@@ -244,10 +245,21 @@ struct HsaQueue {
   uint32_t mask = 0;
   int64_t pending = -1;  // slot written but not committed (header invalid, doorbell not rung)
   uint32_t pending_word = 0;
+  const unsigned char* karg_dirty = nullptr;  // last kernarg byte written through the BAR, not yet flushed
 
   void* slot(uint64_t idx) { return (char*)q->base_address + 64 * (idx & mask); }
+  // device-memory kernargs: out of the write-combining buffer and the HDP before the GPU reads them
+  // (the read-back completes only after every earlier posted write has landed)
+  void flush_kargs() {
+    if (!karg_dirty) return;
+    _mm_sfence();
+    *(volatile uint32_t*)d->hdp.HDP_MEM_FLUSH_CNTL = 1u;
+    (void)*(volatile const unsigned char*)karg_dirty;
+    karg_dirty = nullptr;
+  }
   void commit() {
     if (pending < 0) return;
+    flush_kargs();
     __atomic_store_n((uint32_t*)slot((uint64_t)pending), pending_word, __ATOMIC_RELEASE);
     hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)pending);
     pending = -1;
@@ -473,7 +485,8 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
     set_error(std::string("hsa_launch: launch shape out of range for ") + k.name);
     return EAO_E_ARG;
   }
-  q->commit();
+  // the new slot's arguments are written before the lane's pending packet is committed, so one
+  // kernarg flush covers both
   uint64_t idx;
   if (int rc = q->reserve(&idx)) return rc;
   unsigned char* ka = q->karg + kKargSlot * (idx & q->mask);
@@ -493,11 +506,8 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
   put64(9, 0), put64(10, 0), put64(11, 0);
   put16(12, 3);
   put32(13, dyn_lds);
-  if (q->karg_dev) {  // written through the BAR: out of the write-combining buffer and the HDP
-    _mm_sfence();
-    *(volatile uint32_t*)q->d->hdp.HDP_MEM_FLUSH_CNTL = 1u;
-    (void)*(volatile unsigned char*)(ka + k.karg - 1);
-  }
+  if (q->karg_dev) q->karg_dirty = ka + k.karg - 1;
+  q->commit();
   hsa_kernel_dispatch_packet_t* p = (hsa_kernel_dispatch_packet_t*)q->slot(idx);
   p->workgroup_size_x = (uint16_t)b.x;
   p->workgroup_size_y = (uint16_t)b.y;

@@ -107,4 +107,15 @@ hsa3() {
   done > gpurun_out/r5_hsa3_probe.log 2>&1
 }
 
+# hsa4: device kernargs by default: association suite, A/B against HIP streams and host kernargs, bench
+hsa4() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_assoc.py tests/test_gpu_chain.py tests/test_gpu_shard.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_hsa4_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## hsa dev kernargs" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hip streams" && EAO_HSA_LANES=0 timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hsa host kernargs" && EAO_HSA_KARG=host timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_hsa4_probe.log 2>&1 &&
+  timeout -k 10 300 python -u bench.py > gpurun_out/r5_hsa4_bench.log 2>&1
+}
+
 "$@"
