@@ -8,9 +8,10 @@
 //     agent scope (device data from kernels on other lanes), release at system scope; the
 //     kernel arguments go to a per-slot kernarg ring with the COV5 hidden arguments the kernel
 //     declares filled in (grid / block counts, dynamic LDS);
-//   * the lane's last packet is held uncommitted (header not yet valid, doorbell not rung) so a
-//     Done recorded right after it rides on that packet's completion signal instead of an extra
-//     barrier packet; any other use of the lane commits it first;
+//   * the lane's packets are held uncommitted (headers not yet valid, doorbell not rung) until a
+//     Done is recorded on it: the Done rides on the last packet's completion signal instead of an
+//     extra barrier packet, and the packets of a forest batch or a frame start go out behind one
+//     kernarg flush and one doorbell;
 //   * a cross-lane wait is a barrier-AND packet on the waiting lane, skipped when the signal has
 //     already completed;
 //   * each record takes the next signal of a ring of kSignals, reused only after its previous
@@ -243,8 +244,10 @@ struct HsaQueue {
   bool karg_dev = false;  // kernargs in device memory (EAO_HSA_KARG=dev)
   DevRt* d = nullptr;
   uint32_t mask = 0;
-  int64_t pending = -1;  // slot written but not committed (header invalid, doorbell not rung)
-  uint32_t pending_word = 0;
+  // packets written but not committed (headers still invalid, doorbell not rung): slots [p0, p1]
+  // and their header words; committed together by a record, a sync or a close
+  int64_t p0 = -1, p1 = -1;
+  uint32_t pword[kQueueSize] = {};
   const unsigned char* karg_dirty = nullptr;  // last kernarg byte written through the BAR, not yet flushed
 
   void* slot(uint64_t idx) { return (char*)q->base_address + 64 * (idx & mask); }
@@ -257,12 +260,18 @@ struct HsaQueue {
     (void)*(volatile const unsigned char*)karg_dirty;
     karg_dirty = nullptr;
   }
+  void add_pending(uint64_t idx, uint32_t word) {
+    if (p0 < 0) p0 = (int64_t)idx;
+    p1 = (int64_t)idx;
+    pword[idx & mask] = word;
+  }
   void commit() {
-    if (pending < 0) return;
+    if (p0 < 0) return;
     flush_kargs();
-    __atomic_store_n((uint32_t*)slot((uint64_t)pending), pending_word, __ATOMIC_RELEASE);
-    hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)pending);
-    pending = -1;
+    for (int64_t i = p0; i <= p1; i++)
+      __atomic_store_n((uint32_t*)slot((uint64_t)i), pword[(uint64_t)i & mask], __ATOMIC_RELEASE);
+    hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)p1);
+    p0 = p1 = -1;
   }
   // a free slot: every packet before the previous one has completed once its successor started
   // (barrier bits), so slots and kernarg slots more than two behind the read index are idle
@@ -280,17 +289,16 @@ struct HsaQueue {
     *out = idx;
     return EAO_OK;
   }
-  int barrier(const hsa_signal_t* dep, int ndep, hsa_signal_t done) {
-    commit();
+  // a barrier-AND packet (pending unless `now`)
+  int barrier(const hsa_signal_t* dep, int ndep, hsa_signal_t done, bool now) {
     uint64_t idx;
     if (int rc = reserve(&idx)) return rc;
     hsa_barrier_and_packet_t* p = (hsa_barrier_and_packet_t*)slot(idx);
     std::memset((char*)p + 4, 0, sizeof(*p) - 4);
     for (int i = 0; i < ndep && i < 5; i++) p->dep_signal[i] = dep[i];
     p->completion_signal = done;
-    pending = (int64_t)idx;
-    pending_word = header(HSA_PACKET_TYPE_BARRIER_AND, HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE);
-    commit();
+    add_pending(idx, header(HSA_PACKET_TYPE_BARRIER_AND, HSA_FENCE_SCOPE_NONE, HSA_FENCE_SCOPE_NONE));
+    if (now) commit();
     return EAO_OK;
   }
 };
@@ -366,7 +374,7 @@ int lane_sync(const Lane& l) {
       set_error("HSA lane: signal");
       return EAO_E_HIP;
     }
-    int rc = q->barrier(nullptr, 0, s);
+    int rc = q->barrier(nullptr, 0, s, true);
     const double t0 = now_us();
     while (rc == EAO_OK && hsa_signal_load_scacquire(s) > 0) {
       if (now_us() - t0 > kTimeoutUs) {
@@ -426,12 +434,15 @@ int lane_record(const Lane& l, Done& d) {
   }
   hsa_signal_store_relaxed(s, 1);
   d.sig = s.handle;
-  if (q->pending >= 0) {  // ride on the lane's last packet
-    ((hsa_kernel_dispatch_packet_t*)q->slot((uint64_t)q->pending))->completion_signal = s;
+  if (q->p1 >= 0) {  // ride on the lane's last packet (a dispatch or a barrier-AND: same offset)
+    static_assert(offsetof(hsa_kernel_dispatch_packet_t, completion_signal) ==
+                      offsetof(hsa_barrier_and_packet_t, completion_signal),
+                  "completion signal offset");
+    ((hsa_kernel_dispatch_packet_t*)q->slot((uint64_t)q->p1))->completion_signal = s;
     q->commit();
     return EAO_OK;
   }
-  return q->barrier(nullptr, 0, s);
+  return q->barrier(nullptr, 0, s, true);
 }
 
 int lane_wait(const Lane& l, const Done& d) {
@@ -449,7 +460,7 @@ int lane_wait(const Lane& l, const Done& d) {
   }
   hsa_signal_t s{d.sig};
   if (hsa_signal_load_relaxed(s) <= 0) return EAO_OK;  // already complete
-  return l.q->barrier(&s, 1, hsa_signal_t{0});
+  return l.q->barrier(&s, 1, hsa_signal_t{0}, false);
 }
 
 hipError_t done_query(const Done& d) {
@@ -485,8 +496,8 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
     set_error(std::string("hsa_launch: launch shape out of range for ") + k.name);
     return EAO_E_ARG;
   }
-  // the new slot's arguments are written before the lane's pending packet is committed, so one
-  // kernarg flush covers both
+  // held uncommitted with the lane's other pending packets: the record that follows commits them
+  // behind one kernarg flush and one doorbell
   uint64_t idx;
   if (int rc = q->reserve(&idx)) return rc;
   unsigned char* ka = q->karg + kKargSlot * (idx & q->mask);
@@ -507,7 +518,6 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
   put16(12, 3);
   put32(13, dyn_lds);
   if (q->karg_dev) q->karg_dirty = ka + k.karg - 1;
-  q->commit();
   hsa_kernel_dispatch_packet_t* p = (hsa_kernel_dispatch_packet_t*)q->slot(idx);
   p->workgroup_size_x = (uint16_t)b.x;
   p->workgroup_size_y = (uint16_t)b.y;
@@ -522,9 +532,9 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
   p->kernarg_address = ka;
   p->reserved2 = 0;
   p->completion_signal = hsa_signal_t{0};
-  q->pending = (int64_t)idx;
-  q->pending_word = (uint32_t)header(HSA_PACKET_TYPE_KERNEL_DISPATCH, (hsa_fence_scope_t)g_acq, HSA_FENCE_SCOPE_SYSTEM) |
-                    (3u << 16);  // setup: three grid dimensions
+  q->add_pending(idx, (uint32_t)header(HSA_PACKET_TYPE_KERNEL_DISPATCH, (hsa_fence_scope_t)g_acq,
+                                       HSA_FENCE_SCOPE_SYSTEM) |
+                          (3u << 16));  // setup: three grid dimensions
   return EAO_OK;
 }
 

@@ -1133,11 +1133,16 @@ class ReplayEngine {
       for (IfBatch& b : ifb) done_close(b.done);
       done_close(gpu0);
     }
-    if (int rc = lanes_open(if_stream, kIfStreams, want, A->dev)) return rc;
-    if (want)
-      if (int rc = lanes_open(&fs_lane, 1, true, A->dev)) return rc;
-    lanes_hsa = want;
-    return EAO_OK;
+    lanes_hsa = false;
+    if (want) {  // HSA queues are a per-process hardware resource: without them, HIP streams
+      if (lanes_open(if_stream, kIfStreams, true, A->dev) == EAO_OK && lanes_open(&fs_lane, 1, true, A->dev) == EAO_OK) {
+        lanes_hsa = true;
+        return EAO_OK;
+      }
+      for (Lane& l : if_stream) lane_close(l);
+      lane_close(fs_lane);
+    }
+    return lanes_open(if_stream, kIfStreams, false, A->dev);
   }
   int resolve_trivial(Obj* o) {  // pending objects the forest does not apply to
     if (o->pending == 2) mean_std(o);
@@ -1804,8 +1809,10 @@ class ReplayEngine {
     for (int k : wait_slots)
       if (k != lk)
         if (int rc0 = lane_wait(ls, ifb[k].done)) return rc0;
-    // one launch reads the packed inputs in place from pinned host memory (no staging
-    // kernel on the chain) and writes the results straight back into pinned host memory
+    // one launch reads the packed inputs in place from pinned host memory (a staging copy to
+    // device memory ahead of the forest waits leaves the kernel's duration unchanged,
+    // profiles/r05_ab_fs_stage_rejected.txt) and writes the results straight back into pinned
+    // host memory
     const unsigned char* din = h_in;
     const int* drm = (const int*)din;
     const int* dpm = (const int*)(din + o_pm);

@@ -118,4 +118,23 @@ hsa4() {
   timeout -k 10 300 python -u bench.py > gpurun_out/r5_hsa4_bench.log 2>&1
 }
 
+# fsst: the frame start's inputs staged to device memory ahead of its forest waits (EAO_FS_STAGE=1)
+fsst() {
+  EAO_FS_STAGE=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_fsst_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## in place" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## staged" && EAO_FS_STAGE=1 timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_fsst_probe.log 2>&1 &&
+  rm -rf gpurun_out/tl_kt && EAO_FS_STAGE=1 bash tools/gpu/timeline.sh && cp gpurun_out/tl_summary.txt gpurun_out/tl_fsst_summary.txt && rm -rf gpurun_out/tl_kt
+}
+
+# hsa5: batched lane commits (one kernarg flush + doorbell per record): suite, A/B against HIP streams
+hsa5() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_assoc.py tests/test_gpu_chain.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r5_hsa5_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## hsa lanes" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## hip streams" && EAO_HSA_LANES=0 timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_hsa5_probe.log 2>&1
+}
+
 "$@"
