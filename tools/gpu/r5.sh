@@ -137,4 +137,13 @@ hsa5() {
   done > gpurun_out/r5_hsa5_probe.log 2>&1
 }
 
+# eager: forests launched per detection (EAO_EAGER_KICK=1) on the HSA lanes
+eager() {
+  EAO_EAGER_KICK=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_eager_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## end-of-loop kick" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## eager kick" && EAO_EAGER_KICK=1 timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_eager_probe.log 2>&1
+}
+
 "$@"
