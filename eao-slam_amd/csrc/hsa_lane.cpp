@@ -247,6 +247,7 @@ struct HsaQueue {
   // packets written but not committed (headers still invalid, doorbell not rung): slots [p0, p1]
   // and their header words; committed together by a record, a sync or a close
   int64_t p0 = -1, p1 = -1;
+  hsa_signal_t sync{};  // lane_sync's completion signal
   uint32_t pword[kQueueSize] = {};
   const unsigned char* karg_dirty = nullptr;  // last kernarg byte written through the BAR, not yet flushed
 
@@ -270,13 +271,17 @@ struct HsaQueue {
     flush_kargs();
     for (int64_t i = p0; i <= p1; i++)
       __atomic_store_n((uint32_t*)slot((uint64_t)i), pword[(uint64_t)i & mask], __ATOMIC_RELEASE);
+    // the queue's write index moves only here, past complete packets (a tool's intercepting
+    // queue reads up to the write index when the doorbell rings)
+    hsa_queue_store_write_index_screlease(q, (uint64_t)p1 + 1);
     hsa_signal_store_screlease(q->doorbell_signal, (hsa_signal_value_t)p1);
     p0 = p1 = -1;
   }
   // a free slot: every packet before the previous one has completed once its successor started
   // (barrier bits), so slots and kernarg slots more than two behind the read index are idle
+  uint64_t widx = 0;  // next slot to fill (this lane is the queue's only producer)
   int reserve(uint64_t* out) {
-    const uint64_t idx = hsa_queue_add_write_index_relaxed(q, 1);
+    const uint64_t idx = widx++;
     const double t0 = now_us();
     while (idx - hsa_queue_load_read_index_scacquire(q) >= (uint64_t)q->size - 2) {
       if (now_us() - t0 > kTimeoutUs) {
@@ -304,9 +309,15 @@ struct HsaQueue {
 };
 
 bool hsa_lanes_available(int dev) {
+  // EAO_HSA_LANES=0: HIP streams; =1: HSA lanes even under a profiler. By default a process
+  // profiled by rocprofv3 (its tool library named in ROCP_TOOL_LIBRARIES) uses HIP streams: the
+  // tool's queue interception faulted on the host (SIGSEGV inside the doorbell handling, at the
+  // first commit on queues created after the process had already run lanes; every run without
+  // the tool is clean), so profiles of the association show its HIP-stream form
   static const bool off = [] {
     const char* v = std::getenv("EAO_HSA_LANES");
-    return v && v[0] == '0';
+    if (v) return v[0] == '0';
+    return std::getenv("ROCP_TOOL_LIBRARIES") != nullptr;
   }();
   if (off) return false;
   std::lock_guard<std::mutex> lk(rt().mu);
@@ -354,6 +365,14 @@ int lanes_open(Lane* l, int n, bool hsa, int dev) {
       return EAO_E_HIP;
     }
     q->mask = q->q->size - 1;
+    q->widx = hsa_queue_load_write_index_relaxed(q->q);
+    if (hsa_signal_create(0, 0, nullptr, &q->sync) != HSA_STATUS_SUCCESS) {
+      set_error("HSA lane: signal");
+      hsa_amd_memory_pool_free(q->karg);
+      hsa_queue_destroy(q->q);
+      delete q;
+      return EAO_E_HIP;
+    }
     l[i].q = q;
   }
   return EAO_OK;
@@ -368,22 +387,19 @@ static hsa_signal_t next_signal(DevRt* d) {
 int lane_sync(const Lane& l) {
   if (l.s) EAO_HIP_CHECK(hipStreamSynchronize(l.s));
   if (HsaQueue* q = l.q) {
-    // a barrier packet's completion after everything queued
-    hsa_signal_t s;
-    if (hsa_signal_create(1, 0, nullptr, &s) != HSA_STATUS_SUCCESS) {
-      set_error("HSA lane: signal");
-      return EAO_E_HIP;
-    }
-    int rc = q->barrier(nullptr, 0, s, true);
+    // a barrier packet's completion after everything queued, on the lane's own sync signal
+    // (created with the lane, destroyed only when it closes: a profiler's interception of the
+    // completion may still refer to it after the value has dropped)
+    hsa_signal_store_relaxed(q->sync, 1);
+    int rc = q->barrier(nullptr, 0, q->sync, true);
     const double t0 = now_us();
-    while (rc == EAO_OK && hsa_signal_load_scacquire(s) > 0) {
+    while (rc == EAO_OK && hsa_signal_load_scacquire(q->sync) > 0) {
       if (now_us() - t0 > kTimeoutUs) {
         set_error("HSA lane: not drained after 10 s (GPU hung?)");
         rc = EAO_E_HIP;
       }
       __builtin_ia32_pause();
     }
-    hsa_signal_destroy(s);
     return rc;
   }
   return EAO_OK;
@@ -396,6 +412,7 @@ void lane_close(Lane& l) {
     t.q = q;
     (void)lane_sync(t);
     hsa_queue_destroy(q->q);
+    hsa_signal_destroy(q->sync);
     hsa_amd_memory_pool_free(q->karg);
     delete q;
   }

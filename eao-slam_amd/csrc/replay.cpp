@@ -1127,7 +1127,8 @@ class ReplayEngine {
   int lanes_init() {
     const bool want = !sharded() && hsa_lanes_available(A->dev);
     if (if_stream[0].s || if_stream[0].q) {
-      if (if_stream[0].hsa() == want) return EAO_OK;
+      lanes_hsa = if_stream[0].hsa();  // adopted from the previous replay on this engine
+      if (lanes_hsa == want) return EAO_OK;
       for (Lane& l : if_stream) lane_close(l);
       lane_close(fs_lane);
       for (IfBatch& b : ifb) done_close(b.done);
