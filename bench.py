@@ -169,6 +169,28 @@ def pmc_valu(kernel, frames):
     return None if v is None else v * 64
 
 
+def cu_masked_stream(dev, per_xcd, layout):
+    """A HIP stream whose kernels run on `per_xcd` CUs of every XCD (hipExtStreamCreateWithCUMask),
+    wrapped for torch; the other CUs stay free for the association's latency-bound launches."""
+    import ctypes
+    import torch
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    nx = 8
+    per = ncu // nx
+    bits = [0] * ((ncu + 31) // 32)
+    for i in range(ncu):
+        xcd, cu = (i % nx, i // nx) if layout == "interleaved" else (i // per, i % per)
+        if cu < per_xcd:
+            bits[i // 32] |= 1 << (i % 32)
+    arr = (ctypes.c_uint32 * len(bits))(*bits)
+    h = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(bits)), arr)
+    if rc != 0:
+        raise RuntimeError("hipExtStreamCreateWithCUMask failed: %d" % rc)
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
 def pingpong(n, m):
     """Frame index of step t when m rendered frames are cycled forth and back."""
     p = np.arange(n) % (2 * m - 2) if m > 1 else np.zeros(n, np.int64)
@@ -208,6 +230,11 @@ def main():
                     help="config c: the object-sharded exchange path also at world 1 (one-rank RCCL communicator)")
     ap.add_argument("--poll", action="store_true", help="A/B: poll the extraction stream while the association runs")
     ap.add_argument("--line-batches", type=int, default=1, help="line detection in this many launches per step")
+    ap.add_argument("--frame-cus", type=int, default=0,
+                    help="A/B: the frame work's stream limited to this many CUs of each XCD (0: all), the rest "
+                         "left to the association's launches")
+    ap.add_argument("--cu-layout", choices=["interleaved", "linear"], default="interleaved",
+                    help="A/B: CU-mask bit order (interleaved: bit i = CU i / 8 of XCD i % 8)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame drop-in leg (dropin_leg)")
     ap.add_argument("--dropin-frames", type=int, default=405, help="frames of the per-frame drop-in leg")
     args = ap.parse_args()
@@ -260,7 +287,7 @@ def main():
     poses = rposes[idx].astype(np.float32)
     # the extraction / matching stream runs on a dedicated HIP stream (a NULL handle would
     # select the engine's own stream, which torch events do not see); buffers are made on it
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.Stream(dev) if not args.frame_cus else cu_masked_stream(dev, args.frame_cus, args.cu_layout)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
     assert sptr != 0
