@@ -196,10 +196,9 @@ DevRt* dev_rt(int dev) {
     d.why = "HSA lanes: no HSA agent at the HIP device's PCI address";
     return &d;
   }
-  if (g_dev_karg) {
-    hsa_amd_agent_iterate_memory_pools(d.gpu, dev_pool_cb, &d);
-    hsa_agent_get_info(d.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &d.hdp);
-  }
+  // device memory the host writes through the BAR (kernargs, bar_alloc) and its HDP flush
+  hsa_amd_agent_iterate_memory_pools(d.gpu, dev_pool_cb, &d);
+  hsa_agent_get_info(d.gpu, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_HDP_FLUSH, &d.hdp);
   hsa_status_t s = hsa_code_object_reader_create_from_memory(eao_assoc_co, (size_t)(eao_assoc_co_end - eao_assoc_co),
                                                              &d.rd);
   if (s == HSA_STATUS_SUCCESS)
@@ -249,17 +248,18 @@ struct HsaQueue {
   int64_t p0 = -1, p1 = -1;
   hsa_signal_t sync{};  // lane_sync's completion signal
   uint32_t pword[kQueueSize] = {};
-  const unsigned char* karg_dirty = nullptr;  // last kernarg byte written through the BAR, not yet flushed
+  const unsigned char* bar_dirty = nullptr;  // last byte written through the BAR (kernargs, inputs), not yet flushed
 
   void* slot(uint64_t idx) { return (char*)q->base_address + 64 * (idx & mask); }
-  // device-memory kernargs: out of the write-combining buffer and the HDP before the GPU reads them
-  // (the read-back completes only after every earlier posted write has landed)
+  // BAR writes (device-memory kernargs, bar_alloc inputs): out of the write-combining buffer and
+  // the HDP before the GPU reads them (the read-back completes only after every earlier posted
+  // write has landed)
   void flush_kargs() {
-    if (!karg_dirty) return;
+    if (!bar_dirty) return;
     _mm_sfence();
     *(volatile uint32_t*)d->hdp.HDP_MEM_FLUSH_CNTL = 1u;
-    (void)*(volatile const unsigned char*)karg_dirty;
-    karg_dirty = nullptr;
+    (void)*(volatile const unsigned char*)bar_dirty;
+    bar_dirty = nullptr;
   }
   void add_pending(uint64_t idx, uint32_t word) {
     if (p0 < 0) p0 = (int64_t)idx;
@@ -490,6 +490,25 @@ hipError_t done_query(const Done& d) {
   return hsa_signal_load_scacquire(hsa_signal_t{d.sig}) <= 0 ? hipSuccess : hipErrorNotReady;
 }
 
+void* bar_alloc(int dev, size_t bytes) {
+  std::lock_guard<std::mutex> lk(rt().mu);
+  DevRt* d = dev_rt(dev);
+  if (!d->ok || !d->have_dev_pool || !d->hdp.HDP_MEM_FLUSH_CNTL) return nullptr;
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(d->dev_pool, bytes, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  if (hsa_amd_agents_allow_access(1, &rt().cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+    hsa_amd_memory_pool_free(p);
+    return nullptr;
+  }
+  return p;
+}
+void bar_free(void* p) {
+  if (p) hsa_amd_memory_pool_free(p);
+}
+void lane_bar_written(const Lane& l, const void* last) {
+  if (l.q) l.q->bar_dirty = (const unsigned char*)last;
+}
+
 int hsa_kernel_id(const char* prefix) {
   const size_t n = std::strlen(prefix);
   for (int k = 0; k < kNCo; k++)
@@ -534,7 +553,7 @@ int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsi
   put64(9, 0), put64(10, 0), put64(11, 0);
   put16(12, 3);
   put32(13, dyn_lds);
-  if (q->karg_dev) q->karg_dirty = ka + k.karg - 1;
+  if (q->karg_dev) q->bar_dirty = ka + k.karg - 1;
   hsa_kernel_dispatch_packet_t* p = (hsa_kernel_dispatch_packet_t*)q->slot(idx);
   p->workgroup_size_x = (uint16_t)b.x;
   p->workgroup_size_y = (uint16_t)b.y;

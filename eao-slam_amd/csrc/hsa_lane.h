@@ -43,6 +43,13 @@ int lane_record(const Lane& l, Done& d);
 int lane_wait(const Lane& l, const Done& d);
 // hipSuccess (complete), hipErrorNotReady, or an error
 hipError_t done_query(const Done& d);
+// device memory the host writes directly through the BAR (write-combined; never read it back on
+// the host): nullptr when the device's memory is not host-visible
+void* bar_alloc(int dev, size_t bytes);
+void bar_free(void* p);
+// the host wrote BAR memory ending at `last` that launches on lane l read: the lane's next commit
+// flushes it (write-combining fence, HDP flush, read-back) before its doorbell
+void lane_bar_written(const Lane& l, const void* last);
 
 // the generated kernel table (gen_co.py)
 struct CoKernel {

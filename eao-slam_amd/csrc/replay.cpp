@@ -79,6 +79,12 @@ static const bool g_la_eager = [] {
   const char* v = getenv("EAO_LOOKAHEAD_EAGER");
   return v && v[0] == '1';
 }();
+// HSA lanes: a forest batch's packed inputs written straight into device memory through the BAR
+// instead of pinned memory + k_stage (EAO_BAR_INPUTS=0: A/B switch)
+static const bool g_bar_inputs = [] {
+  const char* v = getenv("EAO_BAR_INPUTS");
+  return !(v && v[0] == '0');
+}();
 static const bool g_sentinel = [] {
   const char* v = getenv("EAO_SENTINEL_WAIT");
   return !(v && v[0] == '0');
@@ -603,6 +609,10 @@ class ReplayEngine {
     Done done;  // the batch's launches complete (its lane's last packet / event)
     unsigned char *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
+    // HSA lanes: the packed inputs written by the host straight into device memory through the
+    // BAR (bar_alloc), so the batch needs no staging kernel
+    unsigned char* bar_in = nullptr;
+    size_t cap_bar = 0;
     double* contrib = nullptr;  // [50][max_points]
     // sharded: the per-rank record layout fixed at the launch (mask bytes, speculative
     // pairs, padded record size) and, in the device form, this rank's record in device
@@ -737,6 +747,7 @@ class ReplayEngine {
     }
     for (IfBatch& sl : ifb) {
       done_close(sl.done);
+      bar_free(sl.bar_in);
       if (sl.h_in) (void)hipHostFree(sl.h_in);
       if (sl.h_out) (void)hipHostFree(sl.h_out);
       if (sl.d_in) (void)hipFree(sl.d_in);
@@ -1345,26 +1356,40 @@ class ReplayEngine {
         fill64(b.h_out, (size_t)np);
         fill32(b.h_out + b.sp_out, (size_t)ns * (sizeof(eao_np_stats) / 4));
       }
-      int* meta = (int*)b.h_in;
-      float* pts = (float*)(b.h_in + o_pts);
+      // the packed inputs: pinned host memory staged by k_stage, or (HSA lanes) device memory
+      // written here through the BAR -- write-only (a host read of it is an uncached PCIe round trip)
+      unsigned char* hin = b.h_in;
+      unsigned char* din = b.d_in;
+      if (if_stream[k % kIfStreams].hsa() && g_bar_inputs) {
+        if (in_bytes > b.cap_bar) {
+          bar_free(b.bar_in);
+          b.cap_bar = 0;
+          const size_t c = std::max(in_bytes, 2 * b.cap_bar);
+          b.bar_in = (unsigned char*)bar_alloc(A->dev, c);
+          if (b.bar_in) b.cap_bar = c;
+        }
+        if (b.bar_in) hin = din = b.bar_in;
+      }
+      int* meta = (int*)hin;
+      float* pts = (float*)(hin + o_pts);
       for (int j = 0; j < nl; j++) {
         Obj* o = b.objs[b.lc[j]];
-        meta[j] = b.loff[b.lc[j]];
+        int w = b.loff[b.lc[j]];
+        meta[j] = w;
         meta[nl + j] = (int)o->pts.size();
         meta[2 * nl + j] = (int)o->pts.size() / 2;
-        int w = meta[j];
         for (MapPt* p : o->pts) {
           std::memcpy(&pts[3 * (size_t)w], p->pos, sizeof(float) * 3);
-          if (ns) b.h_in[o_oval + w] = p->bad ? 0 : 1;  // out_point is never set (Q7)
+          if (ns) hin[o_oval + w] = p->bad ? 0 : 1;  // out_point is never set (Q7)
           w++;
         }
       }
       if (ns) {
-        int* spm = (int*)(b.h_in + o_spm);
-        float* th = (float*)(b.h_in + o_th);
-        const double** osp = (const double**)(b.h_in + o_osp);
-        float* fpt = (float*)(b.h_in + o_fp);
-        uint8_t* fval = b.h_in + o_fval;
+        int* spm = (int*)(hin + o_spm);
+        float* th = (float*)(hin + o_th);
+        const double** osp = (const double**)(hin + o_osp);
+        float* fpt = (float*)(hin + o_fp);
+        uint8_t* fval = hin + o_fval;
         for (size_t z = 0; z < sdets.size(); z++) {
           int w = sdoff[z];
           for (MapPt* p : sdets[z]->pts) {
@@ -1384,8 +1409,8 @@ class ReplayEngine {
         }
       }
       if (xdev()) {
-        int* pk = (int*)(b.h_in + o_pk);
-        float* pth = (float*)(b.h_in + o_pkth);
+        int* pk = (int*)(hin + o_pk);
+        float* pth = (float*)(hin + o_pkth);
         size_t w = 0;
         for (int j = 0; j < nl; j++) {
           Obj* o = b.objs[b.lc[j]];
@@ -1402,29 +1427,32 @@ class ReplayEngine {
       prof[2] += 1;
       Tick tl(&prof[19]);
       // compute-queue staging (k_stage), as at the frame start: no DMA-engine hand-off
-      if (int rc0 = A->stage_in(b.d_in, b.h_in, in_bytes, st)) return rc0;
-      const int* dm = (const int*)b.d_in;
+      if (din == hin)
+        lane_bar_written(st, hin + in_bytes - 1);  // flushed before the batch's doorbell
+      else if (int rc0 = A->stage_in(din, hin, in_bytes, st))
+        return rc0;
+      const int* dm = (const int*)din;
       // scores go straight to pinned host memory (a device-to-host copy costs
       // ~35 us of round trip per launch on this box) and, for the speculative
       // NP pairs, to device memory too
-      int rc = A->iforest_batch(nl, (const float*)(b.d_in + o_pts), dm, dm + nl, 50, 12345,
+      int rc = A->iforest_batch(nl, (const float*)(din + o_pts), dm, dm + nl, 50, 12345,
                                 (const uint32_t*)(dm + 2 * nl), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
                                 (double*)b.d_out);
       if (rc) return rc;
       if (ns) {
-        const int* spm = (const int*)(b.d_in + o_spm);
-        const float* dfp = (const float*)(b.d_in + o_fp);
+        const int* spm = (const int*)(din + o_spm);
+        const float* dfp = (const float*)(din + o_fp);
         // device-form exchange: the stats go straight into this rank's record
         eao_np_stats* sp_dst = xdev() ? (eao_np_stats*)(b.d_x + al16(b.xmb[srank])) : (eao_np_stats*)(b.h_out + b.sp_out);
-        rc = A->np_batch(ns, dfp, b.d_in + o_fval, spm, spm + ns, (const float*)(b.d_in + o_pts), b.d_in + o_oval,
-                         spm + 2 * ns, spm + 3 * ns, sp_dst, st, max_olen, (const double* const*)(b.d_in + o_osp),
-                         (const float*)(b.d_in + o_th));
+        rc = A->np_batch(ns, dfp, din + o_fval, spm, spm + ns, (const float*)(din + o_pts), din + o_oval,
+                         spm + 2 * ns, spm + 3 * ns, sp_dst, st, max_olen, (const double* const*)(din + o_osp),
+                         (const float*)(din + o_th));
         if (rc) return rc;
         prof[9] += ns;
       }
       if (xdev()) {
-        const int* dpk = (const int*)(b.d_in + o_pk);
-        rc = A->pack_masks(nl, dpk, (const float*)(b.d_in + o_pkth), (const double*)b.d_out, b.d_x, st.s);
+        const int* dpk = (const int*)(din + o_pk);
+        rc = A->pack_masks(nl, dpk, (const float*)(din + o_pkth), (const double*)b.d_out, b.d_x, st.s);
         if (rc) return rc;
       }
       if (int rc1 = lane_record(st, b.done)) return rc1;

@@ -146,4 +146,13 @@ eager() {
   done > gpurun_out/r5_eager_probe.log 2>&1
 }
 
+# bar: forest batch inputs written through the BAR (no k_stage) against pinned + k_stage
+bar() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_assoc.py tests/test_gpu_chain.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_bar_tests.log 2>&1 &&
+  for r in 1 2; do
+    echo "## bar inputs" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## pinned + k_stage" && EAO_BAR_INPUTS=0 timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_bar_probe.log 2>&1
+}
+
 "$@"
