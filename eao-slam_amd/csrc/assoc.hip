@@ -1361,7 +1361,8 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
     sc = thb;
   }
   // each score stored once, final (the host's early-exit wait reads pinned `scores`; replay.cpp
-  // spin_ready, rules 1-3); the batch's pinned inputs were copied to the device by k_stage before
+  // spin_ready, rules 1-3); the batch's inputs were read by the tree kernel before (k_stage's copy
+  // of the pinned inputs, or the host's BAR writes on the HSA lanes)
   scores[g] = sc;
   if (scores2) scores2[g] = sc;
 }
