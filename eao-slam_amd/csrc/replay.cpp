@@ -85,6 +85,11 @@ static const bool g_bar_inputs = [] {
   const char* v = getenv("EAO_BAR_INPUTS");
   return !(v && v[0] == '0');
 }();
+// ... and the frame start's (EAO_BAR_FS=0: A/B switch)
+static const bool g_bar_fs = [] {
+  const char* v = getenv("EAO_BAR_FS");
+  return g_bar_inputs && !(v && v[0] == '0');
+}();
 static const bool g_sentinel = [] {
   const char* v = getenv("EAO_SENTINEL_WAIT");
   return !(v && v[0] == '0');
@@ -677,6 +682,8 @@ class ReplayEngine {
   // forest slots, streams and staging outlive the replay: the next replay on
   // the same engine adopts them (allocation is not per replay)
   Done gpu0;            // frame-start launch completion (spin-waited)
+  unsigned char* fs_bar = nullptr;  // the frame start's inputs in device memory (HSA lanes, BAR)
+  size_t cap_fs_bar = 0;
   bool rn_dev = false;  // rects_np_launch writes its outputs to d_out (device-form exchange)
   struct Pool {
     std::vector<IfBatch> ifb;
@@ -726,6 +733,7 @@ class ReplayEngine {
         std::fclose(f);
       }
     done_close(gpu0);
+    bar_free(fs_bar);
     if (A && !A->replay_pool && !ifb.empty()) {
       Pool* p = new Pool();
       p->ifb.swap(ifb);
@@ -1771,6 +1779,20 @@ class ReplayEngine {
     }
     int rc = stage(in_bytes, o_ok + nb);
     if (rc) return rc;
+    if (int rc0 = lanes_init()) return rc0;
+    // the packed inputs: pinned host memory the kernel reads in place, or (HSA lanes) device
+    // memory written here through the BAR -- write-only (never read back on the host)
+    unsigned char* hin = h_in;
+    if (lanes_hsa && g_bar_fs) {
+      if (in_bytes > cap_fs_bar) {
+        bar_free(fs_bar);
+        cap_fs_bar = 0;
+        const size_t c = std::max(in_bytes, 2 * cap_fs_bar);
+        fs_bar = (unsigned char*)bar_alloc(A->dev, c);
+        if (fs_bar) cap_fs_bar = c;
+      }
+      if (fs_bar) hin = fs_bar;
+    }
     // outputs: pinned host memory (read after the spin), or -- sharded, device-form
     // exchange -- this rank's record in device memory (d_out), all-gathered by the caller
     unsigned char* ob = rn_dev ? d_out : h_out;
@@ -1778,11 +1800,11 @@ class ReplayEngine {
       fill32(h_out, (size_t)npairs * (sizeof(eao_np_stats) / 4) + 4 * (size_t)nb);
       std::memset(h_out + o_ok, kSent8, (size_t)nb);
     }
-    int* rmeta = (int*)h_in;
-    int* pmeta = (int*)(h_in + o_pm);
-    float* pts = (float*)(h_in + o_pts);
-    uint8_t* valid = h_in + o_val;
-    std::memcpy(h_in + o_T, pz.T, sizeof(float) * 16);
+    int* rmeta = (int*)hin;
+    int* pmeta = (int*)(hin + o_pm);
+    float* pts = (float*)(hin + o_pts);
+    uint8_t* valid = hin + o_val;
+    std::memcpy(hin + o_T, pz.T, sizeof(float) * 16);
     {
       Tick tpk(&prof[54]);
       prof[55] += (double)total;
@@ -1800,19 +1822,20 @@ class ReplayEngine {
     int max_olen = 0;
     for (int k = 0; k < npairs; k++) {
       const auto& pr = pairs[k];
+      const int olen = (int)pr.second->pts.size();
       pmeta[k] = offs[pr.first];
       pmeta[npairs + k] = (int)pr.first->pts.size();
       pmeta[2 * npairs + k] = offs[pr.second];
-      pmeta[3 * npairs + k] = (int)pr.second->pts.size();
-      if (pmeta[3 * npairs + k] > NP_MAXN && !os_p[k]) {  // chained: the kernel checks after the erasure
+      pmeta[3 * npairs + k] = olen;
+      if (olen > NP_MAXN && !os_p[k]) {  // chained: the kernel checks after the erasure
         set_error("replay: object exceeds the NP kernel capacity");
         return EAO_E_CAPACITY;
       }
-      max_olen = std::max(max_olen, pmeta[3 * npairs + k]);
+      max_olen = std::max(max_olen, olen);
     }
     if (chained) {
-      const double** osp = (const double**)(h_in + o_osp);
-      float* oth = (float*)(h_in + o_oth);
+      const double** osp = (const double**)(hin + o_osp);
+      float* oth = (float*)(hin + o_oth);
       for (int b = 0; b < nb; b++) {
         osp[b] = os_l[b];
         oth[b] = th_l[b];
@@ -1826,7 +1849,6 @@ class ReplayEngine {
     // stream's last work (in-queue order: no cross-queue event wait on the chain, which
     // costs 10-25 us between the forest's end and this launch's start); the others, if
     // any, through event waits
-    if (int rc0 = lanes_init()) return rc0;
     Lane ls = lanes_hsa ? fs_lane : Lane(A->stream);
     int lk = -1;
     for (int k : wait_slots)
@@ -1838,11 +1860,11 @@ class ReplayEngine {
     for (int k : wait_slots)
       if (k != lk)
         if (int rc0 = lane_wait(ls, ifb[k].done)) return rc0;
-    // one launch reads the packed inputs in place from pinned host memory (a staging copy to
-    // device memory ahead of the forest waits leaves the kernel's duration unchanged,
-    // profiles/r05_ab_fs_stage_rejected.txt) and writes the results straight back into pinned
+    // one launch reads the packed inputs in place (pinned host memory, or the BAR-written device
+    // copy, flushed before the lane's doorbell) and writes the results straight back into pinned
     // host memory
-    const unsigned char* din = h_in;
+    const unsigned char* din = hin;
+    if (hin != h_in) lane_bar_written(ls, hin + in_bytes - 1);
     const int* drm = (const int*)din;
     const int* dpm = (const int*)(din + o_pm);
     const float* dpts = (const float*)(din + o_pts);

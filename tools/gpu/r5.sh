@@ -155,4 +155,13 @@ bar() {
   done > gpurun_out/r5_bar_probe.log 2>&1
 }
 
+# barfs: the frame start's inputs written through the BAR too (EAO_BAR_FS=0: pinned, read in place)
+barfs() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_chain.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_barfs_tests.log 2>&1 &&
+  for r in 1 2 3; do
+    echo "## bar fs" && timeout -k 10 200 python -u tools/replay_probe.py &&
+    echo "## pinned fs" && EAO_BAR_FS=0 timeout -k 10 200 python -u tools/replay_probe.py || exit 1
+  done > gpurun_out/r5_barfs_probe.log 2>&1
+}
+
 "$@"
