@@ -25,7 +25,7 @@ else:  # BASELINE configs[1]: the demo list, real detections
     frames, flag = synth.assoc_stream_fr3_real(), "EAO"
 packed = ea.Replay.pack(frames)
 a = ea.Assoc()
-for rep in range(3):
+for rep in range(int(os.environ.get("EAO_PROBE_PASSES", "3"))):
     rp = ea.Replay(a, flag)
     t0 = time.perf_counter()
     rp.run(packed)
