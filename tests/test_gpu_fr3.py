@@ -60,3 +60,18 @@ def test_fr3_full_2582():
     det = _check("replay_fr3_full.npz", 0, 2582)
     assert len(det) == 17204
     assert {1, 2, 3, 4, 5} <= set(det[:, 0].tolist())  # every association route is taken
+
+
+def test_fr3_demo_eao_405_hip_streams():
+    """The same replay with the association's launches on HIP streams (EAO_HSA_LANES=0) instead
+    of the HSA lanes (AQL packets, BAR-written inputs): the lane kind is fixed per process, so
+    the check runs in one child process."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_fr3 as t; "
+            "t._check('replay_fr3_demo_eao.npz', None, None); print('ok')"
+            % (root, os.path.join(root, "tests"), os.path.join(root, "eao-slam_amd", "python")))
+    env = dict(os.environ, EAO_HSA_LANES="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout[-2000:] + r.stderr[-2000:]
