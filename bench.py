@@ -377,12 +377,15 @@ def main():
     def associate(out):
         # the previous pass's replay is torn down first, so its forest slots, streams and
         # pinned staging pass to this one (eao_replay_destroy hands them to the engine)
+        t0 = time.perf_counter()
         if last["replay"] is not None:
             last["replay"].close()
         rp = ea.Replay(assoc, cfg["flag"])
         last["replay"] = rp
+        t1 = time.perf_counter()
         out["det"] = rp.run(packed)  # eao_replay_run: frame-by-frame association + local mapping
         out["replay"] = rp  # object state read back after the timed region
+        out["t_setup"], out["t_run"] = t1 - t0, time.perf_counter() - t1
 
     orb.set_timing(True)
     ev_g0, ev_g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -408,7 +411,9 @@ def main():
         if not args.thread:
             # the frame work is only enqueued (asynchronous launches on the extraction stream),
             # so it runs on the GPU while this thread replays the association, the critical path
+            tf = time.perf_counter()
             front()
+            out["t_front"] = time.perf_counter() - tf
             associate(out)
         else:
             # A/B: the association on a second Python thread (it waits for the GIL while the
@@ -426,6 +431,7 @@ def main():
             th.join()
         ev_done.synchronize()
         if record is not None:
+            record["split"].append([out.get("t_front", 0.0), out["t_setup"], out["t_run"]])
             record["stage_ms"].append(orb.stage_ms())
             record["match_ms"].append(ev_m0.elapsed_time(ev_m1))
             record["gray_ms"].append(ev_g0.elapsed_time(ev_g1))
@@ -435,7 +441,7 @@ def main():
     for _ in range(args.warmup):
         step(None)
 
-    rec = {"stage_ms": [], "match_ms": [], "gray_ms": [], "lines_ms": []}
+    rec = {"stage_ms": [], "match_ms": [], "gray_ms": [], "lines_ms": [], "split": []}
     eao_dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -504,6 +510,10 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": dom_bytes * F, "avg_launch_ms": float(stage[dom])},
             "stages_ms_per_step": {n: float(v) for n, v in zip(STAGES, stage)},
+            # host time of the step's parts (ms): enqueueing the frame work, tearing down the last
+            # replay and creating this one, eao_replay_run
+            "step_split_ms": dict(zip(("front_enqueue", "replay_setup", "replay_run"),
+                                      (float(v) * 1e3 for v in np.mean(np.array(rec["split"]), 0)))),
             "roofline_valu": valu_roof(KERNELS[dom_name], F, float(stage[dom])),
             "extract_ms_per_step": ext_ms,
             "extract_fps": F / (ext_ms * 1e-3),
