@@ -3226,6 +3226,21 @@ class ReplayEngine {
     } tr_end{this};
     phase = 3;
     int rc;
+    // ComputeMeanAndStandard of every object with >= 10 points (LocalMapping.cc:772-790), after
+    // the pending forests complete. An object without a forest in flight is not touched by the
+    // flush (a completion changes only its own object's points and cuboid, and other objects'
+    // projected rects / reobj votes), so its statistics are computed first, while the forests
+    // still run on the GPU; the others after their completion. Same values, same per-object order.
+    std::vector<char> ms_done(objs.size(), 0);
+    {
+      Tick t1(&prof[25]);
+      for (size_t i = 0; i < objs.size(); i++) {
+        Obj* o = objs[i].get();
+        if (o->pending || o->pts.size() < 10 || o->bad) continue;
+        mean_std(o);
+        ms_done[i] = 1;
+      }
+    }
     {
       Tick t0(&prof[24]);
       rc = flush(-1);
@@ -3233,9 +3248,9 @@ class ReplayEngine {
     if (rc) return rc;
     {
       Tick t1(&prof[25]);
-      for (auto& up : objs) {
-        Obj* o = up.get();
-        if (o->pts.size() < 10 || o->bad) continue;
+      for (size_t i = 0; i < objs.size(); i++) {
+        Obj* o = objs[i].get();
+        if (ms_done[i] || o->pts.size() < 10 || o->bad) continue;
         mean_std(o);
       }
     }
