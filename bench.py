@@ -155,12 +155,12 @@ def _pmc_value(fname, kernel, counter):
     return None
 
 
-PMC_FILES = {"fetch": "r05b_pmc_fetch.txt", "write": "r05b_pmc_write.txt", "sq": "r05b_pmc_sq.txt"}
+PMC_FILES = {"fetch": "r05d_pmc_fetch.txt", "write": "r05d_pmc_write.txt", "sq": "r05d_pmc_sq.txt"}
 
 
 def pmc_valu(kernel, frames):
     """VALU lane-ops per launch of `kernel` from the committed SQ counter pass
-    (profiles/r05b_pmc_sq.txt: SQ_INSTS_VALU wave instructions x 64 lanes) over the same
+    (profiles/r05d_pmc_sq.txt: SQ_INSTS_VALU wave instructions x 64 lanes) over the same
     405-frame launch -- a profiled figure of the same launch shape, not a measurement of
     this run; None for another shape or when the summary is absent."""
     if frames != 405:
