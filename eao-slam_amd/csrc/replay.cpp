@@ -688,6 +688,8 @@ class ReplayEngine {
   struct Pool {
     std::vector<IfBatch> ifb;
     Lane if_stream[kIfStreams], fs_lane;
+    unsigned char* fs_bar = nullptr;
+    size_t cap_fs_bar = 0;
     unsigned char *h_in = nullptr, *d_in = nullptr, *h_out = nullptr, *d_out = nullptr;
     size_t cap_in = 0, cap_out = 0;
   };
@@ -697,6 +699,7 @@ class ReplayEngine {
     tmp.ifb.swap(p->ifb);
     for (int k = 0; k < kIfStreams; k++) tmp.if_stream[k] = p->if_stream[k];
     tmp.fs_lane = p->fs_lane;
+    tmp.fs_bar = p->fs_bar;
     tmp.h_in = p->h_in;
     tmp.d_in = p->d_in;
     tmp.h_out = p->h_out;
@@ -716,6 +719,8 @@ class ReplayEngine {
     }
     for (int k = 0; k < kIfStreams; k++) if_stream[k] = p->if_stream[k];
     fs_lane = p->fs_lane;
+    fs_bar = p->fs_bar;
+    cap_fs_bar = p->cap_fs_bar;
     h_in = p->h_in;
     d_in = p->d_in;
     h_out = p->h_out;
@@ -733,7 +738,6 @@ class ReplayEngine {
         std::fclose(f);
       }
     done_close(gpu0);
-    bar_free(fs_bar);
     if (A && !A->replay_pool && !ifb.empty()) {
       Pool* p = new Pool();
       p->ifb.swap(ifb);
@@ -743,6 +747,9 @@ class ReplayEngine {
       }
       p->fs_lane = fs_lane;
       fs_lane = Lane();
+      p->fs_bar = fs_bar;
+      p->cap_fs_bar = cap_fs_bar;
+      fs_bar = nullptr;
       p->h_in = h_in;
       p->d_in = d_in;
       p->h_out = h_out;
@@ -765,6 +772,7 @@ class ReplayEngine {
     }
     for (Lane& st : if_stream) lane_close(st);
     lane_close(fs_lane);
+    bar_free(fs_bar);  // (null when handed to the engine's pool above)
     if (h_in) (void)hipHostFree(h_in);
     if (h_out) (void)hipHostFree(h_out);
     if (d_in) (void)hipFree(d_in);
