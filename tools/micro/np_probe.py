@@ -12,8 +12,11 @@ import eao_accel as ea  # noqa: E402
 
 a = ea.Assoc()
 rng = np.random.default_rng(0)
-for m, n in ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500), (30, 8000), (100, 5000), (300, 7000),
-             (60, 2000)):
+SIZES = ((30, 100), (60, 300), (120, 500), (200, 1200), (300, 2500), (30, 8000), (100, 5000), (300, 7000),
+         (60, 2000))
+if len(sys.argv) > 1:  # "m,n m,n ..." (e.g. the fr3 frame-start pairs: 74,1162 175,1162 300,1162)
+    SIZES = tuple(tuple(int(x) for x in a.split(",")) for a in sys.argv[1:])
+for m, n in SIZES:
     pairs = []
     for _ in range(4):
         f = rng.normal(0, 0.1, (m, 3)).astype(np.float32)
