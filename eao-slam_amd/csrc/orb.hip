@@ -97,6 +97,7 @@ __global__ __launch_bounds__(256) void k_resize_tile(const uint8_t* __restrict__
 // Items are numbered column-group-fastest, so a wave's stores cover 256 contiguous bytes.
 // Arithmetic identical to k_resize_tile (OpenCV INTER_LINEAR 8U, ORBextractor.cc:1120).
 constexpr int RESIZE_RS = 4;
+constexpr int RESIZE_IPT = 4;  // items per thread of a k_resize_lds tile (OrbEngine::plan)
 __device__ __forceinline__ int resize_src_row(int dy, double scale_y, int sh, int k) {
   const float fy = (float)((dy + 0.5) * scale_y - 0.5);  // OrbEngine::plan's resize_yrows
   return min(max((int)floorf(fy) + k, 0), sh - 1);
@@ -124,6 +125,58 @@ __device__ __forceinline__ void resize_item_load(ResizeItem& I, int g, int e0, i
     I.b[k] = *(const int*)(ibeta + 2 * dy);
   }
 }
+// the rows [e0, e1) of an item from a source image in LDS (row r at img + (r - ys0) * stride, one
+// readable byte past every row): the last two source rows' horizontal sums kept; put(dy, w) takes
+// the 4 output bytes of row dy. `one` is 1: a kernel argument where the compiler would otherwise
+// merge a tap pair into one unaligned ds_read_u16 (k_pyr_tail: 2.5x slower)
+template <class Put>
+__device__ __forceinline__ void resize_item_rows(const ResizeItem& I, const unsigned char* img, int ys0, int stride,
+                                                 int e0, int e1, int one, Put put) {
+  auto hsum = [&](int r, int (&h)[4]) {
+    const unsigned char* row = img + (r - ys0) * stride;
+#pragma unroll
+    for (int u = 0; u < 4; u++) h[u] = row[I.sx[u]] * (I.a[u] & 0xffff) + row[I.sx[u] + one] * (I.a[u] >> 16);
+  };
+  int ra = -1, rb = -1, ha[4], hb[4];
+#pragma unroll
+  for (int k = 0; k < RESIZE_RS; k++) {
+    const int dy = e0 + k;
+    if (dy >= e1) break;
+    const int r0 = I.r[k] & 0xffff, r1 = I.r[k] >> 16;
+    int d0[4], d1[4];
+    if (r0 == rb) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) d0[u] = hb[u];
+    } else if (r0 == ra) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) d0[u] = ha[u];
+    } else {
+      hsum(r0, d0);
+    }
+    if (r1 == rb) {
+#pragma unroll
+      for (int u = 0; u < 4; u++) d1[u] = hb[u];
+    } else {
+      hsum(r1, d1);
+    }
+    uint32_t w = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      // no saturation: 0 <= v <= 255 already (taps >= 0, a0 + a1 <= 2049, b0 + b1 <= 2049:
+      // v <= (255 * 2049^2 + 2^21) >> 22 = 255), and the clamp made the compiler pack two
+      // bytes with v_ashr_pk_u8_i32, whose result's upper half is not zero on gfx950: the
+      // v_lshl_or of bytes 2 / 3 then OR'ed stale bits into them (round-5 miscompile)
+      const uint32_t v = (uint32_t)(d0[u] * (I.b[k] & 0xffff) + d1[u] * (I.b[k] >> 16) + (1 << 21)) >> 22;
+      w |= v << (8 * u);
+      ha[u] = d0[u];
+      hb[u] = d1[u];
+    }
+    ra = r0;
+    rb = r1;
+    put(dy, w);
+  }
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__ src, int spitch, long long sstride,
                                                      uint8_t* __restrict__ dst, int dpitch, long long dstride,
@@ -191,49 +244,97 @@ __global__ __launch_bounds__(1024) void k_resize_lds(const uint8_t* __restrict__
       seg_rows(it, g, e0, e1);
       resize_item_load(I, g, e0, e1, dw, xmax, xofs, ialpha, yrows, ibeta);
     }
-    auto hsum = [&](int r, int (&h)[4]) {
-      const uint8_t* row = smem + (r - ys0) * sw16;
+    resize_item_rows(I, smem, ys0, sw16, e0, e1, 1,
+                     [&](int dy, uint32_t w) { *(uint32_t*)(df + (long long)dy * dpitch + 4 * g) = w; });
+  }
+}
+
+// The pyramid's small levels in one launch (OrbEngine::plan's tail_a): one workgroup per frame
+// makes levels [a, nl) from level a - 1, whose plane is staged in LDS; each level is computed
+// from the previous level's LDS image (items of 4 columns x RESIZE_RS rows, column-group fastest,
+// as k_resize_lds) and stored to its plane and, for the next level, into the other LDS image
+// (images ping-pong between offsets 0 and img_b; one readable byte past each). The levels' resize
+// tables (contiguous from level a: nx column and ny row entries) are staged in LDS at tab_b with the
+// source image. Launched per level, these levels were latency: 62 us of the 640x480 pyramid's
+// 0.30 ms for 15 % of its bytes.
+__global__ __launch_bounds__(1024) void k_pyr_tail(uint8_t* __restrict__ pyr, long long pstride,
+                                                   const LevelDev* __restrict__ lv, int a, int nl, int img_b,
+                                                   int tab_b, int nx, int ny, int one, const int* __restrict__ xofs,
+                                                   const short* __restrict__ ialpha, const int* __restrict__ yrows,
+                                                   const short* __restrict__ ibeta) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, nb = blockDim.x;
+  uint8_t* pf = pyr + (long long)blockIdx.x * pstride;
+  const int tx0 = lv[a].tab_x, ty0 = lv[a].tab_y;
+  int* sX = (int*)(smem + tab_b);
+  int* sIA = sX + nx;  // (a0, a1) pairs
+  int2* sY = (int2*)(sIA + nx);
+  int* sIB = (int*)(sY + ny);  // (b0, b1) pairs
+  // a workgroup's time is its chain of memory round trips: every staging load (tables and image,
+  // up to 8 16-byte chunks per thread) is issued before the first LDS store
+  int cs = 0;  // the current image's row stride
+  {
+    const LevelDev S = lv[a - 1];
+    cs = (S.w + 15) & ~15;
+    const int cpr = cs >> 4, nc = S.h * cpr;
+    const uint8_t* sp = pf + S.plane_off;
+    const bool hx = tid < nx, hy = tid < ny;
+    const int tX = hx ? xofs[tx0 + tid] : 0, tA = hx ? *(const int*)(ialpha + 2 * (tx0 + tid)) : 0;
+    const int2 tY = hy ? *(const int2*)(yrows + 2 * (ty0 + tid)) : make_int2(0, 0);
+    const int tB = hy ? *(const int*)(ibeta + 2 * (ty0 + tid)) : 0;
+    for (int c = tid; c < nc; c += 8 * nb) {
+      uint4 v[8];
 #pragma unroll
-      for (int u = 0; u < 4; u++) h[u] = row[I.sx[u]] * (I.a[u] & 0xffff) + row[I.sx[u] + 1] * (I.a[u] >> 16);
-    };
-    int ra = -1, rb = -1, ha[4], hb[4];
-#pragma unroll
-    for (int k = 0; k < RESIZE_RS; k++) {
-      const int dy = e0 + k;
-      if (dy >= e1) break;
-      const int r0 = I.r[k] & 0xffff, r1 = I.r[k] >> 16;
-      int d0[4], d1[4];
-      if (r0 == rb) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) d0[u] = hb[u];
-      } else if (r0 == ra) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) d0[u] = ha[u];
-      } else {
-        hsum(r0, d0);
+      for (int u = 0; u < 8; u++) {
+        const int cc = min(c + u * nb, nc - 1), r = cc / cpr, k = cc - r * cpr;
+        v[u] = *(const uint4*)(sp + (long long)r * S.pitch + 16 * k);
       }
-      if (r1 == rb) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) d1[u] = hb[u];
-      } else {
-        hsum(r1, d1);
-      }
-      uint32_t w = 0;
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        // no saturation: 0 <= v <= 255 already (taps >= 0, a0 + a1 <= 2049, b0 + b1 <= 2049:
-        // v <= (255 * 2049^2 + 2^21) >> 22 = 255), and the clamp made the compiler pack two
-        // bytes with v_ashr_pk_u8_i32, whose result's upper half is not zero on gfx950: the
-        // v_lshl_or of bytes 2 / 3 then OR'ed stale bits into them (round-5 miscompile)
-        const uint32_t v = (uint32_t)(d0[u] * (I.b[k] & 0xffff) + d1[u] * (I.b[k] >> 16) + (1 << 21)) >> 22;
-        w |= v << (8 * u);
-        ha[u] = d0[u];
-        hb[u] = d1[u];
-      }
-      ra = r0;
-      rb = r1;
-      *(uint32_t*)(df + (long long)dy * dpitch + 4 * g) = w;
+      for (int u = 0; u < 8; u++)
+        if (c + u * nb < nc) ((uint4*)smem)[c + u * nb] = v[u];
     }
+    if (hx) {
+      sX[tid] = tX;
+      sIA[tid] = tA;
+    }
+    if (hy) {
+      sY[tid] = tY;
+      sIB[tid] = tB;
+    }
+    for (int i = nb + tid; i < nx; i += nb) {  // (levels wider than a workgroup)
+      sX[i] = xofs[tx0 + i];
+      sIA[i] = *(const int*)(ialpha + 2 * (tx0 + i));
+    }
+    for (int i = nb + tid; i < ny; i += nb) {
+      sY[i] = *(const int2*)(yrows + 2 * (ty0 + i));
+      sIB[i] = *(const int*)(ibeta + 2 * (ty0 + i));
+    }
+  }
+  __syncthreads();
+  unsigned char* cur = smem;
+  unsigned char* nxt = smem + img_b;
+  for (int l = a; l < nl; l++) {
+    const LevelDev L = lv[l];
+    const int ds = (L.w + 15) & ~15;
+    const int G = (L.w + 3) >> 2, nit = G * ((L.h + RESIZE_RS - 1) / RESIZE_RS);
+    uint8_t* dp = pf + L.plane_off;
+    const bool keep = l + 1 < nl;
+    for (int it = tid; it < nit; it += nb) {
+      const int seg = it / G, g = it - seg * G;
+      const int e0 = seg * RESIZE_RS, e1 = min(e0 + RESIZE_RS, L.h);
+      ResizeItem I;
+      resize_item_load(I, g, e0, e1, L.w, L.xmax, sX + (L.tab_x - tx0), (const short*)(sIA + (L.tab_x - tx0)),
+                       (const int*)(sY + (L.tab_y - ty0)), (const short*)(sIB + (L.tab_y - ty0)));
+      resize_item_rows(I, cur, 0, cs, e0, e1, one, [&](int dy, uint32_t w) {
+        *(uint32_t*)(dp + (long long)dy * L.pitch + 4 * g) = w;
+        if (keep) *(uint32_t*)(nxt + dy * ds + 4 * g) = w;
+      });
+    }
+    __syncthreads();
+    unsigned char* t = cur;
+    cur = nxt;
+    nxt = t;
+    cs = ds;
   }
 }
 
@@ -1316,27 +1417,61 @@ int OrbEngine::plan(const eao_orb_params& prm, int device) {
   }
   pyr_bytes = (long long)((poff + 255) & ~255LL);
   // k_resize_lds tiles: RESIZE_RS-row segments of 4-column groups, up to 4 segments per tile while
-  // a tile's items fit one 1024-thread workgroup; LDS = the tile's source rows (+16 B: a tap past
+  // a tile's items fit RESIZE_IPT per thread of a 1024-thread workgroup; a workgroup of a quarter of
+  // the tile's items (4 per thread: 3-wave workgroups at 640x480's level 1) -- more workgroups per CU,
+  // so more tiles' loads in flight: 0.257 -> 0.238 ms per 405 frames at 640x480, 1.19 -> 0.94 ms per
+  // 256 at 1920x1080 (2 / 3 / 6 / 8 items per thread and 2 / 3 / 8 segments measured slower,
+  // profiles/r05_ab_resize_items_per_thread.txt); LDS = the tile's source rows (+16 B: a tap past
   // the last row's end is read with coefficient 0)
   resize_plan.assign(nl, ResizePlan{});
   for (int l = 1; l < nl; l++) {
     const LevelDev& L = levels[l];
     const int G = (L.w + 3) / 4;
-    const int segs = std::max(1, std::min(4, 1024 / G));
     ResizePlan& R = resize_plan[l];
-    R.tr = RESIZE_RS * segs;
-    R.tiles = (L.h + R.tr - 1) / R.tr;
-    R.block = std::min(1024, (G * segs + 63) / 64 * 64);
-    int rows = 0;
-    for (int t = 0; t < R.tiles; t++) {
-      const int d0 = t * R.tr, d1 = std::min(d0 + R.tr, L.h);
-      rows = std::max(rows, resize_yrows[2 * (L.tab_y + d1 - 1) + 1] - resize_yrows[2 * (L.tab_y + d0)] + 1);
+    for (int segs = std::max(1, std::min(4, 1024 * RESIZE_IPT / G)); segs >= 1; segs--) {  // fewer if too wide
+      R.tr = RESIZE_RS * segs;
+      R.tiles = (L.h + R.tr - 1) / R.tr;
+      R.block = std::min(1024, ((G * segs + RESIZE_IPT - 1) / RESIZE_IPT + 63) / 64 * 64);
+      int rows = 0;
+      for (int t = 0; t < R.tiles; t++) {
+        const int d0 = t * R.tr, d1 = std::min(d0 + R.tr, L.h);
+        rows = std::max(rows, resize_yrows[2 * (L.tab_y + d1 - 1) + 1] - resize_yrows[2 * (L.tab_y + d0)] + 1);
+      }
+      R.lds = (size_t)rows * ((levels[l - 1].w + 15) & ~15) + 16;
+      if (R.lds <= 64 * 1024) break;
     }
-    R.lds = (size_t)rows * ((levels[l - 1].w + 15) & ~15) + 16;
     if (R.lds > 64 * 1024) {
       set_error("eao_orb_create: image too wide for the pyramid kernel's LDS tile");
       return EAO_E_ARG;
     }
+  }
+  // k_pyr_tail: from the first level a >= 2 whose source level and itself fit LDS together (the
+  // later levels are smaller: they ping-pong in the same two images); EAO_PYR_TAIL=0: per-level
+  // launches throughout (A/B switch)
+  {
+    static const bool tail_ok = [] {
+      const char* v = getenv("EAO_PYR_TAIL");
+      return !(v && v[0] == '0');
+    }();
+    auto img = [&](int l) { return (size_t)((levels[l].w + 15) & ~15) * levels[l].h + 16; };
+    tail_a = nl;
+    for (int a = 2; tail_ok && a < nl; a++)
+      if (img(a - 1) + img(a) <= 160 * 1024 - 64) {
+        tail_a = a;
+        tail_img_b = (int)((img(a - 1) + 15) & ~(size_t)15);
+        tail_tab_b = (int)((tail_img_b + img(a) + 15) & ~(size_t)15);
+        tail_nx = tail_ny = 0;
+        for (int l = a; l < nl; l++) {
+          tail_nx += levels[l].w;
+          tail_ny += levels[l].h;
+        }
+        tail_lds = tail_tab_b + 8 * (size_t)tail_nx + 12 * (size_t)tail_ny;
+        if (tail_lds > 160 * 1024 - 64) {
+          tail_a = nl;
+          continue;
+        }
+        break;
+      }
   }
   {
     // FAST bands: the cells of a level row share their ROI rows
@@ -1445,6 +1580,13 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
     return v && v[0] == '0' ? 0 : 1;
   }();
   for (int l = 1; l < nl; l++) {
+    if (resize_lds && l == tail_a) {  // the small levels: one launch
+      hipLaunchKernelGGL(k_pyr_tail, dim3(nframes), dim3(1024), tail_lds, s, d_pyr, pyr_bytes,
+                         (const LevelDev*)d_levels, tail_a, nl, tail_img_b, tail_tab_b, tail_nx, tail_ny, 1,
+                         (const int*)d_xofs, (const short*)d_ia,
+                         (const int*)d_yrows, (const short*)d_ib);
+      break;
+    }
     const LevelDev& L = levels[l];
     const LevelDev& S = levels[l - 1];
     const uint8_t* src = l == 1 ? d_frames : d_pyr + S.plane_off;

@@ -34,10 +34,11 @@ def test_pyramid_exact(frames):
         assert np.array_equal(a, b), "level %d differs at %d px" % (l, int((a != b).sum()))
 
 
-@pytest.mark.parametrize("w,h", [(641, 481), (1000, 700), (1280, 720), (1920, 1080), (3840, 2160)])
+@pytest.mark.parametrize("w,h", [(641, 481), (320, 240), (800, 600), (1000, 700), (1280, 720), (1920, 1080), (3840, 2160)])
 def test_pyramid_exact_sizes(w, h):
     # k_resize_lds: unaligned rows (odd widths: byte staging of level 0), a partial last column
-    # group / row tile, wide levels with one 4-row segment per 1024-thread tile (4K)
+    # group / row tile, wide levels with one 4-row segment per 1024-thread tile (4K); k_pyr_tail:
+    # levels 2-7 (320x240), 5-7 (641x481), 6-7 (800x600), 7 (1000x700), none (1280x720 and up)
     img = np.random.default_rng(w + h).integers(0, 256, (h, w), dtype=np.uint8)
     orb = ea.Orb(width=w, height=h, nfeatures=2000)
     g = orb.pyramid(img)

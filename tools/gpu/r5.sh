@@ -164,4 +164,26 @@ barfs() {
   done > gpurun_out/r5_barfs_probe.log 2>&1
 }
 
+# ptail: the pyramid's small levels in one k_pyr_tail launch: ORB parity, stage times against
+# EAO_PYR_TAIL=0 (per-level launches), alternating, and the kernels' durations (rocprofv3)
+ptail() {
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_orb.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_ptail_tests.log 2>&1 &&
+  for r in 1 2 3; do
+    echo "## tail" && timeout -k 10 200 python -u tools/orb_stages.py &&
+    echo "## per-level" && EAO_PYR_TAIL=0 timeout -k 10 200 python -u tools/orb_stages.py || exit 1
+  done > gpurun_out/r5_ptail_stages.log 2>&1 &&
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/ptail_prof -o run -- python3 $GRAFT_REPO_ROOT/tools/orb_stages.py --reps 2 > $GRAFT_REPO_ROOT/gpurun_out/r5_ptail_prof.log 2>&1)
+}
+
+# ipt: k_resize_lds with 1 / 2 / 3 items per thread (smaller workgroups, more of them per CU)
+ipt() {
+  for r in 1 2; do
+    for k in "1 4" "3 4" "4 4" "6 4" "8 4" "4 2" "4 3"; do
+      set -- $k
+      echo "## ipt $1 segs $2" && EAO_RESIZE_IPT=$1 EAO_RESIZE_SEGS=$2 timeout -k 10 200 python -u tools/orb_stages.py || exit 1
+    done
+  done > gpurun_out/r5_ipt_stages.log 2>&1 &&
+  EAO_RESIZE_IPT=4 timeout -k 10 400 python -u -m pytest tests/test_gpu_orb.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_ipt_tests.log 2>&1
+}
+
 "$@"
