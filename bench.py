@@ -124,7 +124,7 @@ def algorithmic_bytes(n_kps):
 
 
 STAGES = ["pyramid", "fast", "distribute", "describe"]  # the level blur is fused into k_describe
-KERNELS = {"pyramid": "k_resize_tile (x7)", "fast": "k_fast_band", "distribute": "k_distribute",
+KERNELS = {"pyramid": "k_resize_lds (x4) + k_pyr_tail", "fast": "k_fast_band", "distribute": "k_distribute",
            "describe": "k_describe"}
 
 
@@ -510,6 +510,14 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": dom_bytes * F, "avg_launch_ms": float(stage[dom])},
             "stages_ms_per_step": {n: float(v) for n, v in zip(STAGES, stage)},
+            # the pyramid's own line (HBM-bound: every level read once and written once; its launches
+            # are timed together, so no per-launch traffic here -- the per-level PMC passes are in
+            # profiles/r05_pmc_fetch.txt / r05_pmc_write.txt)
+            "roofline_pyramid": {"bound": "hbm", "kernel": KERNELS["pyramid"],
+                                 "achieved": ab["pyramid"] * F / (float(stage[0]) * 1e-3) / 1e9,
+                                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                 "frac": ab["pyramid"] * F / (float(stage[0]) * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                                 "algorithmic_bytes_per_step": ab["pyramid"] * F, "ms_per_step": float(stage[0])},
             # host time of the step's parts (ms): enqueueing the frame work, tearing down the last
             # replay and creating this one, eao_replay_run
             "step_split_ms": dict(zip(("front_enqueue", "replay_setup", "replay_run"),
