@@ -237,6 +237,9 @@ def main():
                     help="A/B: CU-mask bit order (interleaved: bit i = CU i / 8 of XCD i % 8)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame drop-in leg (dropin_leg)")
     ap.add_argument("--dropin-frames", type=int, default=405, help="frames of the per-frame drop-in leg")
+    ap.add_argument("--chain-frames", type=int, default=120,
+                    help="frames of the chained leg (tools/chain.py: the association on the same frames' own "
+                         "keypoints and matches); 0 skips it")
     args = ap.parse_args()
     if args.cpu_frames is None:
         args.cpu_frames = 3 if args.config == "b" else 60
@@ -556,12 +559,70 @@ def main():
         result["dropin_per_frame"] = dropin_leg(ea, gpu, assoc_frames[:kd], d_color[:kd].cpu().numpy(),
                                                 d_frames[:kd].cpu().numpy(), poses[:kd], cfg["flag"],
                                                 check=not args.no_cpu_baseline)
+    if rank == 0 and world == 1 and not args.no_dropin and args.chain_frames > 0:
+        result["chained_per_frame"] = chained_leg(ea, args.chain_frames, check=not args.no_cpu_baseline)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result, default=float), flush=True)
     return 0
+
+
+def chained_leg(ea, n, check=True):
+    """The hot path chained on its own data, one frame at a time (tools/chain.py, as Tracking
+    chains it: src/Tracking.cc:1266-1281, 2434-2468): frame t's ORB extraction -> the motion
+    search against frame t-1's tracked map points -> the matched keypoints, with the map points
+    they carry, into frame t's object association (LocalMapping's object pass at keyframes). The
+    batched step above replays recorded fr3 observations; here the association consumes what the
+    same frames' extraction and matching produced. Host clock per call; every stage's outputs
+    checked against the oracle running the same chain (check)."""
+    from tools import chain
+
+    class Timed(chain.EngineBackend):
+        def __init__(self):
+            super().__init__(ea)
+            self.ms = {"extract": [], "match": [], "assoc": []}
+
+        def _t(self, k, f, *a):
+            t0 = time.perf_counter()
+            r = f(*a)
+            self.ms[k].append((time.perf_counter() - t0) * 1e3)
+            return r
+
+        def extract(self, g):
+            return self._t("extract", super().extract, g)
+
+        def match(self, *a):
+            return self._t("match", super().match, *a)
+
+        def replay_frame(self, *a):
+            return self._t("assoc", super().replay_frame, *a)
+
+        def local_mapping(self):
+            return self._t("assoc", super().local_mapping)
+
+    chain.run(chain.EngineBackend(ea), 3)  # warm every entry point
+    be = Timed()
+    g = chain.run(be, n)
+    call_s = sum(float(np.sum(v)) for v in be.ms.values()) * 1e-3
+    res = {"frames": n, "frames_per_s": n / call_s,
+           "ms_per_frame": {k: float(np.sum(v)) / n for k, v in be.ms.items()},
+           "matches_per_frame": float(np.mean([f["nmatch"] for f in g[1:]])),
+           "data": "tools/chain.py: synth's textured plane along synth.camera_path, map points back-projected "
+                   "at keyframes, boxes projected from object regions; host buffers, one frame per call; "
+                   "frames_per_s over the calls' time (the caller's frame rendering and map bookkeeping "
+                   "excluded)"}
+    if check:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as orc  # checker only
+        o = chain.run(chain.OracleBackend(orc), n)
+        bad = [t for t, (a, b) in enumerate(zip(g, o))
+               if not (np.array_equal(a["kps"], b["kps"]) and np.array_equal(a["desc"], b["desc"])
+                       and a["nmatch"] == b["nmatch"] and np.array_equal(a["match"], b["match"])
+                       and np.array_equal(a["ids"], b["ids"]) and np.array_equal(a["det"], b["det"]))]
+        res["parity"] = {"frames_checked": n, "frames_differing": bad[:10], "all_equal": not bad}
+    return res
 
 
 def bow_leg(ea, torch, stream, F, cap, gpu, d_kps, d_desc, d_cnt, kps, cnt, with_cpu=True, reps=3):
