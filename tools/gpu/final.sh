@@ -1,7 +1,7 @@
 # Closing measurements of a round (prefix P): GPU suite, smoke, EAO bench (+ kernel trace), Config C
 # sharded at world 1, Full, Config B, replay probe, FAST counter passes (FETCH / WRITE / SQ).
 set -o pipefail
-P=${P:-r4}
+P=${P:-r5}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rs > gpurun_out/${P}_gputest.log 2>&1 &&
