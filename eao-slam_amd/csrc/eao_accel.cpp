@@ -154,7 +154,12 @@ int eao_orb_debug_pyramid(eao_orb* h, const uint8_t* gray, uint8_t* out) {
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   const int w = e.p.width, hh = e.p.height;
   EAO_HIP_CHECK(hipMemcpy(e.d_img, gray, (size_t)w * hh, hipMemcpyHostToDevice));
+  // the batch form of the pyramid (k_pyr_tail for the small levels) on this one image; the
+  // single-frame extraction's per-level form is checked through its keypoints / descriptors
+  const int keep = e.tail_min_frames;
+  e.tail_min_frames = 1;
   int rc = e.run(e.d_img, 1, w, e.d_out_kps, e.d_out_desc, e.d_out_cnt, e.cap, e.stream);
+  e.tail_min_frames = keep;
   if (rc) return rc;
   EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
   std::memcpy(out, gray, (size_t)w * hh);

@@ -66,6 +66,7 @@ class OrbEngine {
   // levels [tail_a, nlevels) made by one k_pyr_tail launch (tail_a = nlevels: none); its LDS images
   // at 0 and tail_img_b, tail_lds bytes in all
   int tail_a = 0, tail_img_b = 0, tail_tab_b = 0, tail_nx = 0, tail_ny = 0;
+  int tail_min_frames = 128;  // smaller batches keep per-level launches (eao_orb_debug_pyramid: 1)
   size_t tail_lds = 0;
   std::vector<int2> slot_map;
   long long pyr_bytes = 0, cand_stride = 0, sel_stride = 0;

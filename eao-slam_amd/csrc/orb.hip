@@ -1580,7 +1580,9 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
     return v && v[0] == '0' ? 0 : 1;
   }();
   for (int l = 1; l < nl; l++) {
-    if (resize_lds && l == tail_a) {  // the small levels: one launch
+    // the small levels in one launch -- for batches: one workgroup per frame makes a single frame's
+    // levels in series (22 us at 640x480, against ~13 us for its per-level launches)
+    if (resize_lds && l == tail_a && nframes >= tail_min_frames) {
       hipLaunchKernelGGL(k_pyr_tail, dim3(nframes), dim3(1024), tail_lds, s, d_pyr, pyr_bytes,
                          (const LevelDev*)d_levels, tail_a, nl, tail_img_b, tail_tab_b, tail_nx, tail_ny, 1,
                          (const int*)d_xofs, (const short*)d_ia,

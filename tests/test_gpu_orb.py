@@ -38,7 +38,8 @@ def test_pyramid_exact(frames):
 def test_pyramid_exact_sizes(w, h):
     # k_resize_lds: unaligned rows (odd widths: byte staging of level 0), a partial last column
     # group / row tile, wide levels with one 4-row segment per 1024-thread tile (4K); k_pyr_tail:
-    # levels 2-7 (320x240), 5-7 (641x481), 6-7 (800x600), 7 (1000x700), none (1280x720 and up)
+    # levels 2-7 (320x240), 5-7 (641x481), 6-7 (800x600), 7 (1000x700), none (1280x720 and up); the
+    # debug pyramid takes the batch form (k_pyr_tail) also for one image
     img = np.random.default_rng(w + h).integers(0, 256, (h, w), dtype=np.uint8)
     orb = ea.Orb(width=w, height=h, nfeatures=2000)
     g = orb.pyramid(img)
