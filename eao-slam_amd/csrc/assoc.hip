@@ -42,6 +42,10 @@ __device__ unsigned long long g_if_stamp[32];
 #define NP_STAMP(k)
 #endif
 
+// The association's kernels are one latency chain that the bench's frame work (ORB, lines) shares
+// CUs with: their waves issue at the highest priority, the frame work's throughput waves fill in
+__device__ __forceinline__ void assoc_prio() { __builtin_amdgcn_s_setprio(3); }
+
 // ---------------------------------------------------------------- NP test
 __device__ __forceinline__ void cswap(float& a, float& b, bool up) {
   if ((a > b) == up) {
@@ -570,6 +574,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                   const int* __restrict__ ooff, const int* __restrict__ olen,
                                                   int Pmax, const double* const* __restrict__ os_ptr,
                                                   const float* __restrict__ oth, eao_np_stats* __restrict__ out) {
+  assoc_prio();
   np_pair_body(blockIdx.x, fp, fv, foff, flen, op, ov, ooff, olen, Pmax, os_ptr, oth, out);
 }
 
@@ -682,6 +687,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                                   const int* __restrict__ rlen, int* __restrict__ rect,
                                                   uint8_t* __restrict__ ok, const double* const* __restrict__ ros,
                                                   const float* __restrict__ rth) {
+  assoc_prio();
   const int b = blockIdx.x;
   if (b < npairs)
     np_pair_body(b, fp, fv, foff, flen, op, ov, ooff, olen, Pmax, os_ptr, oth, out);
@@ -848,6 +854,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(8))) void k_
                                                       const long long* __restrict__ tab_off,
                                                       const int* __restrict__ tab_D,
                                                       const uint32_t* __restrict__ tab_states, int jslots) {
+  assoc_prio();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const IfLds L(maxN, maxS, jslots);
   const int ctl_n = if_ctl_n(maxS);  // CalculateC entries staged in LDS
@@ -1337,6 +1344,7 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
                                                      const double* __restrict__ contrib,
                                                      double* __restrict__ scores,
                                                      double* __restrict__ scores2, double x0a, double x0b) {
+  assoc_prio();
   const int c = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= len[c]) return;
