@@ -186,4 +186,17 @@ ipt() {
   EAO_RESIZE_IPT=4 timeout -k 10 400 python -u -m pytest tests/test_gpu_orb.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_ipt_tests.log 2>&1
 }
 
+# prio: the association kernels at wave priority 3 against the previous build (lib/ab/noprio), the
+# bench step alternating, and the replay probe (no frame work beside it)
+prio() {
+  for r in 1 2 3; do
+    echo "## prio" && timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-dropin | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value'],1), round(d['ms_per_step'],2), d['step_split_ms'])" &&
+    echo "## noprio" && EAO_ACCEL_LIB=eao-slam_amd/lib/ab/noprio/libeao_accel.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-dropin | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(round(d['value'],1), round(d['ms_per_step'],2), d['step_split_ms'])" || exit 1
+  done > gpurun_out/r5_prio_bench.log 2>&1 &&
+  for r in 1 2; do
+    echo "## prio" && timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" &&
+    echo "## noprio" && EAO_ACCEL_LIB=eao-slam_amd/lib/ab/noprio/libeao_accel.so timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" || exit 1
+  done > gpurun_out/r5_prio_probe.log 2>&1
+}
+
 "$@"
