@@ -450,7 +450,9 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
           }
         }
     }
+    NP_STAMP(6);
     __syncthreads();
+    NP_STAMP(7);
     if (NH > 1) {  // fold the private copies into copy 0
       for (int i = t; i < HS; i += NPT) {
         int v = H[i];

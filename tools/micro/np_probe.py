@@ -33,3 +33,6 @@ for m, n in SIZES:
     ph = np.diff(st[:6].astype(np.int64))  # EAO_NP_PROF builds (make -C eao-slam_amd prof)
     print("m=%4d n=%5d 4 pairs: %.1f us/call | cycles count %d frame/pad %d sort %d counts %d sums %d"
           % ((m, n, (time.perf_counter() - t0) / 20 * 1e6) + tuple(int(v) for v in ph)), flush=True)
+    if int(st[6]) > int(st[3]) and int(st[7]) >= int(st[6]):  # the rank path's searches + atomics, barrier
+        print("   rank path: searches+atomics %d, barrier wait %d, fold+prefix+final %d"
+              % (int(st[6]) - int(st[3]), int(st[7]) - int(st[6]), int(st[4]) - int(st[7])), flush=True)
