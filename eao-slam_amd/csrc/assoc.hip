@@ -167,10 +167,12 @@ constexpr int NPT = 1024;
 // pairs with m * nvalid up to this take the direct counts (np_pair_body); host-set at engine init
 // (EAO_NP_DIRECT=<max>, 0: always the sort / rank paths)
 __device__ int g_np_direct_max = 131072;
-// LDS behind the sort arrays for the rank path (launches with P >= 2048 only): 3 Pm frame
-// values and 3 (Pm + 1) counters, four copies at Pm = 256 (15.4 KB), one at Pm = 512
-constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * 256 + sizeof(int) * 4 * 3 * 257 + 64;
-static_assert(sizeof(float) * 3 * 512 + sizeof(int) * 3 * 513 <= NP_LDS_EXTRA, "rank-path LDS");
+// LDS behind the sort arrays for the rank path (launches with P >= 2048 only): the frame values
+// (3 axes at a stride of NP_DS = the largest Pm, so they can be placed before m and Pm are known)
+// and 3 (Pm + 1) counters, four copies at Pm = 256 (18.1 KB), one at Pm = 512
+constexpr int NP_DS = 512;
+constexpr size_t NP_LDS_EXTRA = sizeof(float) * 3 * NP_DS + sizeof(int) * 4 * 3 * 257 + 64;
+static_assert(sizeof(float) * 3 * NP_DS + sizeof(int) * 3 * 513 <= NP_LDS_EXTRA, "rank-path LDS");
 __device__ __forceinline__ void np_pair_body(const int p, const float* __restrict__ fp,
                                                   const uint8_t* __restrict__ fv,
                                                   const int* __restrict__ foff,
@@ -189,6 +191,7 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   // packed counts #{object values < x} | #{<= x} << 16 per axis
   __shared__ float s_fp[3][NPT];
   __shared__ int s_cnt[3][NPT];
+  __shared__ int s_dn, s_dnan;  // the rank path's frame values placed early: count, a NaN among them
   const int t = threadIdx.x;
   const float* F = fp + 3 * (long long)foff[p];
   const uint8_t* FV = fv + foff[p];
@@ -219,6 +222,7 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   if (t < 9) red[t] = 0;
   if (t == 9) red[9 * 16 - 1] = 0;
   if (t < 4) wpos[t] = 0;
+  if (t == 0) s_dn = s_dnan = 0;
 #pragma unroll
   for (int a = 0; a < 3; a++) {  // (read after the compaction's barrier, by the direct path only)
     s_fp[a][t] = fv0 ? f0[a] : __int_as_float(0x7fc00000);
@@ -226,6 +230,26 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   }
   __syncthreads();
   float* S[3] = {dsm, dsm + Pmax, dsm + 2 * Pmax};
+  float* D[3] = {dsm + 3 * Pmax, dsm + 3 * Pmax + NP_DS, dsm + 3 * Pmax + 2 * NP_DS};
+  // the rank path's compacted frame values (order irrelevant: sorted later), placed now from the
+  // prefetched points when every frame point has a thread and the launch has the rank path's LDS:
+  // no second pass over the frame points (a global round trip and two barriers)
+  const bool early_d = mt <= NPT && Pmax >= 2048;
+  if (early_d) {
+    const uint64_t mk = ballot(fv0);
+    int base = 0;
+    if (lane == 0 && mk) base = atomicAdd(&s_dn, popc64(mk));
+    base = __shfl(base, 0, 64);
+    if (fv0) {
+      const int d = base + popc64(mk & lanes_below());
+      if (d < NP_DS) {
+        D[0][d] = f0[0];
+        D[1][d] = f0[1];
+        D[2][d] = f0[2];
+      }
+      if (f0[0] != f0[0] || f0[1] != f0[1] || f0[2] != f0[2]) s_dnan = 1;
+    }
+  }
   // one pass over the object: the valid kept points compacted into the sort arrays
   // (order irrelevant: sorted next; a wave places its lanes by ballot rank after one
   // LDS atomic for its base) and the counts m, nvalid, nt
@@ -308,8 +332,7 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
   // (below 2048 object values the object's own sort is the cheaper one, np_probe.py;
   // up to 512 frame values the counters fit NP_LDS_EXTRA)
   bool rank = !wpos[3] && P >= 2048 && Pmax >= 2048 && Pm < P && Pm <= 512;
-  float* D[3] = {dsm + 3 * Pmax, dsm + 3 * Pmax + Pm, dsm + 3 * Pmax + 2 * Pm};
-  int* H = (int*)(dsm + 3 * Pmax + 3 * Pm);  // [NH][3][Pm + 1]
+  int* H = (int*)(dsm + 3 * Pmax + 3 * NP_DS);  // [NH][3][Pm + 1]
   // Direct counts (small pairs, no sort and one barrier): the sample counts of a frame value x
   // need only lt = #{object values < x} and le = #{<= x} (the rank path's identity: sample k is
   // sorted[k step], so #{samples < x} = ceil(lt / step), also for step = 1), counted by brute
@@ -366,7 +389,14 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
     }
     goto sums;
   }
-  if (rank) {
+  if (rank && early_d) {  // the frame values are in D already
+    if (s_dnan) {
+      rank = false;  // a NaN frame value: the sort path (S is intact)
+    } else {
+      for (int i = t; i < NH * HS; i += NPT) H[i] = 0;
+      for (int i = m + t; i < Pm; i += NPT) D[0][i] = D[1][i] = D[2][i] = INFINITY;
+    }
+  } else if (rank) {
     __syncthreads();  // every thread has read wpos
     if (t == 0) wpos[3] = 0;
     for (int i = t; i < NH * HS; i += NPT) H[i] = 0;

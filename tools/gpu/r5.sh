@@ -199,4 +199,15 @@ prio() {
   done > gpurun_out/r5_prio_probe.log 2>&1
 }
 
+# npearly: the rank path's frame values placed during the first pass: NP / association suites,
+# phase stamps (profiling library), replay A/B against the previous build (lib/ab/prev)
+npearly() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_assoc.py tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_chain.py tests/test_gpu_golden.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_npearly_tests.log 2>&1 &&
+  EAO_ACCEL_LIB=eao-slam_amd/lib/prof/libeao_accel.so timeout -k 10 200 python -u tools/micro/np_probe.py 175,1162 300,1162 175,2500 > gpurun_out/r5_npearly_phases.log 2>&1 &&
+  for r in 1 2 3; do
+    echo "## early" && timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" &&
+    echo "## prev" && EAO_ACCEL_LIB=eao-slam_amd/lib/ab/prev/libeao_accel.so timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" || exit 1
+  done > gpurun_out/r5_npearly_probe.log 2>&1
+}
+
 "$@"
