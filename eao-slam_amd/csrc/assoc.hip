@@ -96,6 +96,76 @@ __device__ __forceinline__ void reg_merge(float (&v)[4], int base, int K, int jm
   reg_step<1>(v, base, K);
 }
 
+// reg_step / reg_merge on a 128-element half-run, two values per lane (J <= 64)
+template <int J>
+__device__ __forceinline__ void reg_step2(float (&v)[2], int base, int K) {
+  const int lane = threadIdx.x & 63;
+  const float o[2] = {v[0], v[1]};
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    const int i = base + r * 64 + lane;
+    const bool up = (i & K) == 0;
+    float pv;
+    bool lo;
+    if constexpr (J < 64) {
+      pv = __int_as_float(xor_lane<J>(__float_as_int(o[r])));
+      lo = (lane & J) == 0;
+    } else {
+      pv = o[r ^ 1];
+      lo = r == 0;
+    }
+    const float x = lo ? o[r] : pv, y = lo ? pv : o[r];
+    const bool sw = (x > y) == up;
+    v[r] = sw ? pv : o[r];
+  }
+}
+__device__ __forceinline__ void reg_merge2(float (&v)[2], int base, int K, int jmax) {
+  if (jmax >= 64) reg_step2<64>(v, base, K);
+  if (jmax >= 32) reg_step2<32>(v, base, K);
+  if (jmax >= 16) reg_step2<16>(v, base, K);
+  if (jmax >= 8) reg_step2<8>(v, base, K);
+  if (jmax >= 4) reg_step2<4>(v, base, K);
+  if (jmax >= 2) reg_step2<2>(v, base, K);
+  reg_step2<1>(v, base, K);
+}
+
+// The same network for P = 256 on six waves (a 128-element half of an axis each, two values per
+// lane): stages K <= 128 in registers, then K = 256's stride-128 step from the partner half read
+// through LDS and its strides 64 .. 1 in registers -- half the register work per wave of the
+// one-wave-per-axis form, the same compare-exchanges in the same order (identical result).
+__device__ void block_sort3_256(float* S0, float* S1, float* S2) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* A = (w >> 1) == 0 ? S0 : ((w >> 1) == 1 ? S1 : S2);
+  const int base = (w & 1) << 7;
+  float v[2] = {0.f, 0.f};
+  if (w < 6) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) v[r] = A[base + r * 64 + lane];
+    for (int K = 2; K <= 128; K <<= 1) reg_merge2(v, base, K, K >> 1);
+#pragma unroll
+    for (int r = 0; r < 2; r++) A[base + r * 64 + lane] = v[r];
+  }
+  __syncthreads();
+  float pv[2] = {0.f, 0.f};
+  if (w < 6) {
+#pragma unroll
+    for (int r = 0; r < 2; r++) pv[r] = A[(base ^ 128) + r * 64 + lane];  // the partner half
+  }
+  __syncthreads();  // (both halves read before either is overwritten)
+  if (w < 6) {
+    const bool lo = base == 0;  // stage K = 256, stride 128: ascending everywhere (i < 256)
+#pragma unroll
+    for (int r = 0; r < 2; r++) {
+      const float x = lo ? v[r] : pv[r], y = lo ? pv[r] : v[r];
+      v[r] = (x > y) ? pv[r] : v[r];
+    }
+    reg_merge2(v, base, 256, 64);
+#pragma unroll
+    for (int r = 0; r < 2; r++) A[base + r * 64 + lane] = v[r];
+  }
+  __syncthreads();
+}
+
 // Ascending bitonic sort of three LDS arrays, P = 2^e >= 256 (INF padded): every
 // (256-element run, array) is one wave's job, sorted in registers (stages K <= 256,
 // no barrier) -- three waves already for P = 256; for K >= 512 the strides >= 256 go
@@ -167,6 +237,8 @@ constexpr int NPT = 1024;
 // pairs with m * nvalid up to this take the direct counts (np_pair_body); host-set at engine init
 // (EAO_NP_DIRECT=<max>, 0: always the sort / rank paths)
 __device__ int g_np_direct_max = 131072;
+// the six-wave form of the P = 256 sort (EAO_NP_SORT256=0: the one-wave-per-axis form, A/B)
+__device__ int g_np_sort256 = 1;
 // LDS behind the sort arrays for the rank path (launches with P >= 2048 only): the frame values
 // (3 axes at a stride of NP_DS = the largest Pm, so they can be placed before m and Pm are known)
 // and 3 (Pm + 1) counters, four copies at Pm = 256 (18.1 KB), one at Pm = 512
@@ -431,7 +503,10 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
     for (int i = nvalid + t; i < P; i += NPT) S[0][i] = S[1][i] = S[2][i] = INFINITY;
   __syncthreads();
   NP_STAMP(2);
-  block_sort3_fast(rank ? D[0] : S[0], rank ? D[1] : S[1], rank ? D[2] : S[2], rank ? Pm : P);
+  if ((rank ? Pm : P) == 256 && g_np_sort256)
+    block_sort3_256(rank ? D[0] : S[0], rank ? D[1] : S[1], rank ? D[2] : S[2]);
+  else
+    block_sort3_fast(rank ? D[0] : S[0], rank ? D[1] : S[1], rank ? D[2] : S[2], rank ? Pm : P);
   NP_STAMP(3);
   if (rank) {
     // the compacted object values from LDS, two per thread in flight: 12 search chains
@@ -1459,6 +1534,10 @@ int AssocEngine::init(int device, int mp) {
   if (const char* v = std::getenv("EAO_NP_DIRECT")) {  // A/B: the NP direct-count threshold (m * n)
     const int mx = std::atoi(v);
     EAO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_np_direct_max), &mx, sizeof(int)));
+  }
+  if (const char* v = std::getenv("EAO_NP_SORT256")) {  // A/B (HIP-launched kernels only)
+    const int on = std::atoi(v) != 0;
+    EAO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_np_sort256), &on, sizeof(int)));
   }
   pow_x0[0] = pow_threshold((double)0.6f);
   pow_x0[1] = pow_threshold((double)0.65f);

@@ -210,4 +210,17 @@ npearly() {
   done > gpurun_out/r5_npearly_probe.log 2>&1
 }
 
+# sort256: the six-wave P = 256 sort in the NP kernels: suites, phase stamps (EAO_NP_SORT256=0 / 1,
+# profiling library), replay A/B against the previous build (lib/ab/prev)
+sort256() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_assoc.py tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_chain.py tests/test_gpu_golden.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_sort256_tests.log 2>&1 &&
+  for k in 0 1 0 1; do
+    echo "## EAO_NP_SORT256=$k" && EAO_NP_SORT256=$k EAO_ACCEL_LIB=eao-slam_amd/lib/prof/libeao_accel.so timeout -k 10 200 python -u tools/micro/np_probe.py 175,1162 300,200 100,240 || exit 1
+  done > gpurun_out/r5_sort256_phases.log 2>&1 &&
+  for r in 1 2 3; do
+    echo "## sort256" && timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" &&
+    echo "## prev" && EAO_ACCEL_LIB=eao-slam_amd/lib/ab/prev/libeao_accel.so timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" || exit 1
+  done > gpurun_out/r5_sort256_probe.log 2>&1
+}
+
 "$@"
