@@ -96,6 +96,19 @@ __device__ __forceinline__ void reg_merge(float (&v)[4], int base, int K, int jm
   reg_step<1>(v, base, K);
 }
 
+// wave-wide int sum in VALU lane moves (DPP within rows, permlane swaps across them; the pattern
+// of wave_minmax_key) instead of six dependent ds_bpermute round trips; every lane gets the sum
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false);  // row_mirror
+  auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = (int)a[0] + (int)a[1];
+  a = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (int)a[0] + (int)a[1];
+}
+
 // reg_step / reg_merge on a 128-element half-run, two values per lane (J <= 64)
 template <int J>
 __device__ __forceinline__ void reg_step2(float (&v)[2], int base, int K) {
@@ -363,8 +376,8 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
       }
     }
   }
-  mc = wave_sum(mc);
-  ntk = wave_sum(ntk);
+  mc = wave_sum_dpp(mc);
+  ntk = wave_sum_dpp(ntk);
   if (lane == 0) {
     if (mc) atomicAdd(&wpos[1], mc);
     if (ntk) atomicAdd(&wpos[2], ntk);
@@ -639,7 +652,7 @@ sums:
   // block sums: wave sums, then one LDS atomic per wave and counter
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    c9[k] = wave_sum(c9[k]);
+    c9[k] = wave_sum_dpp(c9[k]);
     if (lane == 0 && c9[k]) atomicAdd(&red[k], c9[k]);
   }
   __syncthreads();

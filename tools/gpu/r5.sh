@@ -223,4 +223,15 @@ sort256() {
   done > gpurun_out/r5_sort256_probe.log 2>&1
 }
 
+# dppsum: the NP kernels' wave sums in DPP / permlane moves: suites, phase stamps, replay A/B
+# against the previous build (lib/ab/prev)
+dppsum() {
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_assoc.py tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_chain.py tests/test_gpu_golden.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_dppsum_tests.log 2>&1 &&
+  EAO_ACCEL_LIB=eao-slam_amd/lib/prof/libeao_accel.so timeout -k 10 200 python -u tools/micro/np_probe.py 175,1162 300,1162 > gpurun_out/r5_dppsum_phases.log 2>&1 &&
+  for r in 1 2 3; do
+    echo "## dppsum" && timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" &&
+    echo "## prev" && EAO_ACCEL_LIB=eao-slam_amd/lib/ab/prev/libeao_accel.so timeout -k 10 200 python -u tools/replay_probe.py | grep "pass 2" || exit 1
+  done > gpurun_out/r5_dppsum_probe.log 2>&1
+}
+
 "$@"
