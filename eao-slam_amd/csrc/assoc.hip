@@ -109,6 +109,18 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
   return (int)a[0] + (int)a[1];
 }
 
+// inclusive wave-wide int prefix sum in DPP moves: row_shr 1 / 2 / 4 / 8 within rows (zero shifted
+// in), then row_bcast:15 / :31 carry the row totals into the later rows
+__device__ __forceinline__ int wave_scan_dpp(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // reg_step / reg_merge on a 128-element half-run, two values per lane (J <= 64)
 template <int J>
 __device__ __forceinline__ void reg_step2(float (&v)[2], int base, int K) {
@@ -585,13 +597,9 @@ __device__ __forceinline__ void np_pair_body(const int p, const float* __restric
       int carry = 0;
       for (int c0 = 0; c0 < m; c0 += 64) {
         const int j = c0 + lane;
-        int v = j < m ? Ha[j] : 0;
-        for (int o = 1; o < 64; o <<= 1) {
-          const int u = __shfl_up(v, o, 64);
-          if (lane >= o) v += u;
-        }
+        const int v = wave_scan_dpp(j < m ? Ha[j] : 0);
         if (j < m) Ha[j] = v + carry;
-        carry += __shfl(v, 63, 64);
+        carry += __builtin_amdgcn_readlane(v, 63);
       }
     }
     __syncthreads();

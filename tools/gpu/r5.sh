@@ -223,7 +223,7 @@ sort256() {
   done > gpurun_out/r5_sort256_probe.log 2>&1
 }
 
-# dppsum: the NP kernels' wave sums in DPP / permlane moves: suites, phase stamps, replay A/B
+# dppsum (also the prefix scan A/B): the NP kernels' wave sums in DPP / permlane moves: suites, phase stamps, replay A/B
 # against the previous build (lib/ab/prev)
 dppsum() {
   timeout -k 10 500 python -u -m pytest tests/test_gpu_assoc.py tests/test_gpu_fr3.py tests/test_gpu_replay.py tests/test_gpu_chain.py tests/test_gpu_golden.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r5_dppsum_tests.log 2>&1 &&
