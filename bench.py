@@ -155,7 +155,7 @@ def _pmc_value(fname, kernel, counter):
     return None
 
 
-PMC_FILES = {"fetch": "r05h_pmc_fetch.txt", "write": "r05h_pmc_write.txt", "sq": "r05h_pmc_sq.txt"}
+PMC_FILES = {"fetch": "r05n_pmc_fetch.txt", "write": "r05n_pmc_write.txt", "sq": "r05n_pmc_sq.txt"}
 
 
 def pmc_valu(kernel, frames):
