@@ -75,7 +75,7 @@ METRIC = "frames/sec (extract+match+EAO-assoc) on 640x480; CPU-ref parity on ass
 CONFIGS = {
     "eao": dict(flag="EAO", start=None, n=None, cpu_assoc=405,
                 workload="mono_tum EAO fr3_long_office 640x480 (BASELINE configs[1]: rgb_seq_pose.txt, 405 frames)"),
-    "full": dict(flag="Full", start=0, n=2582, cpu_assoc=600,
+    "full": dict(flag="Full", start=0, n=2582, cpu_assoc=2582,
                  workload="mono_tum Full fr3_long_office 640x480 (BASELINE configs[2]: rgb_full_demo.txt, "
                           "2582 frames)"),
 }

@@ -76,7 +76,10 @@ class AssocEngine {
   // the device scores at d_scores + meta[3 c] (meta[3 c + 1] points, th[c] the threshold);
   // meta / th may be pinned host memory read in place
   int pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores, unsigned char* d_dst,
-                 hipStream_t s);
+                 const Lane& s);
+  // on HSA lane s, after the launches before it: zero [zero, zero + zero_bytes) (may be empty),
+  // then store v into *flag (the sharded exchange's GPU-side ready flag, shard.h ExReady)
+  int publish(const Lane& s, void* zero, size_t zero_bytes, uint64_t* flag, uint64_t v);
   // host (pinned) to device copy as a kernel on stream s (16-byte aligned buffers)
   int stage_in(void* d_dst, const void* h_src, size_t bytes, const Lane& s);
   // can one k_iforest_tree workgroup hold a cloud of max_len points, max_sample samples

@@ -1556,7 +1556,8 @@ int AssocEngine::init(int device, int mp) {
     const int mx = std::atoi(v);
     EAO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_np_direct_max), &mx, sizeof(int)));
   }
-  if (const char* v = std::getenv("EAO_NP_SORT256")) {  // A/B (HIP-launched kernels only)
+  // (the HSA lanes' own code object takes the same two switches when it is loaded, hsa_lane.cpp)
+  if (const char* v = std::getenv("EAO_NP_SORT256")) {  // A/B
     const int on = std::atoi(v) != 0;
     EAO_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_np_sort256), &on, sizeof(int)));
   }
@@ -1793,11 +1794,38 @@ __global__ __launch_bounds__(256) void k_pack_masks(const int* __restrict__ meta
 }
 
 int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
-                            unsigned char* d_dst, hipStream_t s) {
+                            unsigned char* d_dst, const Lane& s) {
   if (nclouds <= 0) return EAO_OK;
-  hipLaunchKernelGGL(k_pack_masks, dim3(4, nclouds), dim3(256), 0, s, meta, th, d_scores, d_dst);
+  if (s.hsa()) {
+    static const int kid = hsa_kernel_id("eao::k_pack_masks(");
+    return hsa_launch(s.q, kid, dim3(4, nclouds), dim3(256), 0u, meta, th, d_scores, d_dst);
+  }
+  hipLaunchKernelGGL(k_pack_masks, dim3(4, nclouds), dim3(256), 0, s.s, meta, th, d_scores, d_dst);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
+}
+
+// The sharded exchange's ready flag (shard.h, ExReady): launched on an HSA lane after the kernels
+// that wrote a record (the lane's barrier bits order it after them, and their system-scope
+// releases made their stores visible), it zeroes an optional range (an empty record) and then
+// stores v into the lane's flag word -- HIP signal memory the RCCL stream waits on with
+// hipStreamWaitValue64 (Gte): the all-gather starts on the GPU as soon as the record is complete.
+__global__ __launch_bounds__(256) void k_publish(unsigned char* __restrict__ zero, unsigned zero_bytes,
+                                                 unsigned long long* flag, unsigned long long v) {
+  for (unsigned i = threadIdx.x; i < zero_bytes; i += blockDim.x) zero[i] = 0;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int AssocEngine::publish(const Lane& s, void* zero, size_t zero_bytes, uint64_t* flag, uint64_t v) {
+  if (!s.hsa() || !flag || zero_bytes > 0xffffffffu) {
+    set_error("publish: an HSA lane and a flag word are needed");
+    return EAO_E_ARG;
+  }
+  static const int kid = hsa_kernel_id("eao::k_publish(");
+  return hsa_launch(s.q, kid, dim3(1), dim3(256), 0u, (unsigned char*)zero, (unsigned)zero_bytes,
+                    (unsigned long long*)flag, (unsigned long long)v);
 }
 
 int AssocEngine::stage_in(void* dst, const void* src, size_t bytes, const Lane& s) {

@@ -12,6 +12,7 @@
 
 #include "assoc.h"
 #include "common.h"
+#include "hsa_lane.h"
 #include "match.h"
 #include "orb.h"
 
@@ -45,6 +46,16 @@ static int need_device(int device) {
     return EAO_E_NODEVICE;
   }
   return EAO_OK;
+}
+
+int eao_lane_selftest(int device, int* out1) {
+  if (int rc = need_device(device)) return rc;
+  if (hipSetDevice(device) != hipSuccess) return EAO_E_HIP;
+  if (!eao::hsa_lanes_available(device)) {
+    set_error("eao_lane_selftest: HSA lanes unavailable on this device (or EAO_HSA_LANES=0)");
+    return EAO_E_STATE;
+  }
+  return eao::lane_selftest(device, out1);
 }
 
 int eao_orb_create(const eao_orb_params* p, int device, eao_orb** out) {

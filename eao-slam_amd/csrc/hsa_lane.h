@@ -6,8 +6,8 @@
 // launch / event record / event wait / launch sequence ~12 us, against ~0.2 us per AQL packet and
 // ~0.6 us for the same sequence with a barrier-AND packet, and the packets' agent-scope acquire
 // starts a dependent kernel ~1-4 us sooner (profiles/r05_dispatch_lat.txt, tools/micro/dispatch_lat.cpp).
-// A Done is the matching completion marker: a HIP event, or an HSA signal attached to the lane's
-// last packet.
+// A Done is the matching completion marker: a HIP event, or a use of an HSA signal of the lane's
+// ring, attached to the lane's last packet.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,6 +27,9 @@ struct Lane {
 struct Done {
   hipEvent_t e = nullptr;
   uint64_t sig = 0;  // hsa_signal_t handle (HSA lanes)
+  HsaQueue* q = nullptr;  // the lane whose signal ring holds it,
+  uint32_t slot = 0;      // the ring slot
+  uint64_t use = 0;       // and the slot's use it marks (a later use of the slot: this one completed)
 };
 
 // HSA lanes usable on HIP device `dev` (the code object loaded, an agent matched by PCI address);
@@ -68,6 +71,8 @@ const CoKernel* hsa_kernel_meta(int id);
 // explicit arguments laid out in `args` at the kernel's offsets
 int hsa_submit(HsaQueue* q, int id, dim3 g, dim3 b, uint32_t dyn_lds, const unsigned char* args);
 int hsa_arg_mismatch(int id, int i, int size);  // sets the error, returns EAO_E_STATE
+// self-test of the HSA lanes' markers and commits (eao_lane_selftest); report[0] = packets written
+int lane_selftest(int dev, int* report);
 
 // hipLaunchKernelGGL's counterpart on an HSA lane: the arguments are placed at the offsets the
 // code object declares, each checked against the declared size (pass them as the kernel's

@@ -90,6 +90,11 @@ static const bool g_bar_fs = [] {
   const char* v = getenv("EAO_BAR_FS");
   return g_bar_inputs && !(v && v[0] == '0');
 }();
+// sharded replays on the HSA lanes (EAO_SHARD_HSA=0: HIP streams, A/B switch)
+static const bool g_shard_hsa = [] {
+  const char* v = getenv("EAO_SHARD_HSA");
+  return !(v && v[0] == '0');
+}();
 static const bool g_sentinel = [] {
   const char* v = getenv("EAO_SENTINEL_WAIT");
   return !(v && v[0] == '0');
@@ -593,6 +598,12 @@ class ReplayEngine {
   // other GPU result and whenever a pending object's points are needed; an
   // object's outliers are erased (complete) the first time its points are read
   static constexpr int kIfBatches = 8, kIfStreams = 4;
+  // a device-form record's readiness for the exchange: the Done it was recorded on and, on HSA
+  // lanes, the producer lane's ready flag and the value k_publish stores there after it
+  struct ExRef {
+    int lane = -1;  // ready flag index (forest lanes 0..kIfStreams-1, the frame start's lane kIfStreams)
+    uint64_t value = 0;
+  };
   struct IfBatch {
     std::vector<Obj*> objs;
     int left = 0;  // objects not yet completed
@@ -626,6 +637,7 @@ class ReplayEngine {
     size_t xbytes = 0;
     unsigned char* d_x = nullptr;
     size_t cap_x = 0;
+    ExRef xr;  // when d_x is complete (HSA lanes: the lane's ready flag value)
   };
   std::vector<IfBatch> ifb;
   // the forest lanes, and the frame start's own lane (HSA form; the HIP form launches the
@@ -638,6 +650,28 @@ class ReplayEngine {
   uint64_t if_seq = 0;
   int if_next = 0;
   int pend_err = 0;
+
+  uint64_t xpub[kIfStreams + 1] = {};  // values published so far per lane
+  ExRef fs_xr;                          // the frame start's record (d_out)
+  // after the launches on HSA lane l (flag index li): zero [zero, zero + bytes) and publish the
+  // lane's next flag value; *xr = where the exchange waits for it
+  int publish(const Lane& l, int li, void* zero, size_t bytes, ExRef* xr) {
+    uint64_t* f = ex ? ex->ready_flag(li) : nullptr;
+    if (!f) {
+      set_error("replay: no ready flag for the sharded exchange on HSA lanes");
+      return EAO_E_STATE;
+    }
+    xr->lane = li;
+    xr->value = ++xpub[li];
+    return A->publish(l, zero, bytes, f, xr->value);
+  }
+  // flag index of a lane of this replay
+  int lane_index(const Lane& l) const {
+    if (l.q && l.q == fs_lane.q) return kIfStreams;
+    for (int k = 0; k < kIfStreams; k++)
+      if (l.q && l.q == if_stream[k].q) return k;
+    return -1;
+  }
 
   // object sharding (shard.h): the GPU work of object o runs on
   // rank o->id % sworld and its result records are all-gathered
@@ -666,13 +700,19 @@ class ReplayEngine {
   }
   // device form: this rank's `bytes` at d_send (ready behind `ev`) gathered on the GPU;
   // *recv = the [sworld][bytes] records in pinned host memory
-  int exchange_device(const void* d_send, const Done& ev, size_t bytes, const unsigned char** recv) {
+  int exchange_device(const void* d_send, const Done& ev, const ExRef& xr, size_t bytes, const unsigned char** recv) {
     const double t0 = now_us();
-    if (!ev.e) {  // sharded replays launch on HIP lanes (if_init)
-      set_error("replay: the device-form exchange needs HIP lanes");
+    ExReady rd;
+    if (ev.e) {
+      rd.ev = ev.e;  // HIP lanes: a GPU-side event wait
+    } else if (xr.lane >= 0) {
+      rd.flag = ex->ready_flag(xr.lane);  // HSA lanes: a GPU-side wait on the lane's ready flag
+      rd.value = xr.value;
+    } else if (ev.sig) {
+      set_error("replay: an HSA-lane record without its ready flag");
       return EAO_E_STATE;
     }
-    int rc = ex->allgather_device(d_send, ev.e, bytes, recv);
+    int rc = ex->allgather_device(d_send, rd, bytes, recv);
     xstat[0] += 1;
     xstat[1] += (double)bytes;
     xstat[2] += now_us() - t0;
@@ -1152,7 +1192,9 @@ class ReplayEngine {
   // or EAO_HSA_LANES=0. Lanes adopted from a previous replay of the other kind are replaced.
   bool lanes_hsa = false;
   int lanes_init() {
-    const bool want = !sharded() && hsa_lanes_available(A->dev);
+    // sharded replays too: the host form waits on the lanes' markers, the device form's RCCL
+    // stream on the lanes' ready flags (EAO_SHARD_HSA=0: HIP streams, A/B)
+    const bool want = (!sharded() || (g_shard_hsa && (!xdev() || ex->ready_flag(0)))) && hsa_lanes_available(A->dev);
     if (if_stream[0].s || if_stream[0].q) {
       lanes_hsa = if_stream[0].hsa();  // adopted from the previous replay on this engine
       if (lanes_hsa == want) return EAO_OK;
@@ -1321,7 +1363,12 @@ class ReplayEngine {
         if (xdev() && !b.launched) {  // nothing owned: an empty record, ready behind b.ev
           const Lane& st = if_stream[k % kIfStreams];
           if_tail[k % kIfStreams] = -1;
-          EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st.s));
+          b.xr = ExRef();
+          if (st.hsa()) {
+            if (int rc = publish(st, k % kIfStreams, b.d_x, b.xbytes, &b.xr)) return rc;
+          } else {
+            EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st.s));
+          }
           if (int rc = lane_record(st, b.done)) return rc;
         }
       }
@@ -1378,9 +1425,12 @@ class ReplayEngine {
       unsigned char* din = b.d_in;
       if (if_stream[k % kIfStreams].hsa() && g_bar_inputs) {
         if (in_bytes > b.cap_bar) {
+          // the slot's previous launch may still read the old buffer (its wait can end on the
+          // outputs before the kernels retire): it completes before the buffer goes
+          if (b.bar_in && (b.done.e || b.done.sig)) EAO_HIP_CHECK(spin_event_plain(b.done));
+          const size_t c = std::max(in_bytes, 2 * b.cap_bar);
           bar_free(b.bar_in);
           b.cap_bar = 0;
-          const size_t c = std::max(in_bytes, 2 * b.cap_bar);
           b.bar_in = (unsigned char*)bar_alloc(A->dev, c);
           if (b.bar_in) b.cap_bar = c;
         }
@@ -1468,8 +1518,10 @@ class ReplayEngine {
       }
       if (xdev()) {
         const int* dpk = (const int*)(din + o_pk);
-        rc = A->pack_masks(nl, dpk, (const float*)(din + o_pkth), (const double*)b.d_out, b.d_x, st.s);
+        rc = A->pack_masks(nl, dpk, (const float*)(din + o_pkth), (const double*)b.d_out, b.d_x, st);
         if (rc) return rc;
+        b.xr = ExRef();
+        if (st.hsa() && (rc = publish(st, k % kIfStreams, nullptr, 0, &b.xr))) return rc;
       }
       if (int rc1 = lane_record(st, b.done)) return rc1;
       tr(5, k, nl, maxN);
@@ -1486,7 +1538,7 @@ class ReplayEngine {
     const unsigned char* recv = nullptr;
     if (xdev()) {
       // the owner's kernels wrote the record into b.d_x; gathered on the GPU behind b.ev
-      if (int rc = exchange_device(b.d_x, b.done, bytes, &recv)) return rc;
+      if (int rc = exchange_device(b.d_x, b.done, b.xr, bytes, &recv)) return rc;
     } else {
       if (b.launched) EAO_HIP_CHECK(spin_event(b.done));
       xsend.assign(bytes, 0);
@@ -1793,9 +1845,11 @@ class ReplayEngine {
     unsigned char* hin = h_in;
     if (lanes_hsa && g_bar_fs) {
       if (in_bytes > cap_fs_bar) {
+        // the previous frame start may still read the old buffer (see the forest batches)
+        if (fs_bar && (gpu0.e || gpu0.sig)) EAO_HIP_CHECK(spin_event_plain(gpu0));
+        const size_t c = std::max(in_bytes, 2 * cap_fs_bar);
         bar_free(fs_bar);
         cap_fs_bar = 0;
-        const size_t c = std::max(in_bytes, 2 * cap_fs_bar);
         fs_bar = (unsigned char*)bar_alloc(A->dev, c);
         if (fs_bar) cap_fs_bar = c;
       }
@@ -1883,6 +1937,8 @@ class ReplayEngine {
                      dosp, doth, npairs, dpts, dval, dpm, dpm + npairs, dpts, dval, dpm + 2 * npairs, dpm + 3 * npairs,
                      (eao_np_stats*)ob, ls, max_olen, dosp ? dosp + nb : nullptr, doth ? doth + nb : nullptr);
     if (rc) return rc;
+    fs_xr = ExRef();
+    if (rn_dev && ls.hsa() && (rc = publish(ls, lane_index(ls), nullptr, 0, &fs_xr))) return rc;
     if (int rc0 = lane_record(ls, gpu0)) return rc0;
     tr(2, lk, (int)wait_slots.size(), npairs);
     if (phase == 0) {  // the frame start's launch: time since the frame began
@@ -1958,8 +2014,15 @@ class ReplayEngine {
       if (int rc = stage(0, bytes)) return rc;
       int rc;
       if (L.empty() && P.empty()) {  // nothing owned: an empty record
-        EAO_HIP_CHECK(hipMemsetAsync(d_out, 0, bytes, A->stream));
-        if (int rc0 = lane_record(Lane(A->stream), gpu0)) return rc0;
+        if (int rc0 = lanes_init()) return rc0;
+        fs_xr = ExRef();
+        if (lanes_hsa) {
+          if (int rc0 = publish(fs_lane, kIfStreams, d_out, bytes, &fs_xr)) return rc0;
+          if (int rc0 = lane_record(fs_lane, gpu0)) return rc0;
+        } else {
+          EAO_HIP_CHECK(hipMemsetAsync(d_out, 0, bytes, A->stream));
+          if (int rc0 = lane_record(Lane(A->stream), gpu0)) return rc0;
+        }
       } else {
         rn_dev = true;
         rc = rects_np_launch(L, P, R, S);
@@ -1968,7 +2031,7 @@ class ReplayEngine {
       }
       idle_work(gpu0);  // the next frame's steps 1-6, while the GPU is busy
       const unsigned char* recv = nullptr;
-      if ((rc = exchange_device(d_out, gpu0, bytes, &recv))) return rc;
+      if ((rc = exchange_device(d_out, gpu0, fs_xr, bytes, &recv))) return rc;
       std::vector<int> il(sworld, 0), ip(sworld, 0);
       rects.assign(5 * list.size(), 0);
       stats.resize(pairs.size());

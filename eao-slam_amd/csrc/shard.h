@@ -9,8 +9,18 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdint>
 
 namespace eao {
+
+// when a device-form record is complete: after a HIP event (records written on HIP streams), or
+// once the word *flag holds >= value (records written on an HSA lane, whose k_publish stores the
+// value after them; the flag is signal memory from the exchanger's ready_flag)
+struct ExReady {
+  hipEvent_t ev = nullptr;
+  const uint64_t* flag = nullptr;
+  uint64_t value = 0;
+};
 
 struct Exchanger {
   virtual ~Exchanger() {}
@@ -18,12 +28,18 @@ struct Exchanger {
   // buffers, recv[r * bytes, (r + 1) * bytes) = rank r's send
   virtual int allgather(const void* send, void* recv, size_t bytes) = 0;
   // device form (RCCL): the records are gathered from device memory into device memory.
-  // d_send holds this rank's `bytes` once `ready` has completed (the kernels that wrote
-  // it were recorded on it); the collective waits for that event on the GPU, and the
+  // d_send holds this rank's `bytes` once `ready` holds (the kernels that wrote it were
+  // recorded on its event, or published its flag value); the collective waits on the GPU, and the
   // [world][bytes] result is copied to the host once: *h_recv points at it (pinned,
   // valid until the next exchange).
   virtual bool device_form() const { return false; }
-  virtual int allgather_device(const void* d_send, hipEvent_t ready, size_t bytes, const unsigned char** h_recv) {
+  // the GPU-side ready flag of producer lane `i` (0..7; nullptr: none): signal memory holding the
+  // last value published on that lane, monotone per lane
+  virtual uint64_t* ready_flag(int i) {
+    (void)i;
+    return nullptr;
+  }
+  virtual int allgather_device(const void* d_send, const ExReady& ready, size_t bytes, const unsigned char** h_recv) {
     (void)d_send;
     (void)ready;
     (void)bytes;

@@ -52,9 +52,12 @@ struct RcclExchanger : Exchanger {
   unsigned char *h_recv = nullptr, *d_recv = nullptr;
   size_t cap = 0;    // bytes per rank
   unsigned seq = 0;  // k_recv_out's flag value of the latest call
+  uint64_t* rflag[8] = {};  // producer lanes' ready flags (signal memory), made on first use
 
   ~RcclExchanger() override {
     if (stream) (void)hipStreamSynchronize(stream);
+    for (uint64_t* f : rflag)
+      if (f) (void)hipFree(f);
     if (done) (void)hipEventDestroy(done);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
@@ -92,10 +95,26 @@ struct RcclExchanger : Exchanger {
     return EAO_E_ARG;
   }
   bool device_form() const override { return true; }
-  int allgather_device(const void* d_send, hipEvent_t ready, size_t bytes, const unsigned char** out) override {
+  uint64_t* ready_flag(int i) override {
+    if (i < 0 || i >= 8) return nullptr;
+    if (!rflag[i]) {
+      void* p = nullptr;
+      if (hipSetDevice(dev) != hipSuccess || hipExtMallocWithFlags(&p, sizeof(uint64_t), hipMallocSignalMemory) != hipSuccess)
+        return nullptr;
+      if (hipMemset(p, 0, sizeof(uint64_t)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return nullptr;
+      }
+      rflag[i] = (uint64_t*)p;  // 0: below every published value (>= 1)
+    }
+    return rflag[i];
+  }
+  int allgather_device(const void* d_send, const ExReady& ready, size_t bytes, const unsigned char** out) override {
     if (bytes == 0) return EAO_E_ARG;
     if (int rc = grow(bytes)) return rc;
-    if (ready) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready, 0));
+    if (ready.ev) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready.ev, 0));
+    if (ready.flag)  // the HSA lane's k_publish stores the value once the record is complete
+      EAO_HIP_CHECK(hipStreamWaitValue64(stream, (void*)ready.flag, ready.value, hipStreamWaitValueGte));
     EAO_NCCL_CHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
     unsigned* flag = (unsigned*)(h_recv + cap * world);
     const unsigned want = ++seq;
@@ -180,7 +199,9 @@ extern "C" int eao_rccl_selftest(int device, int bytes) {
       break;
     }
     const unsigned char* recv = nullptr;
-    rc = x->allgather_device(d_send, ev, n, &recv);
+    eao::ExReady rd;
+    rd.ev = ev;
+    rc = x->allgather_device(d_send, rd, n, &recv);
     if (!rc && std::memcmp(recv, send.data(), n) != 0) {
       eao::set_error("eao_rccl_selftest: gathered bytes differ");
       rc = EAO_E_HIP;

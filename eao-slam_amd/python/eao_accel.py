@@ -114,6 +114,14 @@ def rccl_selftest(device=0, nbytes=1000):
     check(lib().eao_rccl_selftest(int(device), int(nbytes)), "eao_rccl_selftest")
 
 
+def lane_selftest(device=0):
+    """eao_lane_selftest: the HSA launch lanes' completion markers, barrier lifetimes and ring-end
+    commits; returns the packets written."""
+    out = np.zeros(1, np.int32)
+    check(lib().eao_lane_selftest(int(device), P(out)), "eao_lane_selftest")
+    return int(out[0])
+
+
 def device_ok(dev=0):
     return bool(lib().eao_device_ok(dev))
 

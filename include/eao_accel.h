@@ -391,6 +391,11 @@ int eao_replay_shard_rccl(eao_replay* r, int rank, int world, const uint8_t* uni
 int eao_replay_shard_callback(eao_replay* r, int rank, int world, eao_allgather_fn fn, void* ctx);
 /* [0] exchanges, [1] bytes per rank, [2] us spent in the exchange */
 int eao_replay_shard_stats(eao_replay* r, double* out3);
+/* Self-test of the association's HSA launch lanes on `device` (no reference counterpart): completion
+   markers held across many reuses of their signal slot, barrier packets on reused slots (held and
+   committed), and runs of held packets meeting the ring end. 0 = ok (out1[0] = packets written);
+   EAO_E_NODEVICE without a gfx950 device; else the failing step in eao_last_error(). */
+int eao_lane_selftest(int device, int* out1);
 
 /* development instrumentation: s_memtime stamps of the last isolation-forest
    tree launch (workgroup (0,0)), 32 entries: [0..7] phase boundaries, [10] node count,

@@ -127,7 +127,7 @@ struct DeviceLoopExchanger : Exchanger {
     return EAO_E_ARG;
   }
   bool device_form() const override { return true; }
-  int allgather_device(const void* d_send, hipEvent_t, size_t bytes, const unsigned char** out) override {
+  int allgather_device(const void* d_send, const ExReady&, size_t bytes, const unsigned char** out) override {
     recv.assign(bytes * world, 0xcd);
     if (world == 1) {
       std::memcpy(recv.data(), d_send, bytes);
@@ -144,8 +144,12 @@ Exchanger* make_rccl_exchanger(int, int, int world, const void*, int* rc) {
   *rc = 0;
   return new DeviceLoopExchanger(world);
 }
+int AssocEngine::publish(const Lane&, void*, size_t, uint64_t*, uint64_t) {
+  set_error("harness: no HSA lanes");  // the harness's lanes are HIP-stream lanes (never called)
+  return EAO_E_STATE;
+}
 int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
-                            unsigned char* d_dst, hipStream_t) {
+                            unsigned char* d_dst, const Lane&) {
   for (int c = 0; c < nclouds; c++) {
     const int off = meta[3 * c], n = meta[3 * c + 1], out = meta[3 * c + 2];
     for (int j = 0; j < (n + 7) / 8; j++) {
