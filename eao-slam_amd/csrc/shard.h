@@ -40,9 +40,23 @@ struct Exchanger {
     return nullptr;
   }
   virtual int allgather_device(const void* d_send, const ExReady& ready, size_t bytes, const unsigned char** h_recv) {
+    int t = -1;
+    if (int rc = start_device(d_send, ready, bytes, &t)) return rc;
+    return wait_device(t, h_recv);
+  }
+  // the same in two halves: start_device enqueues the exchange (the GPU waits for `ready`, gathers,
+  // copies back) and returns at once with a ticket; wait_device(ticket) returns the gathered
+  // records (valid until the next start_device). Tickets may be waited in any order; every rank
+  // starts its exchanges in the same order (the collectives' order).
+  virtual int start_device(const void* d_send, const ExReady& ready, size_t bytes, int* ticket) {
     (void)d_send;
     (void)ready;
     (void)bytes;
+    (void)ticket;
+    return -1;
+  }
+  virtual int wait_device(int ticket, const unsigned char** h_recv) {
+    (void)ticket;
     (void)h_recv;
     return -1;
   }

@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "../../include/eao_accel.h"
 #include "common.h"
@@ -48,10 +49,19 @@ struct RcclExchanger : Exchanger {
   int dev = 0, world = 1;
   ncclComm_t comm = nullptr;
   hipStream_t stream = nullptr;
-  hipEvent_t done = nullptr;  // the gathered records' copy-back (its errors)
-  unsigned char *h_recv = nullptr, *d_recv = nullptr;
-  size_t cap = 0;    // bytes per rank
-  unsigned seq = 0;  // k_recv_out's flag value of the latest call
+  hipEvent_t done = nullptr;  // the latest copy-back (its errors)
+  unsigned char* d_recv = nullptr;
+  size_t dcap = 0;   // bytes of d_recv
+  unsigned seq = 0;  // k_recv_out's flag value of the latest exchange
+  // pinned landing slots of the exchanges in flight: [world][bytes] records + the flag word
+  struct Slot {
+    unsigned char* h = nullptr;
+    size_t cap = 0;
+    unsigned want = 0;
+    bool busy = false;
+    unsigned* flag() const { return (unsigned*)(h + cap); }
+  };
+  std::vector<Slot> slots;
   uint64_t* rflag[8] = {};  // producer lanes' ready flags (signal memory), made on first use
 
   ~RcclExchanger() override {
@@ -61,7 +71,8 @@ struct RcclExchanger : Exchanger {
     if (done) (void)hipEventDestroy(done);
     if (comm) (void)ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
-    if (h_recv) (void)hipHostFree(h_recv);
+    for (Slot& sl : slots)
+      if (sl.h) (void)hipHostFree(sl.h);
     if (d_recv) (void)hipFree(d_recv);
   }
   int init(int d, int rank, int w, const void* uid) {
@@ -72,22 +83,43 @@ struct RcclExchanger : Exchanger {
     ncclUniqueId id;
     std::memcpy(&id, uid, sizeof id);
     EAO_NCCL_CHECK(ncclCommInitRank(&comm, world, id, rank));
-    return grow(4096);
+    return EAO_OK;
   }
-  int grow(size_t bytes) {
-    if (bytes <= cap) return EAO_OK;
-    const size_t c = std::max(bytes, 2 * cap);
-    // every pointer is released and cleared before reallocating, so a failed
-    // allocation below never leaves the destructor a stale pointer to free again
-    if (stream) EAO_HIP_CHECK(hipStreamSynchronize(stream));
-    if (h_recv) (void)hipHostFree(h_recv);
+  // the gathered records' device buffer: exchanges on the stream run one after the other, so one
+  // buffer serves them all (growing it waits for those in flight)
+  int grow_dev(size_t n) {
+    if (n <= dcap) return EAO_OK;
+    const size_t c = std::max(n, 2 * dcap);
+    EAO_HIP_CHECK(hipStreamSynchronize(stream));
     if (d_recv) (void)hipFree(d_recv);
-    h_recv = d_recv = nullptr;
-    cap = 0;
-    EAO_HIP_CHECK(hipHostMalloc((void**)&h_recv, c * world + 64, 0));  // + the flag word
-    EAO_HIP_CHECK(hipMalloc((void**)&d_recv, c * world));
-    *(volatile unsigned*)(h_recv + c * world) = seq;
-    cap = c;
+    d_recv = nullptr;
+    dcap = 0;
+    EAO_HIP_CHECK(hipMalloc((void**)&d_recv, c));
+    dcap = c;
+    return EAO_OK;
+  }
+  // a free landing slot of >= n bytes (a free slot that is too small is regrown)
+  int take_slot(size_t n, int* out) {
+    int k = -1;
+    for (int i = 0; i < (int)slots.size() && k < 0; i++)
+      if (!slots[i].busy && slots[i].cap >= n) k = i;
+    for (int i = 0; i < (int)slots.size() && k < 0; i++)
+      if (!slots[i].busy) k = i;
+    if (k < 0) {
+      slots.emplace_back();
+      k = (int)slots.size() - 1;
+    }
+    Slot& sl = slots[k];
+    if (sl.cap < n) {
+      const size_t c = std::max<size_t>(std::max(n, 2 * sl.cap), 4096);
+      if (sl.h) (void)hipHostFree(sl.h);
+      sl.h = nullptr;
+      sl.cap = 0;
+      EAO_HIP_CHECK(hipHostMalloc((void**)&sl.h, c + 64, 0));  // + the flag word
+      sl.cap = c;
+      *(volatile unsigned*)sl.flag() = 0;
+    }
+    *out = k;
     return EAO_OK;
   }
   int allgather(const void*, void*, size_t) override {
@@ -109,34 +141,48 @@ struct RcclExchanger : Exchanger {
     }
     return rflag[i];
   }
-  int allgather_device(const void* d_send, const ExReady& ready, size_t bytes, const unsigned char** out) override {
+  int start_device(const void* d_send, const ExReady& ready, size_t bytes, int* ticket) override {
     if (bytes == 0) return EAO_E_ARG;
-    if (int rc = grow(bytes)) return rc;
+    if (int rc = grow_dev(bytes * world)) return rc;
+    int k = -1;
+    if (int rc = take_slot(bytes * world, &k)) return rc;
+    Slot& sl = slots[k];
     if (ready.ev) EAO_HIP_CHECK(hipStreamWaitEvent(stream, ready.ev, 0));
     if (ready.flag)  // the HSA lane's k_publish stores the value once the record is complete
       EAO_HIP_CHECK(hipStreamWaitValue64(stream, (void*)ready.flag, ready.value, hipStreamWaitValueGte));
     EAO_NCCL_CHECK(ncclAllGather(d_send, d_recv, bytes, ncclUint8, comm, stream));
-    unsigned* flag = (unsigned*)(h_recv + cap * world);
-    const unsigned want = ++seq;
-    hipLaunchKernelGGL(k_recv_out, dim3(1), dim3(256), 0, stream, d_recv, h_recv, bytes * world, flag, want);
+    sl.want = ++seq;
+    hipLaunchKernelGGL(k_recv_out, dim3(1), dim3(256), 0, stream, d_recv, sl.h, bytes * world, sl.flag(), sl.want);
     EAO_HIP_CHECK(hipGetLastError());
     if (!done) EAO_HIP_CHECK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
     EAO_HIP_CHECK(hipEventRecord(done, stream));
+    sl.busy = true;
+    *ticket = k;
+    return EAO_OK;
+  }
+  int wait_device(int ticket, const unsigned char** out) override {
+    if (ticket < 0 || ticket >= (int)slots.size() || !slots[ticket].busy) {
+      set_error("rccl exchanger: wait on an unknown exchange");
+      return EAO_E_STATE;
+    }
+    Slot& sl = slots[ticket];
+    const unsigned* flag = sl.flag();
     // the replay thread spins (a blocking synchronisation may park it and pay a wake-up per
-    // exchange) on the flag; the event reports a failed launch (queried every 64 spins)
+    // exchange) on the flag; the latest event reports a failed launch (queried every 64 spins)
     for (unsigned k = 1;; k++) {
-      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == want) break;
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == sl.want) break;
       if ((k & 63) == 0) {
         const hipError_t r = hipEventQuery(done);
         if (r != hipSuccess && r != hipErrorNotReady) EAO_HIP_CHECK(r);
-        if (r == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != want) {
+        if (r == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != sl.want) {
           set_error("rccl exchanger: copy-back completed without its flag");
           return EAO_E_HIP;
         }
       }
       __builtin_ia32_pause();
     }
-    *out = h_recv;
+    sl.busy = false;  // its bytes stay until a later start_device takes the slot
+    *out = sl.h;
     return EAO_OK;
   }
 };
