@@ -70,13 +70,10 @@ class AssocEngine {
                     uint32_t trees, uint32_t seed, const uint32_t* d_sample, double* d_scores,
                     const Lane& s, int max_len, int max_sample, int npts_total,
                     double* contrib = nullptr,   // [trees][npts_total] scratch, default d_contrib
-                    double* scores2 = nullptr);  // optional second copy of the scores
-  // sharded forests (shard.h, device form): per launched cloud c the outlier bit mask
-  // (score > threshold, bit k of byte k / 8) written at byte meta[3 c + 2] of d_dst from
-  // the device scores at d_scores + meta[3 c] (meta[3 c + 1] points, th[c] the threshold);
-  // meta / th may be pinned host memory read in place
-  int pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores, unsigned char* d_dst,
-                 const Lane& s);
+                    double* scores2 = nullptr,   // optional second copy of the scores
+                    // sharded, device form: also each cloud's outlier bit mask into pdst, as pack_masks
+                    // (pk = the pack meta [3 nclouds], pth = the thresholds)
+                    const int* pk = nullptr, const float* pth = nullptr, unsigned char* pdst = nullptr);
   // on HSA lane s, after the launches before it: zero [zero, zero + zero_bytes) (may be empty),
   // then store v into *flag (the sharded exchange's GPU-side ready flag, shard.h ExReady)
   int publish(const Lane& s, void* zero, size_t zero_bytes, uint64_t* flag, uint64_t v);

@@ -1471,11 +1471,14 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
                                                      int ntrees, int npts_total,
                                                      const double* __restrict__ contrib,
                                                      double* __restrict__ scores,
-                                                     double* __restrict__ scores2, double x0a, double x0b) {
+                                                     double* __restrict__ scores2, double x0a, double x0b,
+                                                     const int* __restrict__ pk, const float* __restrict__ pth,
+                                                     unsigned char* __restrict__ pdst) {
   assoc_prio();
   const int c = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= len[c]) return;
+  const int n = len[c];
+  if (i >= n) return;  // (their lanes add 0 bits to the wave's mask below)
   const long long g = (long long)off[c] + i;
   double total = 0;
 #pragma unroll 10
@@ -1501,6 +1504,19 @@ __global__ __launch_bounds__(256) void k_iforest_sum(const int* __restrict__ off
   // of the pinned inputs, or the host's BAR writes on the HSA lanes)
   scores[g] = sc;
   if (scores2) scores2[g] = sc;
+  // sharded, device-form exchange: this cloud's outlier bit mask (score > the object's threshold,
+  // bit k of byte k / 8) straight into the batch's record at byte pk[3 c + 2] -- one ballot per
+  // wave, its bytes stored by the wave's first lane, active whenever any lane is (only the cloud's
+  // own (n + 7) / 8 bytes)
+  if (pdst) {
+    const uint64_t m = __ballot(sc > (double)pth[c]);
+    const int w0 = i & ~63;
+    if ((i & 63) == 0) {
+      unsigned char* d = pdst + pk[3 * c + 2] + (w0 >> 3);
+      const int nb = min(8, ((n + 7) >> 3) - (w0 >> 3));
+      for (int b = 0; b < nb; b++) d[b] = (unsigned char)(m >> (8 * b));
+    }
+  }
 }
 
 
@@ -1714,7 +1730,8 @@ int AssocEngine::iforest_table(uint32_t seed, uint32_t trees, hipStream_t s) {
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len,
                                uint32_t trees, uint32_t seed, const uint32_t* d_sample,
                                double* scores, const Lane& s, int maxN, int maxS, int npts_total,
-                               double* contrib, double* scores2) {
+                               double* contrib, double* scores2, const int* pk, const float* pth,
+                               unsigned char* pdst) {
   if (!contrib) contrib = d_contrib;
   if (nclouds <= 0) return EAO_OK;
   if ((int)trees > max_trees || nclouds > max_clouds || (contrib == d_contrib && npts_total > max_points)) {
@@ -1750,7 +1767,7 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
       return rc;
     return hsa_launch(s.q, ksum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0u, off, len, d_sample,
                       (const double*)d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2, pow_x0[0],
-                      pow_x0[1]);
+                      pow_x0[1], pk, pth, pdst);
   }
   hipLaunchKernelGGL(small ? k_iforest_tree<64> : k_iforest_tree<1024>, dim3(trees, nclouds), dim3(small ? 64 : 1024),
                      L.total, s.s, pts, off, len, d_mtinit, d_sample, maxN, maxS, npts_total, d_ctab, contrib, tab_n,
@@ -1758,7 +1775,7 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
   EAO_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(k_iforest_sum, dim3((maxN + 255) / 256, nclouds), dim3(256), 0, s.s, off, len,
                      d_sample, d_ctab, (int)trees, npts_total, (const double*)contrib, scores, scores2,
-                     pow_x0[0], pow_x0[1]);
+                     pow_x0[0], pow_x0[1], pk, pth, pdst);
   EAO_HIP_CHECK(hipGetLastError());
   return EAO_OK;
 }
@@ -1776,35 +1793,6 @@ __global__ __launch_bounds__(256) void k_stage(const unsigned char* __restrict__
 // Outlier bit masks of a sharded forest batch (the record the owner all-gathers, replay.cpp
 // exchange_batch): one thread per mask byte, 8 score tests each (score > th: the erase test of
 // Object.cc:1285-1289, with the exact threshold of k_iforest_sum's scores).
-__global__ __launch_bounds__(256) void k_pack_masks(const int* __restrict__ meta, const float* __restrict__ th,
-                                                    const double* __restrict__ scores,
-                                                    unsigned char* __restrict__ dst) {
-  const int c = blockIdx.y;
-  const int off = meta[3 * c], n = meta[3 * c + 1], out = meta[3 * c + 2];
-  const double t = (double)th[c];
-  const int nbytes = (n + 7) >> 3;
-  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < nbytes; j += gridDim.x * blockDim.x) {
-    unsigned v = 0;
-    for (int b = 0; b < 8; b++) {
-      const int k = 8 * j + b;
-      if (k < n && scores[off + k] > t) v |= 1u << b;
-    }
-    dst[out + j] = (unsigned char)v;
-  }
-}
-
-int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
-                            unsigned char* d_dst, const Lane& s) {
-  if (nclouds <= 0) return EAO_OK;
-  if (s.hsa()) {
-    static const int kid = hsa_kernel_id("eao::k_pack_masks(");
-    return hsa_launch(s.q, kid, dim3(4, nclouds), dim3(256), 0u, meta, th, d_scores, d_dst);
-  }
-  hipLaunchKernelGGL(k_pack_masks, dim3(4, nclouds), dim3(256), 0, s.s, meta, th, d_scores, d_dst);
-  EAO_HIP_CHECK(hipGetLastError());
-  return EAO_OK;
-}
-
 // The sharded exchange's ready flag (shard.h, ExReady): launched on an HSA lane after the kernels
 // that wrote a record (the lane's barrier bits order it after them, and their system-scope
 // releases made their stores visible), it zeroes an optional range (an empty record) and then

@@ -90,6 +90,13 @@ static const bool g_bar_fs = [] {
   const char* v = getenv("EAO_BAR_FS");
   return g_bar_inputs && !(v && v[0] == '0');
 }();
+// sharded exchanges started where their result is read (EAO_SHARD_EAGER=1: with their launches --
+// no gain measured, and one stream's waits then queue in launch order, not in the order of need:
+// profiles/r06_ab_shard_eager.txt)
+static const bool g_shard_eager = [] {
+  const char* v = getenv("EAO_SHARD_EAGER");
+  return v && v[0] == '1';
+}();
 // sharded replays on the HSA lanes (EAO_SHARD_HSA=0: HIP streams, A/B switch)
 static const bool g_shard_hsa = [] {
   const char* v = getenv("EAO_SHARD_HSA");
@@ -603,6 +610,7 @@ class ReplayEngine {
   struct ExRef {
     int lane = -1;  // ready flag index (forest lanes 0..kIfStreams-1, the frame start's lane kIfStreams)
     uint64_t value = 0;
+    int ticket = -1;  // the exchange, once started (Exchanger::start_device)
   };
   struct IfBatch {
     std::vector<Obj*> objs;
@@ -632,7 +640,7 @@ class ReplayEngine {
     double* contrib = nullptr;  // [50][max_points]
     // sharded: the per-rank record layout fixed at the launch (mask bytes, speculative
     // pairs, padded record size) and, in the device form, this rank's record in device
-    // memory, written by the forest batch's own kernels (pack_masks, np_batch)
+    // memory, written by the forest batch's own kernels (k_iforest_sum's masks, np_batch)
     std::vector<size_t> xmb, xnsr;
     size_t xbytes = 0;
     unsigned char* d_x = nullptr;
@@ -700,7 +708,10 @@ class ReplayEngine {
   }
   // device form: this rank's `bytes` at d_send (ready behind `ev`) gathered on the GPU;
   // *recv = the [sworld][bytes] records in pinned host memory
-  int exchange_device(const void* d_send, const Done& ev, const ExRef& xr, size_t bytes, const unsigned char** recv) {
+  // Started where the result is read (or, EAO_SHARD_EAGER=1, when the record's launches are
+  // enqueued: every rank launches in the same order, so the collectives keep one order); the
+  // all-gather waits for the record on the GPU, the host for the gathered copy.
+  int exchange_start(const void* d_send, const Done& ev, ExRef& xr, size_t bytes) {
     const double t0 = now_us();
     ExReady rd;
     if (ev.e) {
@@ -712,9 +723,18 @@ class ReplayEngine {
       set_error("replay: an HSA-lane record without its ready flag");
       return EAO_E_STATE;
     }
-    int rc = ex->allgather_device(d_send, rd, bytes, recv);
+    int rc = ex->start_device(d_send, rd, bytes, &xr.ticket);
     xstat[0] += 1;
     xstat[1] += (double)bytes;
+    xstat[2] += now_us() - t0;
+    return rc;
+  }
+  int exchange_device(const void* d_send, const Done& ev, ExRef& xr, size_t bytes, const unsigned char** recv) {
+    if (xr.ticket < 0)
+      if (int rc = exchange_start(d_send, ev, xr, bytes)) return rc;
+    const double t0 = now_us();
+    const int rc = ex->wait_device(xr.ticket, recv);
+    xr.ticket = -1;
     xstat[2] += now_us() - t0;
     return rc;
   }
@@ -1339,6 +1359,11 @@ class ReplayEngine {
       const int nl = (int)b.lc.size(), ns = (int)lsp.size();
       for (int c = 0; c < nb; c++) b.objs[c]->slot = k;
       b.left = nb;
+      if (b.xr.ticket >= 0) {  // the slot's previous exchange, started but never read: drained
+        const unsigned char* r = nullptr;
+        if (int rc = ex->wait_device(b.xr.ticket, &r)) return rc;
+        b.xr = ExRef();
+      }
       b.xdone = !sharded();
       b.launched = nl > 0;
       if (sharded()) {
@@ -1370,6 +1395,8 @@ class ReplayEngine {
             EAO_HIP_CHECK(hipMemsetAsync(b.d_x, 0, b.xbytes, st.s));
           }
           if (int rc = lane_record(st, b.done)) return rc;
+          if (g_shard_eager)
+            if (int rc = exchange_start(b.d_x, b.done, b.xr, b.xbytes)) return rc;
         }
       }
       if (!b.launched) continue;
@@ -1501,9 +1528,11 @@ class ReplayEngine {
       // scores go straight to pinned host memory (a device-to-host copy costs
       // ~35 us of round trip per launch on this box) and, for the speculative
       // NP pairs, to device memory too
+      // device-form exchange: the outlier bit masks go into this rank's record from the score kernel
       int rc = A->iforest_batch(nl, (const float*)(din + o_pts), dm, dm + nl, 50, 12345,
                                 (const uint32_t*)(dm + 2 * nl), (double*)b.h_out, st, maxN, maxN / 2, np, b.contrib,
-                                (double*)b.d_out);
+                                (double*)b.d_out, xdev() ? (const int*)(din + o_pk) : nullptr,
+                                xdev() ? (const float*)(din + o_pkth) : nullptr, xdev() ? b.d_x : nullptr);
       if (rc) return rc;
       if (ns) {
         const int* spm = (const int*)(din + o_spm);
@@ -1517,13 +1546,12 @@ class ReplayEngine {
         prof[9] += ns;
       }
       if (xdev()) {
-        const int* dpk = (const int*)(din + o_pk);
-        rc = A->pack_masks(nl, dpk, (const float*)(din + o_pkth), (const double*)b.d_out, b.d_x, st);
-        if (rc) return rc;
         b.xr = ExRef();
         if (st.hsa() && (rc = publish(st, k % kIfStreams, nullptr, 0, &b.xr))) return rc;
       }
       if (int rc1 = lane_record(st, b.done)) return rc1;
+      if (xdev() && g_shard_eager)
+        if (int rc1 = exchange_start(b.d_x, b.done, b.xr, b.xbytes)) return rc1;
       tr(5, k, nl, maxN);
     }
     return EAO_OK;
@@ -2029,6 +2057,7 @@ class ReplayEngine {
         rn_dev = false;
         if (rc) return rc;
       }
+      if (g_shard_eager && (rc = exchange_start(d_out, gpu0, fs_xr, bytes))) return rc;
       idle_work(gpu0);  // the next frame's steps 1-6, while the GPU is busy
       const unsigned char* recv = nullptr;
       if ((rc = exchange_device(d_out, gpu0, fs_xr, bytes, &recv))) return rc;

@@ -55,7 +55,7 @@ int AssocEngine::np_batch(int npairs, const float* fp, const uint8_t* fv, const 
 }
 int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, const int* len, uint32_t trees,
                                uint32_t seed, const uint32_t* sample, double* scores, const Lane&, int, int,
-                               int, double*, double* scores2) {
+                               int, double*, double* scores2, const int* pk, const float* pth, unsigned char* pdst) {
   // fault injection (tests): EAO_HARNESS_FAIL_IFOREST=N fails the N-th forest launch (1-based)
   static int calls = 0;
   static const int fail_at = std::getenv("EAO_HARNESS_FAIL_IFOREST") ? std::atoi(std::getenv("EAO_HARNESS_FAIL_IFOREST")) : 0;
@@ -70,6 +70,13 @@ int AssocEngine::iforest_batch(int nclouds, const float* pts, const int* off, co
       for (int i = 0; i < len[c]; i++) scores[off[c] + i] = NAN;  // Build() failed: nothing erased
     if (scores2)
       for (int i = 0; i < len[c]; i++) scores2[off[c] + i] = scores[off[c] + i];
+    if (pdst)  // k_iforest_sum's outlier bit mask of the device-form exchange
+      for (int j = 0; j < (len[c] + 7) / 8; j++) {
+        unsigned v = 0;
+        for (int b = 0; b < 8 && 8 * j + b < len[c]; b++)
+          if (scores[off[c] + 8 * j + b] > (double)pth[c]) v |= 1u << b;
+        pdst[pk[3 * c + 2] + j] = (unsigned char)v;
+      }
   }
   return 0;
 }
@@ -112,7 +119,7 @@ extern "C" eao_assoc* harness_assoc_create() { auto* a = new eao_assoc(); a->e.d
 // The RCCL exchanger is product-only. In its place eao_replay_shard_rccl gets a
 // device-form exchanger over the all-gather callback set by harness_set_device_exchange
 // (gloo from Python): "device" memory is host memory here, so the replay's device-form
-// code paths (records written by pack_masks / np_batch / rects_np into device buffers,
+// code paths (records written by iforest_batch / np_batch / rects_np into device buffers,
 // gathered from there) run on the CPU against the oracle.
 namespace eao {
 namespace {
@@ -127,14 +134,36 @@ struct DeviceLoopExchanger : Exchanger {
     return EAO_E_ARG;
   }
   bool device_form() const override { return true; }
-  int allgather_device(const void* d_send, const ExReady&, size_t bytes, const unsigned char** out) override {
-    recv.assign(bytes * world, 0xcd);
+  // started exchanges gather at once (the callback is synchronous), in start order on every rank;
+  // the ticket's records wait in their own buffer
+  std::vector<std::vector<unsigned char>> tickets;
+  std::vector<bool> busy;
+  int start_device(const void* d_send, const ExReady&, size_t bytes, int* ticket) override {
+    int k = 0;
+    while (k < (int)busy.size() && busy[k]) k++;
+    if (k == (int)busy.size()) {
+      busy.push_back(false);
+      tickets.emplace_back();
+    }
+    std::vector<unsigned char>& r = tickets[k];
+    r.assign(bytes * world, 0xcd);
     if (world == 1) {
-      std::memcpy(recv.data(), d_send, bytes);
-    } else if (!g_dev_fn || g_dev_fn(g_dev_ctx, d_send, recv.data(), bytes)) {
+      std::memcpy(r.data(), d_send, bytes);
+    } else if (!g_dev_fn || g_dev_fn(g_dev_ctx, d_send, r.data(), bytes)) {
       set_error("harness device exchanger: all-gather failed");
       return EAO_E_ARG;
     }
+    busy[k] = true;
+    *ticket = k;
+    return EAO_OK;
+  }
+  int wait_device(int ticket, const unsigned char** out) override {
+    if (ticket < 0 || ticket >= (int)busy.size() || !busy[ticket]) {
+      set_error("harness device exchanger: unknown ticket");
+      return EAO_E_STATE;
+    }
+    busy[ticket] = false;
+    recv = tickets[ticket];
     *out = recv.data();
     return EAO_OK;
   }
@@ -147,19 +176,6 @@ Exchanger* make_rccl_exchanger(int, int, int world, const void*, int* rc) {
 int AssocEngine::publish(const Lane&, void*, size_t, uint64_t*, uint64_t) {
   set_error("harness: no HSA lanes");  // the harness's lanes are HIP-stream lanes (never called)
   return EAO_E_STATE;
-}
-int AssocEngine::pack_masks(int nclouds, const int* meta, const float* th, const double* d_scores,
-                            unsigned char* d_dst, const Lane&) {
-  for (int c = 0; c < nclouds; c++) {
-    const int off = meta[3 * c], n = meta[3 * c + 1], out = meta[3 * c + 2];
-    for (int j = 0; j < (n + 7) / 8; j++) {
-      unsigned v = 0;
-      for (int b = 0; b < 8 && 8 * j + b < n; b++)
-        if (d_scores[off + 8 * j + b] > (double)th[c]) v |= 1u << b;
-      d_dst[out + j] = (unsigned char)v;
-    }
-  }
-  return EAO_OK;
 }
 }  // namespace eao
 extern "C" void harness_set_device_exchange(eao_allgather_fn fn, void* ctx) {
