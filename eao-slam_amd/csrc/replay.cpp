@@ -97,6 +97,12 @@ static const bool g_shard_eager = [] {
   const char* v = getenv("EAO_SHARD_EAGER");
   return v && v[0] == '1';
 }();
+// ComputeMeanAndStandard skipped when its inputs repeat its last call's (EAO_MS_MEMO=0: always
+// computed, A/B and check)
+static const bool g_ms_memo = [] {
+  const char* v = getenv("EAO_MS_MEMO");
+  return !(v && v[0] == '0');
+}();
 // sharded replays on the HSA lanes (EAO_SHARD_HSA=0: HIP streams, A/B switch)
 static const bool g_shard_hsa = [] {
   const char* v = getenv("EAO_SHARD_HSA");
@@ -281,6 +287,15 @@ struct Obj {  // Object_Map
   std::vector<Dfr> dfr;
   float dfrT[16];
   bool proj_dfr = false;  // a projected-rect recompute is among them
+  // ComputeMeanAndStandard's inputs at its last call (ReplayEngine::mean_std): a call whose inputs
+  // are all the same -- the point list, no point moved or turned bad since (the engine's epoch),
+  // the frames' positions, the angles and the cuboid centre it starts from -- computes the same
+  // outputs into the same state, and is skipped
+  uint64_t ms_epoch = ~0ull;
+  std::vector<MapPt*> ms_pts;
+  std::vector<float> ms_fp;  // the frames' P(), 3 per frame
+  float ms_rot[3] = {0, 0, 0};
+  double ms_cc_in[3] = {0, 0, 0}, ms_cc_out[3] = {0, 0, 0};
 };
 const float* Det::P() const { return alias ? alias->center : pos; }
 
@@ -1098,7 +1113,50 @@ class ReplayEngine {
   // ComputeMeanAndStandard scratch: the object's positions gathered once per call (SoA), and
   // their images under the inverse cuboid pose
   std::vector<float> ms_p[3], ms_t[3];
+  uint64_t pt_epoch = 1;  // bumped whenever a map point's position or bad flag changes
+  // mean_std(o) with exactly the inputs of its last call: it would write the values o holds now
+  bool mean_std_same(const Obj* o) const {
+    if (!g_ms_memo || o->ms_epoch != pt_epoch || o->pts.size() != o->ms_pts.size() ||
+        o->frames.size() * 3 != o->ms_fp.size() || o->rotY != o->ms_rot[0] || o->rotP != o->ms_rot[1] ||
+        o->rotR != o->ms_rot[2])
+      return false;
+    for (int a = 0; a < 3; a++)  // the centre update_pose starts from (frames >= 5): a fixed point
+      if (o->frames.size() >= 5 && !(o->center_c[a] == o->ms_cc_out[a] && o->ms_cc_in[a] == o->ms_cc_out[a]))
+        return false;
+    if (!o->pts.empty() && std::memcmp(o->pts.data(), o->ms_pts.data(), sizeof(MapPt*) * o->pts.size()) != 0)
+      return false;
+    for (size_t k = 0; k < o->frames.size(); k++) {
+      const float* fp = o->frames[k]->P();
+      if (std::memcmp(fp, &o->ms_fp[3 * k], sizeof(float) * 3) != 0) return false;
+    }
+    return true;
+  }
   void mean_std(Obj* o) {
+    if (mean_std_same(o)) {
+      prof[27] += 1;
+      return;
+    }
+    double cc_in[3];
+    for (int a = 0; a < 3; a++) cc_in[a] = o->center_c[a];
+    o->ms_epoch = ~0ull;
+    struct Memo {  // the inputs of this call, recorded on every return
+      Obj* o;
+      const double* cc;
+      const uint64_t ep;
+      ~Memo() {
+        o->ms_epoch = ep;
+        o->ms_pts = o->pts;
+        o->ms_fp.resize(3 * o->frames.size());
+        for (size_t k = 0; k < o->frames.size(); k++) std::memcpy(&o->ms_fp[3 * k], o->frames[k]->P(), sizeof(float) * 3);
+        o->ms_rot[0] = o->rotY;
+        o->ms_rot[1] = o->rotP;
+        o->ms_rot[2] = o->rotR;
+        for (int a = 0; a < 3; a++) {
+          o->ms_cc_in[a] = cc[a];
+          o->ms_cc_out[a] = o->center_c[a];
+        }
+      }
+    } memo{o, cc_in, pt_epoch};
     double T0 = now_us();
     for (int a = 0; a < 3; a++) o->sum[a] = 0;
     const size_t n0 = o->pts.size();
@@ -2650,6 +2708,9 @@ class ReplayEngine {
     for (int i = 0; i < n; i++) {
       MapPt* p = mp_lookup(ids[i]);
       if (!p) continue;  // never tracked: nothing holds it
+      if ((pos && std::memcmp(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3) != 0) ||
+          (bad && p->bad != (bad[i] != 0)))
+        pt_epoch++;
       if (pos) {
         std::memcpy(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3);
         p->proj_epoch = 0;
@@ -2802,9 +2863,11 @@ class ReplayEngine {
         for (int i = (int)s.k; i < e; i++) {
           if (ahead && !mp_lookup(in.ids[i])) s.created.push_back(in.ids[i]);
           MapPt* p = mappoint(in.ids[i]);
+          const bool nb = in.bad ? in.bad[i] != 0 : false;
+          if (std::memcmp(p->pos, in.pos + 3 * (size_t)i, sizeof(float) * 3) != 0 || p->bad != nb) pt_epoch++;
           for (int a = 0; a < 3; a++) p->pos[a] = in.pos[3 * i + a];
           p->proj_epoch = 0;
-          p->bad = in.bad ? in.bad[i] != 0 : false;
+          p->bad = nb;
           s.tr[i] = p;
         }
         s.k = (size_t)e;
