@@ -103,6 +103,11 @@ static const bool g_ms_memo = [] {
   const char* v = getenv("EAO_MS_MEMO");
   return !(v && v[0] == '0');
 }();
+// EAO_MS_VERIFY=1: every skip also checks each held point against the object's change mark
+static const bool g_ms_verify = [] {
+  const char* v = getenv("EAO_MS_VERIFY");
+  return v && v[0] == '1';
+}();
 // sharded replays on the HSA lanes (EAO_SHARD_HSA=0: HIP streams, A/B switch)
 static const bool g_shard_hsa = [] {
   const char* v = getenv("EAO_SHARD_HSA");
@@ -217,6 +222,7 @@ struct MapPt {
   float fu = 0, fv = 0;  // MapPoint::feature (current-frame keypoint)
   float pu = 0, pv = 0;  // projection under the current pose (cached per pose epoch)
   unsigned proj_epoch = 0;
+  uint64_t ver = 0;  // the engine's point epoch at the last change of pos / bad
   // object_id_vector: a handful of (object id, count) entries per point,
   // only ever looked up (never iterated), so a flat vector suffices
   std::vector<std::pair<int, int>> votes;
@@ -292,10 +298,15 @@ struct Obj {  // Object_Map
   // the frames' positions, the angles and the cuboid centre it starts from -- computes the same
   // outputs into the same state, and is skipped
   uint64_t ms_epoch = ~0ull;
+  uint64_t pt_chg = 0;  // the point epoch of the last change of a point it may hold (one that voted for it)
   std::vector<MapPt*> ms_pts;
   std::vector<float> ms_fp;  // the frames' P(), 3 per frame
   float ms_rot[3] = {0, 0, 0};
   double ms_cc_in[3] = {0, 0, 0}, ms_cc_out[3] = {0, 0, 0};
+  // the point list big_to_small left at its last call: none of them inside bts_box at epoch bts_epoch
+  uint64_t bts_epoch = ~0ull;
+  float bts_box[6] = {0, 0, 0, 0, 0, 0};
+  std::vector<MapPt*> bts_pts;
 };
 const float* Det::P() const { return alias ? alias->center : pos; }
 
@@ -1114,9 +1125,26 @@ class ReplayEngine {
   // their images under the inverse cuboid pose
   std::vector<float> ms_p[3], ms_t[3];
   uint64_t pt_epoch = 1;  // bumped whenever a map point's position or bad flag changes
+  // a point that changes marks the objects it voted for: every object that holds a point got its
+  // vote first (vote / vote_insert before each pts.push_back) and votes are never withdrawn
+  void point_changed(MapPt* p) {
+    p->ver = ++pt_epoch;
+    for (auto& v : p->votes)
+      if ((size_t)v.first < objs.size()) objs[v.first]->pt_chg = pt_epoch;
+  }
+  bool points_unchanged(const Obj* o, uint64_t since) const {
+    if (o->pt_chg > since) return false;
+    if (g_ms_verify)
+      for (const MapPt* p : o->pts)
+        if (p->ver > since) {
+          fprintf(stderr, "eao: point %d of object %d changed unmarked\n", p->id, o->id);
+          abort();
+        }
+    return true;
+  }
   // mean_std(o) with exactly the inputs of its last call: it would write the values o holds now
   bool mean_std_same(const Obj* o) const {
-    if (!g_ms_memo || o->ms_epoch != pt_epoch || o->pts.size() != o->ms_pts.size() ||
+    if (!g_ms_memo || o->ms_epoch == ~0ull || o->pts.size() != o->ms_pts.size() ||
         o->frames.size() * 3 != o->ms_fp.size() || o->rotY != o->ms_rot[0] || o->rotP != o->ms_rot[1] ||
         o->rotR != o->ms_rot[2])
       return false;
@@ -1125,6 +1153,7 @@ class ReplayEngine {
         return false;
     if (!o->pts.empty() && std::memcmp(o->pts.data(), o->ms_pts.data(), sizeof(MapPt*) * o->pts.size()) != 0)
       return false;
+    if (!points_unchanged(o, o->ms_epoch)) return false;
     for (size_t k = 0; k < o->frames.size(); k++) {
       const float* fp = o->frames[k]->P();
       if (std::memcmp(fp, &o->ms_fp[3 * k], sizeof(float) * 3) != 0) return false;
@@ -2710,7 +2739,7 @@ class ReplayEngine {
       if (!p) continue;  // never tracked: nothing holds it
       if ((pos && std::memcmp(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3) != 0) ||
           (bad && p->bad != (bad[i] != 0)))
-        pt_epoch++;
+        point_changed(p);
       if (pos) {
         std::memcpy(p->pos, pos + 3 * (size_t)i, sizeof(float) * 3);
         p->proj_epoch = 0;
@@ -2864,7 +2893,7 @@ class ReplayEngine {
           if (ahead && !mp_lookup(in.ids[i])) s.created.push_back(in.ids[i]);
           MapPt* p = mappoint(in.ids[i]);
           const bool nb = in.bad ? in.bad[i] != 0 : false;
-          if (std::memcmp(p->pos, in.pos + 3 * (size_t)i, sizeof(float) * 3) != 0 || p->bad != nb) pt_epoch++;
+          if (std::memcmp(p->pos, in.pos + 3 * (size_t)i, sizeof(float) * 3) != 0 || p->bad != nb) point_changed(p);
           for (int a = 0; a < 3; a++) p->pos[a] = in.pos[3 * i + a];
           p->proj_epoch = 0;
           p->bad = nb;
@@ -3329,16 +3358,25 @@ class ReplayEngine {
   void big_to_small(Obj* a, Obj* s) {  // Object.cc:1926-2040
     Tick tbs(&prof[37]);
     double tq = now_us();
-    size_t w = 0;
-    for (size_t i = 0; i < a->pts.size(); i++) {
-      const float* P = a->pts[i]->pos;
-      const bool in = P[0] > s->xmn && P[0] < s->xmx && P[1] > s->ymn && P[1] < s->ymx && P[2] > s->zmn &&
-                      P[2] < s->zmx;
-      if (!in) a->pts[w++] = a->pts[i];
+    const float box[6] = {s->xmn, s->xmx, s->ymn, s->ymx, s->zmn, s->zmx};
+    // the same box over the list it left last time, no point moved since: nothing to erase
+    if (!(g_ms_memo && a->bts_epoch != ~0ull && std::memcmp(box, a->bts_box, sizeof box) == 0 &&
+          a->pts == a->bts_pts && points_unchanged(a, a->bts_epoch))) {
+      prof[31] += 1;
+      size_t w = 0;
+      for (size_t i = 0; i < a->pts.size(); i++) {
+        const float* P = a->pts[i]->pos;
+        const bool in = P[0] > box[0] && P[0] < box[1] && P[1] > box[2] && P[1] < box[3] && P[2] > box[4] &&
+                        P[2] < box[5];
+        if (!in) a->pts[w++] = a->pts[i];
+      }
+      a->pts.resize(w);
     }
-    a->pts.resize(w);
     prof[38] += now_us() - tq;
-    mean_std(a);
+    mean_std(a);  // drops bad points only: the list stays clear of the box
+    a->bts_epoch = pt_epoch;
+    std::memcpy(a->bts_box, box, sizeof box);
+    a->bts_pts = a->pts;
   }
 
   void deal_overlap(Obj* a, Obj* b, float ox, float oy, float oz) {  // Object.cc:2077-2178

@@ -293,3 +293,17 @@ def test_host_resume_after_failed_stream_with_other_frames(harness):
     assert a["rows"] == b["rows"]
     assert a["held"] == b["held"] and a["ints"] == b["ints"] and a["pts"] == b["pts"]
     assert np.allclose(a["floats"], b["floats"], rtol=1e-6, atol=1e-6)
+
+
+def test_host_mean_std_skips_checked_point_by_point(harness):
+    """The ComputeMeanAndStandard / BigToSmall skips (replay.cpp mean_std_same, big_to_small) trust
+    each object's change mark, set through the votes of a point that moves or turns bad. With
+    EAO_MS_VERIFY=1 every skip also compares each held point's own change epoch (abort on a miss);
+    the point-record streams, where LocalMapping moves points no frame re-reports, run under it in a
+    fresh process (the switch is read at load) and still equal the oracle."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-p", "no:cacheprovider", os.path.join(here, "test_replay_host.py"),
+                          "-k", "point_updates or run_updates or fr3_real_stream"],
+                         env=dict(os.environ, EAO_MS_VERIFY="1"), capture_output=True, text=True, timeout=900)
+    assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
+    assert "5 passed" in out.stdout, out.stdout[-500:]

@@ -32,7 +32,7 @@ passes = int(([a for a in sys.argv[1:] if a.isdigit()] or ["2"])[0])
 frames, flag = (synth.assoc_stream_fr3_real(0, 2582), "Full") if full else (synth.assoc_stream_fr3_real(), "EAO")
 packed = ea.Replay.pack(frames)
 HOST = ["#ms_skip", "update", "ms_pass12", "ms_pass3", "ms_pose", "ms_corners", "lm_stats", "lm_merge_overlap", "lm_overlap",
-        "big_to_small", "bts_filter", "steps1-3", "steps4-9", "local_mapping", "assoc_loop", "frame"]
+        "big_to_small", "bts_filter", "#bts_scan", "lm_forest", "#lm_forests", "lm_flush", "steps1-3", "steps4-9", "local_mapping", "assoc_loop", "frame"]
 
 
 class A:
