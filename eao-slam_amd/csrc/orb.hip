@@ -705,41 +705,17 @@ __device__ __forceinline__ int child_of(uint32_t k, int mx, int my) {
   return x < mx ? (y < my ? 0 : 2) : (y < my ? 1 : 3);
 }
 
-template <int QCAP>
-__global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ cand,
-                                                   long long cand_stride,
-                                                   const int* __restrict__ cell_cnt, int ncells,
-                                                   const LevelDev* __restrict__ levels,
-                                                   const CellDev* __restrict__ cells,
-                                                   uint32_t* __restrict__ qbuf, long long qstride,
-                                                   uint32_t* __restrict__ sel, long long sel_stride,
-                                                   int* __restrict__ sel_cnt, int nlevels) {
-  __shared__ QShared<QCAP> S;
+// the quadtree of one (level, frame) over n keys already in B0, ping-ponging with B1: global
+// memory (LK false) or the workgroup's dynamic LDS (LK true, single frames: every divide's key
+// reads and partition writes are then LDS round trips instead of L2 ones -- the walk is a chain
+// of ~140 dependent divides at level 0)
+template <int QCAP, bool LK>
+__device__ __forceinline__ void dist_tree(QShared<QCAP>& S, uint32_t* B0, uint32_t* B1, int n, const LevelDev& L,
+                                          uint32_t* __restrict__ S_out, int* __restrict__ sel_cnt_out, int lane) {
   constexpr int QOS = QShared<QCAP>::QOS;
-  // grid (frames, levels): workgroups are dispatched x fastest, so every frame's level-0
-  // quadtree (the longest walk) starts first and the shorter levels fill in behind it
-  const int l = blockIdx.y, f = blockIdx.x, lane = threadIdx.x;
-  const LevelDev& L = levels[l];
-  const uint32_t* C = cand + f * cand_stride;
-  // ping-pong halves of this (frame, level): [2 cand_off, 2 cand_off + 2 cand_cap) of the frame area
-  uint32_t* B0 = qbuf + f * qstride + 2 * (long long)L.cand_off;
-  uint32_t* B1 = B0 + L.cand_cap;
-  uint32_t* bufs[2] = {B0, B1};
-  // ---- gather candidates in vToDistributeKeys order (cells row-major)
-  int n = 0;
-  for (int k = 0; k < L.cell_count; k++) {
-    const CellDev& c = cells[L.cell_begin + k];
-    const int cnt = min(cell_cnt[f * ncells + L.cell_begin + k], c.cap);
-    for (int i = lane; i < cnt; i += 64) B0[n + i] = C[c.slot + i];
-    n += cnt;
-  }
-  __syncthreads();
-  uint32_t* S_out = sel + f * sel_stride + L.sel_off;
+  // a select, not an array: the pointers keep their address space (ds_* on the LDS path)
+  auto bufs = [&](int b) -> uint32_t* { return b ? B1 : B0; };
   const int N = L.nfeat;
-  if (n == 0) {
-    if (lane == 0) sel_cnt[f * nlevels + l] = 0;
-    return;
-  }
   // ---- free list
   for (int i = lane; i < QCAP; i += 64) {
     S.freel[i] = (int16_t)(QCAP - 1 - i);
@@ -823,8 +799,8 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
     const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2);
     const int hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
     const int mx = q.x0 + hx, my = q.y0 + hy;
-    const uint32_t* src = bufs[q.buf] + q.beg;
-    uint32_t* dst = bufs[q.buf ^ 1] + q.beg;
+    const uint32_t* src = bufs(q.buf) + q.beg;
+    uint32_t* dst = bufs(q.buf ^ 1) + q.beg;
     // keys are read in groups of RK * 64 with all RK loads in flight
     // together; a node of <= RK * 64 keys keeps them in registers for the
     // scatter pass, larger nodes read each group again
@@ -1012,7 +988,7 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
     uint32_t bk = 0;
     if (s >= 0) {
       const int cnt = S.node[s].cnt;
-      const uint32_t* src = bufs[S.node[s].buf] + S.node[s].beg;
+      const uint32_t* src = bufs(S.node[s].buf) + S.node[s].beg;
       int best_s = -1;
       for (int idx = 0; idx < cnt; idx++) {
         const uint32_t k = src[idx];
@@ -1027,7 +1003,540 @@ __global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ 
     if (s >= 0 && p < L.sel_cap) S_out[p] = bk;
     outn += popc64(m);
   }
-  if (lane == 0) sel_cnt[f * nlevels + l] = overflow ? -1 : min(outn, L.sel_cap);
+  if (lane == 0) *sel_cnt_out = overflow ? -1 : min(outn, L.sel_cap);
+}
+
+// lds_keys > 0: the keys of a (level, frame) with n <= lds_keys are distributed in the dynamic
+// LDS (2 x lds_keys words), larger ones in qbuf
+template <int QCAP>
+__global__ __launch_bounds__(64) void k_distribute(const uint32_t* __restrict__ cand,
+                                                   long long cand_stride,
+                                                   const int* __restrict__ cell_cnt, int ncells,
+                                                   const LevelDev* __restrict__ levels,
+                                                   const CellDev* __restrict__ cells,
+                                                   uint32_t* __restrict__ qbuf, long long qstride,
+                                                   uint32_t* __restrict__ sel, long long sel_stride,
+                                                   int* __restrict__ sel_cnt, int nlevels, int lds_keys) {
+  __shared__ QShared<QCAP> S;
+  extern __shared__ uint32_t qk_lds[];
+  // grid (frames, levels): workgroups are dispatched x fastest, so every frame's level-0
+  // quadtree (the longest walk) starts first and the shorter levels fill in behind it
+  const int l = blockIdx.y, f = blockIdx.x, lane = threadIdx.x;
+  const LevelDev& L = levels[l];
+  const uint32_t* C = cand + f * cand_stride;
+  uint32_t* S_out = sel + f * sel_stride + L.sel_off;
+  int* sc = sel_cnt + f * nlevels + l;
+  // the cells' counts 64 at a time (one lane per cell: independent loads, not a chain of
+  // scalar ones over the level's ~340 cells)
+  auto cell_count = [&](int k) -> int {
+    return k < L.cell_count ? min(cell_cnt[f * ncells + L.cell_begin + k], cells[L.cell_begin + k].cap) : 0;
+  };
+  int n = 0;
+  for (int k0 = 0; k0 < L.cell_count; k0 += 64) n += wave_sum(cell_count(k0 + lane));
+  if (n == 0) {
+    if (lane == 0) *sc = 0;
+    return;
+  }
+  // ---- gather candidates in vToDistributeKeys order (cells row-major): per 64 cells, an
+  // exclusive scan of their counts places each cell, and the wave copies the group's keys as
+  // one flat range (a key finds its cell by binary search over the scan, staged in LDS)
+  auto gather = [&](uint32_t* B0) {
+    int* gpre = (int*)S.skey;  // free until the tree's first compaction
+    int* gslot = gpre + 64;
+    int o = 0;
+    for (int k0 = 0; k0 < L.cell_count; k0 += 64) {
+      const int k = k0 + lane;
+      const int cnt = cell_count(k);
+      int pre = cnt;  // inclusive scan
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(pre, d, 64);
+        if (lane >= d) pre += u;
+      }
+      gpre[lane] = pre - cnt;
+      gslot[lane] = k < L.cell_count ? cells[L.cell_begin + k].slot : 0;
+      const int tot = __shfl(pre, 63, 64);
+      __syncthreads();
+      for (int t = lane; t < tot; t += 64) {
+        int lo = 0;  // last cell with gpre <= t
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+          if (gpre[lo + step] <= t) lo += step;
+        B0[o + t] = C[gslot[lo] + (t - gpre[lo])];
+      }
+      o += tot;
+      __syncthreads();
+    }
+  };
+  if (n <= lds_keys) {
+    gather(qk_lds);
+    dist_tree<QCAP, true>(S, qk_lds, qk_lds + lds_keys, n, L, S_out, sc, lane);
+  } else {
+    // ping-pong halves of this (frame, level): [2 cand_off, 2 cand_off + 2 cand_cap) of the frame area
+    uint32_t* B0 = qbuf + f * qstride + 2 * (long long)L.cand_off;
+    gather(B0);
+    dist_tree<QCAP, false>(S, B0, B0 + L.cand_cap, n, L, S_out, sc, lane);
+  }
+}
+
+// ---------------------------------------------------------------- quadtree, single frames
+// k_distribute_mw: the same DistributeOctTree as k_distribute, NW waves per (level, frame), for
+// launches of a few frames (the drop-in's single calls), where one wave's chain of ~140 divides
+// per level-0 tree is the latency. The divides of a pass (every expandable node of the list), and
+// the candidates of one final-phase round, depend only on their own node: they are counted in
+// parallel (a wave per node), one wave places them -- children's ids, list positions, expandable
+// list and the point where the final phase reaches N, all exclusive scans over the divides in the
+// sequential order --, and they are partitioned in parallel. The sequential pool bound (QCAP nodes
+// alive; overflow -> -1) is evaluated on the same scans; the physical pool has room for the
+// parents still held while their children are written.
+template <int QCAP>
+struct QSharedMW {
+  static constexpr int QOS = 5 * QCAP;
+  static constexpr int PC = 2 * QCAP + 64;  // physical node slots (< 4096: 12 bits in the sort key)
+  QNode node[PC];
+  int16_t order[QOS];
+  int16_t freel[PC];
+  int16_t vcur[QCAP];
+  int16_t vprev[QCAP];
+  int16_t dv[QCAP];  // the round's divides in the sequential order (slots)
+  unsigned long long skey[QCAP];
+  int dcnt[QCAP][4];  // per divide: keys per child
+  int dch[QCAP];      // per divide: children of the earlier divides
+  int dex[QCAP];      // per divide: expandable children of the earlier divides
+  int ctl[16];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int QCAP, int NW>
+__device__ __forceinline__ void dist_tree_mw(QSharedMW<QCAP>& S, uint32_t* B0, uint32_t* B1, int n,
+                                             const LevelDev& L, uint32_t* __restrict__ S_out,
+                                             int* __restrict__ sel_cnt_out) {
+  constexpr int QOS = QSharedMW<QCAP>::QOS, PC = QSharedMW<QCAP>::PC, NT = 64 * NW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  auto bufs = [&](int b) -> uint32_t* { return b ? B1 : B0; };
+  const int N = L.nfeat;
+  for (int i = tid; i < PC; i += NT) {
+    S.freel[i] = (int16_t)(PC - 1 - i);
+    S.node[i].alive = 0;
+  }
+  // ---- initial nodes (ORBextractor.cc:543-585): a stable partition of the keys by initial node,
+  // B0 -> B1, each wave over one contiguous range of keys
+  const int nIni = min(L.nIni, 16);
+  const float hX = L.hX;
+  int* icnt = &S.dcnt[0][0];  // [NW][16]
+  const int per = ((n + NW - 1) / NW + 63) & ~63;
+  const int r0 = min(n, wv * per), r1 = min(n, r0 + per);
+  for (int i = 0; i < nIni; i++) {
+    int cnt = 0;
+    for (int c0 = r0; c0 < r1; c0 += 64) {
+      const int idx = c0 + lane;
+      const bool in = idx < r1 && (int)((float)kp_x(B0[idx]) / hX) == i;
+      cnt += popc64(ballot(in));
+    }
+    if (lane == 0) icnt[wv * 16 + i] = cnt;
+  }
+  __syncthreads();
+  {
+    int base = 0;
+    for (int i = 0; i < nIni; i++) {
+      int off = base;
+      for (int w = 0; w < NW; w++) {
+        if (w == wv) break;
+        off += icnt[w * 16 + i];
+      }
+      for (int c0 = r0; c0 < r1; c0 += 64) {
+        const int idx = c0 + lane;
+        const bool in = idx < r1 && (int)((float)kp_x(B0[idx]) / hX) == i;
+        const uint64_t m = ballot(in);
+        if (in) B1[off + popc64(m & lanes_below())] = B0[idx];
+        off += popc64(m);
+      }
+      for (int w = 0; w < NW; w++) base += icnt[w * 16 + i];
+    }
+  }
+  if (tid == 0) {
+    int base = 0, alive = 0, nfp = PC;
+    int slots[16];
+    for (int i = 0; i < nIni; i++) {
+      int cnt = 0;
+      for (int w = 0; w < NW; w++) cnt += icnt[w * 16 + i];
+      slots[i] = -1;
+      if (cnt > 0) {
+        const int s = S.freel[--nfp];
+        slots[i] = s;
+        QNode& q = S.node[s];
+        q.x0 = (int16_t)(int)(hX * (float)i);
+        q.x1 = (int16_t)(int)(hX * (float)(i + 1));
+        q.y0 = 0;
+        q.y1 = (int16_t)(L.maxBY - L.minBY);
+        q.beg = base;
+        q.cnt = cnt;
+        q.id = i;  // every initial node takes an id, empty or not
+        q.buf = 1;
+        q.nomore = cnt == 1;
+        q.alive = 1;
+        alive++;
+      }
+      base += cnt;
+    }
+    int p = QOS - alive;
+    for (int i = 0; i < nIni; i++)
+      if (slots[i] >= 0) {
+        S.order[p] = (int16_t)slots[i];
+        S.node[slots[i]].pos = p;
+        p++;
+      }
+    S.ctl[0] = alive;
+    S.ctl[1] = nfp;
+  }
+  __syncthreads();
+  int alive = S.ctl[0], nfp = S.ctl[1];
+  int next_id = nIni;
+  int head = QOS - alive;
+  bool overflow = false;
+  int nvcur = 0;
+
+  // keys per child of the round's divide d
+  auto count = [&](int d) {
+    const QNode q = S.node[S.dv[d]];
+    const int mx = q.x0 + (int)ceilf((float)(q.x1 - q.x0) / 2), my = q.y0 + (int)ceilf((float)(q.y1 - q.y0) / 2);
+    const uint32_t* src = bufs(q.buf) + q.beg;
+    int c4[4] = {0, 0, 0, 0};
+    for (int c0 = 0; c0 < q.cnt; c0 += 256) {
+      int ch[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int idx = c0 + 64 * j + lane;
+        ch[j] = idx < q.cnt ? child_of(src[idx], mx, my) : 4;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) c4[c] += popc64(ballot(ch[j] == c));
+    }
+    if (lane < 4) S.dcnt[d][lane] = lane == 0 ? c4[0] : lane == 1 ? c4[1] : lane == 2 ? c4[2] : c4[3];
+  };
+  // one wave: children / expandable prefixes over the nd divides, the sequential overflow and
+  // (final phase) the divide after which alive reaches N; ctl[2..5] = executed, children,
+  // expandables, overflow
+  auto place = [&](int nd, bool final_phase) {
+    if (wv == 0) {
+      int chT = 0, exT = 0, ndo = nd, ovf = 0;
+      for (int c0 = 0; c0 < nd; c0 += 64) {
+        const int d = c0 + lane;
+        const bool valid = d < nd;
+        int ch = 0, ex = 0;
+        if (valid)
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            const int k = S.dcnt[d][c];
+            ch += k > 0;
+            ex += k > 1;
+          }
+        int pch = ch, pex = ex;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(pch, o, 64), v = __shfl_up(pex, o, 64);
+          if (lane >= o) {
+            pch += u;
+            pex += v;
+          }
+        }
+        if (valid) {
+          S.dch[d] = chT + pch - ch;
+          S.dex[d] = exT + pex - ex;
+        }
+        const int ab = alive + chT + pch - ch - d;  // alive before divide d
+        const uint64_t mo = ballot(valid && ch > QCAP - ab);
+        const uint64_t ms = ballot(final_phase && valid && ab + ch - 1 >= N);
+        const int fo = mo ? __builtin_ctzll(mo) : 64, fs = ms ? __builtin_ctzll(ms) : 64;
+        if (fo < 64 && fo <= fs) {
+          ovf = 1;
+          break;
+        }
+        if (fs < 64) {
+          ndo = c0 + fs + 1;
+          chT += __shfl(pch, fs, 64);
+          exT += __shfl(pex, fs, 64);
+          break;
+        }
+        chT += __shfl(pch, 63, 64);
+        exT += __shfl(pex, 63, 64);
+      }
+      if (lane == 0) {
+        S.ctl[2] = ndo;
+        S.ctl[3] = chT;
+        S.ctl[4] = exT;
+        S.ctl[5] = ovf;
+      }
+    }
+  };
+  // partition divide d's keys into the other buffer, write its children, erase it
+  auto scatter = [&](int d) {
+    const int s = S.dv[d];
+    const QNode q = S.node[s];
+    const int hx = (int)ceilf((float)(q.x1 - q.x0) / 2), hy = (int)ceilf((float)(q.y1 - q.y0) / 2);
+    const int mx = q.x0 + hx, my = q.y0 + hy;
+    const uint32_t* src = bufs(q.buf) + q.beg;
+    uint32_t* dst = bufs(q.buf ^ 1) + q.beg;
+    int c4[4], off4[4], run4[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c = 0; c < 4; c++) c4[c] = S.dcnt[d][c];
+    off4[0] = 0;
+    off4[1] = c4[0];
+    off4[2] = c4[0] + c4[1];
+    off4[3] = off4[2] + c4[2];
+    for (int c0 = 0; c0 < q.cnt; c0 += 256) {
+      uint32_t kr[4];
+      int ch[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const int idx = c0 + 64 * j + lane;
+        kr[j] = idx < q.cnt ? src[idx] : 0u;
+        ch[j] = idx < q.cnt ? child_of(kr[j], mx, my) : 4;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const uint64_t m = ballot(ch[j] == c);
+          if (ch[j] == c) dst[off4[c] + run4[c] + popc64(m & lanes_below())] = kr[j];
+          run4[c] += popc64(m);
+        }
+    }
+    const int16_t rx0[4] = {q.x0, (int16_t)mx, q.x0, (int16_t)mx};
+    const int16_t ry0[4] = {q.y0, q.y0, (int16_t)my, (int16_t)my};
+    const int16_t rx1[4] = {(int16_t)mx, q.x1, (int16_t)mx, q.x1};
+    const int16_t ry1[4] = {(int16_t)my, (int16_t)my, q.y1, q.y1};
+    if (lane == 0) {
+      int g = S.dch[d], e = S.dex[d];
+      for (int c = 0; c < 4; c++) {
+        if (c4[c] == 0) continue;
+        const int ns = S.freel[nfp - 1 - g];
+        QNode& dn = S.node[ns];
+        dn.x0 = rx0[c];
+        dn.y0 = ry0[c];
+        dn.x1 = rx1[c];
+        dn.y1 = ry1[c];
+        dn.beg = q.beg + off4[c];
+        dn.cnt = c4[c];
+        dn.id = next_id + g;
+        dn.buf = q.buf ^ 1;
+        dn.nomore = c4[c] == 1;
+        dn.alive = 1;
+        dn.pos = head - 1 - g;
+        S.order[head - 1 - g] = (int16_t)ns;
+        if (c4[c] > 1) S.vcur[e++] = (int16_t)ns;
+        g++;
+      }
+      S.order[q.pos] = -1;
+      S.node[s].alive = 0;
+    }
+  };
+  // one round: count, place, partition; false on the sequential pool overflow
+  auto round = [&](int nd, bool final_phase) -> bool {
+    for (int d = wv; d < nd; d += NW) count(d);
+    __syncthreads();
+    place(nd, final_phase);
+    __syncthreads();
+    const int ndo = S.ctl[2], T = S.ctl[3], E = S.ctl[4];
+    if (S.ctl[5]) return false;
+    for (int d = wv; d < ndo; d += NW) scatter(d);
+    __syncthreads();
+    // the parents' slots back to the pool (after every child took its slot)
+    for (int d = tid; d < ndo; d += NT) S.freel[nfp - T + d] = S.dv[d];
+    alive += T - ndo;
+    next_id += T;
+    head -= T;
+    nfp += ndo - T;
+    nvcur = E;
+    return true;
+  };
+  // move live entries of order[head..QOS) to the tail, preserving order
+  auto compact = [&]() {
+    __syncthreads();
+    if (wv == 0) {
+      int w = 0;
+      for (int c0 = head; c0 < QOS; c0 += 64) {
+        const int idx = c0 + lane;
+        const int v = idx < QOS ? S.order[idx] : -1;
+        const uint64_t m = ballot(v >= 0);
+        if (v >= 0) S.skey[w + popc64(m & lanes_below())] = (unsigned long long)v;
+        w += popc64(m);
+      }
+      if (lane == 0) S.ctl[6] = w;
+    }
+    __syncthreads();
+    const int w = S.ctl[6];
+    head = QOS - w;
+    for (int i = tid; i < w; i += NT) {
+      const int s = (int)S.skey[i];
+      S.order[head + i] = (int16_t)s;
+      S.node[s].pos = head + i;
+    }
+    __syncthreads();
+  };
+
+  bool finish = false;
+  while (!finish && !overflow) {
+    const int prevSize = alive;
+    // the pass divides every expandable node, in list order
+    if (wv == 0) {
+      int nd = 0;
+      for (int c0 = head; c0 < QOS; c0 += 64) {
+        const int i = c0 + lane;
+        const int s = i < QOS ? (int)S.order[i] : -1;
+        const uint64_t m = ballot(s >= 0 && !S.node[s >= 0 ? s : 0].nomore);
+        if (s >= 0 && !S.node[s].nomore) S.dv[nd + popc64(m & lanes_below())] = (int16_t)s;
+        nd += popc64(m);
+      }
+      if (lane == 0) S.ctl[7] = nd;
+    }
+    __syncthreads();
+    if (!round(S.ctl[7], false)) {
+      overflow = true;
+      break;
+    }
+    compact();
+    if (alive >= N || alive == prevSize) {
+      finish = true;
+    } else if (alive + nvcur * 3 > N) {
+      while (!finish && !overflow) {
+        const int prev2 = alive;
+        const int nv = nvcur;
+        // the expandable children by (size, id), largest first
+        int P = 1;
+        while (P < nv) P <<= 1;
+        for (int i = tid; i < P; i += NT) {
+          if (i < nv) {
+            const int sl = S.vcur[i];
+            const QNode& q = S.node[sl];
+            S.skey[i] = ((unsigned long long)(uint32_t)q.cnt << 32) | ((unsigned long long)(uint32_t)q.id << 12) |
+                        (unsigned long long)sl;
+          } else
+            S.skey[i] = ~0ull;
+        }
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)
+          for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < P; i += NT) {
+              const int ixj = i ^ j;
+              if (ixj > i) {
+                const unsigned long long a = S.skey[i], b = S.skey[ixj];
+                if ((a > b) == ((i & k) == 0)) {
+                  S.skey[i] = b;
+                  S.skey[ixj] = a;
+                }
+              }
+            }
+            __syncthreads();
+          }
+        for (int d = tid; d < nv; d += NT) S.dv[d] = (int16_t)(S.skey[nv - 1 - d] & 0xfffu);
+        __syncthreads();
+        if (!round(nv, true)) {
+          overflow = true;
+          break;
+        }
+        compact();
+        if (alive >= N || alive == prev2) finish = true;
+      }
+    }
+  }
+  // ---- retain the best keypoint per node (largest score, first in the node's key order on
+  // ties), in list order (the list is compact: position i - head)
+  if (!overflow)
+    for (int i = head + tid; i < QOS; i += NT) {
+      const int s = S.order[i];
+      const int cnt = S.node[s].cnt;
+      const uint32_t* src = bufs(S.node[s].buf) + S.node[s].beg;
+      int best_s = -1;
+      uint32_t bk = 0;
+      for (int idx = 0; idx < cnt; idx++) {
+        const uint32_t k = src[idx];
+        if (kp_s(k) > best_s) {
+          best_s = kp_s(k);
+          bk = k;
+        }
+      }
+      if (i - head < L.sel_cap) S_out[i - head] = bk;
+    }
+  if (tid == 0) *sel_cnt_out = overflow ? -1 : min(QOS - head, L.sel_cap);
+}
+
+template <int QCAP, int NW>
+__global__ __launch_bounds__(64 * NW) void k_distribute_mw(const uint32_t* __restrict__ cand, long long cand_stride,
+                                                           const int* __restrict__ cell_cnt, int ncells,
+                                                           const LevelDev* __restrict__ levels,
+                                                           const CellDev* __restrict__ cells,
+                                                           uint32_t* __restrict__ qbuf, long long qstride,
+                                                           uint32_t* __restrict__ sel, long long sel_stride,
+                                                           int* __restrict__ sel_cnt, int nlevels, int lds_keys) {
+  __shared__ QSharedMW<QCAP> S;
+  extern __shared__ uint32_t qk_lds[];
+  const int l = blockIdx.y, f = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const LevelDev& L = levels[l];
+  const uint32_t* C = cand + f * cand_stride;
+  uint32_t* S_out = sel + f * sel_stride + L.sel_off;
+  int* sc = sel_cnt + f * nlevels + l;
+  auto cell_count = [&](int k) -> int {
+    return k < L.cell_count ? min(cell_cnt[f * ncells + L.cell_begin + k], cells[L.cell_begin + k].cap) : 0;
+  };
+  int n = 0;
+  for (int k0 = 0; k0 < L.cell_count; k0 += 64) n += wave_sum(cell_count(k0 + lane));
+  if (n == 0) {
+    if (tid == 0) *sc = 0;
+    return;
+  }
+  // ---- gather in vToDistributeKeys order: wave w takes the groups of 64 cells g = w, w + NW, ..,
+  // placed after the earlier groups' totals
+  const int ng = (L.cell_count + 63) >> 6;
+  auto gather = [&](uint32_t* B0) {
+    int* gtot = S.dch;  // [ng], free until the first round
+    for (int g = wv; g < ng; g += NW) {
+      const int t = wave_sum(cell_count(64 * g + lane));
+      if (lane == 0) gtot[g] = t;
+    }
+    __syncthreads();
+    int* gpre = &S.dcnt[0][0] + 128 * wv;  // per-wave scan table
+    int* gslot = gpre + 64;
+    for (int g = wv; g < ng; g += NW) {
+      int o = 0;
+      for (int h = 0; h < g; h++) o += gtot[h];
+      const int k = 64 * g + lane;
+      const int cnt = cell_count(k);
+      int pre = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int u = __shfl_up(pre, d, 64);
+        if (lane >= d) pre += u;
+      }
+      wave_lds_sync();
+      gpre[lane] = pre - cnt;
+      gslot[lane] = k < L.cell_count ? cells[L.cell_begin + k].slot : 0;
+      wave_lds_sync();
+      const int tot = __shfl(pre, 63, 64);
+      for (int t = lane; t < tot; t += 64) {
+        int lo = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1)
+          if (gpre[lo + step] <= t) lo += step;
+        B0[o + t] = C[gslot[lo] + (t - gpre[lo])];
+      }
+    }
+    __syncthreads();
+  };
+  if (n <= lds_keys) {
+    gather(qk_lds);
+    dist_tree_mw<QCAP, NW>(S, qk_lds, qk_lds + lds_keys, n, L, S_out, sc);
+  } else {
+    uint32_t* B0 = qbuf + f * qstride + 2 * (long long)L.cand_off;
+    gather(B0);
+    dist_tree_mw<QCAP, NW>(S, B0, B0 + L.cand_cap, n, L, S_out, sc);
+  }
 }
 
 // ---------------------------------------------------------------- orientation
@@ -1645,8 +2154,33 @@ int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint
     int need = 0;
     for (int l = 0; l < nl; l++) need = std::max(need, levels[l].nfeat + 4 * levels[l].nIni + 16);
     auto kd = need <= 256 ? k_distribute<256> : need <= 512 ? k_distribute<512> : k_distribute<1024>;
-    hipLaunchKernelGGL(kd, g, dim3(64), 0, s, d_cand, cand_stride, d_cell_cnt, (int)cells.size(), d_levels,
-                       d_cells, d_qbuf, 2 * cand_stride, d_sel, sel_stride, d_sel_cnt, nl);
+    const size_t stat = need <= 256 ? sizeof(QShared<256>) : need <= 512 ? sizeof(QShared<512>) : sizeof(QShared<1024>);
+    // a few frames (the drop-in's single calls): one (level, frame) per CU at most, so each quadtree
+    // takes the CU's LDS for its keys; batches keep the keys in qbuf (LDS per workgroup sets how
+    // many of the 405 x 8 quadtrees are resident at once)
+    static const int lds_on = [] {
+      const char* v = getenv("EAO_DIST_LDS");
+      return v && v[0] == '0' ? 0 : 1;
+    }();
+    static const int mw_on = [] {
+      const char* v = getenv("EAO_DIST_MW");
+      return v && v[0] == '0' ? 0 : 1;
+    }();
+    if (mw_on && nframes * nl <= 256) {
+      // a few frames: NW waves per tree (k_distribute_mw)
+      constexpr int NW = 8;
+      auto km = need <= 256 ? k_distribute_mw<256, NW> : need <= 512 ? k_distribute_mw<512, NW> : k_distribute_mw<1024, NW>;
+      const size_t mstat = need <= 256 ? sizeof(QSharedMW<256>) : need <= 512 ? sizeof(QSharedMW<512>) : sizeof(QSharedMW<1024>);
+      const int lds_keys = lds_on ? (int)std::min<size_t>(16384, ((size_t)152 * 1024 - mstat) / 8) : 0;
+      hipLaunchKernelGGL(km, g, dim3(64 * NW), (size_t)8 * lds_keys, s, d_cand, cand_stride, d_cell_cnt,
+                         (int)cells.size(), d_levels, d_cells, d_qbuf, 2 * cand_stride, d_sel, sel_stride, d_sel_cnt, nl,
+                         lds_keys);
+    } else {
+      int lds_keys = 0;
+      if (lds_on && nframes * nl <= 256) lds_keys = (int)std::min<size_t>(16384, ((size_t)152 * 1024 - stat) / 8);
+      hipLaunchKernelGGL(kd, g, dim3(64), (size_t)8 * lds_keys, s, d_cand, cand_stride, d_cell_cnt, (int)cells.size(),
+                         d_levels, d_cells, d_qbuf, 2 * cand_stride, d_sel, sel_stride, d_sel_cnt, nl, lds_keys);
+    }
   }
   if (timing) EAO_HIP_CHECK(hipEventRecord(ev[3], s));
   // orientation + blur at the pattern taps + descriptors
