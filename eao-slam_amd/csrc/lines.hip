@@ -313,7 +313,8 @@ __global__ __launch_bounds__(256) void k_line_maps(const uint8_t* __restrict__ i
 // counts in column order places every column, and the column's anchors are written in row order.
 __global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict__ amask, int W, int H, int nty,
                                                       int ncp, uint32_t* __restrict__ anchors, int acap,
-                                                      int* __restrict__ nanchor) {
+                                                      int* __restrict__ nanchor, uint32_t* __restrict__ pl_reset = nullptr,
+                                                      int* __restrict__ ctl_reset = nullptr) {
   __shared__ int wsum[8], base;
   const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const uint16_t* AM = amask + (long long)f * nty * ncp;
@@ -360,6 +361,10 @@ __global__ __launch_bounds__(512) void k_line_anchors(const uint16_t* __restrict
     __syncthreads();
   }
   if (t == 0) nanchor[f] = base;
+  // k_lines_fused's length words (pending) and control words, single frames
+  if (pl_reset)
+    for (int i = t; i < 2 * min(base, acap); i += blockDim.x) pl_reset[i] = 0xFFFFFFFFu;
+  if (ctl_reset && t < 4) ctl_reset[t] = 0;
 }
 
 // ---------------------------------------------------------------- edge drawing
@@ -398,6 +403,21 @@ __device__ __forceinline__ void tile_load(const uint16_t* __restrict__ M, int MP
 // last step increased x -- and on a Vertical one DOWN exactly when the last step increased y.
 // The walk's state is those two bits (px, py), initialised from dir (an anchor's first step
 // leaves along dir: its own direction).
+// a 4-byte store another CU reads without an acquire (WT: written through, sc1; MI355X_MICROARCH
+// "Valid forms"), or a plain one
+template <bool WT>
+__device__ __forceinline__ void st_wt(uint32_t* p, uint32_t v) {
+  if (WT) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool WT>
+__device__ __forceinline__ uint32_t ld_wt(const uint32_t* p) {
+  if (WT) return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <bool WT = false>
 __device__ __forceinline__ bool ed_walk_st(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
                                            MoveTile& T, int x, int y, int st, uint32_t* __restrict__ P, uint32_t& off,
                                            uint32_t cap) {
@@ -430,7 +450,7 @@ __device__ __forceinline__ bool ed_walk_st(const uint16_t* __restrict__ M, int W
     // every lane stores the same word to the same address (no per-step exec-mask switch;
     // the wave is the only writer of the frame's edge map)
     bits[idx >> 5] = bw | bit;
-    *Pw++ = (uint32_t)pk;
+    st_wt<WT>(Pw++, (uint32_t)pk);
     rem--;
     const int nib = (mw >> sh) & 15;  // (0, 0) at the border: the pixel is marked, the walk stops next
     const int dpk = __builtin_amdgcn_readlane(t_pk, nib);
@@ -599,6 +619,7 @@ __device__ __forceinline__ int ls_state(int dir) { return dir == LN_RIGHT ? 2 : 
 // moves, the pixels of the path so far that fall in the new tile are marked again from the LDS copy
 // of the path. Writes the pixels (packed x | y << 16) to out[0 .. n), returns n | (capped << 31) and,
 // for a capped walk, the next pixel and state in *next (pixel | st << 30).
+template <bool WT = false>
 __device__ __forceinline__ uint32_t ls_walk(const uint16_t* __restrict__ M, int MP, int H, MoveTile& T, uint32_t* path,
                                             int x, int y, int st, uint32_t* __restrict__ out, uint32_t* next) {
   const int lane = lane_id(), ndx = (lane & 3) - 1, ndy = ((lane >> 2) & 3) - 1;
@@ -620,7 +641,7 @@ __device__ __forceinline__ uint32_t ls_walk(const uint16_t* __restrict__ M, int 
     }
     *(uint16_t*)tw = LS_SEEN;  // every lane: the same word (the wave's own tile)
     path[n] = (uint32_t)pk;
-    out[n] = (uint32_t)pk;
+    st_wt<WT>(&out[n], (uint32_t)pk);
     n++;
     const int nib = (mw >> sh) & 15;  // LM_STOP: the walk finds its own pixel next
     const int dpk = __builtin_amdgcn_readlane(t_pk, nib);
@@ -642,7 +663,7 @@ __device__ __forceinline__ uint32_t ls_walk(const uint16_t* __restrict__ M, int 
       tw = (uint8_t*)T.t + 2 * ((yy - T.y0) * LE_TW + (xx - T.x0));
     }
   }
-  if (capped && lane == 0) *next = (uint32_t)pk | (uint32_t)(sh >> 2) << 30;
+  if (capped && lane == 0) st_wt<WT>(next, (uint32_t)pk | (uint32_t)(sh >> 2) << 30);
   return (uint32_t)n | (capped ? 0x80000000u : 0u);
 }
 
@@ -688,6 +709,7 @@ struct LsRing {
 // ed_walk from its stored next pixel and state (whose stores go straight to P). False on overflow
 // (the reference's -1), as ed_walk. p is the lane's pixel of the first round, loaded ahead by the
 // caller; each round loads the next one's before it tests its own.
+template <bool WT = false>
 __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
                                         MoveTile& T, const uint32_t* __restrict__ ps, uint32_t len, uint32_t nextw,
                                         uint32_t p, uint32_t* __restrict__ P, uint32_t part, uint32_t& off, uint32_t cap,
@@ -698,7 +720,7 @@ __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, i
   for (uint32_t c0 = 0; c0 < len; c0 += 64) {
     const uint32_t i = c0 + (uint32_t)lane;
     const bool in = i < len;
-    const uint32_t pn = i + 64 < len ? ps[i + 64] : 0u;  // the next round's pixel, in flight
+    const uint32_t pn = i + 64 < len ? ld_wt<WT>(ps + i + 64) : 0u;  // the next round's pixel, in flight
     const int idx = (int)(p >> 16) * W + (int)(p & 0xffffu);
     const bool marked = in && ((bits[idx >> 5] >> (idx & 31)) & 1u);
     const uint64_t mk = ballot(marked);
@@ -720,7 +742,7 @@ __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, i
   }
   if (!capped) return true;  // stopped where the speculative walk stopped (its own revisit)
   const int nx = (int)(nextw & 0xffffu), ny = (int)((nextw >> 16) & 0x3fffu), st = (int)(nextw >> 30);
-  return ed_walk_st(M, W, MP, H, bits, T, nx, ny, st, P, off, cap);
+  return ed_walk_st<WT>(M, W, MP, H, bits, T, nx, ny, st, P, off, cap);
 }
 
 // Phase 2: ed_walker's anchor loop over the speculative walks (wave 0), the records stored by wave 1
@@ -1175,6 +1197,235 @@ __device__ int ed_place_lines(int ne, const uint32_t* __restrict__ S, const uint
   return carry;
 }
 
+// ---------------------------------------------------------------- fused single-frame lines
+// k_lines_fused: k_walk_spec, k_walk_merge and k_edlines_par of one frame as one launch whose
+// phases overlap (the default for single frames; EAO_LINES_ONE_LAUNCH=0 restores the three launches). Workgroup 0: the merge (wave 0,
+// ls_part as k_walk_merge) and the ring writer (wave 1); the other workgroups: every wave first
+// computes speculative walks (grid-strided in anchor order, so the merge finds the walks of its next
+// anchors done long before it reaches them: each walk's length word is released last, and the merge
+// acquires the words of its next 64 anchors before their paths), then takes chains as the merge
+// completes them and runs EDline on each (k_edlines_par's work, now beside the merge instead of
+// after it). A completed chain reaches the ring as two marker records (its fS / sS starts, bit 30 of
+// the index word); the writer stores them with the chain's pixels and releases the count of
+// complete chains to the chip. k_line_anchors resets the length words and the control words.
+constexpr uint32_t LS_PENDING = 0xFFFFFFFFu;  // pl of a walk not written yet (no length word has it)
+constexpr uint32_t LS_MARK = 0x40000000u;      // ring record: a chain start (bit 29: sS, else fS), low bits the chain
+constexpr int LF_WAVES = 4;
+// control words per frame: [0] chains complete, [1] next chain to take, [2] 0 running / 1 done / -1 failed
+constexpr int LF_CTL = 4;
+
+__device__ __forceinline__ void ls_ring_space(LsRing& R, int w, int need) {
+  while (w + need - R.rseen > LS_RING) {
+    R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (w + need - R.rseen > LS_RING) __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+__global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
+    const uint16_t* __restrict__ moves, const uint16_t* __restrict__ code, const int16_t* __restrict__ dxi,
+    const int16_t* __restrict__ dyi, int W, int H, int MP, const uint32_t* __restrict__ anchors,
+    const int* __restrict__ nanchor, int acap, uint32_t* __restrict__ ps, uint32_t* __restrict__ pl,
+    uint32_t* __restrict__ pe, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2, int pcap,
+    uint32_t* __restrict__ chains, uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
+    uint32_t* __restrict__ gstarts, int* __restrict__ ctl, uint32_t* __restrict__ lscratch,
+    uint32_t* __restrict__ ccount, float min_length, int* __restrict__ diag) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds_lf[];
+  __shared__ int s_w, s_r, s_done, s_ne;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
+  uint32_t* fS = gstarts;
+  uint32_t* sS = gstarts + ep;
+  uint32_t* P1 = p1;
+  uint32_t* P2 = p2;
+  const int na = nanchor[0];
+  if (threadIdx.x == 0) s_w = s_r = s_done = 0;
+  __syncthreads();
+  if (blockIdx.x == 0 && wave < 2) {
+    uint32_t* bits = lds_lf;
+    uint16_t* tile = (uint16_t*)(bits + nbp);
+    LsRing R{(uint2*)(tile + LE_TW * LE_TH), &s_w, &s_r, 0};
+    if (wave == 0) {
+      MoveTile T{tile, -LE_TW, -LE_TH};
+      for (int i = lane; i < nb; i += 64) bits[i] = 0;
+      LS_FENCE();
+      uint32_t b1 = 0, b2 = 0;
+      int ne = 0, w = 0;
+      bool fail = na > acap;
+      for (int a0 = 0; a0 < na && !fail; a0 += 64) {
+        const int a = a0 + lane;
+        const uint32_t ap = a < na ? anchors[a] : 0u;
+        const int aidx = (int)(ap >> 16) * W + (int)(ap & 0xffffu);
+        // the walks of these 64 anchors: written, and released after their paths
+        uint32_t l1 = 0, l2 = 0;
+        while (true) {
+          l1 = a < na ? ld_wt<true>(&pl[2 * a]) : 0u;
+          l2 = a < na ? ld_wt<true>(&pl[2 * a + 1]) : 0u;
+          if (!ballot(l1 == LS_PENDING || l2 == LS_PENDING)) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        // paths and continuation words: stored sc1 and drained before their length word, loaded sc1
+        const uint32_t e1 = a < na ? ld_wt<true>(&pe[2 * a]) : 0u, e2 = a < na ? ld_wt<true>(&pe[2 * a + 1]) : 0u;
+        auto first = [&](int k, uint32_t& q1, uint32_t& q2) {
+          const long long wk = 2 * (long long)(a0 + k);
+          const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k) & 0x7fffffffu;
+          const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k) & 0x7fffffffu;
+          q1 = (uint32_t)lane < n1 ? ld_wt<true>(ps + wk * LS_CAP + lane) : 0u;
+          q2 = (uint32_t)lane < n2 ? ld_wt<true>(ps + (wk + 1) * LS_CAP + lane) : 0u;
+        };
+        uint64_t pend = ballot(a < na) & ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
+        int k = pend ? __builtin_ctzll(pend) : -1;
+        uint32_t c1 = 0, c2 = 0;
+        if (k >= 0) first(k, c1, c2);
+        while (k >= 0) {
+          pend &= pend - 1;
+          const int kn = pend ? __builtin_ctzll(pend) : -1;
+          uint32_t n1 = 0, n2 = 0;
+          if (kn >= 0) first(kn, n1, n2);
+          if (ne > ecap) {
+            fail = true;
+            break;
+          }
+          const long long wk = 2 * (long long)(a0 + k);
+          const uint32_t L1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k), L2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k);
+          uint32_t o1 = b1, o2 = b2;
+          if (!ls_part<true>(moves, W, MP, H, bits, T, ps + wk * LS_CAP, L1, (uint32_t)__builtin_amdgcn_readlane((int)e1, k), c1,
+                       P1, 0u, o1, (uint32_t)pcap, R, w)) {
+            fail = true;
+            break;
+          }
+          const int idx = __builtin_amdgcn_readlane(aidx, k);
+          if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));
+          LS_FENCE();
+          if (!ls_part<true>(moves, W, MP, H, bits, T, ps + (wk + 1) * LS_CAP, L2, (uint32_t)__builtin_amdgcn_readlane((int)e2, k),
+                       c2, P2, 1u, o2, (uint32_t)pcap, R, w)) {
+            fail = true;
+            break;
+          }
+          // a capped walk's continuation stored its pixels itself (sc1): drained before the chain's
+          // markers reach the writer, whose count then covers them
+          if (((L1 | L2) >> 31) != 0) vm_drain();
+          if ((int)((o1 - b1) + (o2 - b2)) >= LN_MIN_LEN + 1) {
+            b1 = o1;
+            b2 = o2;
+            ne++;
+            if (ne <= ecap + 1) {  // the chain's end: its starts through the ring (the writer publishes)
+              ls_ring_space(R, w, 2);
+              if (lane < 2) R.r[(w + lane) & (LS_RING - 1)] = make_uint2(LS_MARK | (lane ? 0x20000000u : 0u) | (uint32_t)ne, lane ? b2 : b1);
+              w += 2;
+              if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+          }
+          pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
+          k = pend ? __builtin_ctzll(pend) : -1;
+          if (k >= 0 && k == kn) {
+            c1 = n1;
+            c2 = n2;
+          } else if (k >= 0) {
+            first(k, c1, c2);
+          }
+        }
+      }
+      if (ne > ecap) fail = true;
+      if (lane == 0) {
+        s_ne = fail ? -1 : ne;
+        __hip_atomic_store(&s_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    } else {
+      // the writer: ring records to P1 / P2 and chain starts to fS / sS; after each batch that
+      // completed chains, the count released to the chip
+      if (lane == 0) {
+        st_wt<true>(fS, 0u);
+        st_wt<true>(sS, 0u);
+      }
+      int r = 0;
+      while (true) {
+        const int d = __hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int w = __hip_atomic_load(&s_w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (r < w) {
+          int pub = 0;
+          for (int i = r + lane; i < w; i += 64) {
+            const uint2 e = R.r[i & (LS_RING - 1)];
+            if (e.x & LS_MARK) {
+              const int c = (int)(e.x & 0x1fffffffu);
+              st_wt<true>(((e.x & 0x20000000u) ? sS : fS) + c, e.y);
+              pub = max(pub, c);
+            } else if (diag && ((e.x & 0x7fffffffu) >= (uint32_t)pcap || px_x(e.y) >= (uint32_t)W || px_y(e.y) >= (uint32_t)H)) {
+              atomicOr(diag, 1);
+            } else {
+              st_wt<true>(((e.x >> 31) ? P2 : P1) + (e.x & 0x7fffffffu), e.y);
+            }
+          }
+          r = w;
+          LS_FENCE();
+          if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          pub = wave_max_int(pub);
+          if (pub > 0) {
+            vm_drain();  // the chains' pixels and starts (sc1), then their count
+            if (lane == 0) st_wt<true>((uint32_t*)&ctl[0], (uint32_t)pub);
+          }
+        } else if (d) {
+          break;
+        } else {
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      const int ne = s_ne;
+      if (lane == 0) {
+        nedge[0] = ne;  // for k_lines_place (the next launch)
+        vm_drain();
+        st_wt<true>((uint32_t*)&ctl[2], (uint32_t)(ne < 0 ? -1 : 1));
+      }
+    }
+    return;
+  }
+  // ---- speculative walks (workgroups >= 1), then EDline on the completed chains (every wave)
+  if (blockIdx.x > 0) {
+    uint8_t* base = (uint8_t*)lds_lf + (size_t)wave * (sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP);
+    MoveTile T{(uint16_t*)base, -LE_TW, -LE_TH};
+    uint32_t* path = (uint32_t*)(base + sizeof(uint16_t) * LE_TW * LE_TH);
+    const int nsw = (gridDim.x - 1) * LF_WAVES;
+    for (int w = (blockIdx.x - 1) * LF_WAVES + wave; w < 2 * min(na, acap); w += nsw) {
+      const uint32_t ap = anchors[w >> 1];
+      const int x = (int)(ap & 0xffffu), y = (int)(ap >> 16);
+      const bool horiz = (code[(long long)y * W + x] & LN_HORIZ) != 0;
+      const int dir = (w & 1) == 0 ? (horiz ? LN_RIGHT : LN_DOWN) : (horiz ? LN_LEFT : LN_UP);
+      const uint32_t r = ls_walk<true>(moves, MP, H, T, path, x, y, ls_state(dir), ps + (long long)w * LS_CAP, pe + w);
+      vm_drain();  // the path and continuation word (sc1) before the length word
+      if (lane == 0) st_wt<true>(&pl[w], r);
+      LS_FENCE();
+    }
+  }
+  const double logNT = 2.0 * (log10((double)W) + log10((double)H));
+  int* CNT = (int*)ccount;
+  while (true) {
+    int e = 0;
+    if (lane == 0) e = __hip_atomic_fetch_add(&ctl[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    e = __shfl(e, 0, 64);
+    int st = 0, rd = 0;
+    while (true) {  // chain e complete, or the merge over
+      st = (int)ld_wt<true>((const uint32_t*)&ctl[2]);
+      rd = (int)ld_wt<true>((const uint32_t*)&ctl[0]);
+      if (rd > e || st != 0) break;
+      // a few us between polls: ~100 waiting waves must not load the fabric the frame's other
+      // kernels (the drop-in's extraction and matching beside the lines) depend on
+      __builtin_amdgcn_s_sleep(127);
+    }
+    if (st < 0 || rd <= e) break;
+    const uint32_t f0 = ld_wt<true>(fS + e), f1 = ld_wt<true>(fS + e + 1), s0 = ld_wt<true>(sS + e),
+                   s1 = ld_wt<true>(sS + e + 1);
+    const uint32_t q0 = f0 + s0 - (uint32_t)e, q1 = f1 + s1 - (uint32_t)e - 1;
+    if (diag && (f1 < f0 || s1 <= s0 || f1 > (uint32_t)pcap || s1 > (uint32_t)pcap)) {
+      atomicOr(diag, 8);
+      if (lane == 0) CNT[e] = 0;
+      continue;
+    }
+    for (uint32_t i = lane; i < f1 - f0; i += 64) chains[q0 + i] = ld_wt<true>(P1 + f1 - 1 - i);
+    for (uint32_t i = lane + 1; i < s1 - s0; i += 64) chains[q0 + (f1 - f0) + i - 1] = ld_wt<true>(P2 + s0 + i);
+    if (lane == 0) sid[e] = q0;
+    ed_chain_lines(e, q0, q1, chains, lscratch, code, dxi, dyi, W, H, logNT, min_length, CNT);
+  }
+}
+
 // one workgroup of LN_WAVES waves per frame: chains Q / S -> lines out [cap][6] (sx, sy, ex, ey,
 // angle, length); chains are independent: wave w takes chains w, w + nw, ...
 __global__ __launch_bounds__(64 * LN_WAVES) void k_edlines(const uint16_t* __restrict__ code,
@@ -1340,6 +1591,8 @@ struct LineEngine {
   bool spec = true;      // single frames through the speculative walk (EAO_LINES_SPEC=0: k_edge_lines)
   uint32_t *d_ps = nullptr, *d_pl = nullptr, *d_pe = nullptr;  // its paths / lengths / continuations (one frame)
   uint32_t* d_starts = nullptr;
+  int* d_lctl = nullptr;           // k_lines_fused's control words
+  uint32_t* d_lstarts = nullptr;   // k_lines_fused's chain starts (fS / sS)
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
   uint8_t* d_blur = nullptr;
@@ -1358,7 +1611,7 @@ struct LineEngine {
   ~LineEngine() {
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
                  d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts,
-                 d_ps,   d_pl,   d_pe};
+                 d_ps,   d_pl,   d_pe,   d_lctl, d_lstarts};
     for (void* q : p)
       if (q) (void)hipFree(q);
     if (h_n) (void)hipHostFree(h_n);
@@ -1443,7 +1696,16 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
     delete L;
     return rc;
   };
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&e.stream, hipStreamNonBlocking) != hipSuccess ||
+  // the engine's stream at the highest priority (EAO_LINES_PRI=0: default priority): its own hardware
+  // queue, so a single frame's one long launch (k_lines_fused) does not hold the matcher's or the
+  // extractor's launches of the same frame behind it in a shared queue
+  static const bool lines_pri = [] {
+    const char* v = getenv("EAO_LINES_PRI");
+    return !(v && v[0] == '0');
+  }();
+  int lo_pri = 0, hi_pri = 0;
+  if (hipSetDevice(device) != hipSuccess || hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri) != hipSuccess ||
+      hipStreamCreateWithPriority(&e.stream, hipStreamNonBlocking, lines_pri ? hi_pri : 0) != hipSuccess ||
       hipMalloc(&e.d_blur, px) != hipSuccess || hipMalloc(&e.d_dx, px * 2) != hipSuccess ||
       hipMalloc(&e.d_dy, px * 2) != hipSuccess || hipMalloc(&e.d_code, px * 2) != hipSuccess ||
       hipMalloc(&e.d_moves, sizeof(uint16_t) * e.MP * height * max_batch) != hipSuccess ||
@@ -1502,9 +1764,40 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   else
     hipLaunchKernelGGL(k_line_maps<4>, bg, dim3(256), 0, s, d_img, pitch, fs, W, H, e.MP, e.k[0], e.k[1], e.k[2], vec,
                        e.d_blur, e.d_dx, e.d_dy, e.d_code, e.d_moves, e.d_amask);
+  // single frames: spec / merge / EDline in one launch (EAO_LINES_ONE_LAUNCH=0: the three kernels;
+  // n: the workgroups beside the merge's)
+  static const int fused_blocks = [] {
+    const char* v = getenv("EAO_LINES_ONE_LAUNCH");
+    return v ? atoi(v) : 64;  // workgroups beside the merge's; 0 = off
+  }();
+  const size_t lf_merge = edge_draw_lds(W, H, e.ecap, true) + 8 * LS_RING;
+  const size_t lf_walk = (size_t)LF_WAVES * (sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP);
+  const size_t lf_lds = std::max(lf_merge, lf_walk);
+  const bool fused = nframes == 1 && e.spec && fused_blocks > 0 && lf_lds <= kLdsMax - 64;
+  if (fused && !e.d_lctl) {
+    const size_t nw = (size_t)2 * e.acap;
+    EAO_HIP_CHECK(hipMalloc(&e.d_lctl, sizeof(int) * LF_CTL));
+    EAO_HIP_CHECK(hipMalloc(&e.d_lstarts, (size_t)2 * ((e.ecap + 2 + 3) & ~3) * 4));
+    if (!e.d_ps) {
+      EAO_HIP_CHECK(hipMalloc(&e.d_ps, nw * LS_CAP * 4));
+      EAO_HIP_CHECK(hipMalloc(&e.d_pl, nw * 4));
+      EAO_HIP_CHECK(hipMalloc(&e.d_pe, nw * 4));
+    }
+  }
   hipLaunchKernelGGL(k_line_anchors, dim3(nframes), dim3(512), 0, s, e.d_amask, W, H, (int)bg.y, (int)bg.x * (LF_TW / 2),
-                     e.d_anch, e.acap, e.d_nanch);
-  if (nframes == 1 && e.spec && edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING <= kLdsMax - 64) {
+                     e.d_anch, e.acap, e.d_nanch, fused ? e.d_pl : nullptr, fused ? e.d_lctl : nullptr);
+  if (fused) {
+    int* diag = lines_check() && d_counts == e.d_nlines ? e.d_nlines + 1 : nullptr;
+    if (diag) EAO_HIP_CHECK(hipMemsetAsync(diag, 0, 4, s));
+    // every workgroup resident at once (the merge waits on walks the others compute, and they on
+    // its chains): one workgroup of lf_lds per CU, fewer than the CUs
+    hipLaunchKernelGGL(k_lines_fused, dim3(1 + std::min(fused_blocks, 192)), dim3(64 * LF_WAVES), lf_lds, s, e.d_moves,
+                       e.d_code, e.d_dx, e.d_dy, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1,
+                       e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge, e.d_lstarts, e.d_lctl, e.d_lscr, e.d_ccnt,
+                       min_length, diag);
+    hipLaunchKernelGGL(k_lines_place, dim3(1), dim3(256), 0, s, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr,
+                       e.d_ccnt, d_lines, d_counts, cap);
+  } else if (nframes == 1 && e.spec && edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING <= kLdsMax - 64) {
     // the latency path: every anchor's two walks in parallel, the in-order merge on one wave, EDline
     // a wave per chain, the placement (k_walk_spec .. k_lines_place)
     if (!e.d_ps) {

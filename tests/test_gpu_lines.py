@@ -233,7 +233,8 @@ def outlines(w=640, h=480):
 
 def test_lines_single_frame_speculative_walk(frames, monkeypatch):
     """Single frames take the speculative walk (every anchor's two walks in parallel with their own
-    marks only, then the in-order merge; k_walk_spec / k_walk_merge), batches the sequential walker
+    marks only, then the in-order merge, EDline on each chain as the merge completes it: one launch,
+    k_lines_fused), batches the sequential walker
     (k_edge_lines): both equal the restatement and each other, on office frames, closed outlines
     with long sides (walks cut at 256 pixels and continued sequentially) and a spiral, at
     min_length 50 and 0."""
