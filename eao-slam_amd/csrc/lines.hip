@@ -713,7 +713,7 @@ template <bool WT = false>
 __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, int MP, int H, uint32_t* bits,
                                         MoveTile& T, const uint32_t* __restrict__ ps, uint32_t len, uint32_t nextw,
                                         uint32_t p, uint32_t* __restrict__ P, uint32_t part, uint32_t& off, uint32_t cap,
-                                        LsRing& R, int& w) {
+                                        LsRing& R, int& w, bool have_mk0 = false, uint64_t mk0 = 0) {
   const int lane = lane_id();
   const bool capped = (len >> 31) != 0;
   len &= 0x7fffffffu;
@@ -722,12 +722,14 @@ __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, i
     const bool in = i < len;
     const uint32_t pn = i + 64 < len ? ld_wt<WT>(ps + i + 64) : 0u;  // the next round's pixel, in flight
     const int idx = (int)(p >> 16) * W + (int)(p & 0xffffu);
-    const bool marked = in && ((bits[idx >> 5] >> (idx & 31)) & 1u);
-    const uint64_t mk = ballot(marked);
+    // the first round's marked pixels may come tested already (mk0: read after every earlier mark)
+    uint64_t mk;
+    if (have_mk0 && c0 == 0) mk = mk0;
+    else mk = ballot(in && ((bits[idx >> 5] >> (idx & 31)) & 1u));
     const uint32_t take = mk ? (uint32_t)__builtin_ctzll(mk) : min(64u, len - c0);  // pixels recorded this round
     if (take > cap - off) return false;  // the arrays fill before the walk stops
     while (w + 64 - R.rseen > LS_RING) {  // the ring may be full: look where the writer is
-      R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (w + 64 - R.rseen > LS_RING) __builtin_amdgcn_s_sleep(1);
     }
     if ((uint32_t)lane < take) {
@@ -735,7 +737,11 @@ __device__ __forceinline__ bool ls_part(const uint16_t* __restrict__ M, int W, i
       R.r[(w + lane) & (LS_RING - 1)] = make_uint2(part << 31 | (off + lane), p);
     }
     w += (int)take;
-    if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // the new write position after the records: relaxed, behind a compiler fence only -- one wave's
+    // LDS operations complete in order, and a workgroup-scope release would wait for every vector
+    // memory operation in flight (the look-ahead's path loads: ~1 us per anchor)
+    LS_FENCE();
+    if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     off += take;
     if (mk) return true;  // stopped at a marked pixel
     p = pn;
@@ -857,7 +863,8 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
     int r = 0;
     while (true) {
       const int d = __hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const int w = __hip_atomic_load(&s_w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int w = __hip_atomic_load(&s_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        LS_FENCE();
       if (r < w) {
         for (int i = r + lane; i < w; i += 64) {
           const uint2 e = R.r[i & (LS_RING - 1)];
@@ -868,7 +875,7 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
         }
         r = w;
         LS_FENCE();
-        if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else if (d) {
         break;
       } else {
@@ -1211,12 +1218,13 @@ __device__ int ed_place_lines(int ne, const uint32_t* __restrict__ S, const uint
 constexpr uint32_t LS_PENDING = 0xFFFFFFFFu;  // pl of a walk not written yet (no length word has it)
 constexpr uint32_t LS_MARK = 0x40000000u;      // ring record: a chain start (bit 29: sS, else fS), low bits the chain
 constexpr int LF_WAVES = 4;
+constexpr int LF_STAGE = 64 * 128;  // staged words per chunk: 64 anchors x 2 walks x 64 pixels
 // control words per frame: [0] chains complete, [1] next chain to take, [2] 0 running / 1 done / -1 failed
 constexpr int LF_CTL = 4;
 
 __device__ __forceinline__ void ls_ring_space(LsRing& R, int w, int need) {
   while (w + need - R.rseen > LS_RING) {
-    R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    R.rseen = __hip_atomic_load(R.rpos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (w + need - R.rseen > LS_RING) __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -1228,9 +1236,9 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
     uint32_t* __restrict__ pe, uint32_t* __restrict__ p1, uint32_t* __restrict__ p2, int pcap,
     uint32_t* __restrict__ chains, uint32_t* __restrict__ sid, int ecap, int* __restrict__ nedge,
     uint32_t* __restrict__ gstarts, int* __restrict__ ctl, uint32_t* __restrict__ lscratch,
-    uint32_t* __restrict__ ccount, float min_length, int* __restrict__ diag) {
+    uint32_t* __restrict__ ccount, float min_length, int* __restrict__ diag, unsigned long long* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds_lf[];
-  __shared__ int s_w, s_r, s_done, s_ne;
+  __shared__ int s_w, s_r, s_done, s_ne, s_stage, s_cons;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nb = (W * H + 31) / 32, nbp = (nb + 3) & ~3, ep = (ecap + 2 + 3) & ~3;
   uint32_t* fS = gstarts;
@@ -1238,12 +1246,66 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
   uint32_t* P1 = p1;
   uint32_t* P2 = p2;
   const int na = nanchor[0];
-  if (threadIdx.x == 0) s_w = s_r = s_done = 0;
+  if (threadIdx.x == 0) s_w = s_r = s_done = s_stage = s_cons = 0;
   __syncthreads();
-  if (blockIdx.x == 0 && wave < 2) {
+  if (blockIdx.x == 0 && wave < 3) {
     uint32_t* bits = lds_lf;
     uint16_t* tile = (uint16_t*)(bits + nbp);
     LsRing R{(uint2*)(tile + LE_TW * LE_TH), &s_w, &s_r, 0};
+    // the stager's double buffer: per chunk of 64 anchors, both walks' first 64 pixels and the
+    // anchors' (length, length, continuation, continuation, edge-map index) words
+    uint32_t* stg = (uint32_t*)(R.r + LS_RING);
+    uint32_t* meta = stg + 2 * LF_STAGE;
+    if (wave == 2) {
+      // the stager (wave 2): waits for the walks of chunk c, loads their first rounds and copies
+      // them to LDS slot c & 1, so the merge wave issues no global loads for them (its vector-memory
+      // waits -- in order -- would otherwise wait for these loads: ~1 us per anchor)
+      const int nae = min(na, acap);
+      for (int a0 = 0, c = 0; a0 < nae; a0 += 64, c++) {
+        while (__hip_atomic_load(&s_cons, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < c - 1) {
+          if (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const int a = a0 + lane;
+        uint32_t l1 = 0, l2 = 0;
+        while (true) {
+          l1 = a < nae ? ld_wt<true>(&pl[2 * a]) : 0u;
+          l2 = a < nae ? ld_wt<true>(&pl[2 * a + 1]) : 0u;
+          if (!ballot(l1 == LS_PENDING || l2 == LS_PENDING)) break;
+          if (__hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const uint32_t e1 = a < nae ? ld_wt<true>(&pe[2 * a]) : 0u, e2 = a < nae ? ld_wt<true>(&pe[2 * a + 1]) : 0u;
+        const uint32_t ap = a < nae ? anchors[a] : 0u;
+        uint32_t* st = stg + (c & 1) * LF_STAGE;
+        uint32_t* mt = meta + (c & 1) * 64 * 5;
+        mt[5 * lane + 0] = l1;
+        mt[5 * lane + 1] = l2;
+        mt[5 * lane + 2] = e1;
+        mt[5 * lane + 3] = e2;
+        mt[5 * lane + 4] = (ap >> 16) * (uint32_t)W + (ap & 0xffffu);
+        for (int j0 = 0; j0 < 64 && a0 + j0 < nae; j0 += 8) {  // 16 loads in flight per lane
+          uint32_t q[16];
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const int k = j0 + j;
+            const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k) & 0x7fffffffu;
+            const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k) & 0x7fffffffu;
+            const long long wk = 2 * (long long)(a0 + k);
+            q[2 * j] = a0 + k < nae && (uint32_t)lane < n1 ? ld_wt<true>(ps + wk * LS_CAP + lane) : 0u;
+            q[2 * j + 1] = a0 + k < nae && (uint32_t)lane < n2 ? ld_wt<true>(ps + (wk + 1) * LS_CAP + lane) : 0u;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            st[(j0 + j) * 128 + lane] = q[2 * j];
+            st[(j0 + j) * 128 + 64 + lane] = q[2 * j + 1];
+          }
+        }
+        LS_FENCE();  // the slot's words before its count (one wave's LDS operations complete in order)
+        if (lane == 0) __hip_atomic_store(&s_stage, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return;
+    }
     if (wave == 0) {
       MoveTile T{tile, -LE_TW, -LE_TH};
       for (int i = lane; i < nb; i += 64) bits[i] = 0;
@@ -1251,32 +1313,42 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
       uint32_t b1 = 0, b2 = 0;
       int ne = 0, w = 0;
       bool fail = na > acap;
-      for (int a0 = 0; a0 < na && !fail; a0 += 64) {
+      // profiling (prof != null): anchors merged; wall-clock ticks in the two parts, the
+      // pending-set update, the chunk starts (waits for the stager), the whole merge
+      int pn_anchor = 0;
+      unsigned long long pt_p1 = 0, pt_p2 = 0, pt_pend = 0, pt_chunk = 0, pt_wait = 0;
+      const unsigned long long pt_start = prof ? wall_clock64() : 0;
+      int c = 0;
+      for (int a0 = 0; a0 < na && !fail; a0 += 64, c++) {
+        const unsigned long long tc0 = prof ? wall_clock64() : 0;
         const int a = a0 + lane;
-        const uint32_t ap = a < na ? anchors[a] : 0u;
-        const int aidx = (int)(ap >> 16) * W + (int)(ap & 0xffffu);
-        // the walks of these 64 anchors: written, and released after their paths
-        uint32_t l1 = 0, l2 = 0;
-        while (true) {
-          l1 = a < na ? ld_wt<true>(&pl[2 * a]) : 0u;
-          l2 = a < na ? ld_wt<true>(&pl[2 * a + 1]) : 0u;
-          if (!ballot(l1 == LS_PENDING || l2 == LS_PENDING)) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        // paths and continuation words: stored sc1 and drained before their length word, loaded sc1
-        const uint32_t e1 = a < na ? ld_wt<true>(&pe[2 * a]) : 0u, e2 = a < na ? ld_wt<true>(&pe[2 * a + 1]) : 0u;
+        // the chunk's walks, staged in LDS by wave 2 (their paths and words were stored sc1 and
+        // drained before their length words, and loaded sc1 there)
+        while (__hip_atomic_load(&s_stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= c) __builtin_amdgcn_s_sleep(1);
+        LS_FENCE();
+        const uint32_t* st = stg + (c & 1) * LF_STAGE;
+        const uint32_t* mt = meta + (c & 1) * 64 * 5;
+        const uint32_t l1 = mt[5 * lane + 0], l2 = mt[5 * lane + 1], e1 = mt[5 * lane + 2], e2 = mt[5 * lane + 3];
+        const int aidx = (int)mt[5 * lane + 4];
         auto first = [&](int k, uint32_t& q1, uint32_t& q2) {
-          const long long wk = 2 * (long long)(a0 + k);
-          const uint32_t n1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k) & 0x7fffffffu;
-          const uint32_t n2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k) & 0x7fffffffu;
-          q1 = (uint32_t)lane < n1 ? ld_wt<true>(ps + wk * LS_CAP + lane) : 0u;
-          q2 = (uint32_t)lane < n2 ? ld_wt<true>(ps + (wk + 1) * LS_CAP + lane) : 0u;
+          q1 = st[k * 128 + lane];
+          q2 = st[k * 128 + 64 + lane];
         };
         uint64_t pend = ballot(a < na) & ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
         int k = pend ? __builtin_ctzll(pend) : -1;
         uint32_t c1 = 0, c2 = 0;
+        bool have1 = false;  // part 1's first-round marks of anchor k tested already (mk1)
+        uint64_t mk1 = 0;
         if (k >= 0) first(k, c1, c2);
+        if (prof) pt_chunk += wall_clock64() - tc0;
         while (k >= 0) {
+          if (prof) {  // the anchor's first-round pixels arriving (profiling: drained here, timed)
+            const unsigned long long tw = wall_clock64();
+            vm_drain();
+            pt_wait += wall_clock64() - tw;
+          }
+          const unsigned long long ta = prof ? wall_clock64() : 0;
+          pn_anchor++;
           pend &= pend - 1;
           const int kn = pend ? __builtin_ctzll(pend) : -1;
           uint32_t n1 = 0, n2 = 0;
@@ -1289,17 +1361,23 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
           const uint32_t L1 = (uint32_t)__builtin_amdgcn_readlane((int)l1, k), L2 = (uint32_t)__builtin_amdgcn_readlane((int)l2, k);
           uint32_t o1 = b1, o2 = b2;
           if (!ls_part<true>(moves, W, MP, H, bits, T, ps + wk * LS_CAP, L1, (uint32_t)__builtin_amdgcn_readlane((int)e1, k), c1,
-                       P1, 0u, o1, (uint32_t)pcap, R, w)) {
+                             P1, 0u, o1, (uint32_t)pcap, R, w, have1, mk1)) {
             fail = true;
             break;
           }
+          const unsigned long long tb = prof ? wall_clock64() : 0;
           const int idx = __builtin_amdgcn_readlane(aidx, k);
-          if (lane == 0) bits[idx >> 5] &= ~(1u << (idx & 31));
+          if (lane == 0) atomicAnd(&bits[idx >> 5], ~(1u << (idx & 31)));  // no return: no wait
           LS_FENCE();
           if (!ls_part<true>(moves, W, MP, H, bits, T, ps + (wk + 1) * LS_CAP, L2, (uint32_t)__builtin_amdgcn_readlane((int)e2, k),
-                       c2, P2, 1u, o2, (uint32_t)pcap, R, w)) {
+                             c2, P2, 1u, o2, (uint32_t)pcap, R, w)) {
             fail = true;
             break;
+          }
+          const unsigned long long tcc = prof ? wall_clock64() : 0;
+          if (prof) {
+            pt_p1 += tb - ta;
+            pt_p2 += tcc - tb;
           }
           // a capped walk's continuation stored its pixels itself (sc1): drained before the chain's
           // markers reach the writer, whose count then covers them
@@ -1312,20 +1390,46 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
               ls_ring_space(R, w, 2);
               if (lane < 2) R.r[(w + lane) & (LS_RING - 1)] = make_uint2(LS_MARK | (lane ? 0x20000000u : 0u) | (uint32_t)ne, lane ? b2 : b1);
               w += 2;
-              if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              LS_FENCE();
+              if (lane == 0) __hip_atomic_store(R.wpos, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
           }
-          pend &= ~ballot(((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0);
+          // the anchors this walk marked, and -- in the same LDS round trip -- the first-round marks of
+          // the next candidate's part 1, valid when it is still the next pending anchor
+          const uint32_t ln1 = kn >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)l1, kn) & 0x7fffffffu : 0u;
+          const int nidx = (int)(n1 >> 16) * W + (int)(n1 & 0xffffu);
+          const bool am = ((bits[aidx >> 5] >> (aidx & 31)) & 1u) != 0;
+          const bool nm = (uint32_t)lane < ln1 && ((bits[nidx >> 5] >> (nidx & 31)) & 1u);
+          pend &= ~ballot(am);
+          const uint64_t nmk = ballot(nm);
           k = pend ? __builtin_ctzll(pend) : -1;
+          have1 = false;
           if (k >= 0 && k == kn) {
             c1 = n1;
             c2 = n2;
+            have1 = true;
+            mk1 = nmk;
           } else if (k >= 0) {
             first(k, c1, c2);
           }
+          if (prof) pt_pend += wall_clock64() - tcc;
         }
+        LS_FENCE();  // the slot's reads done: wave 2 may refill it
+        if (lane == 0) __hip_atomic_store(&s_cons, c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
       if (ne > ecap) fail = true;
+      if (prof && lane == 0) {
+        atomicAdd(&prof[0], (unsigned long long)pn_anchor);
+        atomicAdd(&prof[3], pt_p1);
+        atomicAdd(&prof[4], pt_p2);
+        atomicAdd(&prof[5], pt_pend);
+        atomicAdd(&prof[6], pt_chunk);
+        atomicAdd(&prof[7], wall_clock64() - pt_start);
+        atomicAdd(&prof[8], (unsigned long long)na);
+        atomicAdd(&prof[9], (unsigned long long)ne);
+        atomicAdd(&prof[10], 1ull);
+        atomicAdd(&prof[11], pt_wait);
+      }
       if (lane == 0) {
         s_ne = fail ? -1 : ne;
         __hip_atomic_store(&s_done, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1340,7 +1444,8 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
       int r = 0;
       while (true) {
         const int d = __hip_atomic_load(&s_done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const int w = __hip_atomic_load(&s_w, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int w = __hip_atomic_load(&s_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        LS_FENCE();
         if (r < w) {
           int pub = 0;
           for (int i = r + lane; i < w; i += 64) {
@@ -1357,7 +1462,7 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
           }
           r = w;
           LS_FENCE();
-          if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (lane == 0) __hip_atomic_store(&s_r, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           pub = wave_max_int(pub);
           if (pub > 0) {
             vm_drain();  // the chains' pixels and starts (sc1), then their count
@@ -1592,6 +1697,7 @@ struct LineEngine {
   uint32_t *d_ps = nullptr, *d_pl = nullptr, *d_pe = nullptr;  // its paths / lengths / continuations (one frame)
   uint32_t* d_starts = nullptr;
   int* d_lctl = nullptr;           // k_lines_fused's control words
+  unsigned long long* d_lprof = nullptr;  // its merge counters (EAO_LINES_PROF=1: printed at destroy)
   uint32_t* d_lstarts = nullptr;   // k_lines_fused's chain starts (fS / sS)
   int k[3] = {0, 0, 0};
   hipStream_t stream = nullptr;
@@ -1609,6 +1715,18 @@ struct LineEngine {
   int* h_n = nullptr;  // pinned: the single-frame line count (and, checking, the diagnostic word)
   HostStage stage_in, stage_out;  // single-frame staging: the pinned image in, count + lines back
   ~LineEngine() {
+    if (d_lprof) {
+      unsigned long long h[16] = {0};
+      if (hipMemcpy(h, d_lprof, sizeof h, hipMemcpyDeviceToHost) == hipSuccess && h[10]) {
+        const double n = (double)h[10], us = 0.01;  // wall clock 100 MHz
+        fprintf(stderr,
+                "k_lines_fused merge per call (%llu calls): anchors %.0f (of %.0f), chains %.0f | us: pixels-arrive "
+                "wait %.1f part1 %.1f part2 %.1f pend %.1f chunk starts %.1f total %.1f\n",
+                h[10], h[0] / n, h[8] / n, h[9] / n, h[11] * us / n, h[3] * us / n, h[4] * us / n, h[5] * us / n,
+                h[6] * us / n, h[7] * us / n);
+      }
+      (void)hipFree(d_lprof);
+    }
     void* p[] = {d_blur, d_dx,   d_dy,    d_code,  d_moves, d_amask, d_anch,  d_p1,   d_p2,    d_chain,
                  d_sid,  d_lscr, d_ccnt,  d_nanch, d_nedge, d_img,   d_lines, d_nlines, d_starts,
                  d_ps,   d_pl,   d_pe,   d_lctl, d_lstarts};
@@ -1770,13 +1888,18 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
     const char* v = getenv("EAO_LINES_ONE_LAUNCH");
     return v ? atoi(v) : 64;  // workgroups beside the merge's; 0 = off
   }();
-  const size_t lf_merge = edge_draw_lds(W, H, e.ecap, true) + 8 * LS_RING;
+  const size_t lf_merge = edge_draw_lds(W, H, e.ecap, true) + 8 * LS_RING + 4 * (2 * (size_t)LF_STAGE + 2 * 64 * 5);
   const size_t lf_walk = (size_t)LF_WAVES * (sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP);
   const size_t lf_lds = std::max(lf_merge, lf_walk);
   const bool fused = nframes == 1 && e.spec && fused_blocks > 0 && lf_lds <= kLdsMax - 64;
   if (fused && !e.d_lctl) {
     const size_t nw = (size_t)2 * e.acap;
     EAO_HIP_CHECK(hipMalloc(&e.d_lctl, sizeof(int) * LF_CTL));
+    if (const char* v = getenv("EAO_LINES_PROF"))
+      if (v[0] == '1') {
+        EAO_HIP_CHECK(hipMalloc(&e.d_lprof, 16 * sizeof(unsigned long long)));
+        EAO_HIP_CHECK(hipMemset(e.d_lprof, 0, 16 * sizeof(unsigned long long)));
+      }
     EAO_HIP_CHECK(hipMalloc(&e.d_lstarts, (size_t)2 * ((e.ecap + 2 + 3) & ~3) * 4));
     if (!e.d_ps) {
       EAO_HIP_CHECK(hipMalloc(&e.d_ps, nw * LS_CAP * 4));
@@ -1794,7 +1917,7 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
     hipLaunchKernelGGL(k_lines_fused, dim3(1 + std::min(fused_blocks, 192)), dim3(64 * LF_WAVES), lf_lds, s, e.d_moves,
                        e.d_code, e.d_dx, e.d_dy, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1,
                        e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge, e.d_lstarts, e.d_lctl, e.d_lscr, e.d_ccnt,
-                       min_length, diag);
+                       min_length, diag, e.d_lprof);
     hipLaunchKernelGGL(k_lines_place, dim3(1), dim3(256), 0, s, e.d_sid, e.d_nedge, e.pcap, e.ecap, e.d_lscr,
                        e.d_ccnt, d_lines, d_counts, cap);
   } else if (nframes == 1 && e.spec && edge_draw_lds(W, H, e.ecap, e.gstarts) + 8 * LS_RING <= kLdsMax - 64) {

@@ -39,3 +39,4 @@ if "--check" in sys.argv:
     from oracle import pyoracle as orc  # the checker (development aid only)
     bad = [i for i, c in enumerate(color[:16]) if not np.array_equal(L.detect_color(c), orc.edlines_color(c))]
     print("oracle check of 16 frames: %s" % ("ok" if not bad else "MISMATCH %s" % bad), flush=True)
+L.close()  # EAO_LINES_PROF=1: the merge counters are printed at destroy
