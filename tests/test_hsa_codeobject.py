@@ -17,7 +17,8 @@ LANE_KERNELS = {
     "eao::k_rects_np(": 22,
     "eao::k_np_pairs(": 12,
     "eao::k_stage(": 3,
-    "eao::k_iforest_sum(": 11,
+    "eao::k_iforest_sum(": 14,  # + the packed outlier masks' outputs (sharded replays)
+    "eao::k_publish(": 4,
     "void eao::k_iforest_tree<64>(": 16,
     "void eao::k_iforest_tree<1024>(": 16,
 }
