@@ -555,6 +555,13 @@ def main():
         result["gpu_over_cpu"] = {"all_cores": result["value"] / result["cpu_baseline"]["value"],
                                   "single_thread": result["value"] / result["cpu_baseline"]["single_thread"]["value"]}
     if rank == 0 and world == 1 and not args.no_dropin:
+        # the per-frame legs stand for a process that uses the single-frame entry points only: the
+        # step's engines (their streams, HSA queues and buffers) are released first, so the legs do
+        # not share the device's hardware queues with idle ones
+        for h in (last["replay"], assoc, orb, matcher, lines):
+            if h is not None:
+                h.close()
+        last["replay"] = None
         kd = min(args.dropin_frames, F)
         result["dropin_per_frame"] = dropin_leg(ea, gpu, assoc_frames[:kd], d_color[:kd].cpu().numpy(),
                                                 d_frames[:kd].cpu().numpy(), poses[:kd], cfg["flag"],
