@@ -704,6 +704,39 @@ struct LsRing {
   int rseen;  // the writer's position as last read (re-read only when the ring may be full)
 };
 
+// The ring writer stores 64 records per instruction. A short edge the merge drops leaves records at
+// positions the next walk records again (its start is not advanced), and both can fall in one
+// 64-record chunk: two lanes storing to one address in one instruction, whose winner the hardware
+// does not order. A record is stored only if no later record of its chunk has the same target
+// (the later one is the merge's final word for that position).
+__device__ __forceinline__ bool ring_last_in_chunk(uint32_t key, bool valid) {
+  const int lane = lane_id();
+  // a later record can target an earlier one's position only after a restart: a record at or
+  // below the highest earlier position of its part in the chunk (exclusive prefix maxima, one
+  // per part). Chunks without one -- nearly all -- store every record.
+  const bool rec = valid && !(key & 0x40000000u);  // pixel records (markers have bit 30)
+  const int pos = (int)(key & 0x7fffffffu), part = (int)(key >> 31);
+  int m1 = rec && part == 0 ? pos : -1, m2 = rec && part == 1 ? pos : -1;
+  int p1 = __shfl_up(m1, 1, 64), p2 = __shfl_up(m2, 1, 64);
+  if (lane == 0) p1 = p2 = -1;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t1 = __shfl_up(p1, d, 64), t2 = __shfl_up(p2, d, 64);
+    if (lane >= d) {
+      p1 = max(p1, t1);
+      p2 = max(p2, t2);
+    }
+  }
+  if (!ballot(rec && pos <= (part == 0 ? p1 : p2))) return valid;
+  bool later = false;
+  for (int d = 1; d < 64; d++) {
+    const uint32_t o = (uint32_t)__shfl((int)key, min(lane + d, 63), 64);
+    const bool ov = __shfl((int)valid, min(lane + d, 63), 64) != 0;
+    later |= lane + d < 64 && ov && o == key;
+  }
+  return valid && !later;
+}
+
 // Phase 2, one part of an anchor's chain: the prefix of walk wi not yet marked, recorded at
 // P[off..] (part: P1 / P2) and marked, 64 pixels per round; a path cut at LS_CAP goes on with
 // ed_walk from its stored next pixel and state (whose stores go straight to P). False on overflow
@@ -866,8 +899,10 @@ __global__ __launch_bounds__(128) void k_walk_merge(const uint16_t* __restrict__
       const int w = __hip_atomic_load(&s_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         LS_FENCE();
       if (r < w) {
-        for (int i = r + lane; i < w; i += 64) {
-          const uint2 e = R.r[i & (LS_RING - 1)];
+        for (int c0 = r; c0 < w; c0 += 64) {
+          const int i = c0 + lane;
+          const uint2 e = i < w ? R.r[i & (LS_RING - 1)] : make_uint2(0u, 0u);
+          if (!ring_last_in_chunk(e.x, i < w)) continue;
           if (diag && ((e.x & 0x7fffffffu) >= (uint32_t)pcap || px_x(e.y) >= (uint32_t)W || px_y(e.y) >= (uint32_t)H))
             atomicOr(diag, 1);  // a record out of range (checking mode: not stored)
           else
@@ -1219,7 +1254,8 @@ constexpr uint32_t LS_PENDING = 0xFFFFFFFFu;  // pl of a walk not written yet (n
 constexpr uint32_t LS_MARK = 0x40000000u;      // ring record: a chain start (bit 29: sS, else fS), low bits the chain
 constexpr int LF_WAVES = 4;
 constexpr int LF_STAGE = 64 * 128;  // staged words per chunk: 64 anchors x 2 walks x 64 pixels
-// control words per frame: [0] chains complete, [1] next chain to take, [2] 0 running / 1 done / -1 failed
+// control words per frame: [0] chains complete, [1] next chain to take, [2] 0 running / 1 done / -1 failed,
+// [3] next walk to take
 constexpr int LF_CTL = 4;
 
 __device__ __forceinline__ void ls_ring_space(LsRing& R, int w, int need) {
@@ -1448,8 +1484,11 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
         LS_FENCE();
         if (r < w) {
           int pub = 0;
-          for (int i = r + lane; i < w; i += 64) {
-            const uint2 e = R.r[i & (LS_RING - 1)];
+          for (int c0 = r; c0 < w; c0 += 64) {
+            const int i = c0 + lane;
+            const uint2 e = i < w ? R.r[i & (LS_RING - 1)] : make_uint2(0u, 0u);
+            // (markers' words are unique: bit 30 set, the chain count below it)
+            if (!ring_last_in_chunk(e.x, i < w)) continue;
             if (e.x & LS_MARK) {
               const int c = (int)(e.x & 0x1fffffffu);
               st_wt<true>(((e.x & 0x20000000u) ? sS : fS) + c, e.y);
@@ -1488,8 +1527,15 @@ __global__ __launch_bounds__(64 * LF_WAVES) void k_lines_fused(
     uint8_t* base = (uint8_t*)lds_lf + (size_t)wave * (sizeof(uint16_t) * LE_TW * LE_TH + 4 * LS_CAP);
     MoveTile T{(uint16_t*)base, -LE_TW, -LE_TH};
     uint32_t* path = (uint32_t*)(base + sizeof(uint16_t) * LE_TW * LE_TH);
-    const int nsw = (gridDim.x - 1) * LF_WAVES;
-    for (int w = (blockIdx.x - 1) * LF_WAVES + wave; w < 2 * min(na, acap); w += nsw) {
+    // walks are claimed in anchor order from a counter, not assigned by workgroup: whichever
+    // workgroups are resident do every walk the merge waits for, so the launch progresses with any
+    // number of them on the chip (others of its kind, or other work, may hold the rest of the CUs)
+    const int nw2 = 2 * min(na, acap);
+    for (;;) {
+      int w = 0;
+      if (lane == 0) w = __hip_atomic_fetch_add(&ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w = __shfl(w, 0, 64);
+      if (w >= nw2) break;
       const uint32_t ap = anchors[w >> 1];
       const int x = (int)(ap & 0xffffu), y = (int)(ap >> 16);
       const bool horiz = (code[(long long)y * W + x] & LN_HORIZ) != 0;
@@ -1912,8 +1958,8 @@ int eao_lines_detect_color_batch_device(eao_lines* L, const uint8_t* d_img, int 
   if (fused) {
     int* diag = lines_check() && d_counts == e.d_nlines ? e.d_nlines + 1 : nullptr;
     if (diag) EAO_HIP_CHECK(hipMemsetAsync(diag, 0, 4, s));
-    // every workgroup resident at once (the merge waits on walks the others compute, and they on
-    // its chains): one workgroup of lf_lds per CU, fewer than the CUs
+    // one workgroup of lf_lds per CU; progress needs only workgroup 0 (dispatched first) and one
+    // other resident: walks and chains are claimed from counters, in order
     hipLaunchKernelGGL(k_lines_fused, dim3(1 + std::min(fused_blocks, 192)), dim3(64 * LF_WAVES), lf_lds, s, e.d_moves,
                        e.d_code, e.d_dx, e.d_dy, W, H, e.MP, e.d_anch, e.d_nanch, e.acap, e.d_ps, e.d_pl, e.d_pe, e.d_p1,
                        e.d_p2, e.pcap, e.d_chain, e.d_sid, e.ecap, e.d_nedge, e.d_lstarts, e.d_lctl, e.d_lscr, e.d_ccnt,

@@ -37,6 +37,7 @@ print("single-frame lines: %.3f ms mean, %.3f median, %.3f min over %d frames, d
       % (np.mean(ms), np.median(ms), np.min(ms), F, h.hexdigest()[:16]), flush=True)
 if "--check" in sys.argv:
     from oracle import pyoracle as orc  # the checker (development aid only)
-    bad = [i for i, c in enumerate(color[:16]) if not np.array_equal(L.detect_color(c), orc.edlines_color(c))]
-    print("oracle check of 16 frames: %s" % ("ok" if not bad else "MISMATCH %s" % bad), flush=True)
+    bad = [i for i, c in enumerate(color) if not np.array_equal(L.detect_color(c), orc.edlines_color(c))]
+    print("oracle check of %d frames: %s" % (len(color), "ok" if not bad else "MISMATCH %s" % bad), flush=True)
+
 L.close()  # EAO_LINES_PROF=1: the merge counters are printed at destroy
