@@ -230,9 +230,10 @@ def main():
                     help="config c: the object-sharded exchange path also at world 1 (one-rank RCCL communicator)")
     ap.add_argument("--poll", action="store_true", help="A/B: poll the extraction stream while the association runs")
     ap.add_argument("--line-batches", type=int, default=1, help="line detection in this many launches per step")
-    ap.add_argument("--frame-cus", type=int, default=0,
-                    help="A/B: the frame work's stream limited to this many CUs of each XCD (0: all), the rest "
-                         "left to the association's launches")
+    ap.add_argument("--frame-cus", type=int, default=-1,
+                    help="the frame work's stream limited to this many CUs of each XCD (0: all), the rest left to "
+                         "the association's launches; default: 24 for the Full stream (its frame work overlaps more "
+                         "of the replay: +2 %%, profiles/r06_ab_full_frame_cus.txt), all for the others")
     ap.add_argument("--cu-layout", choices=["interleaved", "linear"], default="interleaved",
                     help="A/B: CU-mask bit order (interleaved: bit i = CU i / 8 of XCD i % 8)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-frame drop-in leg (dropin_leg)")
@@ -290,6 +291,8 @@ def main():
     poses = rposes[idx].astype(np.float32)
     # the extraction / matching stream runs on a dedicated HIP stream (a NULL handle would
     # select the engine's own stream, which torch events do not see); buffers are made on it
+    if args.frame_cus < 0:
+        args.frame_cus = 24 if args.config == "full" else 0
     stream = torch.cuda.Stream(dev) if not args.frame_cus else cu_masked_stream(dev, args.frame_cus, args.cu_layout)
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
@@ -507,7 +510,8 @@ def main():
             "config": {"workload": cfg["workload"] + ", %d frames/rank/step, %d ORB features, 8 levels, assoc flag "
                                                      "%s" % (F, NFEAT, cfg["flag"]),
                        "frames_per_step": F, "features": NFEAT, "levels": NLEV, "assoc_flag": cfg["flag"],
-                       "parallelism": "streams%d" % world},
+                       "parallelism": "streams%d" % world,
+                       "frame_work_cus_per_xcd": args.frame_cus or "all"},
             "roofline": {"bound": "hbm", "kernel": KERNELS[dom_name], "achieved": ach, "peak": PEAK_HBM_GBS,
                          "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,

@@ -307,6 +307,8 @@ struct Obj {  // Object_Map
   uint64_t bts_epoch = ~0ull;
   float bts_box[6] = {0, 0, 0, 0, 0, 0};
   std::vector<MapPt*> bts_pts;
+  // the positions of ms_pts at that call (x block, y block, z block): valid while ms_epoch is
+  std::vector<float> ms_pos;
 };
 const float* Det::P() const { return alias ? alias->center : pos; }
 
@@ -1124,6 +1126,10 @@ class ReplayEngine {
   // ComputeMeanAndStandard scratch: the object's positions gathered once per call (SoA), and
   // their images under the inverse cuboid pose
   std::vector<float> ms_p[3], ms_t[3];
+  // mean_std's input positions when the caller has them in order already (big_to_small over an
+  // object's cached ones): x, y, z blocks of the list's length, no point bad
+  const float* ms_in = nullptr;
+  std::vector<float> bts_p;
   uint64_t pt_epoch = 1;  // bumped whenever a map point's position or bad flag changes
   // a point that changes marks the objects it voted for: every object that holds a point got its
   // vote first (vote / vote_insert before each pts.push_back) and votes are never withdrawn
@@ -1198,17 +1204,35 @@ class ReplayEngine {
     float* py = ms_p[1].data();
     float* pz = ms_p[2].data();
     size_t w = 0;
-    for (size_t i = 0; i < n0; i++) {
-      MapPt* p = o->pts[i];
-      if (p->bad) continue;
-      for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
-      px[w] = p->pos[0];
-      py[w] = p->pos[1];
-      pz[w] = p->pos[2];
-      o->pts[w++] = p;
+    if (ms_in) {  // the same sums in the same order (float, per axis), from contiguous positions
+      for (int a = 0; a < 3; a++) {
+        const float* in = ms_in + a * n0;
+        float* out = ms_p[a].data();
+        float sa = 0;
+        for (size_t i = 0; i < n0; i++) {
+          sa += in[i];
+          out[i] = in[i];
+        }
+        o->sum[a] = sa;
+      }
+      w = n0;
+    } else {
+      for (size_t i = 0; i < n0; i++) {
+        MapPt* p = o->pts[i];
+        if (p->bad) continue;
+        for (int a = 0; a < 3; a++) o->sum[a] += p->pos[a];
+        px[w] = p->pos[0];
+        py[w] = p->pos[1];
+        pz[w] = p->pos[2];
+        o->pts[w++] = p;
+      }
+      o->pts.resize(w);
     }
-    o->pts.resize(w);
     const size_t n = o->pts.size();
+    o->ms_pos.resize(3 * n);  // cached for the next call over this list (big_to_small)
+    std::memcpy(o->ms_pos.data(), px, sizeof(float) * n);
+    std::memcpy(o->ms_pos.data() + n, py, sizeof(float) * n);
+    std::memcpy(o->ms_pos.data() + 2 * n, pz, sizeof(float) * n);
     const float sc = (float)(1. / (double)n);
     for (int a = 0; a < 3; a++) o->center[a] = o->sum[a] * sc + 0.0f;
     float s2[3] = {0, 0, 0};
@@ -3360,20 +3384,49 @@ class ReplayEngine {
     double tq = now_us();
     const float box[6] = {s->xmn, s->xmx, s->ymn, s->ymx, s->zmn, s->zmx};
     // the same box over the list it left last time, no point moved since: nothing to erase
+    bool given = false;
     if (!(g_ms_memo && a->bts_epoch != ~0ull && std::memcmp(box, a->bts_box, sizeof box) == 0 &&
           a->pts == a->bts_pts && points_unchanged(a, a->bts_epoch))) {
       prof[31] += 1;
+      const size_t n = a->pts.size();
       size_t w = 0;
-      for (size_t i = 0; i < a->pts.size(); i++) {
-        const float* P = a->pts[i]->pos;
-        const bool in = P[0] > box[0] && P[0] < box[1] && P[1] > box[2] && P[1] < box[3] && P[2] > box[4] &&
-                        P[2] < box[5];
-        if (!in) a->pts[w++] = a->pts[i];
+      // the list as ComputeMeanAndStandard last saw it, no point changed since: its positions are
+      // cached contiguously, and none of its points is bad
+      if (g_ms_memo && a->ms_epoch != ~0ull && n == a->ms_pts.size() && a->ms_pos.size() == 3 * n &&
+          (n == 0 || std::memcmp(a->pts.data(), a->ms_pts.data(), sizeof(MapPt*) * n) == 0) &&
+          points_unchanged(a, a->ms_epoch)) {
+        if (bts_p.size() < 3 * n) bts_p.resize(3 * n + 192);
+        const float *X = a->ms_pos.data(), *Y = X + n, *Z = Y + n;
+        float* fx = bts_p.data();
+        for (size_t i = 0; i < n; i++) {
+          const bool in = X[i] > box[0] && X[i] < box[1] && Y[i] > box[2] && Y[i] < box[3] && Z[i] > box[4] &&
+                          Z[i] < box[5];
+          if (!in) {
+            a->pts[w] = a->pts[i];
+            fx[w] = X[i];
+            fx[n + w] = Y[i];
+            fx[2 * n + w] = Z[i];
+            w++;
+          }
+        }
+        // blocks of the filtered length for mean_std
+        std::memmove(fx + w, fx + n, sizeof(float) * w);
+        std::memmove(fx + 2 * w, fx + 2 * n, sizeof(float) * w);
+        given = true;
+      } else {
+        for (size_t i = 0; i < n; i++) {
+          const float* P = a->pts[i]->pos;
+          const bool in = P[0] > box[0] && P[0] < box[1] && P[1] > box[2] && P[1] < box[3] && P[2] > box[4] &&
+                          P[2] < box[5];
+          if (!in) a->pts[w++] = a->pts[i];
+        }
       }
       a->pts.resize(w);
     }
     prof[38] += now_us() - tq;
+    if (given) ms_in = bts_p.data();
     mean_std(a);  // drops bad points only: the list stays clear of the box
+    ms_in = nullptr;
     a->bts_epoch = pt_epoch;
     std::memcpy(a->bts_box, box, sizeof box);
     a->bts_pts = a->pts;
