@@ -2026,6 +2026,18 @@ int eao_lines_detect_batch_device(eao_lines* L, const uint8_t* d_gray, int nfram
   return eao_lines_detect_color_batch_device(L, d_gray, nframes, pitch, 1, min_length, d_lines, d_counts, cap, stream);
 }
 
+// single calls: the count (and the checking word) and min(count, cap) lines written by the GPU straight
+// into the handle's pinned buffers, behind the kernels on the engine's stream. A DMA copy would queue on
+// the copy engine behind this frame's 0.5 ms line launch, and with it every other engine's transfers
+// of the same frame (the drop-in's matching waited there: profiles/r06_dropin_copy_engine.txt).
+__global__ __launch_bounds__(256) void k_lines_out(const int* __restrict__ dn, const float* __restrict__ dl, int cap,
+                                                   int nw, int* __restrict__ hn, float* __restrict__ hl) {
+  const int n = dn[0];
+  if (threadIdx.x < nw) hn[threadIdx.x] = dn[threadIdx.x];
+  const int k = 6 * max(0, min(n, cap));
+  for (int i = threadIdx.x; i < k; i += blockDim.x) hl[i] = dl[i];
+}
+
 int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length, float* lines,
                            int cap, int* n_out) {
   if (!L || !img || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
@@ -2048,8 +2060,18 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
   if (rc) return rc;
   const size_t lb = sizeof(float) * 6 * (size_t)std::min(std::max(cap, 0), 4096);
   EAO_HIP_CHECK(e.stage_out.reserve(lb));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, lines_check() ? 8 : 4, hipMemcpyDeviceToHost, s));
-  if (lb) EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_lines, lb, hipMemcpyDeviceToHost, s));
+  static const bool dma_out = [] {
+    const char* v = getenv("EAO_LINES_DMA_OUT");  // 1: the DMA copies back (A/B)
+    return v && v[0] == '1';
+  }();
+  if (dma_out) {
+    EAO_HIP_CHECK(hipMemcpyAsync(e.h_n, e.d_nlines, lines_check() ? 8 : 4, hipMemcpyDeviceToHost, s));
+    if (lb) EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_lines, lb, hipMemcpyDeviceToHost, s));
+  } else {
+    hipLaunchKernelGGL(k_lines_out, dim3(1), dim3(256), 0, s, e.d_nlines, e.d_lines,
+                       std::min(std::max(cap, 0), 4096), lines_check() ? 2 : 1, e.h_n, (float*)e.stage_out.h);
+    EAO_HIP_CHECK(hipGetLastError());
+  }
   EAO_HIP_CHECK(hipStreamSynchronize(s));
   const int n = *e.h_n;
   if (lines_check() && e.h_n[1]) {
