@@ -852,15 +852,27 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
                 nm, cm = mt1.motion(cam, poses[t], MOTION_TH, 1, lk, np.ones(len(lk), np.uint8), pos, ld, kps, desc,
                                     sc1)
                 t_match = time.perf_counter() - tp
-            if overlap:
-                lines, tl = fut.result()
-            t3 = time.perf_counter()
             f = assoc_frames[t]
-            det = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+            if overlap:
+                # the association runs up to its line-dependent tail while the lines are detected
+                # (eao_replay_frame_begin), then takes them (eao_replay_frame_end)
+                t3 = time.perf_counter()
+                rp.frame_begin(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+                t3b = time.perf_counter()
+                lines, tl = fut.result()
+                t3e = time.perf_counter()
+                det = rp.frame_end(lines=f.get("lines"))
+                t_assoc = (t3b - t3) + (time.perf_counter() - t3e)
+            else:
+                t3 = time.perf_counter()
+                det = rp.frame(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+                t_assoc = time.perf_counter() - t3
             if f["kf"]:
+                t5 = time.perf_counter()
                 rp.local_mapping()
+                t_assoc += time.perf_counter() - t5
             t4 = time.perf_counter()
-            st[t] = [((tl if overlap else t1) - t0) * 1e3, (t2 - t1) * 1e3, t_match * 1e3, (t4 - t3) * 1e3,
+            st[t] = [((tl if overlap else t1) - t0) * 1e3, (t2 - t1) * 1e3, t_match * 1e3, t_assoc * 1e3,
                      (t4 - t0 - prep) * 1e3]
             if keep:
                 outs.append((lines, kps, desc, nm, cm, det))
@@ -872,7 +884,12 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
         return st, outs, objs
 
     seq, outs, gobjs = one_pass(False, True)
-    ovl, _, _ = one_pass(True, False)
+    ovl, outs_o, objs_o = one_pass(True, True)
+    # the overlapped pass (split association calls, lines on a second thread) gives the same outputs
+    split_same = (all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and
+                      a[3] == b[3] and np.array_equal(a[5], b[5]) for a, b in zip(outs, outs_o)) and
+                  all(np.array_equal(x, y) for x, y in zip(gobjs[0], objs_o[0])) and
+                  np.array_equal(np.nan_to_num(gobjs[1]), np.nan_to_num(objs_o[1])))
     for h in (orb1, mt1, ln1):
         h.close()
 
@@ -886,8 +903,11 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
            "overlapped": {"frames_per_s": F / (ovl[:, 4].sum() * 1e-3),
                           "ms_per_frame": {n: stats(ovl[:, k]) for k, n in
                                            enumerate(["lines", "extract", "match", "assoc", "frame"])},
-                          "note": "line detection on a second host thread beside extract + match; 'lines' is "
-                                  "its call span, 'frame' the frame's wall time"}}
+                          "note": "line detection on a second host thread beside extract + match, and beside "
+                                  "the association's first call (eao_replay_frame_begin; the lines go to "
+                                  "eao_replay_frame_end); 'lines' is its call span, 'assoc' the two calls, "
+                                  "'frame' the frame's wall time",
+                          "outputs_identical_to_sequential": bool(split_same)}}
     if check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import pyoracle as orc  # checker only

@@ -2952,7 +2952,9 @@ class ReplayEngine {
         return false;
       }
       case 3:
-        associate_lines(o2, &s == &prep ? &s.took_lines : nullptr);  // STEP 3, Tracking.cc:1286
+        // STEP 3, Tracking.cc:1286 (a split frame takes its lines at eao_replay_frame_end: their only
+        // reader is SampleObjYaw, at step 10.6 and at forest completions of later frames)
+        if (!defer_lines || &s == &prep) associate_lines(o2, &s == &prep ? &s.took_lines : nullptr);
         s.phase = 4;
         s.k = 0;
         prof[12] += now_us() - tA;
@@ -3024,8 +3026,74 @@ class ReplayEngine {
     return true;
   }
 
+  // a frame split at its lines (eao_replay_frame_begin / _end): what the tail needs
+  bool defer_lines = false;
+  struct {
+    bool open = false, step10 = false;
+    unsigned long fid = 0;
+    std::vector<Det*> o2;
+  } split;
   int frame(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts,
-            const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out) {
+            const int32_t* ids, const float* pos, const float* uv, const uint8_t* bad, int32_t* out,
+            bool begin_only = false) {
+    if (split.open) return EAO_E_STATE;
+    defer_lines = begin_only;
+    struct DeferOff {
+      bool* f;
+      ~DeferOff() { *f = false; }
+    } defer_off{&defer_lines};
+    bool step10 = false;
+    int rc0 = frame_body(fid, Tcw, nb, boxes, npts, ids, pos, uv, bad, step10, split.o2);
+    if (rc0) return rc0;
+    split.fid = fid;
+    split.step10 = step10;
+    if (begin_only) {
+      split.open = true;
+      return EAO_OK;
+    }
+    return frame_tail(out);
+  }
+  // eao_replay_frame_end: the deferred line association, SampleObjYaw (10.6), the outputs
+  int frame_end(int32_t* out) {
+    if (!split.open) return EAO_E_STATE;
+    split.open = false;
+    associate_lines(split.o2, nullptr);
+    return frame_tail(out);
+  }
+  int frame_tail(int32_t* out) {
+    Tick tk(&prof[0]);
+    const unsigned long fid = split.fid;
+    std::vector<Det*>& o2 = split.o2;
+    if (split.step10 && yaw_on())  // 10.6 SampleObjYaw for regular objects seen this frame (Tracking.cc:1650-1671)
+      for (int i = (int)objs.size() - 1; i >= 0; i--) {
+        Obj* o = objs[i].get();
+        if (o->bad) continue;
+        if ((unsigned long)(long)o->last_add < fid - 5) continue;
+        if (!(yaw_class(o->cls) && (unsigned long)(long)o->last_add == fid)) continue;
+        if (o->pending) {  // cuboid not final yet: sample when its forest completes
+          o->yaw_due = true;
+          std::memcpy(o->yawT, pz.T, sizeof(o->yawT));
+        } else {
+          sample_yaw(o, pz.T);
+        }
+      }
+    for (Det* f : o2) {
+      const int k = f->index;
+      out[4 * k] = f->method;
+      out[4 * k + 1] = f->mnId;
+      out[4 * k + 2] = f->cls;
+      out[4 * k + 3] = (int)f->pts.size();
+    }
+    o2.clear();
+    if (pend_err) {
+      const int e = pend_err;
+      pend_err = 0;
+      return e;
+    }
+    return EAO_OK;
+  }
+  int frame_body(unsigned long fid, const float* Tcw, int nb, const int32_t* boxes, int npts, const int32_t* ids,
+                 const float* pos, const float* uv, const uint8_t* bad, bool& step10, std::vector<Det*>& o2) {
     Tick tk(&prof[0]);
     tr(1, (int)fid);
     frame_t0 = now_us();
@@ -3038,7 +3106,8 @@ class ReplayEngine {
     kept_pos = -1;
     cur_np_done = true;
     np_cache.clear();
-    std::vector<Det*> o2, kept;
+    o2.clear();
+    std::vector<Det*> kept;
     over.assign(objs.size(), 0);
     if (prep.active && (prep.in.fid != fid || prep.in.nb != nb)) discard_lookahead();  // not the stream's next
     if (prep.active) {  // steps 1-6 (partly) ran ahead, while the previous frame waited on the GPU
@@ -3207,31 +3276,7 @@ class ReplayEngine {
           }
         }
       }
-      if (yaw_on())  // 10.6 SampleObjYaw for regular objects seen this frame (Tracking.cc:1650-1671)
-        for (int i = (int)objs.size() - 1; i >= 0; i--) {
-          Obj* o = objs[i].get();
-          if (o->bad) continue;
-          if ((unsigned long)(long)o->last_add < fid - 5) continue;
-          if (!(yaw_class(o->cls) && (unsigned long)(long)o->last_add == fid)) continue;
-          if (o->pending) {  // cuboid not final yet: sample when its forest completes
-            o->yaw_due = true;
-            std::memcpy(o->yawT, pz.T, sizeof(o->yawT));
-          } else {
-            sample_yaw(o, pz.T);
-          }
-        }
-    }
-    for (Det* f : o2) {
-      const int k = f->index;
-      out[4 * k] = f->method;
-      out[4 * k + 1] = f->mnId;
-      out[4 * k + 2] = f->cls;
-      out[4 * k + 3] = (int)f->pts.size();
-    }
-    if (pend_err) {
-      const int e = pend_err;
-      pend_err = 0;
-      return e;
+      step10 = true;  // 10.6 in frame_tail
     }
     return EAO_OK;
   }
@@ -3472,6 +3517,7 @@ class ReplayEngine {
   }
 
   int local_mapping() {
+    if (split.open) return EAO_E_STATE;  // the open frame's tail first
     Tick tk(&prof[1]);
     tr(8);
     struct TrEnd {
@@ -3591,6 +3637,27 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
   EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
   const int rc = r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv,
                             mp_bad, det_out);
+  return rc ? rc : (int)r->r.objs.size();
+}
+
+int eao_replay_frame_begin(eao_replay* r, int frame_id, const float* Tcw, int n_boxes, const int32_t* boxes,
+                           int n_pts, const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                           const uint8_t* mp_bad) {
+  if (!r || !Tcw || n_boxes < 0 || n_pts < 0 || (n_boxes && !boxes) || (n_pts && (!mp_ids || !mp_pos || !kp_uv)))
+    return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
+  return r->r.frame((unsigned long)frame_id, Tcw, n_boxes, boxes, n_pts, mp_ids, mp_pos, kp_uv, mp_bad, nullptr,
+                    true);
+}
+
+int eao_replay_frame_end(eao_replay* r, int32_t* det_out) {
+  if (!r) return EAO_E_ARG;
+  EAO_REPLAY_LOCK(r);
+  if (!r->r.split.open) return EAO_E_STATE;
+  if (!r->r.split.o2.empty() && !det_out) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(r->r.A->dev));
+  const int rc = r->r.frame_end(det_out);
   return rc ? rc : (int)r->r.objs.size();
 }
 

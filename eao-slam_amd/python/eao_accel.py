@@ -588,6 +588,26 @@ class Replay(_Handle):
               "eao_replay_frame")
         return out
 
+    def frame_begin(self, fid, T, boxes, ids, pos, uv, bad=None):
+        """eao_replay_frame_begin: the frame up to its line-dependent tail (the caller's line
+        detection may still be running); finish with frame_end(lines)."""
+        boxes = np.ascontiguousarray(boxes, np.int32).reshape(-1, 5)
+        self._open = boxes
+        bad = np.zeros(len(ids), np.uint8) if bad is None else np.ascontiguousarray(bad, np.uint8)
+        check(lib().eao_replay_frame_begin(self.h, int(fid), P(np.ascontiguousarray(T, np.float32)), len(boxes),
+                                           P(boxes), len(ids), P(np.ascontiguousarray(ids, np.int32)),
+                                           P(np.ascontiguousarray(pos, np.float32)),
+                                           P(np.ascontiguousarray(uv, np.float32)), P(bad)),
+              "eao_replay_frame_begin")
+
+    def frame_end(self, lines=None):
+        """eao_replay_frame_end after staging the frame's lines: the detections' [n][4] rows."""
+        out = np.zeros((len(self._open), 4), np.int32)
+        if lines is not None:
+            self.lines([lines])
+        check(lib().eao_replay_frame_end(self.h, P(out)), "eao_replay_frame_end")
+        return out
+
     def local_mapping(self):
         check(lib().eao_replay_local_mapping(self.h), "eao_replay_local_mapping")
 

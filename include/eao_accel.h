@@ -312,6 +312,18 @@ int eao_replay_frame(eao_replay* r, int frame_id, const float* Tcw, int n_boxes,
                      const int32_t* boxes, int n_pts, const int32_t* mp_ids, const float* mp_pos,
                      const float* kp_uv, const uint8_t* mp_bad, int32_t* det_out);
 int eao_replay_local_mapping(eao_replay* r);
+/* eao_replay_frame in two calls around the frame's line detection: _begin runs the frame
+   (map points, frame statistics, data association, the forest launches, culling) without its
+   lines; the caller then stages the frame's lines (eao_replay_lines, one set) and _end runs
+   AssociateObjAndLines and SampleObjYaw (Tracking.cc:1286, 1650-1671: the lines' only
+   readers) and writes det_out as eao_replay_frame would. Same results as eao_replay_frame with
+   the lines staged before it. Between the two calls eao_replay_frame, _begin,
+   eao_replay_local_mapping and eao_replay_run return EAO_E_STATE; _end without an open frame
+   too. _end returns #objects or < 0. */
+int eao_replay_frame_begin(eao_replay* r, int frame_id, const float* Tcw, int n_boxes, const int32_t* boxes,
+                           int n_pts, const int32_t* mp_ids, const float* mp_pos, const float* kp_uv,
+                           const uint8_t* mp_bad);
+int eao_replay_frame_end(eao_replay* r, int32_t* det_out);
 /* Frame line segments (Frame::all_lines_eigen rows x1, y1, x2, y2 from the line
    detector, src/Frame.cc:324-335) for the next n_frames frames replayed by
    eao_replay_frame / eao_replay_run, one set per frame in order. They feed

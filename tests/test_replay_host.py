@@ -307,3 +307,29 @@ def test_host_mean_std_skips_checked_point_by_point(harness):
                          env=dict(os.environ, EAO_MS_VERIFY="1"), capture_output=True, text=True, timeout=900)
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-2000:])
     assert "5 passed" in out.stdout, out.stdout[-500:]
+
+
+@pytest.mark.parametrize("flag", ["EAO", "Full"])
+def test_host_split_frame_matches_oracle(harness, flag):
+    """eao_replay_frame_begin / _end with the frame's lines staged between them (the drop-in's line
+    detection still running while the association starts): every frame's rows and the object state
+    equal the oracle's one-call frames; a second begin, a local mapping or an end without an open
+    frame are refused (EAO_E_STATE) and change nothing."""
+    frames = synth.assoc_stream_fr3_real()[:150]
+    g = _HostReplay(harness, flag)
+    o = orc.Replay(flag)
+    for i, f in enumerate(frames):
+        g._with(ea.Replay.frame_begin, g, i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+        if i == 3:
+            H = harness
+            assert H.eao_replay_local_mapping(g.h) == -5
+            assert H.eao_replay_frame_begin(g.h, i + 1, ea.P(np.asarray(f["T"], np.float32)), 0, None, 0, None, None,
+                                            None, None) == -5
+        det = g._with(ea.Replay.frame_end, g, f.get("lines"))
+        ref = o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        assert np.array_equal(det, ref), i
+        if f["kf"]:
+            g.local_mapping()
+            o.local_mapping()
+    assert harness.eao_replay_frame_end(g.h, None) == -5
+    _compare(g, o)
