@@ -133,3 +133,26 @@ def test_replay_run_updates_packed():
 def test_replay_none_flag_fr3_405():
     """BASELINE configs[0]'s flag (None: no iForest, no yaw) on the fr3 demo stream."""
     _run_steps("None", synth.assoc_stream_fr3_real())
+
+
+@pytest.mark.parametrize("flag", ["EAO", "Full"])
+def test_replay_split_frames_fr3(flag):
+    """eao_replay_frame_begin / _end on the engine (HSA lanes), the lines staged between the calls as
+    the drop-in's overlapped pass does: every frame's rows and the objects equal the oracle's."""
+    frames = synth.assoc_stream_fr3_real()[:200]
+    a = ea.Assoc()
+    rp = ea.Replay(a, flag)
+    o = orc.Replay(flag)
+    for i, f in enumerate(frames):
+        rp.frame_begin(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
+        det = rp.frame_end(lines=f.get("lines"))
+        ref = o.frame(i + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"], lines=f.get("lines"))
+        assert np.array_equal(det, ref), i
+        if f["kf"]:
+            rp.local_mapping()
+            o.local_mapping()
+    gi, gf, gp = rp.objects()
+    oi, of, op = o.objects()
+    assert np.array_equal(gi, oi) and np.allclose(gf, of, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert all(np.array_equal(x, y) for x, y in zip(gp, op))
+    rp.close()
