@@ -2055,8 +2055,18 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
     const size_t o = e.stage_in.put(nullptr, (size_t)row * e.H);
     for (int y = 0; y < e.H; y++) std::memcpy(e.stage_in.h + o + (size_t)y * row, img + (size_t)y * pitch, row);
   }
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)row * e.H, hipMemcpyHostToDevice, s));
-  int rc = eao_lines_detect_color_batch_device(L, e.d_img, 1, row, channels, min_length, e.d_lines, e.d_nlines, 4096, s);
+  // the maps kernel reads the pinned frame in place over PCIe by default (EAO_LINES_DMA_IN=1: one DMA
+  // copy first): no copy-engine transfer for the other engines' copies of the frame to queue behind
+  static const bool dma_in = [] {
+    const char* v = getenv("EAO_LINES_DMA_IN");
+    return v && v[0] == '1';
+  }();
+  const uint8_t* src = e.d_img;
+  if (dma_in)
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)row * e.H, hipMemcpyHostToDevice, s));
+  else
+    src = e.stage_in.h;
+  int rc = eao_lines_detect_color_batch_device(L, src, 1, row, channels, min_length, e.d_lines, e.d_nlines, 4096, s);
   if (rc) return rc;
   const size_t lb = sizeof(float) * 6 * (size_t)std::min(std::max(cap, 0), 4096);
   EAO_HIP_CHECK(e.stage_out.reserve(lb));
