@@ -114,11 +114,22 @@ int eao_orb_extract(eao_orb* h, const uint8_t* gray, int w, int hh, int stride, 
     const size_t o = e.stage_in.put(nullptr, (size_t)w * hh);
     for (int y = 0; y < hh; y++) std::memcpy(e.stage_in.h + o + (size_t)y * w, gray + (size_t)y * stride, w);
   }
-  EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)w * hh, hipMemcpyHostToDevice, e.stream));
+  // moved by kernel by default (EAO_ORB_DMA=1: copy-engine transfers): see OrbEngine::image_in
+  static const bool dma = [] {
+    const char* v = getenv("EAO_ORB_DMA");
+    return v && v[0] == '1';
+  }();
+  if (dma)
+    EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)w * hh, hipMemcpyHostToDevice, e.stream));
+  else if (int rc0 = e.image_in((size_t)w * hh))
+    return rc0;
   int rc = e.run(e.d_img, 1, w, e.d_out_kps, e.d_out_desc, e.d_out_cnt, e.cap, e.stream);
   if (rc) return rc;
   EAO_HIP_CHECK(e.stage_out.reserve(e.out_bytes));
-  EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_out_blk, e.out_bytes, hipMemcpyDeviceToHost, e.stream));
+  if (dma)
+    EAO_HIP_CHECK(hipMemcpyAsync(e.stage_out.h, e.d_out_blk, e.out_bytes, hipMemcpyDeviceToHost, e.stream));
+  else if ((rc = e.outputs_out()))
+    return rc;
   EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
   const int n = *(const int*)e.stage_out.h;
   *n_out = n;

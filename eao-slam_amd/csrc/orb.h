@@ -100,6 +100,10 @@ class OrbEngine {
   int init(const eao_orb_params& prm, int device);
   int run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint_dev* d_kps, uint8_t* d_desc,
           int* d_counts, int out_cap, hipStream_t s);
+  // single-image calls: the staged image into d_img and the outputs (count, then count keypoints and
+  // descriptors) into stage_out by kernel on `stream` (no copy-engine transfers)
+  int image_in(size_t bytes);
+  int outputs_out();
   ~OrbEngine();
 };
 

@@ -2051,7 +2051,7 @@ int OrbEngine::init(const eao_orb_params& prm, int device) {
   EAO_HIP_CHECK(hipMalloc(&d_sel, sel_stride * sizeof(uint32_t) * B));
   EAO_HIP_CHECK(hipMalloc(&d_sel_cnt, p.nlevels * sizeof(int) * B));
   // single-image staging
-  EAO_HIP_CHECK(hipMalloc(&d_img, (size_t)p.width * p.height));
+  EAO_HIP_CHECK(hipMalloc(&d_img, ((size_t)p.width * p.height + 15) & ~(size_t)15));  // image_in copies 16 B units
   // single-image outputs in one block [count | keypoints | descriptors]: one copy back
   out_kps_off = 16;
   out_desc_off = (out_kps_off + (size_t)cap * sizeof(eao_keypoint_dev) + 15) & ~(size_t)15;
@@ -2071,6 +2071,45 @@ OrbEngine::~OrbEngine() {
   if (stream) (void)hipStreamDestroy(stream);
   for (auto& e : ev)
     if (e) (void)hipEventDestroy(e);
+}
+
+// Single-image calls move their image and outputs by kernel between pinned host memory and HBM: a
+// copy-engine transfer queues behind every other engine's transfers on the device (the drop-in's line
+// calls and matching run beside the extraction), a kernel copy does not.
+__global__ __launch_bounds__(256) void k_stage_in(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+__global__ __launch_bounds__(256) void k_orb_out(const uint8_t* __restrict__ blk, uint8_t* __restrict__ host,
+                                                 int kps_off, int desc_off, int cap) {
+  const int n = max(0, min(*(const int*)blk, cap));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *(int*)host = *(const int*)blk;
+  const int nk = (n * (int)sizeof(eao_keypoint_dev) + 15) >> 4, nd = n * 2;
+  const uint4* ks = (const uint4*)(blk + kps_off);
+  const uint4* ds = (const uint4*)(blk + desc_off);
+  uint4* kd = (uint4*)(host + kps_off);
+  uint4* dd = (uint4*)(host + desc_off);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nk + nd; i += gridDim.x * 256) {
+    if (i < nk)
+      kd[i] = ks[i];
+    else
+      dd[i - nk] = ds[i - nk];
+  }
+}
+
+int OrbEngine::image_in(size_t bytes) {
+  const int n16 = (int)((bytes + 15) >> 4);  // both buffers 16-aligned and rounded up to 16 B
+  hipLaunchKernelGGL(k_stage_in, dim3(std::min(120, (n16 + 255) / 256)), dim3(256), 0, stream,
+                     (const uint4*)stage_in.h, (uint4*)d_img, n16);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
+}
+
+int OrbEngine::outputs_out() {
+  hipLaunchKernelGGL(k_orb_out, dim3(16), dim3(256), 0, stream, d_out_blk, (uint8_t*)stage_out.h, (int)out_kps_off,
+                     (int)out_desc_off, cap);
+  EAO_HIP_CHECK(hipGetLastError());
+  return EAO_OK;
 }
 
 int OrbEngine::run(const uint8_t* d_frames, int nframes, int pitch, eao_keypoint_dev* d_kps,
