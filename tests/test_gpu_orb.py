@@ -77,6 +77,20 @@ def test_extract_init_extractor(frames):
     assert np.array_equal(gd, od)
 
 
+@pytest.mark.parametrize("w,h", [(641, 481), (333, 257)])
+def test_extract_single_call_odd_sizes(w, h):
+    # the single call moves its image in 16-byte units by kernel (OrbEngine::image_in): w*h not a
+    # multiple of 16, and the outputs back by kernel (count, keypoints, descriptors), twice in a row
+    img = synth.render(synth.texture(w * h, 2048), synth.camera_path(1, w)[0], w, h,
+                       K=(0.8 * w, 0.8 * w, 0.5 * w, 0.5 * h))
+    orb = ea.Orb(width=w, height=h, nfeatures=1000)
+    ok, od = orc.extract(img)
+    for _ in range(2):
+        gk, gd = orb.extract(img)
+        _cmp_kps(gk, ok)
+        assert np.array_equal(gd, od)
+
+
 def test_extract_flat_and_noise():
     # edge cases: a flat image (no corners -> 0 keypoints) and pure noise (dense corners)
     orb = ea.Orb()
