@@ -1885,7 +1885,7 @@ int eao_lines_create(int device, int width, int height, int max_batch, eao_lines
       (e.gstarts && hipMalloc(&e.d_starts, (size_t)2 * ((e.ecap + 2 + 3) & ~3) * 4 * max_batch) != hipSuccess) ||
       hipMalloc(&e.d_nanch, 4 * (size_t)max_batch) != hipSuccess ||
       hipMalloc(&e.d_nedge, 4 * (size_t)max_batch) != hipSuccess ||
-      hipMalloc(&e.d_img, (size_t)width * height * 4) != hipSuccess ||
+      hipMalloc(&e.d_img, (size_t)width * height * 4 + 16) != hipSuccess ||  // + the staging kernel's 16 B rounding
       hipMalloc(&e.d_lines, sizeof(float) * 6 * 4096) != hipSuccess || hipMalloc(&e.d_nlines, 8) != hipSuccess ||
       hipHostMalloc((void**)&e.h_n, 2 * sizeof(int), 0) != hipSuccess) {
     set_error("eao_lines_create: device allocation failed");
@@ -2038,6 +2038,10 @@ __global__ __launch_bounds__(256) void k_lines_out(const int* __restrict__ dn, c
   for (int i = threadIdx.x; i < k; i += blockDim.x) hl[i] = dl[i];
 }
 
+__global__ __launch_bounds__(256) void k_lines_stage(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+
 int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length, float* lines,
                            int cap, int* n_out) {
   if (!L || !img || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
@@ -2055,17 +2059,25 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
     const size_t o = e.stage_in.put(nullptr, (size_t)row * e.H);
     for (int y = 0; y < e.H; y++) std::memcpy(e.stage_in.h + o + (size_t)y * row, img + (size_t)y * pitch, row);
   }
-  // the maps kernel reads the pinned frame in place over PCIe by default (EAO_LINES_DMA_IN=1: one DMA
-  // copy first): no copy-engine transfer for the other engines' copies of the frame to queue behind
-  static const bool dma_in = [] {
-    const char* v = getenv("EAO_LINES_DMA_IN");
-    return v && v[0] == '1';
+  // the pinned frame into HBM by a copy kernel (16 B per lane over 120 workgroups, ~50 GB/s) by default:
+  // a copy-engine transfer would queue behind the other engines' transfers of the frame, and the maps
+  // kernel reading the frame in place over PCIe ran 58 us against 16 us from HBM (its tiles' loads are
+  // latency-bound there). EAO_LINES_IN=dma: one DMA copy; =pcie: the maps kernel reads in place (A/B)
+  static const int in_mode = [] {
+    const char* v = getenv("EAO_LINES_IN");
+    return !v ? 0 : v[0] == 'd' ? 1 : v[0] == 'p' ? 2 : 0;
   }();
   const uint8_t* src = e.d_img;
-  if (dma_in)
+  if (in_mode == 1) {
     EAO_HIP_CHECK(hipMemcpyAsync(e.d_img, e.stage_in.h, (size_t)row * e.H, hipMemcpyHostToDevice, s));
-  else
+  } else if (in_mode == 2) {
     src = e.stage_in.h;
+  } else {
+    const int n16 = (int)(((size_t)row * e.H + 15) >> 4);  // stage_in: 16-aligned with slack; d_img: + 16 B
+    hipLaunchKernelGGL(k_lines_stage, dim3(std::min(240, (n16 + 255) / 256)), dim3(256), 0, s,
+                       (const uint4*)e.stage_in.h, (uint4*)e.d_img, n16);
+    EAO_HIP_CHECK(hipGetLastError());
+  }
   int rc = eao_lines_detect_color_batch_device(L, src, 1, row, channels, min_length, e.d_lines, e.d_nlines, 4096, s);
   if (rc) return rc;
   const size_t lb = sizeof(float) * 6 * (size_t)std::min(std::max(cap, 0), 4096);
