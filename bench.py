@@ -831,13 +831,18 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
         st = np.zeros((F, 5))  # lines, extract, match, assoc, frame (ms)
         outs = []
         last = None
-        pool = ThreadPoolExecutor(1) if overlap else None
+        # overlap "thread": the line call on a second host thread; "async": its two halves on this
+        # thread (eao_lines_detect_color_start before the extraction, _finish after frame_begin)
+        pool = ThreadPoolExecutor(1) if overlap == "thread" else None
         for t in range(F):
             prep = 0.0
             t0 = time.perf_counter()
-            if overlap:
+            if overlap == "thread":
                 fut = pool.submit(lambda c: (ln1.detect_color(c), time.perf_counter()), color_h[t])
                 t1 = t0
+            elif overlap:
+                ln1.detect_color_start(color_h[t])
+                t1 = time.perf_counter()
             else:
                 lines = ln1.detect_color(color_h[t])
                 t1 = time.perf_counter()
@@ -859,7 +864,11 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
                 t3 = time.perf_counter()
                 rp.frame_begin(t + 1, f["T"], f["boxes"], f["ids"], f["pos"], f["uv"], f["bad"])
                 t3b = time.perf_counter()
-                lines, tl = fut.result()
+                if overlap == "thread":
+                    lines, tl = fut.result()
+                else:
+                    lines = ln1.detect_finish()
+                    tl = time.perf_counter()
                 t3e = time.perf_counter()
                 det = rp.frame_end(lines=f.get("lines"))
                 t_assoc = (t3b - t3) + (time.perf_counter() - t3e)
@@ -884,18 +893,22 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
         return st, outs, objs
 
     seq, outs, gobjs = one_pass(False, True)
-    ovl, outs_o, objs_o = one_pass(True, True)
-    # the overlapped pass (split association calls, lines on a second thread) gives the same outputs
-    split_same = (all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and
+    ovt, outs_t, objs_t = one_pass("thread", True)
+    ovl, outs_o, objs_o = one_pass("async", True)
+
+    def same(outs_o, objs_o):
+        return (all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and
                       a[3] == b[3] and np.array_equal(a[5], b[5]) for a, b in zip(outs, outs_o)) and
                   all(np.array_equal(x, y) for x, y in zip(gobjs[0], objs_o[0])) and
                   np.array_equal(np.nan_to_num(gobjs[1]), np.nan_to_num(objs_o[1])))
+    # both overlapped passes (split association calls, lines beside them) give the same outputs
+    split_same = same(outs_o, objs_o) and same(outs_t, objs_t)
     for h in (orb1, mt1, ln1):
         h.close()
 
     def stats(a):
         return {"mean": float(np.nanmean(a)), "p50": float(np.nanmedian(a)), "p90": float(np.nanpercentile(a, 90))}
-    res = {"frames": F, "entry_points": "eao_lines_detect_color, eao_orb_extract, eao_match_motion, eao_replay_frame "
+    res = {"frames": F, "entry_points": "eao_lines_detect_color (overlapped: eao_lines_detect_color_start / eao_lines_detect_finish), eao_orb_extract, eao_match_motion, eao_replay_frame "
                                         "(+ eao_replay_local_mapping), host buffers, one frame per call",
            "sequential": {"frames_per_s": F / (seq[:, 4].sum() * 1e-3),
                           "ms_per_frame": {n: stats(seq[:, k]) for k, n in
@@ -903,10 +916,14 @@ def dropin_leg(ea, gpu, assoc_frames, color_h, gray_h, poses, flag, check=True):
            "overlapped": {"frames_per_s": F / (ovl[:, 4].sum() * 1e-3),
                           "ms_per_frame": {n: stats(ovl[:, k]) for k, n in
                                            enumerate(["lines", "extract", "match", "assoc", "frame"])},
-                          "note": "line detection on a second host thread beside extract + match, and beside "
-                                  "the association's first call (eao_replay_frame_begin; the lines go to "
-                                  "eao_replay_frame_end); 'lines' is its call span, 'assoc' the two calls, "
-                                  "'frame' the frame's wall time",
+                          "note": "one host thread: the line detection enqueued first "
+                                  "(eao_lines_detect_color_start), extract + match and the association's first "
+                                  "call (eao_replay_frame_begin) while it runs, its lines taken "
+                                  "(eao_lines_detect_finish) for eao_replay_frame_end; 'lines' is the span from "
+                                  "_start to _finish's return, 'assoc' the two calls, 'frame' the frame's wall time",
+                          "second_thread_form": {
+                              "frames_per_s": F / (ovt[:, 4].sum() * 1e-3),
+                              "note": "eao_lines_detect_color on a second host thread instead of the two halves"},
                           "outputs_identical_to_sequential": bool(split_same)}}
     if check:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -1759,6 +1759,7 @@ struct LineEngine {
   float* d_lines = nullptr;
   int* d_nlines = nullptr;
   int* h_n = nullptr;  // pinned: the single-frame line count (and, checking, the diagnostic word)
+  int pending_cap = -1;  // eao_lines_detect_color_start's cap while its outputs are not taken (-1: none)
   HostStage stage_in, stage_out;  // single-frame staging: the pinned image in, count + lines back
   ~LineEngine() {
     if (d_lprof) {
@@ -2042,11 +2043,15 @@ __global__ __launch_bounds__(256) void k_lines_stage(const uint4* __restrict__ s
   for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
 }
 
-int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length, float* lines,
-                           int cap, int* n_out) {
-  if (!L || !img || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
+int eao_lines_detect_color_start(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length,
+                                 int cap) {
+  if (!L || !img || cap < 0) return EAO_E_ARG;
   LineEngine& e = L->e;
   if ((channels != 1 && channels != 3 && channels != 4) || pitch < e.W * channels) return EAO_E_ARG;
+  if (e.pending_cap >= 0) {
+    set_error("eao_lines_detect_color_start: the previous frame's lines are not taken (eao_lines_detect_finish)");
+    return EAO_E_STATE;
+  }
   EAO_HIP_CHECK(hipSetDevice(e.dev));
   hipStream_t s = e.stream;
   const int row = e.W * channels;
@@ -2094,7 +2099,22 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
                        std::min(std::max(cap, 0), 4096), lines_check() ? 2 : 1, e.h_n, (float*)e.stage_out.h);
     EAO_HIP_CHECK(hipGetLastError());
   }
-  EAO_HIP_CHECK(hipStreamSynchronize(s));
+  e.pending_cap = std::min(std::max(cap, 0), 4096);
+  return EAO_OK;
+}
+
+int eao_lines_detect_finish(eao_lines* L, float* lines, int* n_out) {
+  if (!L || !n_out) return EAO_E_ARG;
+  LineEngine& e = L->e;
+  if (e.pending_cap < 0) {
+    set_error("eao_lines_detect_finish: no frame started (eao_lines_detect_color_start)");
+    return EAO_E_STATE;
+  }
+  const int cap = e.pending_cap;
+  e.pending_cap = -1;
+  if (cap && !lines) return EAO_E_ARG;
+  EAO_HIP_CHECK(hipSetDevice(e.dev));
+  EAO_HIP_CHECK(hipStreamSynchronize(e.stream));
   const int n = *e.h_n;
   if (lines_check() && e.h_n[1]) {
     set_error("eao_lines_detect: checking mode found out-of-range records or chains (diag 0x" +
@@ -2109,6 +2129,15 @@ int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int chan
   const int k = n < cap ? n : cap;
   if (k > 0) std::memcpy(lines, e.stage_out.h, sizeof(float) * 6 * k);
   return n > cap ? EAO_E_CAPACITY : EAO_OK;
+}
+
+int eao_lines_detect_color(eao_lines* L, const uint8_t* img, int pitch, int channels, float min_length, float* lines,
+                           int cap, int* n_out) {
+  if (!L || !img || !n_out || cap < 0 || (cap && !lines)) return EAO_E_ARG;
+  *n_out = 0;
+  const int rc = eao_lines_detect_color_start(L, img, pitch, channels, min_length, cap);
+  if (rc) return rc;
+  return eao_lines_detect_finish(L, lines, n_out);
 }
 
 int eao_lines_detect(eao_lines* L, const uint8_t* gray, int pitch, float min_length, float* lines, int cap,

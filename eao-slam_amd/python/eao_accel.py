@@ -478,6 +478,22 @@ class Lines(_Handle):
                                            ctypes.byref(n)), "eao_lines_detect_color")
         return out[:n.value].copy()
 
+    def detect_color_start(self, img, min_length=50.0, cap=4096):
+        """eao_lines_detect_color_start: stage the frame and enqueue the detection, return at once."""
+        a = np.ascontiguousarray(img, np.uint8)
+        cn = 1 if a.ndim == 2 else a.shape[2]
+        check(lib().eao_lines_detect_color_start(self.h, P(a), a.shape[1] * cn, cn, ctypes.c_float(min_length), cap),
+              "eao_lines_detect_color_start")
+        self._pending_cap = cap
+
+    def detect_finish(self):
+        """eao_lines_detect_finish: wait for the started frame, its lines."""
+        cap = getattr(self, "_pending_cap", 0)
+        out = np.zeros((max(cap, 1), 6), np.float32)
+        n = ctypes.c_int()
+        check(lib().eao_lines_detect_finish(self.h, P(out), ctypes.byref(n)), "eao_lines_detect_finish")
+        return out[:n.value].copy()
+
     def detect_color_batch_device(self, img_ptr, nframes, pitch, channels, min_length, lines_ptr, counts_ptr, cap,
                                   stream=None):
         v = ctypes.c_void_p

@@ -250,6 +250,15 @@ int eao_lines_detect(eao_lines* l, const uint8_t* gray, int pitch, float min_len
    eao_lines_detect. pitch in bytes (>= width * channels). */
 int eao_lines_detect_color(eao_lines* l, const uint8_t* img, int pitch, int channels, float min_length,
                            float* lines, int cap, int* n_out);
+/* eao_lines_detect_color in two halves, so the caller's thread does other work (the frame's
+   extraction, matching and eao_replay_frame_begin) while the line detection runs on the handle's
+   stream: _start stages the frame and enqueues every kernel, then returns; _finish waits and
+   writes min(count, cap of _start) lines, with eao_lines_detect_color's return codes. One frame
+   at a time per handle: _start with lines not yet taken, or _finish without _start, is
+   EAO_E_STATE. img may be reused as soon as _start returns. */
+int eao_lines_detect_color_start(eao_lines* l, const uint8_t* img, int pitch, int channels, float min_length,
+                                 int cap);
+int eao_lines_detect_finish(eao_lines* l, float* lines, int* n_out);
 int eao_lines_detect_color_batch_device(eao_lines* l, const uint8_t* d_img, int nframes, int pitch, int channels,
                                         float min_length, float* d_lines, int32_t* d_counts, int cap,
                                         void* stream);

@@ -106,6 +106,29 @@ def color_frames(frames):
     return [np.ascontiguousarray(np.stack([255 - f, f, f], 2)) for f in frames]
 
 
+def test_lines_color_start_finish(frames):
+    """eao_lines_detect_color_start / _finish: the same lines as the one-call form, the input buffer
+    free for reuse once _start returns, and the one-frame-at-a-time contract (EAO_E_STATE)."""
+    L = ea.Lines()
+    cs = color_frames(frames)
+    with pytest.raises(ea.EaoError, match="-5"):
+        L.detect_finish()
+    for c in cs:
+        buf = c.copy()
+        L.detect_color_start(buf)
+        buf[:] = 0  # the frame was staged by _start
+        with pytest.raises(ea.EaoError, match="-5"):
+            L.detect_color_start(c)
+        g = L.detect_finish()
+        assert np.array_equal(g, orc.edlines_color(c))
+        assert np.array_equal(L.detect_color(c), g)
+    # a small cap: the first cap lines and EAO_E_CAPACITY, then the handle is usable again
+    L.detect_color_start(cs[0], cap=3)
+    with pytest.raises(ea.EaoError, match="-4|capacity"):
+        L.detect_finish()
+    assert np.array_equal(L.detect_color(cs[0]), orc.edlines_color(cs[0]))
+
+
 def test_lines_color_exact(frames):
     """The EAO Frame ctor hands the colour rawImage to detect_raw_lines; detectImpl converts it
     with COLOR_BGR2GRAY (binary_descriptor.cpp:490-495). The engine fuses that conversion into
